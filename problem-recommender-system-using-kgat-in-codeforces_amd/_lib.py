@@ -1,0 +1,93 @@
+"""ctypes binding of libkgat_hip.so (the C-ABI declared in include/kgat_hip.h).
+
+The library is built in-tree (``make -C csrc``, or ``__graft_entry__.build()``)
+and loaded after ``torch`` so that it binds to the HIP runtime torch already
+loaded (both carry the soname libamdhip64.so.7).  There is no fallback: if the
+library is missing every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded first: shares its HIP runtime)
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("KGAT_HIP_LIB", _HERE / "libkgat_hip.so"))
+
+KGAT_MAX_TABLES = 8
+
+c_i32, c_i64, c_f32, c_u64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
+
+
+class CSR(ctypes.Structure):
+    """Mirror of ``kgat_csr``."""
+
+    _fields_ = [
+        ("rowptr", c_vp), ("col", c_vp), ("val", c_vp), ("n_rows", c_i64), ("nnz", c_i64),
+        ("long_rows", c_vp), ("long_seg_off", c_vp), ("seg_row", c_vp), ("seg_beg", c_vp),
+        ("n_long", c_i32), ("n_seg", c_i32), ("seg_len", c_i32), ("long_threshold", c_i32),
+    ]
+
+
+class Tables(ctypes.Structure):
+    """Mirror of ``kgat_tables``."""
+
+    _fields_ = [("ptr", c_vp * KGAT_MAX_TABLES), ("ld", c_i64 * KGAT_MAX_TABLES),
+                ("width", c_i32 * KGAT_MAX_TABLES), ("count", c_i32)]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "kgat_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "kgat_version": (ctypes.c_int, []),
+    "kgat_csr_plan": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "kgat_spmm_csr_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_i64,
+                                         c_vp]),
+    "kgat_biinter_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                            c_i32, c_i32, c_f32, c_u64, c_vp]),
+    "kgat_biinter_bwd_workspace": (c_i64, [c_i64, c_i32, c_i32]),
+    "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32,
+                                            c_u64, c_vp, c_i64, c_vp]),
+    "kgat_bpr_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),
+    "kgat_bpr_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_i32, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp,
+                                        c_vp, c_i64, c_vp]),
+    "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
+    "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
+}
+
+_lib = None
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGNATURES)
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is not built."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"KGAT HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        handle = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().kgat_strerror(status).decode()
+        raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)

@@ -1,0 +1,515 @@
+// a2 -- fused bi-interaction aggregator (src/model/KGAT/aggregator.py:57-65):
+//   H = normalize(dropout(LReLU(W1 (X+S) + b1) + LReLU(W2 (X*S) + b2)))
+// and its backward.  The two d_in x d_out contractions run on the fp32 MFMA
+// (v_mfma_f32_16x16x4_f32, exact fp32 fma chains); everything else (bias,
+// LeakyReLU, dropout, row L2 norm) is fused into the MFMA epilogue, so X and
+// S are read once and H written once.
+//
+// Operand layout (both kernels): a wave owns a 16-row sub-tile.  For the
+// X.W^T products lane l holds row (l & 15) and the contiguous k-range
+// [(l>>4)*K/4, (l>>4+1)*K/4) of its row, so A-operand loads are float4 row
+// reads and the k-order of the MFMA chain is (q*K/4 + step) -- any order of a
+// sum is a valid fp32 schedule.  W is staged once per block in LDS with a
+// 4-float pad per row.
+#include "common.hpp"
+
+namespace kgat {
+
+template <int DIN, int DOUT>
+struct BiShape {
+  static constexpr int KQ = DIN / 4;     // k values per lane (A operand, K = DIN)
+  static constexpr int KO = DOUT / 4;    // k values per lane (A operand, K = DOUT)
+  static constexpr int NCB = DOUT / 16;  // 16-wide output column blocks
+  static constexpr int NIB = DIN / 16;   // 16-wide input column blocks
+  static constexpr int WLD = DIN + 4;    // padded LDS row of W (floats)
+  static constexpr int ILD = DIN + 4;    // padded LDS row of an X/S tile
+  static constexpr int OLD = DOUT + 4;   // padded LDS row of a dA/dB tile
+};
+
+// Load this lane's A-operand slice of a 16-row sub-tile (zeros past n).
+template <int K>
+__device__ __forceinline__ void load_rows(const float* __restrict__ P, int64_t ld, int64_t row, int64_t n, int q,
+                                          float (&out)[K / 4]) {
+  constexpr int KQ = K / 4;
+  if (row < n) {
+    const float4* p = reinterpret_cast<const float4*>(P + row * ld + q * KQ);
+#pragma unroll
+    for (int t = 0; t < KQ / 4; ++t) {
+      const float4 v = p[t];
+      out[4 * t] = v.x;
+      out[4 * t + 1] = v.y;
+      out[4 * t + 2] = v.z;
+      out[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) out[t] = 0.f;
+  }
+}
+
+// acc1[cb] = U . W1^T, acc2[cb] = M . W2^T for every 16-wide column block.
+// w1/w2 rows are wld floats apart (LDS copy in the forward, global in the backward).
+template <int DIN, int DOUT>
+__device__ __forceinline__ void bi_products(const float (&u)[DIN / 4], const float (&m)[DIN / 4],
+                                            const float* w1s, const float* w2s, int wld, int q, int c,
+                                            floatx4 (&acc1)[DOUT / 16], floatx4 (&acc2)[DOUT / 16]) {
+  using B = BiShape<DIN, DOUT>;
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    floatx4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
+    const float* r1 = w1s + (cb * 16 + c) * wld + q * B::KQ;
+    const float* r2 = w2s + (cb * 16 + c) * wld + q * B::KQ;
+#pragma unroll
+    for (int t = 0; t < B::KQ; t += 4) {
+      const float4 x1 = *reinterpret_cast<const float4*>(r1 + t);
+      const float4 x2 = *reinterpret_cast<const float4*>(r2 + t);
+      a1 = mfma16x4(u[t], x1.x, a1);
+      a2 = mfma16x4(m[t], x2.x, a2);
+      a1 = mfma16x4(u[t + 1], x1.y, a1);
+      a2 = mfma16x4(m[t + 1], x2.y, a2);
+      a1 = mfma16x4(u[t + 2], x1.z, a1);
+      a2 = mfma16x4(m[t + 2], x2.z, a2);
+      a1 = mfma16x4(u[t + 3], x1.w, a1);
+      a2 = mfma16x4(m[t + 3], x2.w, a2);
+    }
+    acc1[cb] = a1;
+    acc2[cb] = a2;
+  }
+}
+
+template <int DIN, int DOUT>
+__device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const float* __restrict__ W1,
+                                              const float* __restrict__ W2) {
+  using B = BiShape<DIN, DOUT>;
+  for (int i = threadIdx.x; i < DOUT * DIN / 4; i += blockDim.x) {
+    const int j = (i * 4) / DIN, k = (i * 4) % DIN;
+    *reinterpret_cast<float4*>(w1s + j * B::WLD + k) = reinterpret_cast<const float4*>(W1)[i];
+    *reinterpret_cast<float4*>(w2s + j * B::WLD + k) = reinterpret_cast<const float4*>(W2)[i];
+  }
+}
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
+                                                          const float* __restrict__ S, int64_t lds,
+                                                          const float* __restrict__ W1, const float* __restrict__ b1,
+                                                          const float* __restrict__ W2, const float* __restrict__ b2,
+                                                          float* __restrict__ H, int64_t ldh, int64_t n, float p,
+                                                          uint64_t seed) {
+  using B = BiShape<DIN, DOUT>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
+  float* w1s = smem;
+  float* w2s = smem + DOUT * B::WLD;
+  stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  float bias1[B::NCB], bias2[B::NCB];
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    bias1[cb] = b1[cb * 16 + c];
+    bias2[cb] = b2[cb * 16 + c];
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const int64_t nsub = (n + 15) / 16;
+  for (int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); st < nsub;
+       st += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t r0 = st * 16;
+    float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ];
+    load_rows<DIN>(X, ldx, r0 + c, n, q, xs);
+    load_rows<DIN>(S, lds, r0 + c, n, q, ss);
+#pragma unroll
+    for (int t = 0; t < B::KQ; ++t) {
+      u[t] = xs[t] + ss[t];
+      m[t] = xs[t] * ss[t];
+    }
+    floatx4 acc1[B::NCB], acc2[B::NCB];
+    bi_products<DIN, DOUT>(u, m, w1s, w2s, B::WLD, q, c, acc1, acc2);
+
+    float g[B::NCB][4];
+    float sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cb = 0; cb < B::NCB; ++cb) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = lrelu(acc1[cb][i] + bias1[cb]) + lrelu(acc2[cb][i] + bias2[cb]);
+        if (p > 0.f) {
+          const uint64_t idx = static_cast<uint64_t>(r0 + q * 4 + i) * DOUT + cb * 16 + c;
+          v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
+        }
+        g[cb][i] = v;
+        sq[i] = fmaf(v, v, sq[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float den = fmaxf(sqrtf(sum16(sq[i])), kNormEps);
+      const int64_t row = r0 + q * 4 + i;
+      if (row < n) {
+        float* h = H + row * ldh + c;
+#pragma unroll
+        for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] / den;
+      }
+    }
+  }
+}
+
+// Backward.  Phase A (per wave, own 16 rows): recompute the forward, push dH
+// through normalize / dropout / LeakyReLU to dA = dL/d(pre_sum) and
+// dB = dL/d(pre_mul); du = dA.W1, dm = dB.W2 on MFMA; write
+//   dXd = du + dm * S      dS = du + dm * X.
+// Phase B (block, 64 rows): dW1 += dA^T (X+S), dW2 += dB^T (X*S) with K = rows
+// on MFMA, accumulated in registers across the grid-stride loop and written
+// as one slab per block; db1/db2 are column sums of dA/dB.  A second kernel
+// sums the slabs in block order (deterministic).
+// W1/W2 are read through L1/L2 in the backward (16-64 KB, every wave re-reads
+// them), so the LDS holds only the 64-row X/S/dA/dB tiles.
+template <int DIN, int DOUT>
+struct BwdLds {
+  using B = BiShape<DIN, DOUT>;
+  static constexpr int kX = 64 * B::ILD;
+  static constexpr int kO = 64 * B::OLD;
+  static constexpr int kTiles = 2 * kX + 2 * kO;  // floats
+  static constexpr int kW = 2 * DOUT * B::WLD;
+  // stage W in LDS too when everything fits the 160 KiB of one CU
+  static constexpr bool kWInLds = (kTiles + kW) * 4 <= 160 * 1024;
+  static constexpr int kTotal = kTiles + (kWInLds ? kW : 0);
+};
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256) void biinter_bwd_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
+    const float* __restrict__ dH, int64_t lddh, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ dXd, int64_t lddxd,
+    float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p, uint64_t seed) {
+  using B = BiShape<DIN, DOUT>;
+  using Lds = BwdLds<DIN, DOUT>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tx = smem;             // [64][ILD] X tile
+  float* ts = tx + Lds::kX;     // [64][ILD] S tile
+  float* tda = ts + Lds::kX;    // [64][OLD] dA tile
+  float* tdb = tda + Lds::kO;   // [64][OLD] dB tile
+  const float* w1p = W1;
+  const float* w2p = W2;
+  int wld = DIN;
+  if constexpr (Lds::kWInLds) {
+    float* w1s = smem + Lds::kTiles;
+    float* w2s = w1s + DOUT * B::WLD;
+    stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
+    __syncthreads();
+    w1p = w1s;
+    w2p = w2s;
+    wld = B::WLD;
+  }
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  float bias1[B::NCB], bias2[B::NCB];
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    bias1[cb] = b1[cb * 16 + c];
+    bias2[cb] = b2[cb * 16 + c];
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+
+  // phase-B ownership: output 16x16 blocks of [dW1 | dW2], block id
+  // ob = o-block, ib = i-block, mat; wave w takes ids w, w+4, ...
+  constexpr int kBlocks = 2 * B::NCB * B::NIB;
+  constexpr int kMine = (kBlocks + 3) / 4;
+  floatx4 dw[kMine];
+#pragma unroll
+  for (int k = 0; k < kMine; ++k) dw[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float dbias = 0.f, dbias2 = 0.f;  // column sums owned by waves 0 (dA) / 1 (dB)
+
+  const int64_t ntile = (n + 63) / 64;
+  for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const int64_t r0 = tile * 64 + wave * 16;
+    // ---------------- phase A
+    float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ];
+    load_rows<DIN>(X, ldx, r0 + c, n, q, xs);
+    load_rows<DIN>(S, lds, r0 + c, n, q, ss);
+    {
+      float* px = tx + (wave * 16 + c) * B::ILD + q * B::KQ;
+      float* ps = ts + (wave * 16 + c) * B::ILD + q * B::KQ;
+#pragma unroll
+      for (int t = 0; t < B::KQ; t += 4) {
+        *reinterpret_cast<float4*>(px + t) = make_float4(xs[t], xs[t + 1], xs[t + 2], xs[t + 3]);
+        *reinterpret_cast<float4*>(ps + t) = make_float4(ss[t], ss[t + 1], ss[t + 2], ss[t + 3]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < B::KQ; ++t) {
+      u[t] = xs[t] + ss[t];
+      m[t] = xs[t] * ss[t];
+    }
+    floatx4 a1[B::NCB], a2[B::NCB];
+    bi_products<DIN, DOUT>(u, m, w1p, w2p, wld, q, c, a1, a2);
+
+    float gd[B::NCB][4], dh[B::NCB][4];
+    float sq[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + q * 4 + i;
+#pragma unroll
+      for (int cb = 0; cb < B::NCB; ++cb) {
+        a1[cb][i] += bias1[cb];
+        a2[cb][i] += bias2[cb];
+        float v = lrelu(a1[cb][i]) + lrelu(a2[cb][i]);
+        if (p > 0.f) {
+          const uint64_t idx = static_cast<uint64_t>(row) * DOUT + cb * 16 + c;
+          v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
+        }
+        gd[cb][i] = v;
+        dh[cb][i] = row < n ? dH[row * lddh + cb * 16 + c] : 0.f;
+        sq[i] = fmaf(v, v, sq[i]);
+        dt[i] = fmaf(v, dh[cb][i], dt[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float nrm = sqrtf(sum16(sq[i]));
+      const float dot = sum16(dt[i]);
+      const int64_t row = r0 + q * 4 + i;
+      const bool pass = nrm >= kNormEps;
+      const float inv = pass ? 1.f / nrm : 1.f / kNormEps;
+      const float coef = pass ? dot / (nrm * nrm) : 0.f;
+#pragma unroll
+      for (int cb = 0; cb < B::NCB; ++cb) {
+        // d(g/den): dh/den - g (dh.g)/den^3 while the clamp is inactive
+        float dg = (dh[cb][i] - gd[cb][i] * coef) * inv;
+        if (p > 0.f) {
+          const uint64_t idx = static_cast<uint64_t>(row) * DOUT + cb * 16 + c;
+          dg = dropout_keep(seed, idx, p) ? dg * scale : 0.f;
+        }
+        const float da = dg * lrelu_grad(a1[cb][i]);
+        const float db = dg * lrelu_grad(a2[cb][i]);
+        tda[(wave * 16 + q * 4 + i) * B::OLD + cb * 16 + c] = da;
+        tdb[(wave * 16 + q * 4 + i) * B::OLD + cb * 16 + c] = db;
+      }
+    }
+    __syncthreads();
+
+    // du = dA . W1, dm = dB . W2 over K = DOUT (k = q*KO + step)
+    {
+      float dar[B::KO], dbr[B::KO];
+      const float* pa = tda + (wave * 16 + c) * B::OLD + q * B::KO;
+      const float* pb = tdb + (wave * 16 + c) * B::OLD + q * B::KO;
+#pragma unroll
+      for (int t = 0; t < B::KO; t += 4) {
+        const float4 va = *reinterpret_cast<const float4*>(pa + t);
+        const float4 vb = *reinterpret_cast<const float4*>(pb + t);
+        dar[t] = va.x; dar[t + 1] = va.y; dar[t + 2] = va.z; dar[t + 3] = va.w;
+        dbr[t] = vb.x; dbr[t + 1] = vb.y; dbr[t + 2] = vb.z; dbr[t + 3] = vb.w;
+      }
+#pragma unroll 1
+      for (int ib = 0; ib < B::NIB; ++ib) {
+        floatx4 du = {0.f, 0.f, 0.f, 0.f}, dm = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < B::KO; ++t) {
+          const int k = q * B::KO + t;
+          du = mfma16x4(dar[t], w1p[k * wld + ib * 16 + c], du);
+          dm = mfma16x4(dbr[t], w2p[k * wld + ib * 16 + c], dm);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lr = wave * 16 + q * 4 + i;
+          const int64_t row = r0 + q * 4 + i;
+          const float xv = tx[lr * B::ILD + ib * 16 + c];
+          const float sv = ts[lr * B::ILD + ib * 16 + c];
+          if (row < n) {
+            dXd[row * lddxd + ib * 16 + c] = fmaf(dm[i], sv, du[i]);
+            dS[row * ldds + ib * 16 + c] = fmaf(dm[i], xv, du[i]);
+          }
+        }
+      }
+    }
+
+    // ---------------- phase B: weight gradients over the 64-row tile
+#pragma unroll
+    for (int k = 0; k < kMine; ++k) {
+      const int id = wave + 4 * k;
+      if (id < kBlocks) {
+        const int mat = id / (B::NCB * B::NIB);
+        const int rem = id % (B::NCB * B::NIB);
+        const int ob = rem / B::NIB, ib = rem % B::NIB;
+        const float* tg = mat == 0 ? tda : tdb;
+        floatx4 acc = dw[k];
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+          const int r = 4 * s + q;  // K slot (l>>4) of step s
+          const float a = tg[r * B::OLD + ob * 16 + c];
+          const float xv = tx[r * B::ILD + ib * 16 + c];
+          const float sv = ts[r * B::ILD + ib * 16 + c];
+          acc = mfma16x4(a, mat == 0 ? xv + sv : xv * sv, acc);
+        }
+        dw[k] = acc;
+      }
+    }
+    if (wave < 2) {
+      const float* tg = wave == 0 ? tda : tdb;
+      for (int j = lane; j < DOUT; j += 64) {
+        float s = 0.f;
+        for (int r = 0; r < 64; ++r) s += tg[r * B::OLD + j];
+        if (j == lane) dbias += s; else dbias2 += s;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------- slab write: [dW1 | dW2 | db1 | db2] per block
+  constexpr int kSlab = 2 * DOUT * DIN + 2 * DOUT;
+  float* out = slab + static_cast<int64_t>(blockIdx.x) * kSlab;
+#pragma unroll
+  for (int k = 0; k < kMine; ++k) {
+    const int id = wave + 4 * k;
+    if (id < kBlocks) {
+      const int mat = id / (B::NCB * B::NIB);
+      const int rem = id % (B::NCB * B::NIB);
+      const int ob = rem / B::NIB, ib = rem % B::NIB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        out[mat * DOUT * DIN + (ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw[k][i];
+    }
+  }
+  if (wave < 2) {
+    float* ob = out + 2 * DOUT * DIN + wave * DOUT;
+    if (lane < DOUT) ob[lane] = dbias;
+    if (lane + 64 < DOUT) ob[lane + 64] = dbias2;
+  }
+}
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int nslab, int width,
+                                                          float* __restrict__ dW1, float* __restrict__ dW2,
+                                                          float* __restrict__ db1, float* __restrict__ db2,
+                                                          int din, int dout) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= width) return;
+  float s = 0.f;
+  for (int b = 0; b < nslab; ++b) s += slab[static_cast<int64_t>(b) * width + i];
+  const int wsz = din * dout;
+  if (i < wsz) dW1[i] = s;
+  else if (i < 2 * wsz) dW2[i - wsz] = s;
+  else if (i < 2 * wsz + dout) db1[i - 2 * wsz] = s;
+  else db2[i - 2 * wsz - dout] = s;
+}
+
+template <int DIN, int DOUT>
+static int bwd_grid(int64_t n) {
+  const int lds = BwdLds<DIN, DOUT>::kTotal * 4;
+  int per_cu = (160 * 1024) / lds;
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > 4) per_cu = 4;
+  return blocks_for(n, 64, kCUs * per_cu);
+}
+
+template <int DIN, int DOUT>
+static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
+                      const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
+                      hipStream_t st) {
+  const int grid = blocks_for(n, 64, kCUs * 8);
+  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, W2, b2,
+                     H, ldh, n, p, seed);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+template <int DIN, int DOUT>
+static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH, int64_t lddh,
+                      const float* W1, const float* b1, const float* W2, const float* b2, float* dXd, int64_t lddxd,
+                      float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, float p,
+                      uint64_t seed, float* ws, int64_t ws_floats, hipStream_t st) {
+  const int grid = bwd_grid<DIN, DOUT>(n);
+  const int width = 2 * DOUT * DIN + 2 * DOUT;
+  if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
+  const size_t lds_bytes = BwdLds<DIN, DOUT>::kTotal * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&biinter_bwd_kernel<DIN, DOUT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
+    if (e != hipSuccess) return static_cast<int>(e);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((biinter_bwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds, dH,
+                     lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, ws, n, p, seed);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 255) / 256), dim3(256), 0, st, ws, grid, width, dW1, dW2,
+                     db1, db2, DIN, DOUT);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+}  // namespace kgat
+
+#define KGAT_BI_DISPATCH(CALL)                                  \
+  switch (d_in * 1000 + d_out) {                                \
+    case 16016: return CALL(16, 16);                            \
+    case 32016: return CALL(32, 16);                            \
+    case 32032: return CALL(32, 32);                            \
+    case 64016: return CALL(64, 16);                            \
+    case 64032: return CALL(64, 32);                            \
+    case 64064: return CALL(64, 64);                            \
+    case 128032: return CALL(128, 32);                          \
+    case 128064: return CALL(128, 64);                          \
+    case 128128: return CALL(128, 128);                         \
+    case 32064: return CALL(32, 64);                            \
+    case 16032: return CALL(16, 32);                            \
+    case 64128: return CALL(64, 128);                           \
+    default: return KGAT_ERR_UNSUPPORTED_DIM;                   \
+  }
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                                    const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
+                                    int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                                    void* stream) {
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || n_rows < 0) return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if (n_rows == 0) return KGAT_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_FWD_CALL(a, b) kgat::launch_fwd<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, seed, st)
+  KGAT_BI_DISPATCH(KGAT_FWD_CALL)
+#undef KGAT_FWD_CALL
+}
+
+extern "C" int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int32_t d_out) {
+  const int64_t width = 2LL * d_in * d_out + 2LL * d_out;
+#define KGAT_WS_CALL(a, b) static_cast<int64_t>(kgat::bwd_grid<a, b>(n_rows)) * width
+  switch (d_in * 1000 + d_out) {
+    case 16016: return KGAT_WS_CALL(16, 16);
+    case 32016: return KGAT_WS_CALL(32, 16);
+    case 32032: return KGAT_WS_CALL(32, 32);
+    case 64016: return KGAT_WS_CALL(64, 16);
+    case 64032: return KGAT_WS_CALL(64, 32);
+    case 64064: return KGAT_WS_CALL(64, 64);
+    case 128032: return KGAT_WS_CALL(128, 32);
+    case 128064: return KGAT_WS_CALL(128, 64);
+    case 128128: return KGAT_WS_CALL(128, 128);
+    case 32064: return KGAT_WS_CALL(32, 64);
+    case 16032: return KGAT_WS_CALL(16, 32);
+    case 64128: return KGAT_WS_CALL(64, 128);
+    default: return -1;
+  }
+#undef KGAT_WS_CALL
+}
+
+extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH,
+                                    int64_t lddh, const float* W1, const float* b1, const float* W2, const float* b2,
+                                    float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
+                                    float* dW2, float* db2, int64_t n_rows, int32_t d_in, int32_t d_out,
+                                    float dropout_p, uint64_t seed, float* workspace, int64_t workspace_floats,
+                                    void* stream) {
+  if (!X || !S || !dH || !W1 || !b1 || !W2 || !b2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n_rows < 0)
+    return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || lddh < d_out || lddxd < d_in || ldds < d_in) return KGAT_ERR_INVALID;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_BWD_CALL(a, b)                                                                                   \
+  kgat::launch_bwd<a, b>(X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, \
+                         n_rows, dropout_p, seed, workspace, workspace_floats, st)
+  KGAT_BI_DISPATCH(KGAT_BWD_CALL)
+#undef KGAT_BWD_CALL
+}

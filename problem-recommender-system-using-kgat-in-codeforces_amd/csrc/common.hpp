@@ -1,0 +1,68 @@
+// Shared device helpers for the gfx950 KGAT kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kgat_hip.h"
+
+#define KGAT_LAUNCH_CHECK()                          \
+  do {                                               \
+    hipError_t e_ = hipGetLastError();               \
+    if (e_ != hipSuccess) return static_cast<int>(e_); \
+  } while (0)
+
+namespace kgat {
+
+constexpr int kWave = 64;           // CDNA wavefront
+constexpr int kCUs = 256;           // MI355X compute units
+constexpr float kLeakySlope = 0.01f;  // nn.LeakyReLU() default (aggregator.py:23)
+constexpr float kNormEps = 1e-12f;    // F.normalize default (aggregator.py:65)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// D[16x16] += A[16x4] . B[4x16], exact fp32 fma chain (v_mfma_f32_16x16x4_f32).
+// Lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; lane l receives
+// D[(l>>4)*4 + i][l&15] in element i.
+__device__ __forceinline__ floatx4 mfma16x4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : x * kLeakySlope; }
+__device__ __forceinline__ float lrelu_grad(float x) { return x > 0.f ? 1.f : kLeakySlope; }
+
+// Counter-based dropout mask: a splitmix64 finaliser of (seed, element index).
+// Regenerated bit-identically by every backward kernel, so no mask is stored.
+__device__ __forceinline__ uint32_t mix_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return static_cast<uint32_t>(z >> 32);
+}
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, float p) {
+  return static_cast<float>(mix_hash(seed, idx) >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+// Sum over the 16 lanes that share (lane >> 4).
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+inline int blocks_for(int64_t work, int per_block, int cap) {
+  int64_t b = (work + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return static_cast<int>(b < cap ? b : cap);
+}
+
+}  // namespace kgat

@@ -1,0 +1,130 @@
+// a9 fused Adam, small device utilities, and the host-side CSR plan builder.
+#include <cmath>
+
+#include "common.hpp"
+
+namespace kgat {
+
+// torch.optim.Adam step for one tensor (model.py:404-419), same operation
+// order as torch's single/multi-tensor CPU/GPU paths:
+//   m = m + (1-b1)(g - m)       (lerp, weight < 0.5 branch)
+//   v = v*b2 + ((1-b2) g) g     (mul_ then addcmul_)
+//   p = p + (-step_size) * (m / (sqrt(v)/bc2_sqrt + eps))
+// HBM-bound: 28 B per parameter (read p g m v, write p m v).
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   float step_size, float b1, float b2, float bc2s, float eps) {
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  const int64_t n4 = n / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  auto upd = [&](float& pp, float gg, float& mm, float& vv) {
+    mm = mm + w1 * (gg - mm);
+    vv = vv * b2 + (w2 * gg) * gg;
+    pp = pp + (-step_size) * (mm / (sqrtf(vv) / bc2s + eps));
+  };
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = p4[i], mm = m4[i], vv = v4[i];
+    const float4 gg = g4[i];
+    upd(pp.x, gg.x, mm.x, vv.x);
+    upd(pp.y, gg.y, mm.y, vv.y);
+    upd(pp.z, gg.z, mm.z, vv.z);
+    upd(pp.w, gg.w, mm.w, vv.w);
+    p4[i] = pp;
+    m4[i] = mm;
+    v4[i] = vv;
+  }
+  for (int64_t i = n4 * 4 + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    upd(p[i], g[i], m[i], v[i]);
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ src, const int32_t* __restrict__ idx,
+                                                     int64_t n, float* __restrict__ dst) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = src[idx[i]];
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ dst, int64_t n, float value) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = value;
+}
+
+}  // namespace kgat
+
+extern "C" const char* kgat_strerror(int status) {
+  switch (status) {
+    case KGAT_OK: return "ok";
+    case KGAT_ERR_INVALID: return "kgat: invalid argument (null pointer, bad size, or misaligned buffer)";
+    case KGAT_ERR_UNSUPPORTED_DIM: return "kgat: feature width not supported by the compiled kernels";
+    case KGAT_ERR_WORKSPACE: return "kgat: workspace too small";
+    default: return hipGetErrorString(static_cast<hipError_t>(status));
+  }
+}
+
+extern "C" int kgat_version(void) { return 1; }
+
+extern "C" int kgat_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,
+                             float beta2, float bc2_sqrt, float eps, void* stream) {
+  if (!p || !g || !m || !v || n < 0) return KGAT_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+       reinterpret_cast<uintptr_t>(v)) & 15)
+    return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  const int grid = kgat::blocks_for(n / 4 + 1, 256, kgat::kCUs * 8);
+  hipLaunchKernelGGL(kgat::adam_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, g, m, v,
+                     n, step_size, beta1, beta2, bc2_sqrt, eps);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst, void* stream) {
+  if (!src || !idx || !dst || n < 0) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::gather_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 8)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), src, idx, n, dst);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_fill_f32(float* dst, int64_t n, float value, void* stream) {
+  if (!dst || n < 0) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::fill_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 8)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dst, n, value);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+// Host: rows with degree > long_threshold become long rows cut into
+// ceil(deg / seg_len) segments (see spmm.hip).
+extern "C" int kgat_csr_plan(const int64_t* rowptr, int64_t n_rows, int32_t long_threshold, int32_t seg_len,
+                             int32_t* n_long, int32_t* n_seg, int32_t* long_rows, int32_t* long_seg_off,
+                             int32_t* seg_row, int64_t* seg_beg) {
+  if (!rowptr || n_rows < 0 || long_threshold < 1 || seg_len < 1 || !n_long || !n_seg) return KGAT_ERR_INVALID;
+  int64_t nl = 0, ns = 0;
+  for (int64_t r = 0; r < n_rows; ++r) {
+    const int64_t deg = rowptr[r + 1] - rowptr[r];
+    if (deg > long_threshold) {
+      const int64_t k = (deg + seg_len - 1) / seg_len;
+      if (long_rows) {
+        long_rows[nl] = static_cast<int32_t>(r);
+        long_seg_off[nl] = static_cast<int32_t>(ns);
+        for (int64_t j = 0; j < k; ++j) {
+          seg_row[ns + j] = static_cast<int32_t>(r);
+          seg_beg[ns + j] = rowptr[r] + j * seg_len;
+        }
+      }
+      ++nl;
+      ns += k;
+    }
+  }
+  if (long_rows) long_seg_off[nl] = static_cast<int32_t>(ns);
+  if (nl > 0x7fffffff || ns > 0x7fffffff) return KGAT_ERR_INVALID;
+  *n_long = static_cast<int32_t>(nl);
+  *n_seg = static_cast<int32_t>(ns);
+  return KGAT_OK;
+}

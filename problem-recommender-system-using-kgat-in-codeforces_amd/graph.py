@@ -1,0 +1,286 @@
+"""Collaborative knowledge graph (CKG) layout: host construction + HBM residency.
+
+Host side (numpy, vectorised) restates the reference's input-layout producer
+(src/model/KGAT/preprocess.py:157-246, 268-326, 628-634):
+
+* adjacency blocks in the reference order ``[0, R+1, 1, R+2, ...]`` -- the
+  interaction block user -> U+problem, its inverse, then every KG relation and
+  its inverse (preprocess.py:177-222);
+* each block normalised to ``(D^-1/2 A)^T D^-1/2 = A^T D^-1`` -- entry (t, h)
+  = count(h, t) / outdeg(h) (preprocess.py:224-246);
+* the per-edge arrays sorted by head then tail (preprocess.py:268-326) and the
+  summed attentive matrix (preprocess.py:628-634).
+
+Device side (:class:`DeviceGraph`) keeps, resident in HBM:
+
+* CSR of A (int64 rowptr, int32 col, fp32 val) + its long-row plan;
+* CSR of A^T with ``perm_t`` (CSR(A^T) position -> CSR(A) position) so that
+  refreshed values are re-permuted with one gather instead of a re-sort;
+* the refresh edge list (head, tail, relation, CSR slot, static degree weight).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+LONG_THRESHOLD = 256   # rows with more edges are split across waves (see csrc/spmm.hip)
+SEG_LEN = 512          # edges per long-row segment
+
+
+@dataclass
+class GraphLayout:
+    """Host arrays of the attentive matrix and the refresh edge list."""
+
+    n_nodes: int
+    rel_order: list[int]          # adjacency_relations, reference order
+    heads: np.ndarray             # int64 [E], sorted by (head, tail)
+    rels: np.ndarray              # int64 [E]
+    tails: np.ndarray             # int64 [E]
+    edge_vals: np.ndarray         # fp32 [E] per-relation normalised value
+    rowptr: np.ndarray            # int64 [N+1]  CSR of the coalesced sum
+    col: np.ndarray               # int32 [nnz]
+    val: np.ndarray               # fp32 [nnz]
+    slot: np.ndarray              # int64 [E] CSR position of each edge
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+    def coo(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        rows = np.repeat(np.arange(self.n_nodes, dtype=np.int64), np.diff(self.rowptr))
+        return rows, self.col.astype(np.int64), self.val
+
+
+def adjacency_blocks(user_num: int, interactions: np.ndarray, triplets: np.ndarray,
+                     kg_relation_ids=(0, 1, 2, 3)):
+    """(relation id, heads, tails) per adjacency block, preprocess.py:177-222."""
+    R = len(kg_relation_ids)
+    ui = np.asarray(interactions, dtype=np.int64).reshape(-1, 2)
+    tr = np.asarray(triplets, dtype=np.int64).reshape(-1, 3)
+    users, items = ui[:, 0], ui[:, 1] + user_num
+    out = [(0, users, items), (R + 1, items, users)]
+    for r in kg_relation_ids:
+        sel = tr[:, 1] == r
+        h, t = tr[sel, 0] + user_num, tr[sel, 2] + user_num
+        out += [(r + 1, h, t), (r + 2 + R, t, h)]
+    return out
+
+
+def _normalised(n: int, h: np.ndarray, t: np.ndarray):
+    """Unique (row=t, col=h) entries with value count(h,t)/outdeg(h) (fp64)."""
+    if h.size == 0:
+        e = np.zeros(0, np.int64)
+        return e, e, np.zeros(0, np.float64)
+    key = h * n + t
+    uk, cnt = np.unique(key, return_counts=True)
+    hh, tt = uk // n, uk % n
+    outdeg = np.bincount(h, minlength=n).astype(np.float64)
+    return tt, hh, cnt / outdeg[hh]
+
+
+def layout_from_blocks(n_nodes: int, blocks) -> GraphLayout:
+    rows, cols, rels, vals, order = [], [], [], [], []
+    for bi, (rel, h, t) in enumerate(blocks):
+        r, c, v = _normalised(n_nodes, np.asarray(h, np.int64), np.asarray(t, np.int64))
+        rows.append(r)
+        cols.append(c)
+        vals.append(v)
+        rels.append(np.full(r.size, rel, np.int64))
+        order.append(np.full(r.size, bi, np.int64))
+    rows, cols, rels = np.concatenate(rows), np.concatenate(cols), np.concatenate(rels)
+    vals64, order = np.concatenate(vals), np.concatenate(order)
+    perm = np.lexsort((order, cols, rows))      # head, then tail, then block order
+    rows, cols, rels, vals64 = rows[perm], cols[perm], rels[perm], vals64[perm]
+    # coalesce duplicates (same (row, col) in two relations): values summed in fp64
+    key = rows * n_nodes + cols
+    first = np.ones(key.size, bool)
+    first[1:] = key[1:] != key[:-1]
+    slot = np.cumsum(first) - 1
+    csr_val = np.zeros(int(first.sum()), np.float64)
+    np.add.at(csr_val, slot, vals64)
+    csr_rows, csr_col = rows[first], cols[first]
+    rowptr = np.zeros(n_nodes + 1, np.int64)
+    np.cumsum(np.bincount(csr_rows, minlength=n_nodes), out=rowptr[1:])
+    return GraphLayout(n_nodes=n_nodes, rel_order=[b[0] for b in blocks], heads=rows, rels=rels, tails=cols,
+                       edge_vals=vals64.astype(np.float32), rowptr=rowptr, col=csr_col.astype(np.int32),
+                       val=csr_val.astype(np.float32), slot=slot.astype(np.int64))
+
+
+def build_layout(user_num: int, entity_num: int, interactions: np.ndarray, triplets: np.ndarray,
+                 kg_relation_ids=(0, 1, 2, 3)) -> GraphLayout:
+    """The reference preprocess graph (preprocess.py:617-634) from raw ids."""
+    return layout_from_blocks(user_num + entity_num,
+                              adjacency_blocks(user_num, interactions, triplets, kg_relation_ids))
+
+
+def csr_from_coo(n: int, rows: np.ndarray, cols: np.ndarray, vals: np.ndarray):
+    """Coalesced CSR (duplicates summed) of a COO matrix."""
+    rows, cols = np.asarray(rows, np.int64), np.asarray(cols, np.int64)
+    key = rows * n + cols
+    uk, inv = np.unique(key, return_inverse=True)
+    v = np.zeros(uk.size, np.float64)
+    np.add.at(v, inv, np.asarray(vals, np.float64))
+    r = uk // n
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(r, minlength=n), out=rowptr[1:])
+    return rowptr, (uk % n).astype(np.int32), v.astype(np.float32)
+
+
+def long_row_plan(rowptr: np.ndarray, long_threshold: int = LONG_THRESHOLD, seg_len: int = SEG_LEN):
+    """numpy twin of kgat_csr_plan(): long rows and their edge segments."""
+    deg = np.diff(rowptr)
+    long_rows = np.nonzero(deg > long_threshold)[0]
+    nseg = (deg[long_rows] + seg_len - 1) // seg_len
+    off = np.zeros(long_rows.size + 1, np.int64)
+    np.cumsum(nseg, out=off[1:])
+    seg_row = np.repeat(long_rows, nseg)
+    local = np.arange(seg_row.size, dtype=np.int64) - np.repeat(off[:-1], nseg)
+    seg_beg = rowptr[seg_row] + local * seg_len
+    return (long_rows.astype(np.int32), off.astype(np.int32), seg_row.astype(np.int32), seg_beg.astype(np.int64))
+
+
+def degree_weights(heads: np.ndarray, tails: np.ndarray, rels: np.ndarray, n: int) -> np.ndarray:
+    """1 / (log1p(deg_h) + log1p(deg_t)), degrees counted within each relation (model.py:309-314)."""
+    w = np.empty(heads.size, np.float32)
+    for r in np.unique(rels):
+        sel = np.nonzero(rels == r)[0]
+        dh = np.bincount(heads[sel], minlength=n)[heads[sel]].astype(np.float32)
+        dt = np.bincount(tails[sel], minlength=n)[tails[sel]].astype(np.float32)
+        w[sel] = np.float32(1.0) / (np.log1p(dh) + np.log1p(dt))
+    return w
+
+
+class _DeviceCSR:
+    """A CSR resident on the device plus its ctypes descriptor."""
+
+    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: torch.Tensor, device):
+        self.n_rows = rowptr.size - 1
+        self.rowptr = torch.from_numpy(np.ascontiguousarray(rowptr, np.int64)).to(device)
+        self.col = torch.from_numpy(np.ascontiguousarray(col, np.int32)).to(device)
+        self.val = val
+        lr, off, sr, sb = long_row_plan(rowptr)
+        self.long_rows = torch.from_numpy(lr).to(device)
+        self.long_seg_off = torch.from_numpy(off).to(device)
+        self.seg_row = torch.from_numpy(sr).to(device)
+        self.seg_beg = torch.from_numpy(sb).to(device)
+        self.n_long, self.n_seg = int(lr.size), int(sr.size)
+        self.max_deg = int(np.diff(rowptr).max()) if self.n_rows else 0
+
+    def descriptor(self) -> _lib.CSR:
+        return _lib.CSR(self.rowptr.data_ptr(), self.col.data_ptr(), self.val.data_ptr(), self.n_rows,
+                        self.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
+                        self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
+                        LONG_THRESHOLD)
+
+
+class DeviceGraph:
+    """HBM-resident attentive matrix A, its transpose and the refresh edge list."""
+
+    def __init__(self, layout: GraphLayout, device: torch.device | str):
+        device = torch.device(device)
+        self.device = device
+        self.layout = layout
+        self.n_nodes = layout.n_nodes
+        rowptr, col = layout.rowptr, layout.col
+        self.A = _DeviceCSR(rowptr, col, torch.from_numpy(layout.val.copy()).to(device), device)
+        # transpose: CSR(A^T) positions sorted by (col, row) -> CSR(A) positions
+        rows = np.repeat(np.arange(self.n_nodes, dtype=np.int64), np.diff(rowptr))
+        perm_t = np.lexsort((rows, col.astype(np.int64)))
+        rowptr_t = np.zeros(self.n_nodes + 1, np.int64)
+        np.cumsum(np.bincount(col, minlength=self.n_nodes), out=rowptr_t[1:])
+        self.perm_t = torch.from_numpy(perm_t.astype(np.int32)).to(device)
+        self.AT = _DeviceCSR(rowptr_t, rows[perm_t].astype(np.int32),
+                             torch.empty(col.size, dtype=torch.float32, device=device), device)
+        # refresh edge list (model.py:318-366)
+        self.edge_heads = torch.from_numpy(layout.heads.astype(np.int32)).to(device)
+        self.edge_tails = torch.from_numpy(layout.tails.astype(np.int32)).to(device)
+        self.edge_rels = torch.from_numpy(layout.rels.astype(np.int32)).to(device)
+        self.edge_slot = torch.from_numpy(layout.slot.astype(np.int32)).to(device)
+        self.edge_weight = torch.from_numpy(
+            degree_weights(layout.heads, layout.tails, layout.rels, self.n_nodes)).to(device)
+        self.rel_order = list(layout.rel_order)
+        self.refresh_transpose()
+
+    @property
+    def nnz(self) -> int:
+        return int(self.A.col.numel())
+
+    def refresh_transpose(self) -> None:
+        """valT = val[perm_t] after A's values changed (one gather kernel)."""
+        if self.nnz:
+            _lib.call("kgat_gather_f32", self.A.val.data_ptr(), self.perm_t.data_ptr(), self.nnz,
+                      self.AT.val.data_ptr(), stream_ptr(self.device))
+
+    def to_sparse_coo(self) -> torch.Tensor:
+        """The attentive matrix as the reference's coalesced sparse COO (model.py:83-92)."""
+        rows, cols, _ = self.layout.coo()
+        idx = torch.from_numpy(np.vstack([rows, cols]))
+        return torch.sparse_coo_tensor(idx, self.A.val.detach().cpu(), (self.n_nodes, self.n_nodes)).coalesce()
+
+
+def stream_ptr(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+# --------------------------------------------------------------------------
+# Seeded synthetic CKG: the GPU configs C2/C4/C5
+# --------------------------------------------------------------------------
+def synthetic_ckg(n_nodes: int, n_triples: int, seed: int = 2024, user_frac: float = 0.1,
+                  interaction_frac: float = 0.8, zipf_s: float = 1.1):
+    """(user_num, entity_num, interactions [M,2], triplets [T,3]).
+
+    First 10 % of nodes are users, the rest entities; items (problems) are the
+    first 10 % of entities.  80 % of triples are user -> item interactions with
+    Zipf(1.1) item popularity (item identity shuffled), 20 % are KG triples over
+    the 4 reference relation types with uniform heads/tails inside type ranges.
+    Duplicates are dropped (first occurrence in draw order wins).
+    """
+    rng = np.random.default_rng(seed)
+    U = max(1, int(n_nodes * user_frac))
+    E = n_nodes - U
+    I = max(1, int(E * 0.1))
+    m_target = int(n_triples * interaction_frac)
+    k_target = n_triples - m_target
+    ranks = np.arange(1, I + 1, dtype=np.float64)
+    cdf = np.cumsum(ranks ** (-zipf_s))
+    cdf /= cdf[-1]
+    item_perm = rng.permutation(I)
+
+    def draw_interactions(count):
+        u = rng.integers(0, U, size=count, dtype=np.int64)
+        it = item_perm[np.minimum(np.searchsorted(cdf, rng.random(count)), I - 1)]
+        return u, it
+
+    inter = np.zeros((0, 2), np.int64)
+    need = m_target
+    while need > 0:
+        u, it = draw_interactions(int(need * 1.3) + 1024)
+        cand = np.concatenate([inter, np.stack([u, it], 1)])
+        key = cand[:, 0] * I + cand[:, 1]
+        _, first = np.unique(key, return_index=True)
+        inter = cand[np.sort(first)][:m_target]
+        if inter.shape[0] >= m_target or inter.shape[0] >= U * I:
+            break
+        need = m_target - inter.shape[0]
+    # KG: 4 relation types, tails from 4 disjoint ranges of the non-item entities
+    rest = max(4, E - I)
+    bounds = [I + (rest * k) // 4 for k in range(5)]
+    rel = rng.integers(0, 4, size=k_target, dtype=np.int64)
+    heads = rng.integers(0, I, size=k_target, dtype=np.int64)
+    # HAS_CONTEST_DIVISION (3): contest (range of IN_CONTEST tails, 2) -> division range (3)
+    c_lo, c_hi = bounds[2], bounds[3]
+    sel3 = rel == 3
+    heads[sel3] = rng.integers(c_lo, c_hi, size=int(sel3.sum()), dtype=np.int64)
+    lo = np.array(bounds[:4])[rel]
+    hi = np.array(bounds[1:])[rel]
+    tails = lo + (rng.random(k_target) * (hi - lo)).astype(np.int64)
+    trip = np.stack([heads, rel, np.minimum(tails, E - 1)], 1)
+    key = (trip[:, 0] * 4 + trip[:, 1]) * E + trip[:, 2]
+    _, first = np.unique(key, return_index=True)
+    trip = trip[np.sort(first)]
+    return U, E, inter, trip

@@ -1,0 +1,172 @@
+"""Typed wrappers over the C-ABI: shape/dtype/device checks, then one HIP call.
+
+Every wrapper launches on the current torch stream of the tensors' device and
+returns without synchronising.  Tensors must be fp32 (ids int64), on the GPU,
+with unit stride in the last dimension; violations raise ``ValueError`` before
+anything is launched, HIP/launch errors raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .graph import DeviceGraph, stream_ptr
+
+
+def _req(t: torch.Tensor, name: str, dtype=torch.float32, dim: int | None = None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: must live on the GPU (the HIP path has no CPU fallback)")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if dim is not None and t.dim() != dim:
+        raise ValueError(f"{name}: expected {dim}-D, got {tuple(t.shape)}")
+    if t.dim() >= 1 and t.numel() and t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dimension must be contiguous")
+
+
+def _ld(t: torch.Tensor) -> int:
+    return t.stride(0) if t.dim() == 2 else t.shape[-1]
+
+
+# Optional launch timer for the dominant kernel (bench.py): when set to a list,
+# every spmm() appends (start_event, end_event, d, transpose, accumulate) recorded
+# on the launch stream around its kernels.
+SPMM_EVENTS: list | None = None
+
+
+def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, transpose: bool = False,
+         accumulate: bool = False) -> torch.Tensor:
+    """Y = A . X (or A^T . X); with accumulate, Y += ..."""
+    _req(X, "X", dim=2)
+    n, d = X.shape
+    if n != graph.n_nodes:
+        raise ValueError(f"X has {n} rows, graph has {graph.n_nodes} nodes")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an output tensor")
+        out = torch.empty(n, d, dtype=torch.float32, device=X.device)
+    _req(out, "out", dim=2)
+    if tuple(out.shape) != (n, d):
+        raise ValueError("out shape mismatch")
+    csr = graph.AT if transpose else graph.A
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=X.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
+              int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, transpose, accumulate))
+    return out
+
+
+def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out=None) -> torch.Tensor:
+    for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2")):
+        _req(t, nm, dim=2)
+    _req(b1, "b1", dim=1)
+    _req(b2, "b2", dim=1)
+    n, din = X.shape
+    dout = W1.shape[0]
+    if S.shape != X.shape or W1.shape != (dout, din) or W2.shape != (dout, din) or b1.numel() != dout:
+        raise ValueError("bi-interaction shape mismatch")
+    if not (W1.is_contiguous() and W2.is_contiguous()):
+        raise ValueError("W must be contiguous")
+    if out is None:
+        out = torch.empty(n, dout, dtype=torch.float32, device=X.device)
+    _lib.call("kgat_biinter_fwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
+              W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout, float(dropout_p),
+              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), stream_ptr(X.device))
+    return out
+
+
+def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None):
+    """Returns (dXd, dS, dW1, db1, dW2, db2)."""
+    n, din = X.shape
+    dout = W1.shape[0]
+    _req(dH, "dH", dim=2)
+    if dH.shape != (n, dout):
+        raise ValueError("dH shape mismatch")
+    dev = X.device
+    dXd = torch.empty(n, din, dtype=torch.float32, device=dev) if dXd is None else dXd
+    dS = torch.empty(n, din, dtype=torch.float32, device=dev) if dS is None else dS
+    dW1 = torch.empty_like(W1)
+    dW2 = torch.empty_like(W2)
+    db1 = torch.empty_like(b1)
+    db2 = torch.empty_like(b2)
+    ws_n = int(_lib.lib().kgat_biinter_bwd_workspace(n, din, dout))
+    if ws_n < 0:
+        raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
+    _lib.call("kgat_biinter_bwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), dH.data_ptr(), _ld(dH),
+              W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(),
+              _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
+              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), ws.data_ptr(), ws.numel(),
+              stream_ptr(dev))
+    return dXd, dS, dW1, db1, dW2, db2
+
+
+def make_tables(tables: list[torch.Tensor]) -> _lib.Tables:
+    if not 1 <= len(tables) <= _lib.KGAT_MAX_TABLES:
+        raise ValueError("1..8 tables supported")
+    T = _lib.Tables()
+    for i, t in enumerate(tables):
+        _req(t, f"table{i}", dim=2)
+        T.ptr[i] = t.data_ptr()
+        T.ld[i] = _ld(t)
+        T.width[i] = t.shape[1]
+    T.count = len(tables)
+    return T
+
+
+def bpr_fwd(tables: list[torch.Tensor], users, pos, neg, reg: float):
+    """(loss [1], coef [B])."""
+    for t, nm in ((users, "users"), (pos, "pos"), (neg, "neg")):
+        _req(t, nm, dtype=torch.int64, dim=1)
+    B = users.numel()
+    if pos.numel() != B or neg.numel() != B or B == 0:
+        raise ValueError("batch size mismatch")
+    dev = users.device
+    loss = torch.empty(1, dtype=torch.float32, device=dev)
+    coef = torch.empty(B, dtype=torch.float32, device=dev)
+    T = make_tables(tables)
+    _lib.call("kgat_bpr_fwd_f32", ctypes.byref(T), users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg),
+              loss.data_ptr(), coef.data_ptr(), stream_ptr(dev))
+    return loss, coef
+
+
+def bpr_bwd(tables: list[torch.Tensor], t: int, users, pos, neg, reg: float, coef, grad_out, dst) -> None:
+    """dst[id] += dL/d tables[t][id] for every gathered id (deterministic)."""
+    _req(dst, "dst", dim=2)
+    _req(grad_out, "grad_out")
+    T = make_tables(tables)
+    _lib.call("kgat_bpr_bwd_f32", ctypes.byref(T), t, users.data_ptr(), pos.data_ptr(), neg.data_ptr(),
+              users.numel(), float(reg), coef.data_ptr(), grad_out.data_ptr(), dst.data_ptr(), _ld(dst),
+              stream_ptr(dst.device))
+
+
+def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float) -> None:
+    for t, nm in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _req(t, nm)
+        if not t.is_contiguous():
+            raise ValueError(f"{nm} must be contiguous")
+    _lib.call("kgat_adam_f32", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), step_size, beta1,
+              beta2, bc2_sqrt, eps, stream_ptr(p.device))
+
+
+def fill(t: torch.Tensor, value: float) -> torch.Tensor:
+    _req(t, "t")
+    if not t.is_contiguous():
+        raise ValueError("fill needs a contiguous tensor")
+    _lib.call("kgat_fill_f32", t.data_ptr(), t.numel(), float(value), stream_ptr(t.device))
+    return t
+
+
+def zeros(shape, device) -> torch.Tensor:
+    return fill(torch.empty(shape, dtype=torch.float32, device=device), 0.0)

@@ -1,0 +1,55 @@
+"""Fused dense Adam on the HIP path (src/model/KGAT/model.py:393-419).
+
+Drop-in for ``torch.optim.Adam(params, lr)`` as the reference uses it:
+betas (0.9, 0.999), eps 1e-8, no weight decay, ``zero_grad`` sets grads to
+None and parameters whose grad is None are skipped (their state untouched).
+The reference builds TWO independent instances over the same parameters
+(CF lr 1e-3, KG lr 1e-4); each keeps its own exp_avg / exp_avg_sq.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import kernels
+
+
+class FusedAdam:
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.params = [p for p in params]
+        self.lr = float(lr)
+        self.beta1, self.beta2 = float(betas[0]), float(betas[1])
+        self.eps = float(eps)
+        self.state: dict[int, dict] = {}
+
+    @torch.no_grad()
+    def step(self) -> None:
+        for p in self.params:
+            g = p.grad
+            if g is None:
+                continue
+            if p.is_sparse or g.is_sparse:
+                raise RuntimeError("FusedAdam: sparse parameters/gradients are not supported")
+            st = self.state.get(id(p))
+            if st is None:
+                st = {"step": 0, "exp_avg": kernels.zeros(p.shape, p.device),
+                      "exp_avg_sq": kernels.zeros(p.shape, p.device)}
+                self.state[id(p)] = st
+            st["step"] += 1
+            t = st["step"]
+            bc1 = 1.0 - self.beta1 ** t
+            bc2_sqrt = math.sqrt(1.0 - self.beta2 ** t)
+            kernels.adam(p.data, g.contiguous(), st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, self.beta1,
+                         self.beta2, bc2_sqrt, self.eps)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                kernels.fill(p.grad, 0.0)
+
+    def state_dict(self) -> dict:
+        return {"lr": self.lr, "betas": (self.beta1, self.beta2), "eps": self.eps,
+                "state": {i: dict(self.state[id(p)]) for i, p in enumerate(self.params) if id(p) in self.state}}

@@ -1,0 +1,227 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the CPU oracle and the
+reference-generated golden vectors.  Needs an MI355X: ``pytest -m gpu``.
+
+Tolerance (north_star): embeddings / losses within 1e-4 fp32 (rtol 1e-4,
+atol 1e-5 on O(1) values, atol 1e-6 on gradients of size ~1e-3).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import kgat_cpu as K
+from tests.conftest import KGAT_CASES, golden, load_pkg
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-4, 1e-5
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_pkg()
+
+
+def _mods(pkg):
+    graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+    kernels = __import__(pkg.__name__ + ".kernels", fromlist=["kernels"])
+    return graph, kernels
+
+
+def random_graph(graph_mod, n, avg_deg, hubs=0, hub_deg=0, seed=0):
+    rng = np.random.default_rng(seed)
+    e = n * avg_deg
+    rows = rng.integers(0, n, e)
+    cols = rng.integers(0, n, e)
+    if hubs:
+        hr = rng.integers(0, n, hubs)
+        rows = np.concatenate([rows, np.repeat(hr, hub_deg)])
+        cols = np.concatenate([cols, rng.integers(0, n, hubs * hub_deg)])
+    vals = rng.standard_normal(rows.size).astype(np.float32)
+    rowptr, col, val = graph_mod.csr_from_coo(n, rows, cols, vals)
+    lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
+                                tails=np.zeros(0, np.int64), edge_vals=np.zeros(0, np.float32), rowptr=rowptr,
+                                col=col, val=val, slot=np.zeros(0, np.int64))
+    r = np.repeat(np.arange(n), np.diff(rowptr))
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r, col.astype(np.int64)])), torch.from_numpy(val),
+                                (n, n)).coalesce()
+    return lay, A
+
+
+@pytest.mark.parametrize("d", [16, 32, 64, 128, 256])
+def test_spmm_parity(pkg, d):
+    graph_mod, kernels = _mods(pkg)
+    lay, A = random_graph(graph_mod, 3000, 9, hubs=5, hub_deg=2000, seed=d)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    assert g.A.n_long >= 5 and g.AT.n_long >= 0
+    X = torch.randn(3000, d)
+    Y = kernels.spmm(g, X.to(DEV)).cpu()
+    np.testing.assert_allclose(Y.numpy(), torch.sparse.mm(A, X).numpy(), rtol=RTOL, atol=1e-4)
+    # transpose + accumulate
+    Z0 = torch.randn(3000, d)
+    Z = Z0.to(DEV)
+    kernels.spmm(g, X.to(DEV), out=Z, transpose=True, accumulate=True)
+    ref = torch.sparse.mm(A.t().coalesce(), X) + Z0
+    np.testing.assert_allclose(Z.cpu().numpy(), ref.numpy(), rtol=RTOL, atol=1e-4)
+    # strided (ld > d) input/output views
+    big = torch.randn(3000, d + 32)
+    out = torch.zeros(3000, d + 16, device=DEV)
+    kernels.spmm(g, big.to(DEV)[:, 16:16 + d], out=out[:, :d])
+    np.testing.assert_allclose(out[:, :d].cpu().numpy(), torch.sparse.mm(A, big[:, 16:16 + d]).numpy(),
+                               rtol=RTOL, atol=1e-4)
+
+
+def test_spmm_empty_rows_and_deterministic(pkg):
+    graph_mod, kernels = _mods(pkg)
+    lay, A = random_graph(graph_mod, 1000, 1, hubs=2, hub_deg=3000, seed=7)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    X = torch.randn(1000, 64, device=DEV)
+    a = kernels.spmm(g, X)
+    b = kernels.spmm(g, X)
+    assert torch.equal(a, b)
+    np.testing.assert_allclose(a.cpu().numpy(), torch.sparse.mm(A, X.cpu()).numpy(), rtol=RTOL, atol=1e-4)
+
+
+BI_SHAPES = [(64, 64), (64, 32), (32, 16), (128, 64), (64, 16), (128, 128), (16, 16)]
+
+
+@pytest.mark.parametrize("din,dout", BI_SHAPES)
+def test_biinter_fwd_bwd_parity(pkg, din, dout):
+    _, kernels = _mods(pkg)
+    torch.manual_seed(din * 7 + dout)
+    n = 1000 + 13  # ragged tail sub-tile
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    W1, W2 = torch.randn(dout, din) * 0.2, torch.randn(dout, din) * 0.2
+    b1, b2 = torch.randn(dout) * 0.1, torch.randn(dout) * 0.1
+    dH = torch.randn(n, dout)
+    leaves = [t.clone().requires_grad_(True) for t in (X, S, W1, b1, W2, b2)]
+    x, s, w1, bb1, w2, bb2 = leaves
+    pre1 = torch.nn.functional.linear(x + s, w1, bb1)
+    pre2 = torch.nn.functional.linear(x * s, w2, bb2)
+    h = torch.nn.functional.leaky_relu(pre1, 0.01) + torch.nn.functional.leaky_relu(pre2, 0.01)
+    ref = h / h.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    ref.backward(dH)
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    H = kernels.biinter_fwd(*dv)
+    np.testing.assert_allclose(H.cpu().numpy(), ref.detach().numpy(), rtol=RTOL, atol=ATOL)
+    dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:])
+    # dX (direct) + dS: the autograd X/S grads see x+s and x*s
+    np.testing.assert_allclose(dXd.cpu().numpy(), x.grad.numpy(), rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(dS.cpu().numpy(), s.grad.numpy(), rtol=1e-3, atol=1e-5)
+    for got, want in ((dW1, w1.grad), (db1, bb1.grad), (dW2, w2.grad), (db2, bb2.grad)):
+        np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-3, atol=1e-4)
+
+
+def test_biinter_dropout_consistent(pkg):
+    """fwd/bwd regenerate the same keep mask; masked elements are exactly zero."""
+    _, kernels = _mods(pkg)
+    torch.manual_seed(3)
+    n, din, dout, p = 4096, 64, 64, 0.1
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    W1, W2 = torch.randn(dout, din) * 0.2, torch.randn(dout, din) * 0.2
+    b1, b2 = torch.randn(dout) * 0.1, torch.randn(dout) * 0.1
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    H = kernels.biinter_fwd(*dv, dropout_p=p, seed=1234).cpu()
+    H2 = kernels.biinter_fwd(*dv, dropout_p=p, seed=1234).cpu()
+    assert torch.equal(H, H2)
+    keep = (H != 0).float()
+    frac = 1 - keep.mean().item()
+    assert abs(frac - p) < 0.01, frac
+    leaves = [t.clone().requires_grad_(True) for t in (X, S, W1, b1, W2, b2)]
+    x, s, w1, bb1, w2, bb2 = leaves
+    h = (torch.nn.functional.leaky_relu(torch.nn.functional.linear(x + s, w1, bb1), 0.01)
+         + torch.nn.functional.leaky_relu(torch.nn.functional.linear(x * s, w2, bb2), 0.01))
+    h = h * keep / (1 - p)
+    ref = h / h.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    np.testing.assert_allclose(H.numpy(), ref.detach().numpy(), rtol=RTOL, atol=ATOL)
+    dH = torch.randn(n, dout)
+    ref.backward(dH)
+    dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], dropout_p=p, seed=1234)
+    np.testing.assert_allclose(dXd.cpu().numpy(), x.grad.numpy(), rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(dW1.cpu().numpy(), w1.grad.numpy(), rtol=1e-3, atol=1e-4)
+
+
+def test_adam_parity(pkg):
+    _, kernels = _mods(pkg)
+    torch.manual_seed(0)
+    p = torch.randn(10007)
+    opt = K.AdamOracle(lr=1e-3)
+    P = {"p": p.clone()}
+    pd, m, v = p.to(DEV), torch.zeros(10007, device=DEV), torch.zeros(10007, device=DEV)
+    import math
+    for t in range(1, 4):
+        g = torch.randn(10007)
+        opt.step(P, {"p": g})
+        kernels.adam(pd, g.to(DEV), m, v, 1e-3 / (1 - 0.9 ** t), 0.9, 0.999, math.sqrt(1 - 0.999 ** t), 1e-8)
+    np.testing.assert_allclose(pd.cpu().numpy(), P["p"].numpy(), rtol=1e-6, atol=1e-7)
+
+
+def _model_from_golden(pkg, g):
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    n = U + E
+    layers = g["layers"].tolist()
+    A = torch.sparse_coo_tensor(torch.from_numpy(g["A_idx"]), torch.from_numpy(g["A_val"]), (n, n))
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(g["adjacency_relations"]),
+                              cf_embedding_dim=int(g["dim"]), kg_embedding_dim=int(g["dim"]), attentive_matrix=A,
+                              layer_size=layers, message_dropout=[0.1] * len(layers)))
+    sd = m.state_dict()
+    for k in sd:
+        if not sd[k].is_sparse:
+            sd[k] = torch.from_numpy(g["init/" + k])
+    m.load_state_dict(sd)
+    m.to(DEV)
+    m.eval()
+    return m
+
+
+@pytest.mark.parametrize("case", KGAT_CASES)
+def test_propagation_vs_reference(pkg, case):
+    g = golden("kgat_" + case)
+    m = _model_from_golden(pkg, g)
+    all_emb = m._build_cf_embeddings().cpu().numpy()
+    np.testing.assert_allclose(all_emb, g["all_emb"], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("case", KGAT_CASES)
+def test_cf_train_steps_vs_reference(pkg, case):
+    """Loss, every gradient and the params after each Adam step match the reference run."""
+    g = golden("kgat_" + case)
+    m = _model_from_golden(pkg, g)
+    m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    named = dict(m.named_parameters())
+    s = 0
+    while f"cf{s}/loss" in g:
+        ids = [torch.from_numpy(g[f"cf{s}/{x}"]).to(DEV) for x in ("users", "pos", "neg")]
+        loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF)
+        loss.backward()
+        np.testing.assert_allclose(loss.item(), g[f"cf{s}/loss"], rtol=1e-5)
+        for k, prm in named.items():
+            ref = g.get(f"cf{s}/grad/{k}")
+            if ref is None:
+                assert prm.grad is None, k
+            else:
+                np.testing.assert_allclose(prm.grad.cpu().numpy(), ref, rtol=RTOL, atol=1e-6, err_msg=k)
+        m.update_cf_weights()
+        s += 1
+    for k, v in g.items():
+        if k.startswith("after_cf/"):
+            np.testing.assert_allclose(named[k[9:]].detach().cpu().numpy(), v, rtol=RTOL, atol=1e-6, err_msg=k)
+
+
+def test_cf_step_dropout_train_mode_runs(pkg):
+    """Train mode (dropout active, as main.py:292 runs it): finite loss, grads, deterministic per seed."""
+    g = golden("kgat_L3_d64")
+    m = _model_from_golden(pkg, g)
+    m.train()
+    m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    ids = [torch.from_numpy(g[f"cf0/{x}"]).to(DEV) for x in ("users", "pos", "neg")]
+    torch.manual_seed(5)
+    loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF)
+    loss.backward()
+    assert torch.isfinite(loss).item()
+    assert torch.isfinite(m._user_entity_embedding.weight.grad).all().item()
+    m.update_cf_weights()

@@ -1,0 +1,132 @@
+"""CPU-only checks of the product host code and the C-ABI library boundary.
+
+No GPU compute is launched here: the library is only loaded and its host-side
+helper (kgat_csr_plan) called.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import kgat_cpu as K
+from tests.conftest import ROOT, golden, load_pkg
+
+pkg = load_pkg()
+graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+_lib = __import__(pkg.__name__ + "._lib", fromlist=["_lib"])
+
+
+def test_header_symbols_are_bound_and_exported():
+    header = (ROOT / "include" / "kgat_hip.h").read_text()
+    declared = set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]*?\b(kgat_\w+)\s*\(", header, re.M))
+    bound = set(_lib.exported_symbols())
+    assert declared == bound, (declared ^ bound)
+    lib = _lib.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.kgat_version() >= 1
+    assert b"invalid" in lib.kgat_strerror(1001)
+
+
+@pytest.mark.parametrize("case", ["L1_d64", "L2_d64", "L3_d128"])
+def test_layout_matches_reference_preprocess(case):
+    g = golden("kgat_" + case)
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    lay = graph.build_layout(U, E, g["interactions"], g["triplets"])
+    assert lay.rel_order == g["adjacency_relations"].tolist()
+    np.testing.assert_array_equal(lay.heads, g["kg_heads"])
+    np.testing.assert_array_equal(lay.rels, g["kg_rels"])
+    np.testing.assert_array_equal(lay.tails, g["kg_tails"])
+    np.testing.assert_allclose(lay.edge_vals, g["kg_vals"], rtol=1e-6)
+    rows, cols, vals = lay.coo()
+    np.testing.assert_array_equal(np.vstack([rows, cols]), g["A_idx"])
+    np.testing.assert_allclose(vals, g["A_val"], rtol=1e-6)
+    # CSR slot of every edge points at its (head, tail) entry
+    assert np.all(rows[lay.slot] == lay.heads) and np.all(cols[lay.slot] == lay.tails)
+
+
+def test_degree_weights_match_oracle():
+    g = golden("kgat_L2_d64")
+    n = int(g["user_num"]) + int(g["entity_num"])
+    h, r, t = g["kg_heads"], g["kg_rels"], g["kg_tails"]
+    w = graph.degree_weights(h, t, r, n)
+    for rel in np.unique(r):
+        sel = r == rel
+        hh, tt = torch.from_numpy(h[sel]), torch.from_numpy(t[sel])
+        dh = torch.bincount(hh, minlength=n)
+        dt = torch.bincount(tt, minlength=n)
+        ref = 1.0 / (torch.log1p(dh[hh]) + torch.log1p(dt[tt]))
+        np.testing.assert_allclose(w[sel], ref.numpy(), rtol=1e-6)
+
+
+def test_long_row_plan_matches_c_helper():
+    rng = np.random.default_rng(0)
+    deg = rng.integers(0, 40, 5000)
+    deg[rng.integers(0, 5000, 30)] = rng.integers(300, 5000, 30)
+    rowptr = np.zeros(deg.size + 1, np.int64)
+    np.cumsum(deg, out=rowptr[1:])
+    lr, off, sr, sb = graph.long_row_plan(rowptr, 256, 512)
+    lib = _lib.lib()
+    nl, ns = ctypes.c_int32(), ctypes.c_int32()
+    rp = np.ascontiguousarray(rowptr)
+    assert lib.kgat_csr_plan(rp.ctypes.data, deg.size, 256, 512, ctypes.byref(nl), ctypes.byref(ns),
+                             None, None, None, None) == 0
+    assert (nl.value, ns.value) == (lr.size, sr.size)
+    a, b = np.zeros(nl.value, np.int32), np.zeros(nl.value + 1, np.int32)
+    c, d = np.zeros(ns.value, np.int32), np.zeros(ns.value, np.int64)
+    assert lib.kgat_csr_plan(rp.ctypes.data, deg.size, 256, 512, ctypes.byref(nl), ctypes.byref(ns),
+                             a.ctypes.data, b.ctypes.data, c.ctypes.data, d.ctypes.data) == 0
+    for x, y in ((a, lr), (b, off), (c, sr), (d, sb)):
+        np.testing.assert_array_equal(x, y)
+    # segments tile every long row exactly
+    for i, r in enumerate(lr):
+        begs = sb[off[i]:off[i + 1]]
+        assert begs[0] == rowptr[r] and np.all(np.diff(begs) == 512) and begs[-1] < rowptr[r + 1]
+
+
+def test_synthetic_ckg_shape():
+    U, E, inter, trip = graph.synthetic_ckg(20000, 200000, seed=1)
+    assert U == 2000 and E == 18000
+    assert inter.shape[1] == 2 and trip.shape[1] == 3
+    assert inter[:, 0].max() < U and inter[:, 1].max() < int(E * 0.1)
+    assert len(np.unique(inter[:, 0] * E + inter[:, 1])) == len(inter)
+    assert set(np.unique(trip[:, 1]).tolist()) <= {0, 1, 2, 3}
+    lay = graph.build_layout(U, E, inter, trip)
+    assert lay.nnz == 2 * (len(inter) + len(trip))  # every relation has its inverse, no collisions
+
+
+def test_model_init_matches_reference_rng():
+    """Same creation order => the same initial weights as the reference under one seed."""
+    g = golden("kgat_L3_d64")
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    torch.manual_seed(2024)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(g["adjacency_relations"]),
+                              layer_size=[64, 32, 16]))
+    sd = m.state_dict()
+    for k, v in sd.items():
+        if v.is_sparse:
+            continue
+        np.testing.assert_array_equal(v.numpy(), g["init/" + k], err_msg=k)
+    assert set(k for k in sd if not sd[k].is_sparse) == {k[5:] for k in g if k.startswith("init/")}
+
+
+def test_model_refuses_cpu():
+    g = golden("kgat_L1_d64")
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=10, layer_size=[64]))
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, dtype=torch.long), torch.zeros(2, dtype=torch.long), torch.zeros(2, dtype=torch.long),
+          mode=pkg.KGATMode.TRAIN_CF)
+
+
+def test_oracle_layout_agrees_with_product_layout():
+    g = golden("kgat_L3_d128")
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    lay = graph.build_layout(U, E, g["interactions"], g["triplets"])
+    blocks, rel_ids = K.adjacency_blocks(U, [0, 1, 2, 3], g["interactions"], g["triplets"])
+    A = K.initial_attentive(U + E, K.normalized_blocks(U + E, blocks))
+    np.testing.assert_allclose(lay.coo()[2], A.values().numpy(), rtol=1e-6)
