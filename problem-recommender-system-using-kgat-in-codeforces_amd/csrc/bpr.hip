@@ -81,31 +81,36 @@ __global__ __launch_bounds__(256) void bpr_bwd_kernel(kgat_tables T, int t, cons
   const float* tab = T.ptr[t];
   const int64_t ld = T.ld[t];
   const int w = T.width[t];
-  for (int j = lane; j < w; j += 64) {
-    float g = 0.f;
-    for (int s0 = k; s0 < slots; s0 += 64) {
-      unsigned long long mask = __ballot(s0 + lane < slots && id_of(s0 + lane) == id);
-      // iterate matching slots in increasing order (wave-uniform loop)
-      while (mask) {
-        const int bit = __ffsll(static_cast<long long>(mask)) - 1;
-        mask &= mask - 1;
-        const int s = s0 + bit;
-        const int b = s % batch;
-        const float c = coef[b];
-        const float xu = tab[users[b] * ld + j];
-        float v;
-        if (s < batch) {
-          const float xp = tab[pos[b] * ld + j], xn = tab[neg[b] * ld + j];
-          v = c * (xp - xn) + reg * xu;
-        } else if (s < 2 * batch) {
-          v = c * xu + reg * tab[pos[b] * ld + j];
-        } else {
-          v = -c * xu + reg * tab[neg[b] * ld + j];
+  constexpr int kCols = 4;  // widths up to 256 columns: lane owns columns lane + 64*c
+  float g[kCols] = {0.f, 0.f, 0.f, 0.f};
+  for (int s0 = k; s0 < slots; s0 += 64) {
+    // ballot with every lane active, before any column-dependent branch
+    unsigned long long mask = __ballot(s0 + lane < slots && id_of(s0 + lane) == id);
+    while (mask) {  // matching slots in increasing order (wave-uniform)
+      const int bit = __ffsll(static_cast<long long>(mask)) - 1;
+      mask &= mask - 1;
+      const int s = s0 + bit;
+      const int b = s % batch;
+      const float c = coef[b];
+      const int64_t iu = users[b] * ld, ip = pos[b] * ld, in = neg[b] * ld;
+#pragma unroll
+      for (int cc = 0; cc < kCols; ++cc) {
+        const int j = lane + 64 * cc;
+        if (j < w) {
+          const float xu = tab[iu + j];
+          float v;
+          if (s < batch) v = c * (tab[ip + j] - tab[in + j]) + reg * xu;
+          else if (s < 2 * batch) v = c * xu + reg * tab[ip + j];
+          else v = -c * xu + reg * tab[in + j];
+          g[cc] = fmaf(v, scale, g[cc]);
         }
-        g = fmaf(v, scale, g);
       }
     }
-    dst[id * lddst + j] += g;
+  }
+#pragma unroll
+  for (int cc = 0; cc < kCols; ++cc) {
+    const int j = lane + 64 * cc;
+    if (j < w) dst[id * lddst + j] += g[cc];
   }
 }
 
@@ -133,7 +138,7 @@ extern "C" int kgat_bpr_bwd_f32(const kgat_tables* T, int32_t table, const int64
                                 const float* grad_out, float* dst, int64_t lddst, void* stream) {
   if (int e = check_tables(T)) return e;
   if (table < 0 || table >= T->count || !users || !pos || !neg || !coef || !grad_out || !dst || batch <= 0 ||
-      lddst < T->width[table])
+      lddst < T->width[table] || T->width[table] > 256)
     return KGAT_ERR_INVALID;
   const int blocks = (3 * batch + 3) / 4;
   hipLaunchKernelGGL(kgat::bpr_bwd_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *T,
