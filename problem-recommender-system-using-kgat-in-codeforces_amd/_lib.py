@@ -48,12 +48,16 @@ _SIGNATURES = {
     "kgat_biinter_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                             c_i32, c_i32, c_f32, c_u64, c_vp]),
     "kgat_biinter_bwd_workspace": (c_i64, [c_i64, c_i32, c_i32]),
+    "kgat_spmm_csr_masked_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                                c_i32, c_vp, c_i64, c_vp]),
     "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32,
-                                            c_u64, c_vp, c_i64, c_vp]),
+                                            c_u64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "kgat_bpr_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),
     "kgat_bpr_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_i32, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp,
-                                        c_vp, c_i64, c_vp]),
+                                        c_vp, c_i64, c_vp, c_vp]),
+    "kgat_frontier_build": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "kgat_frontier_reset": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp]),
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),

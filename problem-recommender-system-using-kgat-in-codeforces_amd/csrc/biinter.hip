@@ -26,12 +26,13 @@ struct BiShape {
   static constexpr int OLD = DOUT + 4;   // padded LDS row of a dA/dB tile
 };
 
-// Load this lane's A-operand slice of a 16-row sub-tile (zeros past n).
+// Load this lane's A-operand slice of a 16-row sub-tile (zeros past n, or
+// for a negative source row).
 template <int K>
 __device__ __forceinline__ void load_rows(const float* __restrict__ P, int64_t ld, int64_t row, int64_t n, int q,
                                           float (&out)[K / 4]) {
   constexpr int KQ = K / 4;
-  if (row < n) {
+  if (row >= 0 && row < n) {
     const float4* p = reinterpret_cast<const float4*>(P + row * ld + q * KQ);
 #pragma unroll
     for (int t = 0; t < KQ / 4; ++t) {
@@ -180,7 +181,8 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
     const float* __restrict__ dH, int64_t lddh, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ dXd, int64_t lddxd,
-    float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p, uint64_t seed) {
+    float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p, uint64_t seed,
+    const int32_t* __restrict__ rows, int64_t n_src) {
   using B = BiShape<DIN, DOUT>;
   using Lds = BwdLds<DIN, DOUT>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -224,9 +226,12 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
   for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
     const int64_t r0 = tile * 64 + wave * 16;
     // ---------------- phase A
+    // compact row i reads source row rows[i] (frontier mode) or i
+    int64_t src = r0 + c < n ? r0 + c : -1;
+    if (rows != nullptr && src >= 0) src = rows[src];
     float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ];
-    load_rows<DIN>(X, ldx, r0 + c, n, q, xs);
-    load_rows<DIN>(S, lds, r0 + c, n, q, ss);
+    load_rows<DIN>(X, ldx, src, n_src, q, xs);
+    load_rows<DIN>(S, lds, src, n_src, q, ss);
     {
       float* px = tx + (wave * 16 + c) * B::ILD + q * B::KQ;
       float* ps = ts + (wave * 16 + c) * B::ILD + q * B::KQ;
@@ -246,6 +251,13 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
 
     float gd[B::NCB][4], dh[B::NCB][4];
     float sq[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
+    // node id of each C-layout row: the dropout mask is keyed by the node, as in the forward
+    int64_t node[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + q * 4 + i;
+      node[i] = (rows != nullptr && row < n) ? static_cast<int64_t>(rows[row]) : row;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = r0 + q * 4 + i;
@@ -255,7 +267,7 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
         a2[cb][i] += bias2[cb];
         float v = lrelu(a1[cb][i]) + lrelu(a2[cb][i]);
         if (p > 0.f) {
-          const uint64_t idx = static_cast<uint64_t>(row) * DOUT + cb * 16 + c;
+          const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
           v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
         }
         gd[cb][i] = v;
@@ -268,7 +280,6 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
     for (int i = 0; i < 4; ++i) {
       const float nrm = sqrtf(sum16(sq[i]));
       const float dot = sum16(dt[i]);
-      const int64_t row = r0 + q * 4 + i;
       const bool pass = nrm >= kNormEps;
       const float inv = pass ? 1.f / nrm : 1.f / kNormEps;
       const float coef = pass ? dot / (nrm * nrm) : 0.f;
@@ -277,7 +288,7 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
         // d(g/den): dh/den - g (dh.g)/den^3 while the clamp is inactive
         float dg = (dh[cb][i] - gd[cb][i] * coef) * inv;
         if (p > 0.f) {
-          const uint64_t idx = static_cast<uint64_t>(row) * DOUT + cb * 16 + c;
+          const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
           dg = dropout_keep(seed, idx, p) ? dg * scale : 0.f;
         }
         const float da = dg * lrelu_grad(a1[cb][i]);
@@ -377,19 +388,32 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int nslab, int width,
-                                                          float* __restrict__ dW1, float* __restrict__ dW2,
-                                                          float* __restrict__ db1, float* __restrict__ db2,
-                                                          int din, int dout) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= width) return;
+// Sum the per-block slabs: one 1024-thread block per 64 outputs, 16 waves
+// split the slabs (wave w takes slabs w, w+16, ...), then add the 16 wave
+// partials in wave order -- deterministic.
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(const float* __restrict__ slab, int nslab, int width,
+                                                           float* __restrict__ dW1, float* __restrict__ dW2,
+                                                           float* __restrict__ db1, float* __restrict__ db2,
+                                                           int din, int dout) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int b = 0; b < nslab; ++b) s += slab[static_cast<int64_t>(b) * width + i];
-  const int wsz = din * dout;
-  if (i < wsz) dW1[i] = s;
-  else if (i < 2 * wsz) dW2[i - wsz] = s;
-  else if (i < 2 * wsz + dout) db1[i - 2 * wsz] = s;
-  else db2[i - 2 * wsz - dout] = s;
+  if (i < width) {
+#pragma unroll 8
+    for (int b = wave; b < nslab; b += 16) s += slab[static_cast<int64_t>(b) * width + i];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && i < width) {
+    float t = red[0][lane];
+    for (int w = 1; w < 16; ++w) t += red[w][lane];
+    const int wsz = din * dout;
+    if (i < wsz) dW1[i] = t;
+    else if (i < 2 * wsz) dW2[i - wsz] = t;
+    else if (i < 2 * wsz + dout) db1[i - 2 * wsz] = t;
+    else db2[i - 2 * wsz - dout] = t;
+  }
 }
 
 template <int DIN, int DOUT>
@@ -416,9 +440,11 @@ template <int DIN, int DOUT>
 static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH, int64_t lddh,
                       const float* W1, const float* b1, const float* W2, const float* b2, float* dXd, int64_t lddxd,
                       float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, float p,
-                      uint64_t seed, float* ws, int64_t ws_floats, hipStream_t st) {
+                      uint64_t seed, const int32_t* rows, int64_t src_rows, float* ws, int64_t ws_floats,
+                      hipStream_t st) {
   const int grid = bwd_grid<DIN, DOUT>(n);
   const int width = 2 * DOUT * DIN + 2 * DOUT;
+  const int64_t n_src = rows ? src_rows : n;
   if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
   const size_t lds_bytes = BwdLds<DIN, DOUT>::kTotal * sizeof(float);
   static bool attr_set = false;
@@ -429,9 +455,9 @@ static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
     attr_set = true;
   }
   hipLaunchKernelGGL((biinter_bwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds, dH,
-                     lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, ws, n, p, seed);
+                     lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, ws, n, p, seed, rows, n_src);
   KGAT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 255) / 256), dim3(256), 0, st, ws, grid, width, dW1, dW2,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, grid, width, dW1, dW2,
                      db1, db2, DIN, DOUT);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
@@ -498,8 +524,8 @@ extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S,
                                     int64_t lddh, const float* W1, const float* b1, const float* W2, const float* b2,
                                     float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
                                     float* dW2, float* db2, int64_t n_rows, int32_t d_in, int32_t d_out,
-                                    float dropout_p, uint64_t seed, float* workspace, int64_t workspace_floats,
-                                    void* stream) {
+                                    float dropout_p, uint64_t seed, const int32_t* rows, int64_t src_rows,
+                                    float* workspace, int64_t workspace_floats, void* stream) {
   if (!X || !S || !dH || !W1 || !b1 || !W2 || !b2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n_rows < 0)
     return KGAT_ERR_INVALID;
   if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
@@ -509,7 +535,7 @@ extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_BWD_CALL(a, b)                                                                                   \
   kgat::launch_bwd<a, b>(X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, \
-                         n_rows, dropout_p, seed, workspace, workspace_floats, st)
+                         n_rows, dropout_p, seed, rows, src_rows, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_BWD_CALL)
 #undef KGAT_BWD_CALL
 }

@@ -14,43 +14,107 @@ __device__ __forceinline__ float row_val(const kgat_tables& T, int t, int64_t id
   return T.ptr[t][id * T.ld[t] + j];
 }
 
-// One block: waves stride over samples; per-sample terms are reduced in a
-// fixed order, so the scalar loss is deterministic.
+// One wave per sample: the per-sample loss term goes to term[b] and
+// coef[b] = sigmoid(pos_b - neg_b) - 1 is kept for the backward; a second
+// single-block kernel sums term[] in index order (deterministic).
 __global__ __launch_bounds__(256) void bpr_fwd_kernel(kgat_tables T, const int64_t* __restrict__ users,
                                                       const int64_t* __restrict__ pos,
                                                       const int64_t* __restrict__ neg, int batch, float reg,
-                                                      float* __restrict__ loss, float* __restrict__ coef) {
-  __shared__ float part[4];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float acc = 0.f;
-  for (int b = wave; b < batch; b += 4) {
-    const int64_t u = users[b], p = pos[b], n = neg[b];
-    float sp = 0.f, sn = 0.f, qu = 0.f, qp = 0.f, qn = 0.f;
-    for (int t = 0; t < T.count; ++t) {
-      for (int j = lane; j < T.width[t]; j += 64) {
-        const float xu = row_val(T, t, u, j), xp = row_val(T, t, p, j), xn = row_val(T, t, n, j);
-        sp = fmaf(xu, xp, sp);
-        sn = fmaf(xu, xn, sn);
-        qu = fmaf(xu, xu, qu);
-        qp = fmaf(xp, xp, qp);
-        qn = fmaf(xn, xn, qn);
-      }
+                                                      float* __restrict__ coef, float* __restrict__ term) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= batch) return;
+  const int64_t u = users[b], p = pos[b], n = neg[b];
+  float sp = 0.f, sn = 0.f, qu = 0.f, qp = 0.f, qn = 0.f;
+  for (int t = 0; t < T.count; ++t) {
+    for (int j = lane; j < T.width[t]; j += 64) {
+      const float xu = row_val(T, t, u, j), xp = row_val(T, t, p, j), xn = row_val(T, t, n, j);
+      sp = fmaf(xu, xp, sp);
+      sn = fmaf(xu, xn, sn);
+      qu = fmaf(xu, xu, qu);
+      qp = fmaf(xp, xp, qp);
+      qn = fmaf(xn, xn, qn);
     }
-    sp = wave_sum(sp);
-    sn = wave_sum(sn);
-    qu = wave_sum(qu);
-    qp = wave_sum(qp);
-    qn = wave_sum(qn);
-    const float x = sp - sn;
-    // -logsigmoid(x) = softplus(-x), computed stably
-    const float nls = fmaxf(-x, 0.f) + log1pf(expf(-fabsf(x)));
-    const float sig = 1.f / (1.f + expf(-x));
-    if (lane == 0) coef[b] = sig - 1.f;
-    acc += nls + reg * 0.5f * (qu + qp + qn);
   }
-  if (lane == 0) part[wave] = acc;
+  sp = wave_sum(sp);
+  sn = wave_sum(sn);
+  qu = wave_sum(qu);
+  qp = wave_sum(qp);
+  qn = wave_sum(qn);
+  const float x = sp - sn;
+  // -logsigmoid(x) = softplus(-x), computed stably
+  const float nls = fmaxf(-x, 0.f) + log1pf(expf(-fabsf(x)));
+  if (lane == 0) {
+    coef[b] = 1.f / (1.f + expf(-x)) - 1.f;
+    term[b] = nls + reg * 0.5f * (qu + qp + qn);
+  }
+}
+
+__global__ __launch_bounds__(256) void bpr_sum_kernel(const float* __restrict__ term, int batch,
+                                                      float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < batch; b += 256) s += term[b];
+  red[threadIdx.x] = s;
   __syncthreads();
-  if (threadIdx.x == 0) *loss = (part[0] + part[1] + part[2] + part[3]) / static_cast<float>(batch);
+  for (int o = 128; o > 0; o >>= 1) {
+    if (static_cast<int>(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0] / static_cast<float>(batch);
+}
+
+// Unique ids of the batch [users | pos | neg] in first-occurrence order:
+// rows[0..count) = ids, node_map[id] = its position, rows[count..3B) = -1.
+// node_map must hold -1 for every node on entry (kgat_frontier_reset restores it).
+__global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __restrict__ users,
+                                                              const int64_t* __restrict__ pos,
+                                                              const int64_t* __restrict__ neg, int batch,
+                                                              int32_t* __restrict__ node_map,
+                                                              int32_t* __restrict__ rows,
+                                                              int32_t* __restrict__ count) {
+  constexpr int kMax = 4096;
+  __shared__ int64_t ids[kMax];
+  __shared__ int32_t scan[kMax];
+  const int slots = 3 * batch;
+  for (int k = threadIdx.x; k < slots; k += 1024)
+    ids[k] = k < batch ? users[k] : (k < 2 * batch ? pos[k - batch] : neg[k - 2 * batch]);
+  __syncthreads();
+  for (int k = threadIdx.x; k < slots; k += 1024) {
+    const int64_t id = ids[k];
+    int first = 1;
+    for (int j = 0; j < k; ++j)
+      if (ids[j] == id) { first = 0; break; }
+    scan[k] = first;
+  }
+  __syncthreads();
+  // inclusive scan (Hillis-Steele over the slot array, chunked by 1024)
+  for (int o = 1; o < slots; o <<= 1) {
+    int32_t v[kMax / 1024];
+    int c = 0;
+    for (int k = threadIdx.x; k < slots; k += 1024, ++c) v[c] = k >= o ? scan[k - o] : 0;
+    __syncthreads();
+    c = 0;
+    for (int k = threadIdx.x; k < slots; k += 1024, ++c) scan[k] += v[c];
+    __syncthreads();
+  }
+  const int total = slots > 0 ? scan[slots - 1] : 0;
+  for (int k = threadIdx.x; k < slots; k += 1024) {
+    const int is_first = k == 0 ? 1 : scan[k] - scan[k - 1];
+    if (is_first) {
+      const int p = scan[k] - 1;
+      rows[p] = static_cast<int32_t>(ids[k]);
+      node_map[ids[k]] = p;
+    }
+    if (k >= total) rows[k] = -1;
+  }
+  if (threadIdx.x == 0) *count = total;
+}
+
+__global__ __launch_bounds__(256) void frontier_reset_kernel(const int32_t* __restrict__ rows, int n,
+                                                             int32_t* __restrict__ node_map) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n && rows[i] >= 0) node_map[rows[i]] = -1;
 }
 
 // Gradient rows of table t scattered into dst.  One wave per slot k of the
@@ -62,7 +126,7 @@ __global__ __launch_bounds__(256) void bpr_bwd_kernel(kgat_tables T, int t, cons
                                                       const int64_t* __restrict__ neg, int batch, float reg,
                                                       const float* __restrict__ coef,
                                                       const float* __restrict__ grad_out, float* __restrict__ dst,
-                                                      int64_t lddst) {
+                                                      int64_t lddst, const int32_t* __restrict__ row_map) {
   const int slots = 3 * batch;
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -107,10 +171,11 @@ __global__ __launch_bounds__(256) void bpr_bwd_kernel(kgat_tables T, int t, cons
       }
     }
   }
+  const int64_t drow = row_map ? static_cast<int64_t>(row_map[id]) : id;
 #pragma unroll
   for (int cc = 0; cc < kCols; ++cc) {
     const int j = lane + 64 * cc;
-    if (j < w) dst[id * lddst + j] += g[cc];
+    if (j < w) dst[drow * lddst + j] += g[cc];
   }
 }
 
@@ -127,22 +192,45 @@ extern "C" int kgat_bpr_fwd_f32(const kgat_tables* T, const int64_t* users, cons
                                 int32_t batch, float reg, float* loss, float* coef, void* stream) {
   if (int e = check_tables(T)) return e;
   if (!users || !pos || !neg || !loss || !coef || batch <= 0) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::bpr_fwd_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *T, users,
-                     pos, neg, batch, reg, loss, coef);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(kgat::bpr_fwd_kernel, dim3((batch + 3) / 4), dim3(256), 0, st, *T, users, pos, neg, batch, reg,
+                     coef, coef + batch);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kgat::bpr_sum_kernel, dim3(1), dim3(256), 0, st, coef + batch, batch, loss);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
 
 extern "C" int kgat_bpr_bwd_f32(const kgat_tables* T, int32_t table, const int64_t* users, const int64_t* pos,
                                 const int64_t* neg, int32_t batch, float reg, const float* coef,
-                                const float* grad_out, float* dst, int64_t lddst, void* stream) {
+                                const float* grad_out, float* dst, int64_t lddst, const int32_t* row_map,
+                                void* stream) {
   if (int e = check_tables(T)) return e;
   if (table < 0 || table >= T->count || !users || !pos || !neg || !coef || !grad_out || !dst || batch <= 0 ||
       lddst < T->width[table] || T->width[table] > 256)
     return KGAT_ERR_INVALID;
   const int blocks = (3 * batch + 3) / 4;
   hipLaunchKernelGGL(kgat::bpr_bwd_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), *T,
-                     table, users, pos, neg, batch, reg, coef, grad_out, dst, lddst);
+                     table, users, pos, neg, batch, reg, coef, grad_out, dst, lddst, row_map);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_frontier_build(const int64_t* users, const int64_t* pos, const int64_t* neg, int32_t batch,
+                                   int32_t* node_map, int32_t* rows, int32_t* count, void* stream) {
+  if (!users || !pos || !neg || !node_map || !rows || !count || batch <= 0 || 3 * batch > 4096)
+    return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::frontier_build_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), users,
+                     pos, neg, batch, node_map, rows, count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_frontier_reset(const int32_t* rows, int32_t n, int32_t* node_map, void* stream) {
+  if (!rows || !node_map || n < 0) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::frontier_reset_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), rows, n, node_map);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -16,11 +16,30 @@
 //  * rows with degree > long_threshold (power-law hubs: popular problems)
 //    would serialise one group for thousands of edges, so they are cut into
 //    seg_len-edge segments handled by whole waves (blocks scheduled first),
-//    written as partial sums and reduced in segment order by a fix-up pass.
-//    Every output is therefore produced in a fixed order: deterministic.
+//    written as partial sums and reduced by a fix-up pass (one block per long
+//    row).  Every output is produced in a fixed order: deterministic.
+//
+// Masked mode (the frontier backward of the last layer): the source rows are
+// a compact buffer Xc indexed through src_map[node] (-1 = row is zero), so
+// only edges into the frontier gather anything; the output is initialised
+// from a compact Yc through the same map.  Skipped edges contribute exactly
+// 0, so the result equals the dense product with zero rows.
 #include "common.hpp"
 
 namespace kgat {
+
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2 };
+
+struct SpmmIo {
+  const float* X;         // source rows (dense) or compact source rows (masked)
+  int64_t ldx;
+  float* Y;
+  int64_t ldy;
+  float* part;            // [n_seg][D] long-row segment partials
+  const int32_t* src_map; // masked: node -> compact row or -1
+  const float* Yc;        // masked: compact init rows (nullable)
+  int64_t ldyc;
+};
 
 template <int D>
 struct SpmmShape {
@@ -38,12 +57,21 @@ __device__ __forceinline__ void fma4(float v, const float4& x, float4& acc) {
   acc.w = fmaf(v, x.w, acc.w);
 }
 
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+
 // Accumulate edges [beg, end) of one row into acc.  All lanes of the group
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
-template <int D>
-__device__ __forceinline__ void gather_edges(const kgat_csr& A, const float4* __restrict__ X4, int64_t ldx4,
-                                             int64_t beg, int64_t end, int base, int gl, float4& acc) {
+template <int D, bool MASKED>
+__device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
+                                             int gl, float4& acc) {
   constexpr int L = SpmmShape<D>::kLanes;
+  const float4* X4 = reinterpret_cast<const float4*>(io.X);
+  const int64_t ldx4 = io.ldx / 4;
   for (int64_t cb = beg; cb < end; cb += L) {
     const int n = static_cast<int>(end - cb < L ? end - cb : L);
     int mc = 0;
@@ -51,6 +79,16 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const float4* __
     if (gl < n) {
       mc = A.col[cb + gl];
       mv = A.val[cb + gl];
+      if (MASKED) mc = io.src_map[mc];
+    }
+    if (MASKED) {
+      // only frontier sources gather; the rest add an exact 0
+      for (int j = 0; j < n; ++j) {
+        const int c = __shfl(mc, base + j);
+        const float v = __shfl(mv, base + j);
+        if (c >= 0) fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
+      }
+      continue;
     }
     int j = 0;
     for (; j + 4 <= n; j += 4) {
@@ -75,17 +113,33 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const float4* __
   }
 }
 
-template <int D, bool ACC>
-__global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, const float* __restrict__ X, int64_t ldx,
-                                                        float* __restrict__ Y, int64_t ldy,
-                                                        float* __restrict__ part, int seg_blocks) {
+// Final write of one output row segment (lane gl) in the three modes.
+template <int MODE>
+__device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int gl, float4 acc) {
+  float4* y = reinterpret_cast<float4*>(io.Y + row * io.ldy) + gl;
+  if (MODE == kAccumulate) {
+    const float4 o = *y;
+    acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+  } else if (MODE == kMasked) {
+    if (io.Yc != nullptr) {
+      const int m = io.src_map[row];
+      if (m >= 0) {
+        const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
+        acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+      }
+    }
+  }
+  *y = acc;
+}
+
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
+  constexpr bool MASKED = MODE == kMasked;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
-  const float4* X4 = reinterpret_cast<const float4*>(X);
-  const int64_t ldx4 = ldx / 4;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     // ---- long-row segment: the whole wave, groups take interleaved sub-chunks
@@ -99,7 +153,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, const float*
     // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
     for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
       const int64_t ce = cb + L < end ? cb + L : end;
-      gather_edges<D>(A, X4, ldx4, cb, ce, base, gl, acc);
+      gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc);
     }
 #pragma unroll
     for (int o = L; o < kWave; o <<= 1) {
@@ -108,7 +162,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, const float*
       acc.z += __shfl_xor(acc.z, o);
       acc.w += __shfl_xor(acc.w, o);
     }
-    if (g == 0) reinterpret_cast<float4*>(part)[static_cast<int64_t>(s) * L + gl] = acc;
+    if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
     return;
   }
 
@@ -121,92 +175,93 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, const float*
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    gather_edges<D>(A, X4, ldx4, beg, end, base, gl, acc);
-    float4* y = reinterpret_cast<float4*>(Y + r * ldy) + gl;
-    if (ACC) {
-      const float4 o = *y;
-      acc.x += o.x;
-      acc.y += o.y;
-      acc.z += o.z;
-      acc.w += o.w;
-    }
-    *y = acc;
+    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc);
+    store_row<MODE>(io, r, gl, acc);
   }
 }
 
-// Sum the segment partials of each long row in segment order.
-template <int D, bool ACC>
-__global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, const float* __restrict__ part,
-                                                         float* __restrict__ Y, int64_t ldy) {
+// Sum the segment partials of each long row.  One 256-thread block per long
+// row: G = 256/(D/4) groups stride over the row's segments, then the group
+// partials are added in group order through LDS -- a fixed order, so the
+// result is deterministic, and a 196-segment hub row takes 13 steps, not 196.
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) {
   constexpr int L = D / 4;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (wave >= A.n_long || lane >= L) return;
-  const int row = A.long_rows[wave];
-  const float4* P = reinterpret_cast<const float4*>(part);
+  constexpr int G = 256 / L;
+  __shared__ float4 red[G][L];
+  const int lr = blockIdx.x;
+  const int g = threadIdx.x / L, gl = threadIdx.x % L;
+  const int row = A.long_rows[lr];
+  const float4* P = reinterpret_cast<const float4*>(io.part);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = A.long_seg_off[wave]; s < A.long_seg_off[wave + 1]; ++s) {
-    const float4 p = P[static_cast<int64_t>(s) * L + lane];
-    acc.x += p.x;
-    acc.y += p.y;
-    acc.z += p.z;
-    acc.w += p.w;
+  const int s_end = A.long_seg_off[lr + 1];
+  for (int s = A.long_seg_off[lr] + g; s < s_end; s += G) add4(acc, P[static_cast<int64_t>(s) * L + gl]);
+  red[g][gl] = acc;
+  __syncthreads();
+  if (threadIdx.x < L) {
+    float4 t = red[0][gl];
+    for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
+    store_row<MODE>(io, row, gl, t);
   }
-  float4* y = reinterpret_cast<float4*>(Y + static_cast<int64_t>(row) * ldy) + lane;
-  if (ACC) {
-    const float4 o = *y;
-    acc.x = o.x + acc.x;
-    acc.y = o.y + acc.y;
-    acc.z = o.z + acc.z;
-    acc.w = o.w + acc.w;
-  }
-  *y = acc;
 }
 
-template <int D>
-static int launch_spmm(const kgat_csr& A, const float* X, int64_t ldx, float* Y, int64_t ldy, bool acc,
-                       float* ws, hipStream_t st) {
+template <int D, int MODE>
+static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
   const int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  if (acc)
-    hipLaunchKernelGGL((spmm_main_kernel<D, true>), dim3(grid), dim3(256), 0, st, A, X, ldx, Y, ldy, ws,
-                       seg_blocks);
-  else
-    hipLaunchKernelGGL((spmm_main_kernel<D, false>), dim3(grid), dim3(256), 0, st, A, X, ldx, Y, ldy, ws,
-                       seg_blocks);
+  hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
   KGAT_LAUNCH_CHECK();
   if (A.n_long > 0) {
-    const int fb = (A.n_long + 3) / 4;
-    if (acc)
-      hipLaunchKernelGGL((spmm_fixup_kernel<D, true>), dim3(fb), dim3(256), 0, st, A, ws, Y, ldy);
-    else
-      hipLaunchKernelGGL((spmm_fixup_kernel<D, false>), dim3(fb), dim3(256), 0, st, A, ws, Y, ldy);
+    hipLaunchKernelGGL((spmm_fixup_kernel<D, MODE>), dim3(A.n_long), dim3(256), 0, st, A, io);
     KGAT_LAUNCH_CHECK();
   }
   return KGAT_OK;
 }
+
+template <int MODE>
+static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) {
+  switch (d) {
+    case 16: return launch_mode<16, MODE>(A, io, st);
+    case 32: return launch_mode<32, MODE>(A, io, st);
+    case 64: return launch_mode<64, MODE>(A, io, st);
+    case 128: return launch_mode<128, MODE>(A, io, st);
+    case 256: return launch_mode<256, MODE>(A, io, st);
+    default: return KGAT_ERR_UNSUPPORTED_DIM;
+  }
+}
+
+static bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
 
 }  // namespace kgat
 
 extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx, float* Y, int64_t ldy,
                                  int32_t d, int32_t accumulate, float* workspace, int64_t workspace_floats,
                                  void* stream) {
+  using namespace kgat;
   if (!A || !X || !Y || A->n_rows < 0 || ldx < d || ldy < d || (ldx & 3) || (ldy & 3)) return KGAT_ERR_INVALID;
-  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(Y) & 15)) return KGAT_ERR_INVALID;
+  if (misaligned(X) || misaligned(Y)) return KGAT_ERR_INVALID;
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const bool acc = accumulate != 0;
-  switch (d) {
-    case 16: return kgat::launch_spmm<16>(*A, X, ldx, Y, ldy, acc, workspace, st);
-    case 32: return kgat::launch_spmm<32>(*A, X, ldx, Y, ldy, acc, workspace, st);
-    case 64: return kgat::launch_spmm<64>(*A, X, ldx, Y, ldy, acc, workspace, st);
-    case 128: return kgat::launch_spmm<128>(*A, X, ldx, Y, ldy, acc, workspace, st);
-    case 256: return kgat::launch_spmm<256>(*A, X, ldx, Y, ldy, acc, workspace, st);
-    default: return KGAT_ERR_UNSUPPORTED_DIM;
-  }
+  return accumulate ? dispatch<kAccumulate>(*A, io, d, st) : dispatch<kOverwrite>(*A, io, d, st);
+}
+
+extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
+                                        const float* Yc_init, int64_t ldyc, float* Y, int64_t ldy, int32_t d,
+                                        float* workspace, int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !Y || A->n_rows < 0 || ldxc < d || ldy < d || (ldxc & 3) || (ldy & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(Y) || (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc};
+  return dispatch<kMasked>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }

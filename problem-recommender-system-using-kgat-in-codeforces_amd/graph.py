@@ -204,6 +204,8 @@ class DeviceGraph:
         self.edge_weight = torch.from_numpy(
             degree_weights(layout.heads, layout.tails, layout.rels, self.n_nodes)).to(device)
         self.rel_order = list(layout.rel_order)
+        # node -> frontier position map for the last layer's sparse backward; -1 between steps
+        self.node_map = torch.from_numpy(np.full(self.n_nodes, -1, np.int32)).to(device)
         self.refresh_transpose()
 
     @property

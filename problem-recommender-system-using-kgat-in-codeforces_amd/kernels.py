@@ -67,6 +67,43 @@ def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, t
     return out
 
 
+def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None = None,
+                transpose: bool = False) -> torch.Tensor:
+    """Dense Y = A . X where X is zero outside a frontier: X[node] = Xc[src_map[node]] (src_map -1 => 0),
+    plus Yc_init[src_map[r]] on frontier rows.  Returns a new dense [N, d] tensor."""
+    _req(src_map, "src_map", dtype=torch.int32, dim=1)
+    _req(Xc, "Xc", dim=2)
+    if src_map.numel() != graph.n_nodes:
+        raise ValueError("src_map must cover every node")
+    d = Xc.shape[1]
+    if Yc_init is not None:
+        _req(Yc_init, "Yc_init", dim=2)
+        if Yc_init.shape[1] != d:
+            raise ValueError("Yc_init width mismatch")
+    out = torch.empty(graph.n_nodes, d, dtype=torch.float32, device=Xc.device)
+    csr = graph.AT if transpose else graph.A
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    _lib.call("kgat_spmm_csr_masked_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
+              out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    return out
+
+
+def frontier_build(users, pos, neg, node_map: torch.Tensor):
+    """(rows int32 [3B] -- distinct batch ids in first-occurrence order, -1 padded -- , count int32 [1])."""
+    B = users.numel()
+    rows = torch.empty(3 * B, dtype=torch.int32, device=users.device)
+    count = torch.empty(1, dtype=torch.int32, device=users.device)
+    _lib.call("kgat_frontier_build", users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, node_map.data_ptr(),
+              rows.data_ptr(), count.data_ptr(), stream_ptr(users.device))
+    return rows, count
+
+
+def frontier_reset(rows: torch.Tensor, node_map: torch.Tensor) -> None:
+    _lib.call("kgat_frontier_reset", rows.data_ptr(), rows.numel(), node_map.data_ptr(), stream_ptr(rows.device))
+
+
 def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out=None) -> torch.Tensor:
     for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2")):
         _req(t, nm, dim=2)
@@ -86,11 +123,17 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
     return out
 
 
-def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None):
-    """Returns (dXd, dS, dW1, db1, dW2, db2)."""
-    n, din = X.shape
+def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,
+                rows: torch.Tensor | None = None):
+    """Returns (dXd, dS, dW1, db1, dW2, db2).  With ``rows`` (int32 [n]), dH/dXd/dS are compact:
+    row i belongs to node rows[i] of X and S (-1 = padding)."""
+    src_rows, din = X.shape
     dout = W1.shape[0]
     _req(dH, "dH", dim=2)
+    n = src_rows
+    if rows is not None:
+        _req(rows, "rows", dtype=torch.int32, dim=1)
+        n = rows.numel()
     if dH.shape != (n, dout):
         raise ValueError("dH shape mismatch")
     dev = X.device
@@ -107,8 +150,8 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     _lib.call("kgat_biinter_bwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), dH.data_ptr(), _ld(dH),
               W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(),
               _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
-              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), ws.data_ptr(), ws.numel(),
-              stream_ptr(dev))
+              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              rows.data_ptr() if rows is not None else None, src_rows, ws.data_ptr(), ws.numel(), stream_ptr(dev))
     return dXd, dS, dW1, db1, dW2, db2
 
 
@@ -134,21 +177,24 @@ def bpr_fwd(tables: list[torch.Tensor], users, pos, neg, reg: float):
         raise ValueError("batch size mismatch")
     dev = users.device
     loss = torch.empty(1, dtype=torch.float32, device=dev)
-    coef = torch.empty(B, dtype=torch.float32, device=dev)
+    coef = torch.empty(2 * B, dtype=torch.float32, device=dev)  # [coef | per-sample terms]
     T = make_tables(tables)
     _lib.call("kgat_bpr_fwd_f32", ctypes.byref(T), users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg),
               loss.data_ptr(), coef.data_ptr(), stream_ptr(dev))
     return loss, coef
 
 
-def bpr_bwd(tables: list[torch.Tensor], t: int, users, pos, neg, reg: float, coef, grad_out, dst) -> None:
-    """dst[id] += dL/d tables[t][id] for every gathered id (deterministic)."""
+def bpr_bwd(tables: list[torch.Tensor], t: int, users, pos, neg, reg: float, coef, grad_out, dst,
+            row_map: torch.Tensor | None = None) -> None:
+    """dst[id] += dL/d tables[t][id] for every gathered id (deterministic); with row_map, dst[row_map[id]]."""
     _req(dst, "dst", dim=2)
     _req(grad_out, "grad_out")
+    if row_map is not None:
+        _req(row_map, "row_map", dtype=torch.int32, dim=1)
     T = make_tables(tables)
     _lib.call("kgat_bpr_bwd_f32", ctypes.byref(T), t, users.data_ptr(), pos.data_ptr(), neg.data_ptr(),
               users.numel(), float(reg), coef.data_ptr(), grad_out.data_ptr(), dst.data_ptr(), _ld(dst),
-              stream_ptr(dst.device))
+              row_map.data_ptr() if row_map is not None else None, stream_ptr(dst.device))
 
 
 def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float) -> None:

@@ -88,7 +88,12 @@ class _CFLoss(torch.autograd.Function):
         S_l = A . X_l                       (kgat_spmm_csr_f32)
         X_{l+1} = biinter(X_l, S_l)        (kgat_biinter_fwd_f32)
       loss = BPR over the gathered rows of [X_0 | ... | X_L] (kgat_bpr_fwd_f32)
-    backward: dX_L = scatter(dBPR); for l = L-1..0
+    backward: the last layer's upstream gradient is nonzero only on the
+    distinct batch rows F (<= 3B, model.py:189-191 gathers nothing else), so
+      dH_L[F] = scatter(dBPR) (compact), (dXd, dS, dW) = biinter_bwd on F rows,
+      dX_{L-1} = dXd + A^T . dS  with the A^T gather restricted to F
+    (kgat_spmm_csr_masked_f32; equal to the dense product).  Then for
+    l = L-2..0 densely:
         (dXd, dS_l, dW) = biinter_bwd(...)   (kgat_biinter_bwd_f32)
         dX_l = dXd + A^T . dS_l              (spmm on the transposed CSR, accumulate)
         dX_l += scatter(dBPR_l)              (kgat_bpr_bwd_f32)
@@ -119,10 +124,20 @@ class _CFLoss(torch.autograd.Function):
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
         L = len(drops)
-        dX = kernels.zeros(tables[L].shape, tables[L].device)
-        kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dX)
         wgrads: list[torch.Tensor | None] = [None] * (4 * L)
-        for l in range(L - 1, -1, -1):
+        # ---- last layer on the batch frontier
+        rows, _count = kernels.frontier_build(users, pos, neg, graph.node_map)
+        dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)
+        kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dHc, row_map=graph.node_map)
+        l = L - 1
+        dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
+                                                            drops[l], seeds[l], rows=rows)
+        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True)
+        kernels.frontier_reset(rows, graph.node_map)
+        kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
+        wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
+        # ---- remaining layers densely
+        for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],
                                                               seeds[l])

@@ -290,3 +290,75 @@ def test_cf_step_synthetic_hubs_vs_oracle(pkg, layers, batch):
             assert P[k].grad is None if k in P else True, k
             continue
         np.testing.assert_allclose(prm.grad.cpu().numpy(), P[k].grad.numpy(), rtol=RTOL, atol=1e-6, err_msg=k)
+
+
+def test_frontier_build_and_reset(pkg):
+    _, kernels = _mods(pkg)
+    rng = np.random.default_rng(5)
+    n, B = 500, 256
+    u, p, q = (torch.from_numpy(rng.integers(0, 60, B)) for _ in range(3))
+    node_map = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    rows, count = kernels.frontier_build(u.to(DEV), p.to(DEV), q.to(DEV), node_map)
+    ids = torch.cat([u, p, q]).numpy()
+    _, first = np.unique(ids, return_index=True)
+    want = ids[np.sort(first)]
+    got = rows.cpu().numpy()
+    assert int(count.item()) == want.size
+    np.testing.assert_array_equal(got[:want.size], want)
+    assert np.all(got[want.size:] == -1)
+    nm = node_map.cpu().numpy()
+    np.testing.assert_array_equal(nm[want], np.arange(want.size))
+    kernels.frontier_reset(rows, node_map)
+    assert int((node_map != -1).sum().item()) == 0
+
+
+@pytest.mark.parametrize("d", [32, 64])
+def test_spmm_masked_matches_dense(pkg, d):
+    graph_mod, kernels = _mods(pkg)
+    rng = np.random.default_rng(d)
+    n = 4000
+    h = np.concatenate([rng.integers(0, n, 30000), np.repeat(rng.integers(0, n, 4), 1500)])
+    t = rng.integers(0, n, h.size)
+    rowptr, col, val = graph_mod.csr_from_coo(n, np.concatenate([h, t]), np.concatenate([t, h]),
+                                              rng.random(2 * h.size).astype(np.float32))
+    lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
+                                tails=np.zeros(0, np.int64), edge_vals=np.zeros(0, np.float32), rowptr=rowptr,
+                                col=col, val=val, slot=np.zeros(0, np.int64))
+    g = graph_mod.DeviceGraph(lay, DEV)
+    F = rng.choice(n, 300, replace=False)
+    Xc, Yc = torch.randn(310, d), torch.randn(310, d)
+    node_map = np.full(n, -1, np.int32)
+    node_map[F] = np.arange(300)
+    X = torch.zeros(n, d)
+    X[F] = Xc[:300]
+    Y0 = torch.zeros(n, d)
+    Y0[F] = Yc[:300]
+    for tr in (False, True):
+        out = kernels.spmm_masked(g, torch.from_numpy(node_map).to(DEV), Xc.to(DEV), Yc.to(DEV), transpose=tr)
+        ref = kernels.spmm(g, X.to(DEV), transpose=tr).cpu() + Y0
+        np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_biinter_bwd_rows_matches_dense(pkg):
+    _, kernels = _mods(pkg)
+    torch.manual_seed(9)
+    n, din, dout = 2000, 64, 32
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    W1, W2 = torch.randn(dout, din) * 0.2, torch.randn(dout, din) * 0.2
+    b1, b2 = torch.randn(dout) * 0.1, torch.randn(dout) * 0.1
+    F = torch.from_numpy(np.random.default_rng(1).choice(n, 150, replace=False))
+    rows = torch.cat([F, torch.full((42,), -1)]).int()
+    dHc = torch.zeros(192, dout)
+    dHc[:150] = torch.randn(150, dout)
+    dH = torch.zeros(n, dout)
+    dH[F] = dHc[:150]
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    for p in (0.0, 0.1):
+        dense = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], dropout_p=p, seed=77)
+        comp = kernels.biinter_bwd(dv[0], dv[1], dHc.to(DEV), *dv[2:], dropout_p=p, seed=77, rows=rows.to(DEV))
+        np.testing.assert_allclose(comp[0][:150].cpu().numpy(), dense[0][F.to(DEV)].cpu().numpy(), rtol=1e-5,
+                                   atol=1e-7)
+        np.testing.assert_allclose(comp[1][:150].cpu().numpy(), dense[1][F.to(DEV)].cpu().numpy(), rtol=1e-5,
+                                   atol=1e-7)
+        for a, b in zip(comp[2:], dense[2:]):
+            np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-6)
