@@ -58,6 +58,16 @@ _SIGNATURES = {
                                         c_vp, c_i64, c_vp, c_vp]),
     "kgat_frontier_build": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "kgat_frontier_reset": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp]),
+    "kgat_transr_work_floats": (c_i64, [c_i32, c_i32, c_i32]),
+    "kgat_transr_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32,
+                                           c_vp, c_vp, c_vp]),
+    "kgat_transr_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
+                                           c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_edge_logits_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
+    "kgat_slot_sum_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_row_softmax_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_score_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_i32, c_vp, c_i32, c_vp, c_i64, c_vp]),
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),

@@ -11,6 +11,8 @@
 // reads and the k-order of the MFMA chain is (q*K/4 + step) -- any order of a
 // sum is a valid fp32 schedule.  W is staged once per block in LDS with a
 // 4-float pad per row.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -48,33 +50,30 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ P, int64_t l
   }
 }
 
-// acc1[cb] = U . W1^T, acc2[cb] = M . W2^T for every 16-wide column block.
-// w1/w2 rows are wld floats apart (LDS copy in the forward, global in the backward).
-template <int DIN, int DOUT>
-__device__ __forceinline__ void bi_products(const float (&u)[DIN / 4], const float (&m)[DIN / 4],
-                                            const float* w1s, const float* w2s, int wld, int q, int c,
-                                            floatx4 (&acc1)[DOUT / 16], floatx4 (&acc2)[DOUT / 16]) {
-  using B = BiShape<DIN, DOUT>;
+// a1 = U . W1^T, a2 = M . W2^T for ONE 16-wide output column block cb (the
+// epilogue of each block runs before the next block's MFMAs, so only one
+// block's accumulators are live).  w rows are wld floats apart (LDS copy in the
+// forward, LDS or global in the backward).
+template <int DIN>
+__device__ __forceinline__ void bi_block(const float (&u)[DIN / 4], const float (&m)[DIN / 4], const float* w1s,
+                                         const float* w2s, int wld, int q, int c, int cb, floatx4& a1, floatx4& a2) {
+  constexpr int KQ = DIN / 4;
+  a1 = floatx4{0.f, 0.f, 0.f, 0.f};
+  a2 = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* r1 = w1s + (cb * 16 + c) * wld + q * KQ;
+  const float* r2 = w2s + (cb * 16 + c) * wld + q * KQ;
 #pragma unroll
-  for (int cb = 0; cb < B::NCB; ++cb) {
-    floatx4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
-    const float* r1 = w1s + (cb * 16 + c) * wld + q * B::KQ;
-    const float* r2 = w2s + (cb * 16 + c) * wld + q * B::KQ;
-#pragma unroll
-    for (int t = 0; t < B::KQ; t += 4) {
-      const float4 x1 = *reinterpret_cast<const float4*>(r1 + t);
-      const float4 x2 = *reinterpret_cast<const float4*>(r2 + t);
-      a1 = mfma16x4(u[t], x1.x, a1);
-      a2 = mfma16x4(m[t], x2.x, a2);
-      a1 = mfma16x4(u[t + 1], x1.y, a1);
-      a2 = mfma16x4(m[t + 1], x2.y, a2);
-      a1 = mfma16x4(u[t + 2], x1.z, a1);
-      a2 = mfma16x4(m[t + 2], x2.z, a2);
-      a1 = mfma16x4(u[t + 3], x1.w, a1);
-      a2 = mfma16x4(m[t + 3], x2.w, a2);
-    }
-    acc1[cb] = a1;
-    acc2[cb] = a2;
+  for (int t = 0; t < KQ; t += 4) {
+    const float4 x1 = *reinterpret_cast<const float4*>(r1 + t);
+    const float4 x2 = *reinterpret_cast<const float4*>(r2 + t);
+    a1 = mfma16x4(u[t], x1.x, a1);
+    a2 = mfma16x4(m[t], x2.x, a2);
+    a1 = mfma16x4(u[t + 1], x1.y, a1);
+    a2 = mfma16x4(m[t + 1], x2.y, a2);
+    a1 = mfma16x4(u[t + 2], x1.z, a1);
+    a2 = mfma16x4(m[t + 2], x2.z, a2);
+    a1 = mfma16x4(u[t + 3], x1.w, a1);
+    a2 = mfma16x4(m[t + 3], x2.w, a2);
   }
 }
 
@@ -90,7 +89,7 @@ __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const floa
 }
 
 template <int DIN, int DOUT>
-__global__ __launch_bounds__(256) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
+__global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
@@ -112,27 +111,34 @@ __global__ __launch_bounds__(256) void biinter_fwd_kernel(const float* __restric
   }
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const int64_t nsub = (n + 15) / 16;
-  for (int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); st < nsub;
-       st += static_cast<int64_t>(gridDim.x) * 4) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+  int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  // next sub-tile's rows are loaded while the current one computes
+  float nx[B::KQ], ns[B::KQ];
+  load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
+  load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+  for (; st < nsub; st += stride) {
     const int64_t r0 = st * 16;
-    float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ];
-    load_rows<DIN>(X, ldx, r0 + c, n, q, xs);
-    load_rows<DIN>(S, lds, r0 + c, n, q, ss);
+    float u[B::KQ], m[B::KQ];
 #pragma unroll
     for (int t = 0; t < B::KQ; ++t) {
-      u[t] = xs[t] + ss[t];
-      m[t] = xs[t] * ss[t];
+      u[t] = nx[t] + ns[t];
+      m[t] = nx[t] * ns[t];
     }
-    floatx4 acc1[B::NCB], acc2[B::NCB];
-    bi_products<DIN, DOUT>(u, m, w1s, w2s, B::WLD, q, c, acc1, acc2);
-
+    if (st + stride < nsub) {
+      load_rows<DIN>(X, ldx, (st + stride) * 16 + c, n, q, nx);
+      load_rows<DIN>(S, lds, (st + stride) * 16 + c, n, q, ns);
+    }
     float g[B::NCB][4];
     float sq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int cb = 0; cb < B::NCB; ++cb) {
+      floatx4 acc1, acc2;
+      __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
+      bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = lrelu(acc1[cb][i] + bias1[cb]) + lrelu(acc2[cb][i] + bias2[cb]);
+        float v = lrelu(acc1[i] + bias1[cb]) + lrelu(acc2[i] + bias2[cb]);
         if (p > 0.f) {
           const uint64_t idx = static_cast<uint64_t>(r0 + q * 4 + i) * DOUT + cb * 16 + c;
           v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
@@ -164,27 +170,53 @@ __global__ __launch_bounds__(256) void biinter_fwd_kernel(const float* __restric
 // sums the slabs in block order (deterministic).
 // W1/W2 are read through L1/L2 in the backward (16-64 KB, every wave re-reads
 // them), so the LDS holds only the 64-row X/S/dA/dB tiles.
-template <int DIN, int DOUT>
+template <int DIN, int DOUT, bool WLDS>
 struct BwdLds {
   using B = BiShape<DIN, DOUT>;
   static constexpr int kX = 64 * B::ILD;
   static constexpr int kO = 64 * B::OLD;
   static constexpr int kTiles = 2 * kX + 2 * kO;  // floats
   static constexpr int kW = 2 * DOUT * B::WLD;
-  // stage W in LDS too when everything fits the 160 KiB of one CU
-  static constexpr bool kWInLds = (kTiles + kW) * 4 <= 160 * 1024;
+  // stage W in LDS too (when asked and everything fits the 160 KiB of one CU)
+  static constexpr bool kWInLds = WLDS && (kTiles + kW) * 4 <= 160 * 1024;
   static constexpr int kTotal = kTiles + (kWInLds ? kW : 0);
 };
 
+// One wave's 16-row slice of a tile, loaded one tile ahead (software pipelining:
+// the next tile's HBM reads are in flight while the current tile computes).
 template <int DIN, int DOUT>
-__global__ __launch_bounds__(256) void biinter_bwd_kernel(
+struct BwdRegs {
+  float xs[DIN / 4], ss[DIN / 4];
+  float dh[DOUT / 16][4];
+};
+
+template <int DIN, int DOUT>
+__device__ __forceinline__ void load_bwd_tile(BwdRegs<DIN, DOUT>& R, int64_t r0, int64_t n,
+                                              const int32_t* __restrict__ rows, int64_t n_src,
+                                              const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
+                                              int64_t lds, const float* __restrict__ dH, int64_t lddh, int q,
+                                              int c) {
+  int64_t src = r0 + c < n ? r0 + c : -1;
+  if (rows != nullptr && src >= 0) src = rows[src];
+  load_rows<DIN>(X, ldx, src, n_src, q, R.xs);
+  load_rows<DIN>(S, lds, src, n_src, q, R.ss);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = r0 + q * 4 + i;
+#pragma unroll
+    for (int cb = 0; cb < DOUT / 16; ++cb) R.dh[cb][i] = row < n ? dH[row * lddh + cb * 16 + c] : 0.f;
+  }
+}
+
+template <int DIN, int DOUT, bool WLDS>
+__global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
     const float* __restrict__ dH, int64_t lddh, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ dXd, int64_t lddxd,
     float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p, uint64_t seed,
     const int32_t* __restrict__ rows, int64_t n_src) {
   using B = BiShape<DIN, DOUT>;
-  using Lds = BwdLds<DIN, DOUT>;
+  using Lds = BwdLds<DIN, DOUT, WLDS>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tx = smem;             // [64][ILD] X tile
   float* ts = tx + Lds::kX;     // [64][ILD] S tile
@@ -223,15 +255,27 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
   float dbias = 0.f, dbias2 = 0.f;  // column sums owned by waves 0 (dA) / 1 (dB)
 
   const int64_t ntile = (n + 63) / 64;
+  BwdRegs<DIN, DOUT> nxt;
+  if (static_cast<int64_t>(blockIdx.x) < ntile)
+    load_bwd_tile<DIN, DOUT>(nxt, static_cast<int64_t>(blockIdx.x) * 64 + wave * 16, n, rows, n_src, X, ldx, S, lds,
+                             dH, lddh, q, c);
   for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
     const int64_t r0 = tile * 64 + wave * 16;
     // ---------------- phase A
     // compact row i reads source row rows[i] (frontier mode) or i
-    int64_t src = r0 + c < n ? r0 + c : -1;
-    if (rows != nullptr && src >= 0) src = rows[src];
-    float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ];
-    load_rows<DIN>(X, ldx, src, n_src, q, xs);
-    load_rows<DIN>(S, lds, src, n_src, q, ss);
+    float xs[B::KQ], ss[B::KQ], u[B::KQ], m[B::KQ], dh[B::NCB][4];
+#pragma unroll
+    for (int t = 0; t < B::KQ; ++t) {
+      xs[t] = nxt.xs[t];
+      ss[t] = nxt.ss[t];
+    }
+#pragma unroll
+    for (int cb = 0; cb < B::NCB; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dh[cb][i] = nxt.dh[cb][i];
+    if (tile + gridDim.x < ntile)
+      load_bwd_tile<DIN, DOUT>(nxt, (tile + gridDim.x) * 64 + wave * 16, n, rows, n_src, X, ldx, S, lds, dH, lddh,
+                               q, c);
     {
       float* px = tx + (wave * 16 + c) * B::ILD + q * B::KQ;
       float* ps = ts + (wave * 16 + c) * B::ILD + q * B::KQ;
@@ -246,10 +290,8 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
       u[t] = xs[t] + ss[t];
       m[t] = xs[t] * ss[t];
     }
-    floatx4 a1[B::NCB], a2[B::NCB];
-    bi_products<DIN, DOUT>(u, m, w1p, w2p, wld, q, c, a1, a2);
-
-    float gd[B::NCB][4], dh[B::NCB][4];
+    float gd[B::NCB][4];
+    uint64_t pos_a = 0, pos_b = 0;  // bit (cb*4+i): pre-activation > 0 (LeakyReLU slope select)
     float sq[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
     // node id of each C-layout row: the dropout mask is keyed by the node, as in the forward
     int64_t node[4];
@@ -259,19 +301,21 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
       node[i] = (rows != nullptr && row < n) ? static_cast<int64_t>(rows[row]) : row;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + q * 4 + i;
+    for (int cb = 0; cb < B::NCB; ++cb) {
+      floatx4 a1, a2;
+      __builtin_amdgcn_sched_barrier(0);
+      bi_block<DIN>(u, m, w1p, w2p, wld, q, c, cb, a1, a2);
 #pragma unroll
-      for (int cb = 0; cb < B::NCB; ++cb) {
-        a1[cb][i] += bias1[cb];
-        a2[cb][i] += bias2[cb];
-        float v = lrelu(a1[cb][i]) + lrelu(a2[cb][i]);
+      for (int i = 0; i < 4; ++i) {
+        const float pa = a1[i] + bias1[cb], pb = a2[i] + bias2[cb];
+        pos_a |= static_cast<uint64_t>(pa > 0.f) << (cb * 4 + i);
+        pos_b |= static_cast<uint64_t>(pb > 0.f) << (cb * 4 + i);
+        float v = lrelu(pa) + lrelu(pb);
         if (p > 0.f) {
           const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
           v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
         }
         gd[cb][i] = v;
-        dh[cb][i] = row < n ? dH[row * lddh + cb * 16 + c] : 0.f;
         sq[i] = fmaf(v, v, sq[i]);
         dt[i] = fmaf(v, dh[cb][i], dt[i]);
       }
@@ -291,8 +335,8 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
           const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
           dg = dropout_keep(seed, idx, p) ? dg * scale : 0.f;
         }
-        const float da = dg * lrelu_grad(a1[cb][i]);
-        const float db = dg * lrelu_grad(a2[cb][i]);
+        const float da = dg * (((pos_a >> (cb * 4 + i)) & 1) ? 1.f : kLeakySlope);
+        const float db = dg * (((pos_b >> (cb * 4 + i)) & 1) ? 1.f : kLeakySlope);
         tda[(wave * 16 + q * 4 + i) * B::OLD + cb * 16 + c] = da;
         tdb[(wave * 16 + q * 4 + i) * B::OLD + cb * 16 + c] = db;
       }
@@ -313,6 +357,7 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
       }
 #pragma unroll 1
       for (int ib = 0; ib < B::NIB; ++ib) {
+        __builtin_amdgcn_sched_barrier(0);
         floatx4 du = {0.f, 0.f, 0.f, 0.f}, dm = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < B::KO; ++t) {
@@ -338,6 +383,7 @@ __global__ __launch_bounds__(256) void biinter_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < kMine; ++k) {
       const int id = wave + 4 * k;
+      __builtin_amdgcn_sched_barrier(0);
       if (id < kBlocks) {
         const int mat = id / (B::NCB * B::NIB);
         const int rem = id % (B::NCB * B::NIB);
@@ -416,13 +462,43 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(const float* __restri
   }
 }
 
+// KGAT_BWD_W_LDS=1 stages W1/W2 in LDS in the backward (fewer blocks per CU);
+// default reads them through L1/L2 so two 4-wave blocks fit per CU.
+static bool bwd_w_in_lds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KGAT_BWD_W_LDS");
+    v = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 template <int DIN, int DOUT>
 static int bwd_grid(int64_t n) {
-  const int lds = BwdLds<DIN, DOUT>::kTotal * 4;
+  const int lds = (bwd_w_in_lds() ? BwdLds<DIN, DOUT, true>::kTotal : BwdLds<DIN, DOUT, false>::kTotal) * 4;
   int per_cu = (160 * 1024) / lds;
   if (per_cu < 1) per_cu = 1;
   if (per_cu > 4) per_cu = 4;
   return blocks_for(n, 64, kCUs * per_cu);
+}
+
+template <int DIN, int DOUT, bool WLDS>
+static int launch_bwd_kernel(int grid, const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH,
+                             int64_t lddh, const float* W1, const float* b1, const float* W2, const float* b2,
+                             float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* ws, int64_t n, float p,
+                             uint64_t seed, const int32_t* rows, int64_t n_src, hipStream_t st) {
+  const size_t lds_bytes = BwdLds<DIN, DOUT, WLDS>::kTotal * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&biinter_bwd_kernel<DIN, DOUT, WLDS>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
+    if (e != hipSuccess) return static_cast<int>(e);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((biinter_bwd_kernel<DIN, DOUT, WLDS>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds, dH,
+                     lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, ws, n, p, seed, rows, n_src);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 template <int DIN, int DOUT>
@@ -446,17 +522,15 @@ static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
   const int width = 2 * DOUT * DIN + 2 * DOUT;
   const int64_t n_src = rows ? src_rows : n;
   if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
-  const size_t lds_bytes = BwdLds<DIN, DOUT>::kTotal * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&biinter_bwd_kernel<DIN, DOUT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
-    if (e != hipSuccess) return static_cast<int>(e);
-    attr_set = true;
+  if (bwd_w_in_lds()) {
+    if (int e = launch_bwd_kernel<DIN, DOUT, true>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
+                                                   ldds, ws, n, p, seed, rows, n_src, st))
+      return e;
+  } else {
+    if (int e = launch_bwd_kernel<DIN, DOUT, false>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
+                                                    ldds, ws, n, p, seed, rows, n_src, st))
+      return e;
   }
-  hipLaunchKernelGGL((biinter_bwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds, dH,
-                     lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, ws, n, p, seed, rows, n_src);
-  KGAT_LAUNCH_CHECK();
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, grid, width, dW1, dW2,
                      db1, db2, DIN, DOUT);
   KGAT_LAUNCH_CHECK();

@@ -66,7 +66,10 @@ __global__ __launch_bounds__(256) void bpr_sum_kernel(const float* __restrict__ 
 
 // Unique ids of the batch [users | pos | neg] in first-occurrence order:
 // rows[0..count) = ids, node_map[id] = its position, rows[count..3B) = -1.
-// node_map must hold -1 for every node on entry (kgat_frontier_reset restores it).
+// node_map must hold -1 for every node on entry (kgat_frontier_reset restores
+// it).  O(slots): an atomicMin of (slot - slots - 1) < -1 into node_map[id]
+// elects the first slot of every id, a block scan numbers the winners in slot
+// order, and the winners overwrite node_map[id] with their position.
 __global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __restrict__ users,
                                                               const int64_t* __restrict__ pos,
                                                               const int64_t* __restrict__ neg, int batch,
@@ -74,41 +77,56 @@ __global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __r
                                                               int32_t* __restrict__ rows,
                                                               int32_t* __restrict__ count) {
   constexpr int kMax = 4096;
-  __shared__ int64_t ids[kMax];
-  __shared__ int32_t scan[kMax];
+  constexpr int kPer = kMax / 1024;
+  __shared__ int32_t wsum[16];
   const int slots = 3 * batch;
-  for (int k = threadIdx.x; k < slots; k += 1024)
-    ids[k] = k < batch ? users[k] : (k < 2 * batch ? pos[k - batch] : neg[k - 2 * batch]);
-  __syncthreads();
-  for (int k = threadIdx.x; k < slots; k += 1024) {
-    const int64_t id = ids[k];
-    int first = 1;
-    for (int j = 0; j < k; ++j)
-      if (ids[j] == id) { first = 0; break; }
-    scan[k] = first;
+  const int tid = threadIdx.x;
+  // thread tid owns the contiguous slots [tid*kPer, tid*kPer + kPer)
+  int64_t ids[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = tid * kPer + j;
+    ids[j] = k < slots ? (k < batch ? users[k] : (k < 2 * batch ? pos[k - batch] : neg[k - 2 * batch])) : -1;
+    if (k < slots) atomicMin(&node_map[ids[j]], k - slots - 1);
   }
   __syncthreads();
-  // inclusive scan (Hillis-Steele over the slot array, chunked by 1024)
-  for (int o = 1; o < slots; o <<= 1) {
-    int32_t v[kMax / 1024];
-    int c = 0;
-    for (int k = threadIdx.x; k < slots; k += 1024, ++c) v[c] = k >= o ? scan[k - o] : 0;
-    __syncthreads();
-    c = 0;
-    for (int k = threadIdx.x; k < slots; k += 1024, ++c) scan[k] += v[c];
-    __syncthreads();
+  __threadfence_block();
+  int first[kPer];
+  int local = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = tid * kPer + j;
+    first[j] = 0;
+    if (k < slots) first[j] = __hip_atomic_load(&node_map[ids[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                              k - slots - 1;
+    local += first[j];
   }
-  const int total = slots > 0 ? scan[slots - 1] : 0;
-  for (int k = threadIdx.x; k < slots; k += 1024) {
-    const int is_first = k == 0 ? 1 : scan[k] - scan[k - 1];
-    if (is_first) {
-      const int p = scan[k] - 1;
-      rows[p] = static_cast<int32_t>(ids[k]);
-      node_map[ids[k]] = p;
+  // block exclusive scan of the per-thread counts (slot order = thread order)
+  const int lane = tid & 63, wave = tid >> 6;
+  int incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wave; ++w) base += wsum[w];
+  int total = 0;
+  for (int w = 0; w < 16; ++w) total += wsum[w];
+  int p = base + incl - local;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = tid * kPer + j;
+    if (k < slots && first[j]) {
+      rows[p] = static_cast<int32_t>(ids[j]);
+      node_map[ids[j]] = p;
+      ++p;
     }
-    if (k >= total) rows[k] = -1;
   }
-  if (threadIdx.x == 0) *count = total;
+  for (int k = total + tid; k < slots; k += 1024) rows[k] = -1;
+  if (tid == 0) *count = total;
 }
 
 __global__ __launch_bounds__(256) void frontier_reset_kernel(const int32_t* __restrict__ rows, int n,

@@ -82,11 +82,15 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       if (MASKED) mc = io.src_map[mc];
     }
     if (MASKED) {
-      // only frontier sources gather; the rest add an exact 0
-      for (int j = 0; j < n; ++j) {
+      // only frontier sources gather (usually none in a chunk); skipped edges
+      // add an exact 0, so edge order is preserved among the ones that do
+      uint64_t hit = (__ballot(gl < n && mc >= 0) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
+      while (hit) {
+        const int j = __ffsll(static_cast<long long>(hit)) - 1;
+        hit &= hit - 1;
         const int c = __shfl(mc, base + j);
         const float v = __shfl(mv, base + j);
-        if (c >= 0) fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
+        fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
       }
       continue;
     }

@@ -218,11 +218,91 @@ class DeviceGraph:
             _lib.call("kgat_gather_f32", self.A.val.data_ptr(), self.perm_t.data_ptr(), self.nnz,
                       self.AT.val.data_ptr(), stream_ptr(self.device))
 
+    def refresh_plan(self, heads, rels, tails) -> "RefreshPlan | None":
+        """Edge-scoring plan for UPDATE_ATTENTION's edge list (model.py:318-366).
+
+        Cached across calls with identical edge arrays (compared on device).
+        Returns None when the (head, tail) set is not exactly this CSR's
+        structure -- the caller then rebuilds the graph from the edges.
+        """
+        h = torch.as_tensor(heads).to(self.device).long()
+        r = torch.as_tensor(rels).to(self.device).long()
+        t = torch.as_tensor(tails).to(self.device).long()
+        cached = getattr(self, "_plan", None)
+        if cached is not None and cached.matches(h, r, t):
+            return cached
+        plan = RefreshPlan.build(self, h, r, t)
+        self._plan = plan
+        return plan
+
     def to_sparse_coo(self) -> torch.Tensor:
         """The attentive matrix as the reference's coalesced sparse COO (model.py:83-92)."""
         rows, cols, _ = self.layout.coo()
         idx = torch.from_numpy(np.vstack([rows, cols]))
         return torch.sparse_coo_tensor(idx, self.A.val.detach().cpu(), (self.n_nodes, self.n_nodes)).coalesce()
+
+
+class RefreshPlan:
+    """Device arrays that drive the edge scorer: relation-sorted 16-edge tiles,
+    per-edge tails and static degree weights, and the edge -> CSR slot map."""
+
+    TILE = 16
+
+    def __init__(self):
+        self.key: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None
+
+    def matches(self, h, r, t) -> bool:
+        if self.key is None:
+            return False
+        kh, kr, kt = self.key
+        return (kh.shape == h.shape and torch.equal(kh, h) and torch.equal(kr, r) and torch.equal(kt, t))
+
+    @classmethod
+    def build(cls, g: "DeviceGraph", h_d, r_d, t_d) -> "RefreshPlan | None":
+        n = g.n_nodes
+        h, r, t = h_d.cpu().numpy(), r_d.cpu().numpy(), t_d.cpu().numpy()
+        E = h.size
+        rowptr = g.layout.rowptr
+        nnz = g.nnz
+        csr_keys = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr)) * n + g.layout.col.astype(np.int64)
+        keys = h * n + t
+        slot = np.searchsorted(csr_keys, keys)
+        ok = slot < nnz
+        ok[ok] &= csr_keys[slot[ok]] == keys[ok]
+        if not ok.all():
+            return None
+        covered = np.zeros(nnz, bool)
+        covered[slot] = True
+        if not covered.all():
+            return None
+        p = cls()
+        dev = g.device
+        p.n_edges = E
+        p.tails = torch.from_numpy(t.astype(np.int32)).to(dev)
+        p.weight = torch.from_numpy(degree_weights(h, t, r, n)).to(dev)
+        order = np.lexsort((t, r))  # relation-major, then tail (neighbouring tiles share rows)
+        rs = r[order]
+        starts = np.flatnonzero(np.r_[True, rs[1:] != rs[:-1]]) if E else np.zeros(0, np.int64)
+        ends = np.r_[starts[1:], E]
+        cnt = (ends - starts + cls.TILE - 1) // cls.TILE
+        first_tile = np.zeros(cnt.size + 1, np.int64)
+        np.cumsum(cnt, out=first_tile[1:])
+        local = np.arange(first_tile[-1], dtype=np.int64) - np.repeat(first_tile[:-1], cnt)
+        tile_beg = np.r_[np.repeat(starts, cnt) + cls.TILE * local, E]
+        p.rel_perm = torch.from_numpy(order.astype(np.int32)).to(dev)
+        p.tile_rel = torch.from_numpy(np.repeat(rs[starts], cnt).astype(np.int32)).to(dev)
+        p.tile_beg = torch.from_numpy(tile_beg.astype(np.int32)).to(dev)
+        p.n_tiles = int(first_tile[-1])
+        if E == nnz:  # bijective: scores land directly in slot order
+            p.out_pos = torch.from_numpy(slot.astype(np.int32)).to(dev)
+            p.slot_ptr = p.slot_order = None
+        else:         # duplicate (head, tail) pairs: summed per slot after scoring
+            p.out_pos = None
+            so = np.argsort(slot, kind="stable")
+            p.slot_order = torch.from_numpy(so.astype(np.int32)).to(dev)
+            p.slot_ptr = torch.from_numpy(np.searchsorted(slot[so], np.arange(nnz + 1)).astype(np.int64)).to(dev)
+        p.key = (h_d.clone(), r_d.clone(), t_d.clone())
+        return p
 
 
 def stream_ptr(device: torch.device) -> ctypes.c_void_p:

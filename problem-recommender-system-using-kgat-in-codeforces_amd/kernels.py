@@ -197,6 +197,88 @@ def bpr_bwd(tables: list[torch.Tensor], t: int, users, pos, neg, reg: float, coe
               row_map.data_ptr() if row_map is not None else None, stream_ptr(dst.device))
 
 
+def transr_fwd(emb, rel_emb, trans, heads, rels, pos, neg, reg: float):
+    """(loss [1], work) for the TransR KG loss."""
+    _req(emb, "emb", dim=2)
+    _req(rel_emb, "rel_emb", dim=2)
+    _req(trans, "trans", dim=3)
+    ids = [heads, rels, pos, neg]
+    for t, nm in zip(ids, ("heads", "rels", "pos", "neg")):
+        _req(t, nm, dtype=torch.int64, dim=1)
+    B = heads.numel()
+    d, k = trans.shape[1], trans.shape[2]
+    if emb.shape[1] != d or rel_emb.shape[1] != k or any(t.numel() != B for t in ids) or B == 0:
+        raise ValueError("TransR shape mismatch")
+    if not (trans.is_contiguous() and rel_emb.is_contiguous()):
+        raise ValueError("trans / rel_emb must be contiguous")
+    dev = emb.device
+    loss = torch.empty(1, dtype=torch.float32, device=dev)
+    work = torch.empty(int(_lib.lib().kgat_transr_work_floats(B, d, k)), dtype=torch.float32, device=dev)
+    _lib.call("kgat_transr_fwd_f32", emb.data_ptr(), _ld(emb), rel_emb.data_ptr(), trans.data_ptr(), d, k,
+              heads.data_ptr(), rels.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg), loss.data_ptr(),
+              work.data_ptr(), stream_ptr(dev))
+    return loss, work
+
+
+def transr_bwd(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out):
+    """(d_emb dense [N, d], d_rel [n_rel, k], d_trans [n_rel, d, k])."""
+    dev = emb.device
+    d = emb.shape[1]
+    d_emb = zeros(emb.shape, dev)
+    d_rel = torch.empty(n_rel, k, dtype=torch.float32, device=dev)
+    d_trans = torch.empty(n_rel, d, k, dtype=torch.float32, device=dev)
+    _lib.call("kgat_transr_bwd_f32", emb.data_ptr(), _ld(emb), d, k, heads.data_ptr(), rels.data_ptr(),
+              pos.data_ptr(), neg.data_ptr(), heads.numel(), n_rel, work.data_ptr(), grad_out.data_ptr(),
+              d_emb.data_ptr(), _ld(d_emb), d_rel.data_ptr(), d_trans.data_ptr(), stream_ptr(dev))
+    return d_emb, d_rel, d_trans
+
+
+def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, dropout_p: float = 0.0,
+                seed: int = 0) -> torch.Tensor:
+    """Per-slot (bijective plans) or per-edge attention logits."""
+    for t, nm in ((emb, "emb"), (Wv, "Wv"), (Wo, "Wo")):
+        _req(t, nm, dim=2)
+    _req(trans, "trans", dim=3)
+    d = emb.shape[1]
+    if trans.shape[1:] != (d, d) or Wv.shape != (d, d) or Wo.shape != (d, d):
+        raise ValueError("edge scorer needs cf_embedding_dim == kg_embedding_dim (multi_head_attention.py:13-15)")
+    for t in (trans, Wv, Wo, bv, bo, ln_w, ln_b):
+        if not t.is_contiguous():
+            raise ValueError("edge scorer weights must be contiguous")
+    n_out = graph.nnz if plan.out_pos is not None else plan.n_edges
+    out = torch.empty(max(n_out, 1), dtype=torch.float32, device=emb.device)
+    _lib.call("kgat_edge_logits_f32", emb.data_ptr(), _ld(emb), emb.shape[0], trans.data_ptr(), d, Wv.data_ptr(),
+              bv.data_ptr(), Wo.data_ptr(), bo.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), plan.tails.data_ptr(),
+              plan.weight.data_ptr(), plan.rel_perm.data_ptr(), plan.tile_rel.data_ptr(), plan.tile_beg.data_ptr(),
+              plan.n_tiles, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(), stream_ptr(emb.device))
+    if plan.out_pos is None:
+        slot_logits = torch.empty(max(graph.nnz, 1), dtype=torch.float32, device=emb.device)
+        _lib.call("kgat_slot_sum_f32", plan.slot_ptr.data_ptr(), plan.slot_order.data_ptr(), graph.nnz,
+                  out.data_ptr(), slot_logits.data_ptr(), stream_ptr(emb.device))
+        out = slot_logits
+    return out[:graph.nnz]
+
+
+def row_softmax(graph: DeviceGraph, slot_logits: torch.Tensor) -> None:
+    """A.val <- softmax over each row's stored entries; then A^T values follow."""
+    _req(slot_logits, "slot_logits", dim=1)
+    _lib.call("kgat_row_softmax_f32", graph.A.rowptr.data_ptr(), graph.n_nodes, slot_logits.data_ptr(),
+              graph.A.val.data_ptr(), stream_ptr(slot_logits.device))
+    graph.refresh_transpose()
+
+
+def scores(tables: list[torch.Tensor], users, items) -> torch.Tensor:
+    """[len(users), len(items)] fp32 dot products over the concatenated tables."""
+    _req(users, "users", dtype=torch.int64, dim=1)
+    _req(items, "items", dtype=torch.int64, dim=1)
+    T = make_tables(tables)
+    out = torch.empty(users.numel(), items.numel(), dtype=torch.float32, device=users.device)
+    _lib.call("kgat_score_f32", ctypes.byref(T), users.data_ptr(), users.numel(), items.data_ptr(), items.numel(),
+              out.data_ptr(), _ld(out) if out.numel() else max(1, items.numel()), stream_ptr(users.device))
+    return out
+
+
 def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float) -> None:
     for t, nm in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
         _req(t, nm)

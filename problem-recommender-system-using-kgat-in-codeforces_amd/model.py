@@ -149,6 +149,27 @@ class _CFLoss(torch.autograd.Function):
         return (None, None, None, None, dX, *wgrads)
 
 
+class _KGLoss(torch.autograd.Function):
+    """TransR KG loss as one autograd node (model.py:204-261): kgat_transr_fwd_f32 /
+    kgat_transr_bwd_f32.  Gradients: dense table (zero except the gathered rows,
+    as nn.Embedding's dense backward), relation embeddings, trans matrices."""
+
+    @staticmethod
+    def forward(ctx, heads, rels, pos, neg, reg, emb, rel_emb, trans):
+        loss, work = kernels.transr_fwd(emb, rel_emb, trans, heads, rels, pos, neg, reg)
+        ctx.save_for_backward(heads, rels, pos, neg, work, emb)
+        ctx.shape = (rel_emb.shape[0], rel_emb.shape[1])
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, gout):
+        heads, rels, pos, neg, work, emb = ctx.saved_tensors
+        n_rel, k = ctx.shape
+        gout = gout.reshape(1).to(torch.float32).contiguous()
+        d_emb, d_rel, d_trans = kernels.transr_bwd(emb, n_rel, k, heads, rels, pos, neg, work, gout)
+        return None, None, None, None, None, d_emb, d_rel, d_trans
+
+
 class KGAT(nn.Module):
     def __init__(self, args: KGATArgs) -> None:
         super().__init__()
@@ -269,13 +290,46 @@ class KGAT(nn.Module):
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
-        raise NotImplementedError("TRAIN_KG lands with the TransR kernel")
+        dev = self._user_entity_embedding.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("KGAT runs on the MI355X HIP path only: move the model to a GPU first")
+        ids = [t.to(dev).long().contiguous() for t in (heads, relations, positive_tails, negative_tails)]
+        return _KGLoss.apply(*ids, float(self._regularization_params[1]), self._user_entity_embedding.weight,
+                             self._relation_embedding.weight, self._trans_matrix)
 
     def _update_attention(self, heads, relations, tails, relation_indices) -> None:
-        raise NotImplementedError("UPDATE_ATTENTION lands with the edge-scoring kernel")
+        """Refresh attentive_matrix in HBM (model.py:318-366): no host round trip."""
+        g = self.graph()
+        plan = g.refresh_plan(heads, relations, tails)
+        if plan is None:  # edge set differs from the current structure: rebuild it from the edges
+            h = torch.as_tensor(heads).cpu().numpy().astype(np.int64)
+            t = torch.as_tensor(tails).cpu().numpy().astype(np.int64)
+            n = self._user_num + self._entity_num
+            rowptr, col, val = csr_from_coo(n, h, t, np.zeros(h.size, np.float32))
+            layout = GraphLayout(n_nodes=n, rel_order=[int(x) for x in torch.as_tensor(relation_indices).tolist()],
+                                 heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64), tails=np.zeros(0, np.int64),
+                                 edge_vals=np.zeros(0, np.float32), rowptr=rowptr, col=col, val=val,
+                                 slot=np.zeros(0, np.int64))
+            g = self.attach_graph(layout)
+            plan = g.refresh_plan(heads, relations, tails)
+        mha = self._multi_head_attention
+        p = mha.dropout if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        with torch.no_grad():
+            logits = kernels.edge_logits(g, plan, self._user_entity_embedding.weight.detach(),
+                                         self._trans_matrix.detach(), mha._value_weight.weight.detach(),
+                                         mha._value_weight.bias.detach(), mha._output.weight.detach(),
+                                         mha._output.bias.detach(), mha._layer_norm.weight.detach(),
+                                         mha._layer_norm.bias.detach(), p, seed)
+            kernels.row_softmax(g, logits)
 
     def _calc_score(self, user_ids, item_ids) -> torch.Tensor:
-        raise NotImplementedError("PREDICT lands with the scoring kernel")
+        """Full propagation, then the fused gather + MFMA score GEMM (model.py:368-391)."""
+        tables = self._propagate()
+        dev = tables[0].device
+        u = torch.as_tensor(user_ids).to(dev).long().contiguous()
+        i = torch.as_tensor(item_ids).to(dev).long().contiguous()
+        return kernels.scores(tables, u, i)
 
     # ------------------------------------------------------------- optimizers
     def build_optimizer(self, cf_lr: float, kg_lr: float) -> None:

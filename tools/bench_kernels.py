@@ -1,0 +1,106 @@
+"""Per-kernel timing at the C2 shapes (A/B tool, not the driver's bench).
+
+    python tools/bench_kernels.py [--nodes 1000000] [--triples 10000000] [--reps 20]
+
+Times each HIP entry point with torch.cuda events over `reps` launches after a
+warm-up, on the synthetic C2 graph, and prints one JSON line per kernel with
+the average launch time and algorithmic GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+PKG = "problem-recommender-system-using-kgat-in-codeforces_amd"
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--triples", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    graph = importlib.import_module(PKG + ".graph")
+    K = importlib.import_module(PKG + ".kernels")
+    dev = torch.device("cuda")
+    U, E, inter, trip = graph.synthetic_ckg(args.nodes, args.triples, seed=2024)
+    lay = graph.build_layout(U, E, inter, trip)
+    g = graph.DeviceGraph(lay, dev)
+    n, nnz = lay.n_nodes, lay.nnz
+    out = []
+
+    def rec(name, us, nbytes=None, **kw):
+        r = {"kernel": name, "us": round(us, 2)}
+        if nbytes:
+            r["GBps"] = round(nbytes / (us * 1e-6) / 1e9, 1)
+        r.update(kw)
+        print(json.dumps(r), flush=True)
+        out.append(r)
+
+    torch.manual_seed(0)
+    for d in (64, 32):
+        if args.only and "spmm" not in args.only:
+            break
+        X = torch.randn(n, d, device=dev)
+        Y = torch.empty(n, d, device=dev)
+        byt = 8 * (n + 1) + nnz * (8 + 4 * d) + 4 * n * d
+        rec(f"spmm_fwd_d{d}", timeit(lambda: K.spmm(g, X, out=Y), args.reps), byt)
+        rec(f"spmm_T_acc_d{d}", timeit(lambda: K.spmm(g, X, out=Y, transpose=True, accumulate=True), args.reps),
+            byt + 4 * n * d)
+    B = 256
+    rng = np.random.default_rng(0)
+    users = torch.from_numpy(rng.integers(0, U, B)).to(dev)
+    pos = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+    neg = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+    rows, _ = K.frontier_build(users, pos, neg, g.node_map)
+    Sc = torch.randn(3 * B, 64, device=dev)
+    rec("spmm_masked_T_d64", timeit(lambda: K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True), args.reps))
+    K.frontier_reset(rows, g.node_map)
+    rec("frontier_build+reset", timeit(lambda: K.frontier_reset(K.frontier_build(users, pos, neg, g.node_map)[0],
+                                                                 g.node_map), args.reps))
+    for din, dout in ((64, 64), (64, 32)):
+        X = torch.randn(n, din, device=dev)
+        S = torch.randn(n, din, device=dev)
+        W1 = torch.randn(dout, din, device=dev) * 0.1
+        W2 = torch.randn(dout, din, device=dev) * 0.1
+        b1 = torch.zeros(dout, device=dev)
+        b2 = torch.zeros(dout, device=dev)
+        dH = torch.randn(n, dout, device=dev)
+        rec(f"biinter_fwd_{din}x{dout}", timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5), args.reps),
+            4 * n * (2 * din + dout))
+        rec(f"biinter_bwd_{din}x{dout}",
+            timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5), args.reps),
+            4 * n * (2 * din + dout + 2 * din), w_lds=os.environ.get("KGAT_BWD_W_LDS", "0"))
+    p = torch.randn(n * 64, device=dev)
+    gg = torch.randn_like(p)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    rec("adam_table", timeit(lambda: K.adam(p, gg, m, v, 1e-3, 0.9, 0.999, 0.03, 1e-8), args.reps), 28 * p.numel())
+    tables = [torch.randn(n, 64, device=dev), torch.randn(n, 64, device=dev), torch.randn(n, 32, device=dev)]
+    rec("bpr_fwd", timeit(lambda: K.bpr_fwd(tables, users, pos, neg, 1e-5), args.reps))
+
+
+if __name__ == "__main__":
+    main()
