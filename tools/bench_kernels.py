@@ -92,7 +92,7 @@ def main():
             4 * n * (2 * din + dout))
         rec(f"biinter_bwd_{din}x{dout}",
             timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5), args.reps),
-            4 * n * (2 * din + dout + 2 * din), w_lds=os.environ.get("KGAT_BWD_W_LDS", "0"))
+            4 * n * (2 * din + dout + 2 * din), w_lds=os.environ.get("KGAT_BWD_W_LDS", "1"))
     p = torch.randn(n * 64, device=dev)
     gg = torch.randn_like(p)
     m = torch.zeros_like(p)
