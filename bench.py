@@ -118,6 +118,7 @@ def main() -> None:
     pkg = importlib.import_module(PKG)
     graph_mod = importlib.import_module(PKG + ".graph")
     kernels = importlib.import_module(PKG + ".kernels")
+    replicas = importlib.import_module(PKG + ".replicas")
 
     t0 = time.perf_counter()
     U, E, inter, trip = graph_mod.synthetic_ckg(cfg["nodes"], cfg["triples"], seed=2024)
@@ -129,11 +130,7 @@ def main() -> None:
                                   cf_embedding_dim=cfg["dim"], kg_embedding_dim=cfg["dim"], layer_size=cfg["layers"],
                                   message_dropout=[0.1] * len(cfg["layers"])))
     model.attach_graph(layout, dev)
-    if world > 1:  # identical replicas
-        import torch.distributed as dist
-        for p in model.parameters():
-            if not p.is_sparse:
-                dist.broadcast(p.data, 0)
+    replicas.broadcast_parameters(model)  # identical replicas (no-op at N=1)
     model.train()
     model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
     L = len(cfg["layers"])
@@ -158,12 +155,7 @@ def main() -> None:
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
-        if world > 1:
-            import torch.distributed as dist
-            for p in params:
-                if p.grad is not None:
-                    dist.all_reduce(p.grad)
-                    p.grad.mul_(1.0 / world)
+        replicas.allreduce_gradients(params)  # RCCL over xGMI; no-op at N=1
         model.update_cf_weights()
         return loss
 

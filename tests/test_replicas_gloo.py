@@ -1,0 +1,58 @@
+"""Multi-process (world_size 2, gloo, CPU) checks of the data-parallel replica logic."""
+from __future__ import annotations
+
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.conftest import load_pkg
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank: int, world: int, port: int, q) -> None:
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = load_pkg()
+        rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
+        torch.manual_seed(100 + rank)  # different init per rank ...
+        m = pkg.KGAT(pkg.KGATArgs(user_num=10, entity_num=30, relation_num=10, layer_size=[64, 32]))
+        rep.broadcast_parameters(m)    # ... until rank 0's weights are broadcast
+        emb = m._user_entity_embedding.weight
+        # rank-dependent fake gradients; a big one (the table) and small ones
+        rep.SMALL_BUCKET_BYTES = 4096
+        for p in m.parameters():
+            if not p.is_sparse:
+                p.grad = torch.full_like(p, float(rank + 1))
+        m._relation_embedding.weight.grad = None  # skipped on every rank
+        rep.allreduce_gradients(list(m.parameters()))
+        ok_avg = all(torch.allclose(p.grad, torch.full_like(p, 1.5)) for p in m.parameters()
+                     if not p.is_sparse and p.grad is not None)
+        q.put((rank, ok_avg, emb.detach().clone(), m._relation_embedding.weight.grad is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_and_broadcast_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), "gradients not averaged"
+    assert torch.equal(res[0][2], res[1][2]), "replicas did not start from the same weights"
+    assert all(r[3] for r in res)
