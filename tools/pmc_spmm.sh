@@ -14,4 +14,4 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $ctr rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/$ctr.log; exit $rc; fi
 done
-python3 tools/pmc_parse.py $OUT profiles/pmc_c2.json
+python3 tools/pmc_parse.py $OUT profiles/pmc_c2.json && cp profiles/pmc_c2.json $OUT/
