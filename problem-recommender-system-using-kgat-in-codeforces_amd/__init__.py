@@ -7,5 +7,7 @@ name is not a Python identifier).
 """
 from .graph import DeviceGraph, GraphLayout, build_layout, synthetic_ckg  # noqa: F401
 from .model import KGAT, KGATArgs, KGATMode  # noqa: F401
+from .nfm import NFM, NFMArgs, NFMMode  # noqa: F401
 
-__all__ = ["KGAT", "KGATArgs", "KGATMode", "DeviceGraph", "GraphLayout", "build_layout", "synthetic_ckg"]
+__all__ = ["KGAT", "KGATArgs", "KGATMode", "NFM", "NFMArgs", "NFMMode", "DeviceGraph", "GraphLayout", "build_layout",
+           "synthetic_ckg"]

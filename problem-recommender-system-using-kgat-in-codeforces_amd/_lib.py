@@ -38,6 +38,17 @@ class Tables(ctypes.Structure):
                 ("width", c_i32 * KGAT_MAX_TABLES), ("count", c_i32)]
 
 
+KGAT_NFM_MAX_LAYERS = 4
+
+
+class NFMNet(ctypes.Structure):
+    """Mirror of ``kgat_nfm``."""
+
+    _fields_ = [("V", c_vp), ("ld_v", c_i64), ("w_lin", c_vp), ("b_lin", c_vp), ("W", c_vp * KGAT_NFM_MAX_LAYERS),
+                ("b", c_vp * KGAT_NFM_MAX_LAYERS), ("dims", c_i32 * (KGAT_NFM_MAX_LAYERS + 1)), ("n_layers", c_i32),
+                ("W_out", c_vp), ("dropout_p", c_f32), ("seed", c_u64)]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "kgat_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -68,6 +79,14 @@ _SIGNATURES = {
     "kgat_slot_sum_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_row_softmax_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_score_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_i32, c_vp, c_i32, c_vp, c_i64, c_vp]),
+    "kgat_coo_rowptr": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "kgat_nfm_act_floats": (c_i64, [ctypes.POINTER(NFMNet), c_i64]),
+    "kgat_nfm_fwd_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_nfm_loss_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),
+    "kgat_nfm_bwd_workspace": (c_i64, [ctypes.POINTER(NFMNet), c_i64]),
+    "kgat_nfm_bwd_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_f32,
+                                        c_vp, c_i64, c_vp, c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp,
+                                        c_i64, c_vp]),
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),

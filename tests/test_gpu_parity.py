@@ -449,3 +449,62 @@ def test_predict_scores_and_top20_vs_reference(pkg, case):
         if not np.array_equal(top[r], ref_top[r]):
             vals = np.sort(ref_masked[r].numpy())[::-1][:21]
             assert np.min(np.abs(np.diff(vals))) < 1e-5, (r, top[r], ref_top[r])
+
+
+def _nfm_batch(g, users, items):
+    U = int(g["user_num"])
+    F = U + int(g["entity_num"])
+    I = int(g["item_num"])
+    feat = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([g["feat_row"], g["feat_col"]])),
+                                   torch.from_numpy(g["feat_val"]), (I, int(g["entity_num"]))).to_dense()
+    x = torch.zeros(len(users), F)
+    x[torch.arange(len(users)), torch.from_numpy(np.asarray(users))] = 1.0
+    x[:, U:] = feat[torch.from_numpy(np.asarray(items))]
+    return x.to_sparse()
+
+
+def _nfm_from_golden(pkg, g):
+    m = pkg.NFM(pkg.NFMArgs(user_num=int(g["user_num"]), item_num=int(g["item_num"]), entity_num=int(g["entity_num"]),
+                            embedding_dim=int(g["dim"]), hidden_dim=g["hidden"].tolist()))
+    m.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("init/")})
+    return m.to(DEV)
+
+
+def test_nfm_train_steps_vs_reference(pkg):
+    """NFM BPR loss, every gradient and the Adam step (NFM/model.py:103-147) vs the reference run."""
+    g = golden("nfm_h3_d64")
+    m = _nfm_from_golden(pkg, g)
+    m.eval()
+    m.build_optimizer(lr=1e-4)
+    named = dict(m.named_parameters())
+    for s in range(2):
+        xp = _nfm_batch(g, g[f"tr{s}/users"], g[f"tr{s}/pos"]).to(DEV)
+        xn = _nfm_batch(g, g[f"tr{s}/users"], g[f"tr{s}/neg"]).to(DEV)
+        loss = m(xp, xn, mode=pkg.NFMMode.TRAIN)
+        loss.backward()
+        np.testing.assert_allclose(loss.item(), g[f"tr{s}/loss"], rtol=1e-5)
+        for k, prm in named.items():
+            ref = g.get(f"tr{s}/grad/{k}")
+            assert ref is not None, k
+            np.testing.assert_allclose(prm.grad.cpu().numpy(), ref, rtol=RTOL, atol=1e-6, err_msg=k)
+        m.update_weights()
+    for k, v in g.items():
+        if k.startswith("after/"):
+            np.testing.assert_allclose(named[k[6:]].detach().cpu().numpy(), v, rtol=RTOL, atol=ADAM_ATOL, err_msg=k)
+    users = g["pred_users"]
+    I = int(g["item_num"])
+    x = _nfm_batch(g, np.repeat(users, I), np.tile(np.arange(I), len(users))).to(DEV)
+    sc = m(x, mode=pkg.NFMMode.PREDICT).cpu().numpy()
+    np.testing.assert_allclose(sc, g["pred_scores"], rtol=RTOL, atol=1e-5)
+
+
+def test_nfm_train_mode_dropout_runs(pkg):
+    g = golden("nfm_h3_d64")
+    m = _nfm_from_golden(pkg, g)
+    m.train()
+    xp = _nfm_batch(g, g["tr0/users"], g["tr0/pos"]).to(DEV)
+    xn = _nfm_batch(g, g["tr0/users"], g["tr0/neg"]).to(DEV)
+    loss = m(xp, xn, mode=pkg.NFMMode.TRAIN)
+    loss.backward()
+    assert torch.isfinite(loss).item()
+    assert all(torch.isfinite(p.grad).all().item() for p in m.parameters())

@@ -130,3 +130,14 @@ def test_oracle_layout_agrees_with_product_layout():
     blocks, rel_ids = K.adjacency_blocks(U, [0, 1, 2, 3], g["interactions"], g["triplets"])
     A = K.initial_attentive(U + E, K.normalized_blocks(U + E, blocks))
     np.testing.assert_allclose(lay.coo()[2], A.values().numpy(), rtol=1e-6)
+
+
+def test_nfm_init_matches_reference_rng():
+    g = golden("nfm_h3_d64")
+    torch.manual_seed(2024)
+    m = pkg.NFM(pkg.NFMArgs(user_num=int(g["user_num"]), item_num=int(g["item_num"]), entity_num=int(g["entity_num"]),
+                            embedding_dim=int(g["dim"]), hidden_dim=g["hidden"].tolist()))
+    sd = m.state_dict()
+    assert set(sd) == {k[5:] for k in g if k.startswith("init/")}
+    for k, v in sd.items():
+        np.testing.assert_array_equal(v.numpy(), g["init/" + k], err_msg=k)
