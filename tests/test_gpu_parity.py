@@ -490,7 +490,15 @@ def test_nfm_train_steps_vs_reference(pkg):
         m.update_weights()
     for k, v in g.items():
         if k.startswith("after/"):
-            np.testing.assert_allclose(named[k[6:]].detach().cpu().numpy(), v, rtol=RTOL, atol=ADAM_ATOL, err_msg=k)
+            name = k[6:]
+            # An element whose reference gradient stayed at fp32-cancellation level in every step (e.g. the
+            # wide-head bias: it cancels exactly in y_pos - y_neg, so its true gradient is 0) is moved by Adam a
+            # full +-lr per step in whichever direction the residue's sign points: allow that, nothing else.
+            noise = np.all([np.abs(g[f"tr{s}/grad/{name}"]) < 1e-7 for s in range(2)], axis=0)
+            tol = np.where(noise, 2 * 1e-4 + 1e-7, ADAM_ATOL + RTOL * np.abs(v))
+            got = named[name].detach().cpu().numpy()
+            assert np.all(np.abs(got - v) <= tol), (name, np.max(np.abs(got - v)))
+            assert noise.mean() < 0.01 or name == "_linear.bias", name
     users = g["pred_users"]
     I = int(g["item_num"])
     x = _nfm_batch(g, np.repeat(users, I), np.tile(np.arange(I), len(users))).to(DEV)
