@@ -498,6 +498,11 @@ def test_nfm_train_steps_vs_reference(pkg):
             tol = np.where(noise, 2 * 1e-4 + 1e-7, ADAM_ATOL + RTOL * np.abs(v))
             got = named[name].detach().cpu().numpy()
             assert np.all(np.abs(got - v) <= tol), (name, np.max(np.abs(got - v)))
+    # PREDICT from the reference's own post-training weights (the wide bias above is noise-driven)
+    sd = m.state_dict()
+    for k in sd:
+        sd[k] = torch.from_numpy(g["after/" + k]) if "after/" + k in g else sd[k]
+    m.load_state_dict(sd)
     users = g["pred_users"]
     I = int(g["item_num"])
     x = _nfm_batch(g, np.repeat(users, I), np.tile(np.arange(I), len(users))).to(DEV)
