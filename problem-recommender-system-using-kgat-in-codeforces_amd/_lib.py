@@ -57,11 +57,12 @@ _SIGNATURES = {
     "kgat_spmm_csr_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_i64,
                                          c_vp]),
     "kgat_biinter_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                            c_i32, c_i32, c_f32, c_u64, c_vp]),
+                                            c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_biinter_bwd_workspace": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_spmm_csr_masked_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                                 c_i32, c_vp, c_i64, c_vp]),
-    "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+    "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                            c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32,
                                             c_u64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "kgat_bpr_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),

@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
                                                           float* __restrict__ H, int64_t ldh, int64_t n, float p,
-                                                          uint64_t seed) {
+                                                          uint64_t seed, float* __restrict__ norm_out,
+                                                          uint64_t* __restrict__ mask_out) {
   using B = BiShape<DIN, DOUT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
   float* w1s = smem;
@@ -131,6 +132,7 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
     }
     float g[B::NCB][4];
     float sq[4] = {0.f, 0.f, 0.f, 0.f};
+    uint64_t word = 0;  // saved state: 3 bits per (cb, i) -- pre_sum > 0, pre_mul > 0, kept
 #pragma unroll
     for (int cb = 0; cb < B::NCB; ++cb) {
       floatx4 acc1, acc2;
@@ -138,23 +140,32 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
       bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = lrelu(acc1[i] + bias1[cb]) + lrelu(acc2[i] + bias2[cb]);
+        const float pa = acc1[i] + bias1[cb], pb = acc2[i] + bias2[cb];
+        float v = lrelu(pa) + lrelu(pb);
+        bool keep = true;
         if (p > 0.f) {
           const uint64_t idx = static_cast<uint64_t>(r0 + q * 4 + i) * DOUT + cb * 16 + c;
-          v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
+          keep = dropout_keep(seed, idx, p);
+          v = keep ? v * scale : 0.f;
         }
+        if (B::NCB * 12 <= 64)
+          word |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << ((cb * 4 + i) * 3);
         g[cb][i] = v;
         sq[i] = fmaf(v, v, sq[i]);
       }
     }
+    if (mask_out != nullptr) mask_out[st * 64 + lane] = word;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float den = fmaxf(sqrtf(sum16(sq[i])), kNormEps);
+      const float nrm = sqrtf(sum16(sq[i]));
+      const float den = fmaxf(nrm, kNormEps);
       const int64_t row = r0 + q * 4 + i;
       if (row < n) {
         float* h = H + row * ldh + c;
 #pragma unroll
         for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] / den;
+        // saved norm; negative = the clamp was active (F.normalize's eps)
+        if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
       }
     }
   }
@@ -434,6 +445,249 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
   }
 }
 
+// Backward from the forward's saved state (norm + per-lane mask words).
+// Nothing of the forward is recomputed: with h = H (the saved output) and
+// n = the saved norm,
+//   dG = keep * scale * (dH - h (h . dH)) / n       (dH / eps when clamped)
+//   dA = dG * LReLU'(pre_sum), dB = dG * LReLU'(pre_mul)   (from the sign bits)
+//   du = dA . W1, dm = dB . W2  ->  dXd = du + dm*S, dS = du + dm*X
+//   dW1 += dA^T (X+S), dW2 += dB^T (X*S), db1/db2 += column sums.
+// Every operand is kept in the MFMA C-layout (lane (c, q), element i = row
+// q*4+i, column blk*16+c).  That layout IS the A/B operand layout of the
+// K = rows product (step s takes element s), so the weight gradients are
+// accumulated straight from registers; only dA/dB take an LDS transpose (per
+// wave) for the K = DOUT product.  Each wave works alone -- no block barrier
+// in the loop -- and keeps all 2*DIN*DOUT weight-gradient accumulators in
+// registers (<= 128 per lane), one wave per SIMD, next sub-tile prefetched.
+template <int DIN, int DOUT>
+struct SavedBwd {
+  using B = BiShape<DIN, DOUT>;
+  static constexpr bool kOk = DOUT <= 64 && 2 * DIN * DOUT <= 128 * 64;
+  // W row pitch in LDS chosen so the 4 lane groups (k = q*KO + t) hit 4
+  // different 16-bank groups
+  static constexpr int wpitch() {
+    for (int pad = 0; pad < 64; ++pad)
+      if ((B::KO * (DIN + pad)) % 64 == 16) return DIN + pad;
+    return DIN + 1;
+  }
+  static constexpr int WLDB = wpitch();
+  static constexpr int OLD = DOUT + 4;
+  static constexpr int kWave = 2 * 16 * OLD;                 // dA/dB transpose, per wave
+  static constexpr int kTotal = 2 * DOUT * WLDB + 4 * kWave;  // floats
+};
+
+template <int DIN, int DOUT>
+struct SavedRegs {
+  float x[DIN / 16][4], s[DIN / 16][4];
+  float h[DOUT / 16][4], dh[DOUT / 16][4];
+  float nrm[4];
+  uint64_t mw[4];
+  int32_t node[4];
+};
+
+template <int DIN, int DOUT>
+__device__ __forceinline__ void load_saved(SavedRegs<DIN, DOUT>& R, int64_t r0, int64_t n,
+                                           const int32_t* __restrict__ rows, int64_t n_src,
+                                           const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
+                                           int64_t lds, const float* __restrict__ H, int64_t ldh,
+                                           const float* __restrict__ norm, const uint64_t* __restrict__ mask,
+                                           const float* __restrict__ dH, int64_t lddh, int q, int c) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t row = r0 + q * 4 + i;
+    int64_t node = -1;
+    if (row < n) node = rows != nullptr ? static_cast<int64_t>(rows[row]) : row;
+    if (node >= n_src) node = -1;
+    R.node[i] = static_cast<int32_t>(node);
+    const bool ok = node >= 0;
+#pragma unroll
+    for (int ib = 0; ib < DIN / 16; ++ib) {
+      R.x[ib][i] = ok ? X[node * ldx + ib * 16 + c] : 0.f;
+      R.s[ib][i] = ok ? S[node * lds + ib * 16 + c] : 0.f;
+    }
+#pragma unroll
+    for (int cb = 0; cb < DOUT / 16; ++cb) {
+      R.h[cb][i] = ok ? H[node * ldh + cb * 16 + c] : 0.f;
+      R.dh[cb][i] = row < n ? dH[row * lddh + cb * 16 + c] : 0.f;
+    }
+    R.nrm[i] = ok ? norm[node] : 1.f;
+    // the forward's lane (c, (node>>2)&3) of sub-tile node>>4 holds this row's bits
+    R.mw[i] = ok ? mask[(node >> 4) * 64 + ((node >> 2) & 3) * 16 + c] : 0ull;
+  }
+}
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds, const float* __restrict__ H,
+    int64_t ldh, const float* __restrict__ norm, const uint64_t* __restrict__ mask, const float* __restrict__ dH,
+    int64_t lddh, const float* __restrict__ W1, const float* __restrict__ W2, float* __restrict__ dXd,
+    int64_t lddxd, float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p,
+    const int32_t* __restrict__ rows, int64_t n_src) {
+  using B = BiShape<DIN, DOUT>;
+  using F = SavedBwd<DIN, DOUT>;
+  constexpr int NCB = B::NCB, NIB = B::NIB, KO = B::KO;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* w1s = smem;
+  float* w2s = smem + DOUT * F::WLDB;
+  for (int i = threadIdx.x; i < DOUT * DIN; i += blockDim.x) {
+    const int j = i / DIN, k = i % DIN;
+    w1s[j * F::WLDB + k] = W1[i];
+    w2s[j * F::WLDB + k] = W2[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  float* tda = smem + 2 * DOUT * F::WLDB + wave * F::kWave;
+  float* tdb = tda + 16 * F::OLD;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+
+  floatx4 dw1[NCB][NIB], dw2[NCB][NIB];
+#pragma unroll
+  for (int ob = 0; ob < NCB; ++ob)
+#pragma unroll
+    for (int ib = 0; ib < NIB; ++ib) {
+      dw1[ob][ib] = floatx4{0.f, 0.f, 0.f, 0.f};
+      dw2[ob][ib] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  float gb1[NCB], gb2[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) gb1[cb] = gb2[cb] = 0.f;
+
+  const int64_t nsub = (n + 15) / 16;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+  int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  SavedRegs<DIN, DOUT> R;
+  if (st < nsub) load_saved<DIN, DOUT>(R, st * 16, n, rows, n_src, X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, q, c);
+  for (; st < nsub; st += stride) {
+    const int64_t r0 = st * 16;
+    float x[NIB][4], sv[NIB][4], da[NCB][4], db[NCB][4];
+    {
+      float h[NCB][4], dh[NCB][4], nrm[4];
+      uint64_t mw[4];
+      int32_t node[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int ib = 0; ib < NIB; ++ib) {
+          x[ib][i] = R.x[ib][i];
+          sv[ib][i] = R.s[ib][i];
+        }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          h[cb][i] = R.h[cb][i];
+          dh[cb][i] = R.dh[cb][i];
+        }
+        nrm[i] = R.nrm[i];
+        mw[i] = R.mw[i];
+        node[i] = R.node[i];
+      }
+      if (st + stride < nsub)
+        load_saved<DIN, DOUT>(R, (st + stride) * 16, n, rows, n_src, X, ldx, S, lds, H, ldh, norm, mask, dH, lddh,
+                              q, c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float dot = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) dot = fmaf(h[cb][i], dh[cb][i], dot);
+        dot = sum16(dot);
+        const bool clamped = nrm[i] < 0.f;
+        const float inv = clamped ? 1.f / kNormEps : 1.f / nrm[i];
+        const float proj = clamped ? 0.f : dot;
+        const int sh = (node[i] & 3) * 3;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const uint32_t bits = static_cast<uint32_t>(mw[i] >> (cb * 12 + sh)) & 7u;
+          float dg = (dh[cb][i] - h[cb][i] * proj) * inv;
+          dg = (bits & 4u) ? dg * scale : 0.f;
+          da[cb][i] = (bits & 1u) ? dg : dg * kLeakySlope;
+          db[cb][i] = (bits & 2u) ? dg : dg * kLeakySlope;
+          gb1[cb] += da[cb][i];
+          gb2[cb] += db[cb][i];
+          tda[(q * 4 + i) * F::OLD + cb * 16 + c] = da[cb][i];
+          tdb[(q * 4 + i) * F::OLD + cb * 16 + c] = db[cb][i];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+
+    // du = dA . W1, dm = dB . W2 over K = DOUT (k = q*KO + step)
+    {
+      float dar[KO], dbr[KO];
+      const float* pa = tda + c * F::OLD + q * KO;
+      const float* pb = tdb + c * F::OLD + q * KO;
+#pragma unroll
+      for (int t = 0; t < KO; t += 4) {
+        const float4 va = *reinterpret_cast<const float4*>(pa + t);
+        const float4 vb = *reinterpret_cast<const float4*>(pb + t);
+        dar[t] = va.x; dar[t + 1] = va.y; dar[t + 2] = va.z; dar[t + 3] = va.w;
+        dbr[t] = vb.x; dbr[t + 1] = vb.y; dbr[t + 2] = vb.z; dbr[t + 3] = vb.w;
+      }
+#pragma unroll
+      for (int ib = 0; ib < NIB; ++ib) {
+        floatx4 du = {0.f, 0.f, 0.f, 0.f}, dm = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < KO; ++t) {
+          const int k = q * KO + t;
+          du = mfma16x4(dar[t], w1s[k * F::WLDB + ib * 16 + c], du);
+          dm = mfma16x4(dbr[t], w2s[k * F::WLDB + ib * 16 + c], dm);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = r0 + q * 4 + i;
+          if (row < n) {
+            dXd[row * lddxd + ib * 16 + c] = fmaf(dm[i], sv[ib][i], du[i]);
+            dS[row * ldds + ib * 16 + c] = fmaf(dm[i], x[ib][i], du[i]);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    // weight gradients, K = the 16 rows (step s = C-layout element s)
+#pragma unroll
+    for (int ib = 0; ib < NIB; ++ib) {
+      float u[4], m[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u[i] = x[ib][i] + sv[ib][i];
+        m[i] = x[ib][i] * sv[ib][i];
+      }
+#pragma unroll
+      for (int ob = 0; ob < NCB; ++ob)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          dw1[ob][ib] = mfma16x4(da[ob][s4], u[s4], dw1[ob][ib]);
+          dw2[ob][ib] = mfma16x4(db[ob][s4], m[s4], dw2[ob][ib]);
+        }
+    }
+  }
+
+  // one slab per wave: [dW1 | dW2 | db1 | db2]
+  constexpr int kSlab = 2 * DOUT * DIN + 2 * DOUT;
+  float* out = slab + (static_cast<int64_t>(blockIdx.x) * 4 + wave) * kSlab;
+#pragma unroll
+  for (int ob = 0; ob < NCB; ++ob)
+#pragma unroll
+    for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        out[(ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw1[ob][ib][i];
+        out[DOUT * DIN + (ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw2[ob][ib][i];
+      }
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    float a = gb1[cb], b = gb2[cb];
+    a += __shfl_xor(a, 16);
+    a += __shfl_xor(a, 32);
+    b += __shfl_xor(b, 16);
+    b += __shfl_xor(b, 32);
+    if (q == 0) {
+      out[2 * DOUT * DIN + cb * 16 + c] = a;
+      out[2 * DOUT * DIN + DOUT + cb * 16 + c] = b;
+    }
+  }
+}
+
 // Sum the per-block slabs: one 1024-thread block per 64 outputs, 16 waves
 // split the slabs (wave w takes slabs w, w+16, ...), then add the 16 wave
 // partials in wave order -- deterministic.
@@ -505,34 +759,73 @@ static int launch_bwd_kernel(int grid, const float* X, int64_t ldx, const float*
 template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
-                      hipStream_t st) {
+                      float* norm, uint64_t* mask, hipStream_t st) {
   const int grid = blocks_for(n, 64, kCUs * 8);
   hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, W2, b2,
-                     H, ldh, n, p, seed);
+                     H, ldh, n, p, seed, norm, mask);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
 
 template <int DIN, int DOUT>
-static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH, int64_t lddh,
-                      const float* W1, const float* b1, const float* W2, const float* b2, float* dXd, int64_t lddxd,
-                      float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, float p,
-                      uint64_t seed, const int32_t* rows, int64_t src_rows, float* ws, int64_t ws_floats,
-                      hipStream_t st) {
-  const int grid = bwd_grid<DIN, DOUT>(n);
+static int saved_grid(int64_t n) { return blocks_for(n, 64, kCUs); }
+
+// Workspace floats: slabs of whichever backward variant the shape can take.
+template <int DIN, int DOUT>
+static int64_t bwd_workspace(int64_t n) {
+  const int64_t width = 2LL * DIN * DOUT + 2LL * DOUT;
+  int64_t slabs = bwd_grid<DIN, DOUT>(n);
+  if constexpr (SavedBwd<DIN, DOUT>::kOk) {
+    const int64_t s4 = 4LL * saved_grid<DIN, DOUT>(n);
+    if (s4 > slabs) slabs = s4;
+  }
+  return slabs * width;
+}
+
+template <int DIN, int DOUT>
+static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H, int64_t ldh,
+                      const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
+                      const float* b1, const float* W2, const float* b2, float* dXd, int64_t lddxd, float* dS,
+                      int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, float p, uint64_t seed,
+                      const int32_t* rows, int64_t src_rows, float* ws, int64_t ws_floats, hipStream_t st) {
   const int width = 2 * DOUT * DIN + 2 * DOUT;
   const int64_t n_src = rows ? src_rows : n;
-  if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
-  if (bwd_w_in_lds()) {
-    if (int e = launch_bwd_kernel<DIN, DOUT, true>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
-                                                   ldds, ws, n, p, seed, rows, n_src, st))
-      return e;
-  } else {
-    if (int e = launch_bwd_kernel<DIN, DOUT, false>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
-                                                    ldds, ws, n, p, seed, rows, n_src, st))
-      return e;
+  int nslab = 0;
+  bool saved = false;
+  if constexpr (SavedBwd<DIN, DOUT>::kOk) {
+    if (H != nullptr && norm != nullptr && mask != nullptr) {
+      saved = true;
+      const int grid = saved_grid<DIN, DOUT>(n);
+      nslab = 4 * grid;
+      if (ws == nullptr || ws_floats < static_cast<int64_t>(nslab) * width) return KGAT_ERR_WORKSPACE;
+      const size_t lds_bytes = SavedBwd<DIN, DOUT>::kTotal * sizeof(float);
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
+        if (e != hipSuccess) return static_cast<int>(e);
+        attr_set = true;
+      }
+      hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds,
+                         H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+      KGAT_LAUNCH_CHECK();
+    }
   }
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, grid, width, dW1, dW2,
+  if (!saved) {
+    const int grid = bwd_grid<DIN, DOUT>(n);
+    nslab = grid;
+    if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
+    if (bwd_w_in_lds()) {
+      if (int e = launch_bwd_kernel<DIN, DOUT, true>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
+                                                     ldds, ws, n, p, seed, rows, n_src, st))
+        return e;
+    } else {
+      if (int e = launch_bwd_kernel<DIN, DOUT, false>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd,
+                                                      dS, ldds, ws, n, p, seed, rows, n_src, st))
+        return e;
+    }
+  }
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, nslab, width, dW1, dW2,
                      db1, db2, DIN, DOUT);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
@@ -562,21 +855,23 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
                                     const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
                                     int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
-                                    void* stream) {
+                                    float* norm_out, uint64_t* mask_out, void* stream) {
   if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || n_rows < 0) return KGAT_ERR_INVALID;
   if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 64)) return KGAT_ERR_INVALID;
   if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define KGAT_FWD_CALL(a, b) kgat::launch_fwd<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, seed, st)
+#define KGAT_FWD_CALL(a, b) kgat::launch_fwd<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, seed, \
+                                                  norm_out, mask_out, st)
   KGAT_BI_DISPATCH(KGAT_FWD_CALL)
 #undef KGAT_FWD_CALL
 }
 
 extern "C" int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int32_t d_out) {
-  const int64_t width = 2LL * d_in * d_out + 2LL * d_out;
-#define KGAT_WS_CALL(a, b) static_cast<int64_t>(kgat::bwd_grid<a, b>(n_rows)) * width
+  if (n_rows < 0) return -1;
+#define KGAT_WS_CALL(a, b) kgat::bwd_workspace<a, b>(n_rows)
   switch (d_in * 1000 + d_out) {
     case 16016: return KGAT_WS_CALL(16, 16);
     case 32016: return KGAT_WS_CALL(32, 16);
@@ -595,7 +890,8 @@ extern "C" int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int3
 #undef KGAT_WS_CALL
 }
 
-extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* dH,
+extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                    int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
                                     int64_t lddh, const float* W1, const float* b1, const float* W2, const float* b2,
                                     float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
                                     float* dW2, float* db2, int64_t n_rows, int32_t d_in, int32_t d_out,
@@ -607,9 +903,11 @@ extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S,
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || lddh < d_out || lddxd < d_in || ldds < d_in) return KGAT_ERR_INVALID;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  const int n_state = (H != nullptr) + (norm != nullptr) + (mask != nullptr);
+  if (n_state != 0 && (n_state != 3 || ldh < d_out)) return KGAT_ERR_INVALID;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_BWD_CALL(a, b)                                                                                   \
-  kgat::launch_bwd<a, b>(X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, \
+  kgat::launch_bwd<a, b>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, \
                          n_rows, dropout_p, seed, rows, src_rows, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_BWD_CALL)
 #undef KGAT_BWD_CALL

@@ -104,7 +104,22 @@ def frontier_reset(rows: torch.Tensor, node_map: torch.Tensor) -> None:
     _lib.call("kgat_frontier_reset", rows.data_ptr(), rows.numel(), node_map.data_ptr(), stream_ptr(rows.device))
 
 
-def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out=None) -> torch.Tensor:
+class BiState:
+    """The forward's saved state for the backward (kgat_biinter_fwd_f32 norm_out / mask_out):
+    row norms and per-lane sign/keep bit words, indexed by node."""
+
+    def __init__(self, n: int, device):
+        self.norm = torch.empty(max(n, 1), dtype=torch.float32, device=device)
+        self.mask = torch.empty(max((n + 15) // 16, 1) * 64, dtype=torch.int64, device=device)
+
+
+def saved_state_supported(d_in: int, d_out: int) -> bool:
+    """Shapes whose backward runs from the saved state (see kgat_biinter_bwd_f32)."""
+    return d_out <= 64 and d_in * d_out <= 4096
+
+
+def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out=None,
+                state: BiState | None = None) -> torch.Tensor:
     for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2")):
         _req(t, nm, dim=2)
     _req(b1, "b1", dim=1)
@@ -117,16 +132,20 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
         raise ValueError("W must be contiguous")
     if out is None:
         out = torch.empty(n, dout, dtype=torch.float32, device=X.device)
+    if state is not None and (state.norm.numel() < n or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
+        raise ValueError("bi-interaction state too small or d_out > 64")
     _lib.call("kgat_biinter_fwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
               W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout, float(dropout_p),
-              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), stream_ptr(X.device))
+              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.norm.data_ptr() if state is not None else None,
+              state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
     return out
 
 
 def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,
-                rows: torch.Tensor | None = None):
+                rows: torch.Tensor | None = None, H: torch.Tensor | None = None, state: BiState | None = None):
     """Returns (dXd, dS, dW1, db1, dW2, db2).  With ``rows`` (int32 [n]), dH/dXd/dS are compact:
-    row i belongs to node rows[i] of X and S (-1 = padding)."""
+    row i belongs to node rows[i] of X and S (-1 = padding).  With the forward's output ``H`` and
+    ``state``, the backward reads them instead of recomputing the forward."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     _req(dH, "dH", dim=2)
@@ -136,6 +155,12 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
         n = rows.numel()
     if dH.shape != (n, dout):
         raise ValueError("dH shape mismatch")
+    if (H is None) != (state is None):
+        raise ValueError("H and state go together")
+    if H is not None:
+        _req(H, "H", dim=2)
+        if H.shape != (src_rows, dout):
+            raise ValueError("H shape mismatch")
     dev = X.device
     dXd = torch.empty(n, din, dtype=torch.float32, device=dev) if dXd is None else dXd
     dS = torch.empty(n, din, dtype=torch.float32, device=dev) if dS is None else dS
@@ -147,7 +172,10 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     if ws_n < 0:
         raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
-    _lib.call("kgat_biinter_bwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), dH.data_ptr(), _ld(dH),
+    _lib.call("kgat_biinter_bwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S),
+              H.data_ptr() if H is not None else None, _ld(H) if H is not None else 0,
+              state.norm.data_ptr() if state is not None else None,
+              state.mask.data_ptr() if state is not None else None, dH.data_ptr(), _ld(dH),
               W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(),
               _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
               float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),

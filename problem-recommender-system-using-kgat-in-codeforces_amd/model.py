@@ -81,6 +81,11 @@ class MultiHeadAttention(nn.Module):
             nn.init.xavier_uniform_(lin.weight)
 
 
+def _saved(tables, states, l) -> dict:
+    """Layer l's forward output + saved state for the backward (none: it recomputes)."""
+    return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
+
+
 class _CFLoss(torch.autograd.Function):
     """Whole CF step as one autograd node: propagation + BPR, forward and backward.
 
@@ -102,17 +107,20 @@ class _CFLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
         graph, drops, seeds, reg = cfg
-        tables, sides = [X0], []
+        tables, sides, states = [X0], [], []
         x = X0
         for l in range(len(drops)):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             s = kernels.spmm(graph, x)
-            x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l])
+            st = (kernels.BiState(x.shape[0], x.device)
+                  if kernels.saved_state_supported(W1.shape[1], W1.shape[0]) else None)
+            x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             sides.append(s)
+            states.append(st)
             tables.append(x)
         loss, coef = kernels.bpr_fwd(tables, users, pos, neg, reg)
         ctx.cfg = cfg
-        ctx.tables, ctx.sides, ctx.ws = tables, sides, ws
+        ctx.tables, ctx.sides, ctx.states, ctx.ws = tables, sides, states, ws
         ctx.ids = (users, pos, neg)
         ctx.coef = coef
         return loss.view(())
@@ -120,7 +128,7 @@ class _CFLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         graph, drops, seeds, reg = ctx.cfg
-        tables, sides, ws = ctx.tables, ctx.sides, ctx.ws
+        tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
         L = len(drops)
@@ -131,7 +139,7 @@ class _CFLoss(torch.autograd.Function):
         kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dHc, row_map=graph.node_map)
         l = L - 1
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
-                                                            drops[l], seeds[l], rows=rows)
+                                                            drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
         dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True)
         kernels.frontier_reset(rows, graph.node_map)
         kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
@@ -140,12 +148,12 @@ class _CFLoss(torch.autograd.Function):
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],
-                                                              seeds[l])
+                                                              seeds[l], **_saved(tables, states, l))
             kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
             kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXd)
             wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
             dX = dXd
-        ctx.tables = ctx.sides = None
+        ctx.tables = ctx.sides = ctx.states = None
         return (None, None, None, None, dX, *wgrads)
 
 

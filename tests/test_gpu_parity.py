@@ -147,6 +147,47 @@ def test_biinter_fwd_bwd_parity(pkg, din, dout):
     np.testing.assert_allclose(dS.cpu().numpy(), s.grad.numpy(), rtol=1e-3, atol=1e-5)
     for got, want in ((dW1, w1.grad), (db1, bb1.grad), (dW2, w2.grad), (db2, bb2.grad)):
         np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-3, atol=1e-4)
+    if kernels.saved_state_supported(din, dout):
+        st = kernels.BiState(n, DEV)
+        H2 = kernels.biinter_fwd(*dv, state=st)
+        assert torch.equal(H, H2)
+        got = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], H=H2, state=st)
+        want = (x.grad, s.grad, w1.grad, bb1.grad, w2.grad, bb2.grad)
+        for i, (a, b) in enumerate(zip(got, want)):
+            np.testing.assert_allclose(a.cpu().numpy(), b.numpy(), rtol=1e-3, atol=1e-5 if i < 2 else 1e-4)
+
+
+@pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (32, 16), (16, 16), (128, 32)])
+def test_biinter_saved_state_matches_recompute(pkg, din, dout):
+    """The backward from the forward's saved state (norm + sign/keep bits) equals the
+    recomputing backward: dense and frontier rows, dropout on/off, clamped (all-zero) rows."""
+    _, kernels = _mods(pkg)
+    torch.manual_seed(din + dout)
+    n = 3000 + 7
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    X[100:140] = 0.0  # with b = 0 these rows give g = 0: F.normalize's clamp is active
+    S[100:140] = 0.0
+    W1, W2 = torch.randn(dout, din) * 0.2, torch.randn(dout, din) * 0.2
+    b1, b2 = torch.zeros(dout), torch.zeros(dout)
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    dH = torch.randn(n, dout).to(DEV)
+    F = torch.from_numpy(np.random.default_rng(2).choice(n, 300, replace=False))
+    F[:5] = torch.arange(100, 105)
+    rows = torch.cat([F, torch.full((20,), -1)]).int().to(DEV)
+    dHc = torch.zeros(320, dout, device=DEV)
+    dHc[:300] = torch.randn(300, dout, device=DEV)
+    for p in (0.0, 0.2):
+        st = kernels.BiState(n, DEV)
+        H = kernels.biinter_fwd(*dv, dropout_p=p, seed=5, state=st)
+        assert torch.equal(H, kernels.biinter_fwd(*dv, dropout_p=p, seed=5))
+        norm = st.norm[:n].cpu()
+        assert torch.all(norm[100:140] < 0) and torch.all(norm[:100] > 0)
+        for rr, g in ((None, dH), (rows, dHc)):
+            a = kernels.biinter_bwd(dv[0], dv[1], g, *dv[2:], dropout_p=p, seed=5, rows=rr)
+            b = kernels.biinter_bwd(dv[0], dv[1], g, *dv[2:], dropout_p=p, seed=5, rows=rr, H=H, state=st)
+            for i, (x, y) in enumerate(zip(a, b)):
+                np.testing.assert_allclose(y.cpu().numpy(), x.cpu().numpy(), rtol=1e-4,
+                                           atol=1e-6 if i < 2 else 1e-5, err_msg=f"p={p} rows={rr is not None} {i}")
 
 
 def test_biinter_dropout_consistent(pkg):

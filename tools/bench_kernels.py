@@ -88,11 +88,19 @@ def main():
         b1 = torch.zeros(dout, device=dev)
         b2 = torch.zeros(dout, device=dev)
         dH = torch.randn(n, dout, device=dev)
+        H = torch.empty(n, dout, device=dev)
         rec(f"biinter_fwd_{din}x{dout}", timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5), args.reps),
             4 * n * (2 * din + dout))
         rec(f"biinter_bwd_{din}x{dout}",
             timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5), args.reps),
             4 * n * (2 * din + dout + 2 * din), w_lds=os.environ.get("KGAT_BWD_W_LDS", "1"))
+        st = K.BiState(n, dev)
+        rec(f"biinter_fwd_saved_{din}x{dout}",
+            timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st), args.reps),
+            4 * n * (2 * din + dout) + 36 * n)
+        rec(f"biinter_bwd_saved_{din}x{dout}",
+            timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5, H=H, state=st), args.reps),
+            4 * n * (2 * din + 2 * dout + 2 * din) + 36 * n)
     p = torch.randn(n * 64, device=dev)
     gg = torch.randn_like(p)
     m = torch.zeros_like(p)
