@@ -77,6 +77,23 @@ __device__ __forceinline__ void bi_block(const float (&u)[DIN / 4], const float 
   }
 }
 
+// Dropout draws of the bi-interaction output.  One 64-bit hash per (node,
+// lane column c, group of four 16-wide column blocks) yields four 16-bit
+// uniforms, one per column block: element (node, cb*16 + c) is kept iff its
+// draw >= round(p * 65536).  Shared by the forward and the recomputing backward.
+__device__ __forceinline__ uint32_t bi_drop_threshold(float p) {
+  const float t = p * 65536.f + 0.5f;
+  return t >= 65536.f ? 65536u : static_cast<uint32_t>(t);
+}
+template <int DOUT>
+__device__ __forceinline__ uint64_t bi_drop_hash(uint64_t seed, int64_t node, int group, int c) {
+  constexpr int kGroups = (DOUT / 16 + 3) / 4;
+  return mix_hash64(seed, (static_cast<uint64_t>(node) * kGroups + group) * 16 + c);
+}
+__device__ __forceinline__ bool bi_drop_keep(uint64_t h, int cb, uint32_t thr) {
+  return static_cast<uint32_t>((h >> (16 * (cb & 3))) & 0xFFFFu) >= thr;
+}
+
 template <int DIN, int DOUT>
 __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const float* __restrict__ W1,
                                               const float* __restrict__ W2) {
@@ -111,6 +128,7 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
     bias2[cb] = b2[cb * 16 + c];
   }
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = bi_drop_threshold(p);
   const int64_t nsub = (n + 15) / 16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
   int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -133,6 +151,14 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
     float g[B::NCB][4];
     float sq[4] = {0.f, 0.f, 0.f, 0.f};
     uint64_t word = 0;  // saved state: 3 bits per (cb, i) -- pre_sum > 0, pre_mul > 0, kept
+    constexpr int NG = (B::NCB + 3) / 4;
+    uint64_t dh_[4][NG];
+    if (p > 0.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, r0 + q * 4 + i, gi, c);
+    }
 #pragma unroll
     for (int cb = 0; cb < B::NCB; ++cb) {
       floatx4 acc1, acc2;
@@ -144,8 +170,7 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
         float v = lrelu(pa) + lrelu(pb);
         bool keep = true;
         if (p > 0.f) {
-          const uint64_t idx = static_cast<uint64_t>(r0 + q * 4 + i) * DOUT + cb * 16 + c;
-          keep = dropout_keep(seed, idx, p);
+          keep = bi_drop_keep(dh_[i][cb / 4], cb, thr);
           v = keep ? v * scale : 0.f;
         }
         if (B::NCB * 12 <= 64)
@@ -158,12 +183,12 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float nrm = sqrtf(sum16(sq[i]));
-      const float den = fmaxf(nrm, kNormEps);
+      const float inv = 1.f / fmaxf(nrm, kNormEps);
       const int64_t row = r0 + q * 4 + i;
       if (row < n) {
         float* h = H + row * ldh + c;
 #pragma unroll
-        for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] / den;
+        for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] * inv;
         // saved norm; negative = the clamp was active (F.normalize's eps)
         if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
       }
@@ -255,6 +280,7 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
     bias2[cb] = b2[cb * 16 + c];
   }
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = bi_drop_threshold(p);
 
   // phase-B ownership: output 16x16 blocks of [dW1 | dW2], block id
   // ob = o-block, ib = i-block, mat; wave w takes ids w, w+4, ...
@@ -306,10 +332,16 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
     float sq[4] = {0.f, 0.f, 0.f, 0.f}, dt[4] = {0.f, 0.f, 0.f, 0.f};
     // node id of each C-layout row: the dropout mask is keyed by the node, as in the forward
     int64_t node[4];
+    constexpr int NG = (B::NCB + 3) / 4;
+    uint64_t hsh[4][NG];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = r0 + q * 4 + i;
       node[i] = (rows != nullptr && row < n) ? static_cast<int64_t>(rows[row]) : row;
+      if (p > 0.f) {
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) hsh[i][gi] = bi_drop_hash<DOUT>(seed, node[i], gi, c);
+      }
     }
 #pragma unroll
     for (int cb = 0; cb < B::NCB; ++cb) {
@@ -322,10 +354,7 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
         pos_a |= static_cast<uint64_t>(pa > 0.f) << (cb * 4 + i);
         pos_b |= static_cast<uint64_t>(pb > 0.f) << (cb * 4 + i);
         float v = lrelu(pa) + lrelu(pb);
-        if (p > 0.f) {
-          const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
-          v = dropout_keep(seed, idx, p) ? v * scale : 0.f;
-        }
+        if (p > 0.f) v = bi_drop_keep(hsh[i][cb / 4], cb, thr) ? v * scale : 0.f;
         gd[cb][i] = v;
         sq[i] = fmaf(v, v, sq[i]);
         dt[i] = fmaf(v, dh[cb][i], dt[i]);
@@ -342,10 +371,7 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
       for (int cb = 0; cb < B::NCB; ++cb) {
         // d(g/den): dh/den - g (dh.g)/den^3 while the clamp is inactive
         float dg = (dh[cb][i] - gd[cb][i] * coef) * inv;
-        if (p > 0.f) {
-          const uint64_t idx = static_cast<uint64_t>(node[i]) * DOUT + cb * 16 + c;
-          dg = dropout_keep(seed, idx, p) ? dg * scale : 0.f;
-        }
+        if (p > 0.f) dg = bi_drop_keep(hsh[i][cb / 4], cb, thr) ? dg * scale : 0.f;
         const float da = dg * (((pos_a >> (cb * 4 + i)) & 1) ? 1.f : kLeakySlope);
         const float db = dg * (((pos_b >> (cb * 4 + i)) & 1) ? 1.f : kLeakySlope);
         tda[(wave * 16 + q * 4 + i) * B::OLD + cb * 16 + c] = da;
@@ -455,14 +481,18 @@ __global__ __launch_bounds__(256, 2) void biinter_bwd_kernel(
 // Every operand is kept in the MFMA C-layout (lane (c, q), element i = row
 // q*4+i, column blk*16+c).  That layout IS the A/B operand layout of the
 // K = rows product (step s takes element s), so the weight gradients are
-// accumulated straight from registers; only dA/dB take an LDS transpose (per
-// wave) for the K = DOUT product.  Each wave works alone -- no block barrier
-// in the loop -- and keeps all 2*DIN*DOUT weight-gradient accumulators in
-// registers (<= 128 per lane), one wave per SIMD, next sub-tile prefetched.
+// accumulated straight from registers; only dA/dB take an LDS transpose for
+// the K = DOUT product.  Each wave works alone (no block barrier in the loop)
+// and keeps all 2*DIN*DOUT weight-gradient accumulators in registers (<= 128
+// per lane, one wave per SIMD).  The next sub-tile's rows (X, S, H, dH, norms,
+// mask words) stream into a per-wave LDS image by LDS-DMA (global_load_lds)
+// while the current one computes: no prefetch registers, no per-element
+// address arithmetic.  The DMA image is lane-linear, so the row chunks are
+// XOR-swizzled on the SOURCE address (chunk ^ 4*((row>>2)&3)), which makes
+// the C-layout ds_read_b32 of 4 rows x 16 columns bank-conflict-free.
 template <int DIN, int DOUT>
 struct SavedBwd {
   using B = BiShape<DIN, DOUT>;
-  static constexpr bool kOk = DOUT <= 64 && 2 * DIN * DOUT <= 128 * 64;
   // W row pitch in LDS chosen so the 4 lane groups (k = q*KO + t) hit 4
   // different 16-bank groups
   static constexpr int wpitch() {
@@ -472,51 +502,58 @@ struct SavedBwd {
   }
   static constexpr int WLDB = wpitch();
   static constexpr int OLD = DOUT + 4;
-  static constexpr int kWave = 2 * 16 * OLD;                 // dA/dB transpose, per wave
-  static constexpr int kTotal = 2 * DOUT * WLDB + 4 * kWave;  // floats
+  // per-wave LDS (floats): DMA image [X | S | H | dH | norm(64) | mask(16x16 u64)], dA/dB transpose
+  static constexpr int kX = 16 * DIN, kH = 16 * DOUT;
+  static constexpr int kNorm = 2 * kX + 2 * kH;
+  static constexpr int kMask = kNorm + 64;
+  static constexpr int kImg = kMask + 512;
+  static constexpr int kT = 2 * 16 * OLD;
+  static constexpr int kWave = kImg + kT;
+  static constexpr int kTotal = 2 * DOUT * WLDB + 4 * kWave;
+  static constexpr bool kOk = DOUT <= 64 && 2 * DIN * DOUT <= 128 * 64 && kTotal * 4 <= 160 * 1024;
 };
 
-template <int DIN, int DOUT>
-struct SavedRegs {
-  float x[DIN / 16][4], s[DIN / 16][4];
-  float h[DOUT / 16][4], dh[DOUT / 16][4];
-  float nrm[4];
-  uint64_t mw[4];
-  int32_t node[4];
-};
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
 
-template <int DIN, int DOUT>
-__device__ __forceinline__ void load_saved(SavedRegs<DIN, DOUT>& R, int64_t r0, int64_t n,
-                                           const int32_t* __restrict__ rows, int64_t n_src,
-                                           const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
-                                           int64_t lds, const float* __restrict__ H, int64_t ldh,
-                                           const float* __restrict__ norm, const uint64_t* __restrict__ mask,
-                                           const float* __restrict__ dH, int64_t lddh, int q, int c) {
+__device__ __forceinline__ void dma16(const void* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void dma4(const void* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 4, 0, 0);
+}
+
+// chunk swizzle of a D-float row (D/4 16-byte chunks)
+template <int D>
+__device__ __forceinline__ int chunk_swz(int row) {
+  return ((((row >> 2) & 3) << 2)) & (D / 4 - 1);
+}
+
+// DMA 16 rows of a row-major [*, D] array into img[16][D] (swizzled chunks).
+// node_of(row) gives the source row (negative = none: row 0 is read and the
+// consumer zeroes it).
+template <int D, typename NodeOf>
+__device__ __forceinline__ void dma_rows(float* img, const float* __restrict__ base, int64_t ld, int lane,
+                                         NodeOf node_of) {
+  constexpr int CH = D / 4;     // chunks per row
+  constexpr int RPI = 64 / CH;  // rows per wave instruction
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t row = r0 + q * 4 + i;
-    int64_t node = -1;
-    if (row < n) node = rows != nullptr ? static_cast<int64_t>(rows[row]) : row;
-    if (node >= n_src) node = -1;
-    R.node[i] = static_cast<int32_t>(node);
-    const bool ok = node >= 0;
-#pragma unroll
-    for (int ib = 0; ib < DIN / 16; ++ib) {
-      R.x[ib][i] = ok ? X[node * ldx + ib * 16 + c] : 0.f;
-      R.s[ib][i] = ok ? S[node * lds + ib * 16 + c] : 0.f;
-    }
-#pragma unroll
-    for (int cb = 0; cb < DOUT / 16; ++cb) {
-      R.h[cb][i] = ok ? H[node * ldh + cb * 16 + c] : 0.f;
-      R.dh[cb][i] = row < n ? dH[row * lddh + cb * 16 + c] : 0.f;
-    }
-    R.nrm[i] = ok ? norm[node] : 1.f;
-    // the forward's lane (c, (node>>2)&3) of sub-tile node>>4 holds this row's bits
-    R.mw[i] = ok ? mask[(node >> 4) * 64 + ((node >> 2) & 3) * 16 + c] : 0ull;
+  for (int k = 0; k < 16 / RPI; ++k) {
+    const int row = k * RPI + lane / CH;
+    const int pos = lane % CH;
+    const int64_t node = node_of(row);
+    const int64_t src = (node >= 0 ? node : 0) * ld + ((pos ^ chunk_swz<D>(row)) << 2);
+    dma16(base + src, img + k * RPI * D);
   }
 }
 
-template <int DIN, int DOUT>
+// element (row, col) of a swizzled image
+template <int D>
+__device__ __forceinline__ float img_at(const float* img, int row, int col) {
+  return img[row * D + ((((col >> 2) ^ chunk_swz<D>(row))) << 2) + (col & 3)];
+}
+
+template <int DIN, int DOUT, bool FRONTIER, int EXP = 0>
 __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds, const float* __restrict__ H,
     int64_t ldh, const float* __restrict__ norm, const uint64_t* __restrict__ mask, const float* __restrict__ dH,
@@ -534,10 +571,16 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     w1s[j * F::WLDB + k] = W1[i];
     w2s[j * F::WLDB + k] = W2[i];
   }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: DMA bases live in SGPRs
   const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
-  float* tda = smem + 2 * DOUT * F::WLDB + wave * F::kWave;
+  float* img = smem + 2 * DOUT * F::WLDB + wave * F::kWave;
+  float* ix = img;
+  float* is = img + F::kX;
+  float* ih = img + 2 * F::kX;
+  float* ig = img + 2 * F::kX + F::kH;
+  float* inorm = img + F::kNorm;
+  const uint64_t* imask = reinterpret_cast<const uint64_t*>(img + F::kMask);
+  float* tda = img + F::kImg;
   float* tdb = tda + 16 * F::OLD;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
 
@@ -556,34 +599,94 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
   const int64_t nsub = (n + 15) / 16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
   int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + wave;
-  SavedRegs<DIN, DOUT> R;
-  if (st < nsub) load_saved<DIN, DOUT>(R, st * 16, n, rows, n_src, X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, q, c);
+
+  // issue the DMA of sub-tile t into this wave's image
+  auto issue = [&](int64_t t) {
+    const int64_t r0 = t * 16;
+    const int64_t lim = n - r0;  // rows of this sub-tile that exist
+    int32_t nd = -1;             // frontier mode: node of row (lane & 15)
+    if constexpr (FRONTIER) {
+      const int64_t r = r0 + (lane & 15);
+      nd = r < n ? rows[r] : -1;
+      if (nd >= n_src) nd = -1;
+    }
+    auto node_of = [&](int row) -> int64_t {
+      if constexpr (FRONTIER) return __shfl(nd, row);
+      return row < lim ? r0 + row : -1;
+    };
+    auto crow_of = [&](int row) -> int64_t { return row < lim ? r0 + row : -1; };
+    dma_rows<DIN>(ix, X, ldx, lane, node_of);
+    dma_rows<DIN>(is, S, lds, lane, node_of);
+    dma_rows<DOUT>(ih, H, ldh, lane, node_of);
+    dma_rows<DOUT>(ig, dH, lddh, lane, crow_of);
+    {
+      const int64_t nn = node_of(lane & 15);
+      dma4(norm + (nn >= 0 ? nn : 0), inorm);
+    }
+    // mask image [row][c] (u64): the forward's lane (c, (node>>2)&3) of sub-tile node>>4
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = k * 8 + (lane >> 3);
+      const int64_t nn = node_of(row);
+      const int64_t w = nn >= 0 ? (nn >> 4) * 64 + ((nn >> 2) & 3) * 16 + (lane & 7) * 2 : 0;
+      dma16(mask + w, const_cast<float*>(reinterpret_cast<const float*>(imask)) + k * 256);
+    }
+  };
+
+  __syncthreads();  // W staged
+  if (st < nsub) issue(st);
   for (; st < nsub; st += stride) {
     const int64_t r0 = st * 16;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sub-tile's DMA has landed
     float x[NIB][4], sv[NIB][4], da[NCB][4], db[NCB][4];
     {
       float h[NCB][4], dh[NCB][4], nrm[4];
       uint64_t mw[4];
       int32_t node[4];
+      bool okr[4], inr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        const int row = q * 4 + i;
+        const int64_t cr = r0 + row;
+        inr[i] = cr < n;
+        int64_t nn = cr;
+        if constexpr (FRONTIER) nn = inr[i] ? rows[cr] : -1;
+        okr[i] = inr[i] && nn >= 0 && nn < n_src;
+        node[i] = okr[i] ? static_cast<int32_t>(nn) : 0;
 #pragma unroll
         for (int ib = 0; ib < NIB; ++ib) {
-          x[ib][i] = R.x[ib][i];
-          sv[ib][i] = R.s[ib][i];
+          x[ib][i] = img_at<DIN>(ix, row, ib * 16 + c);
+          sv[ib][i] = img_at<DIN>(is, row, ib * 16 + c);
         }
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
-          h[cb][i] = R.h[cb][i];
-          dh[cb][i] = R.dh[cb][i];
+          h[cb][i] = img_at<DOUT>(ih, row, cb * 16 + c);
+          dh[cb][i] = img_at<DOUT>(ig, row, cb * 16 + c);
         }
-        nrm[i] = R.nrm[i];
-        mw[i] = R.mw[i];
-        node[i] = R.node[i];
+        nrm[i] = inorm[row];
+        mw[i] = imask[row * 16 + c];
       }
-      if (st + stride < nsub)
-        load_saved<DIN, DOUT>(R, (st + stride) * 16, n, rows, n_src, X, ldx, S, lds, H, ldh, norm, mask, dH, lddh,
-                              q, c);
+      const bool partial = FRONTIER || r0 + 16 > n;
+      if (partial) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int ib = 0; ib < NIB; ++ib) {
+            x[ib][i] = okr[i] ? x[ib][i] : 0.f;
+            sv[ib][i] = okr[i] ? sv[ib][i] : 0.f;
+          }
+#pragma unroll
+          for (int cb = 0; cb < NCB; ++cb) {
+            h[cb][i] = okr[i] ? h[cb][i] : 0.f;
+            dh[cb][i] = inr[i] ? dh[cb][i] : 0.f;
+          }
+          nrm[i] = okr[i] ? nrm[i] : 1.f;
+          mw[i] = okr[i] ? mw[i] : 0ull;
+        }
+      }
+      // the image is in registers: stream the next sub-tile into it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (st + stride < nsub) issue(st + stride);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float dot = 0.f;
@@ -612,6 +715,15 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
 
     // du = dA . W1, dm = dB . W2 over K = DOUT (k = q*KO + step)
     {
+      const bool full = r0 + 16 <= n;
+      float* pxd[4];
+      float* psd[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = r0 + q * 4 + i;
+        pxd[i] = dXd + row * lddxd + c;
+        psd[i] = dS + row * ldds + c;
+      }
       float dar[KO], dbr[KO];
       const float* pa = tda + c * F::OLD + q * KO;
       const float* pb = tdb + c * F::OLD + q * KO;
@@ -625,18 +737,22 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
 #pragma unroll
       for (int ib = 0; ib < NIB; ++ib) {
         floatx4 du = {0.f, 0.f, 0.f, 0.f}, dm = {0.f, 0.f, 0.f, 0.f};
+        if constexpr ((EXP & 2) == 0) {
 #pragma unroll
         for (int t = 0; t < KO; ++t) {
           const int k = q * KO + t;
           du = mfma16x4(dar[t], w1s[k * F::WLDB + ib * 16 + c], du);
           dm = mfma16x4(dbr[t], w2s[k * F::WLDB + ib * 16 + c], dm);
         }
+        } else {
+          du[0] += dar[ib] * w1s[ib * 16 + c];
+          dm[0] += dbr[ib] * w2s[ib * 16 + c];
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int64_t row = r0 + q * 4 + i;
-          if (row < n) {
-            dXd[row * lddxd + ib * 16 + c] = fmaf(dm[i], sv[ib][i], du[i]);
-            dS[row * ldds + ib * 16 + c] = fmaf(dm[i], x[ib][i], du[i]);
+          if (full || q * 4 + i < n - r0) {
+            pxd[i][ib * 16] = fmaf(dm[i], sv[ib][i], du[i]);
+            psd[i][ib * 16] = fmaf(dm[i], x[ib][i], du[i]);
           }
         }
       }
@@ -652,6 +768,7 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
         u[i] = x[ib][i] + sv[ib][i];
         m[i] = x[ib][i] * sv[ib][i];
       }
+      if constexpr ((EXP & 1) == 0) {
 #pragma unroll
       for (int ob = 0; ob < NCB; ++ob)
 #pragma unroll
@@ -659,6 +776,10 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
           dw1[ob][ib] = mfma16x4(da[ob][s4], u[s4], dw1[ob][ib]);
           dw2[ob][ib] = mfma16x4(db[ob][s4], m[s4], dw2[ob][ib]);
         }
+      } else {
+        dw1[0][ib][0] += da[ib % NCB][0] * u[0];
+        dw2[0][ib][0] += db[ib % NCB][0] * m[0];
+      }
     }
   }
 
@@ -768,7 +889,9 @@ static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
 }
 
 template <int DIN, int DOUT>
-static int saved_grid(int64_t n) { return blocks_for(n, 64, kCUs); }
+static int saved_grid(int64_t n) {
+  return blocks_for(n, 64, kCUs);
+}
 
 // Workspace floats: slabs of whichever backward variant the shape can take.
 template <int DIN, int DOUT>
@@ -776,10 +899,58 @@ static int64_t bwd_workspace(int64_t n) {
   const int64_t width = 2LL * DIN * DOUT + 2LL * DOUT;
   int64_t slabs = bwd_grid<DIN, DOUT>(n);
   if constexpr (SavedBwd<DIN, DOUT>::kOk) {
-    const int64_t s4 = 4LL * saved_grid<DIN, DOUT>(n);
-    if (s4 > slabs) slabs = s4;
+    const int64_t sl = 4LL * saved_grid<DIN, DOUT>(n);
+    if (sl > slabs) slabs = sl;
   }
   return slabs * width;
+}
+
+template <int DIN, int DOUT>
+static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H, int64_t ldh,
+                        const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
+                        const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, int64_t n, float p,
+                        const int32_t* rows, int64_t n_src, float* ws, int64_t ws_floats, int* nslab,
+                        hipStream_t st) {
+  using F = SavedBwd<DIN, DOUT>;
+  const int width = 2 * DOUT * DIN + 2 * DOUT;
+  const int grid = saved_grid<DIN, DOUT>(n);
+  *nslab = 4 * grid;
+  if (ws == nullptr || ws_floats < static_cast<int64_t>(*nslab) * width) return KGAT_ERR_WORKSPACE;
+  const size_t lds_bytes = F::kTotal * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (const void* fn : {reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false>),
+                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, true>),
+                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 1>),
+                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 2>),
+                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 3>)}) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    attr_set = true;
+  }
+  static int exp_mode = -1;
+  if (exp_mode < 0) {
+    const char* e = getenv("KGAT_BWD_EXP");  // timing experiments only (wrong results when set)
+    exp_mode = e ? atoi(e) : 0;
+  }
+  if (rows != nullptr)
+    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, true>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
+                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+  else if (exp_mode == 1)
+    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 1>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
+                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+  else if (exp_mode == 2)
+    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 2>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
+                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+  else if (exp_mode == 3)
+    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 3>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
+                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+  else
+    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
+                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 template <int DIN, int DOUT>
@@ -795,20 +966,9 @@ static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
   if constexpr (SavedBwd<DIN, DOUT>::kOk) {
     if (H != nullptr && norm != nullptr && mask != nullptr) {
       saved = true;
-      const int grid = saved_grid<DIN, DOUT>(n);
-      nslab = 4 * grid;
-      if (ws == nullptr || ws_floats < static_cast<int64_t>(nslab) * width) return KGAT_ERR_WORKSPACE;
-      const size_t lds_bytes = SavedBwd<DIN, DOUT>::kTotal * sizeof(float);
-      static bool attr_set = false;
-      if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
-        if (e != hipSuccess) return static_cast<int>(e);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S, lds,
-                         H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
-      KGAT_LAUNCH_CHECK();
+      if (int e = launch_saved<DIN, DOUT>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds,
+                                          n, p, rows, n_src, ws, ws_floats, &nslab, st))
+        return e;
     }
   }
   if (!saved) {

@@ -40,6 +40,12 @@ __device__ __forceinline__ uint32_t mix_hash(uint64_t seed, uint64_t idx) {
   z ^= z >> 31;
   return static_cast<uint32_t>(z >> 32);
 }
+__device__ __forceinline__ uint64_t mix_hash64(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, float p) {
   return static_cast<float>(mix_hash(seed, idx) >> 8) * (1.0f / 16777216.0f) >= p;
 }

@@ -100,7 +100,7 @@ def main():
             4 * n * (2 * din + dout) + 36 * n)
         rec(f"biinter_bwd_saved_{din}x{dout}",
             timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5, H=H, state=st), args.reps),
-            4 * n * (2 * din + 2 * dout + 2 * din) + 36 * n)
+            4 * n * (2 * din + 2 * dout + 2 * din) + 36 * n, split=os.environ.get("KGAT_BWD_SPLIT", "auto"))
     p = torch.randn(n * 64, device=dev)
     gg = torch.randn_like(p)
     m = torch.zeros_like(p)
