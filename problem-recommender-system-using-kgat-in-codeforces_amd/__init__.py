@@ -6,8 +6,9 @@ module API.  Import with ``importlib.import_module(
 name is not a Python identifier).
 """
 from .graph import DeviceGraph, GraphLayout, build_layout, synthetic_ckg  # noqa: F401
+from . import evaluation  # noqa: F401
 from .model import KGAT, KGATArgs, KGATMode  # noqa: F401
 from .nfm import NFM, NFMArgs, NFMMode  # noqa: F401
 
-__all__ = ["KGAT", "KGATArgs", "KGATMode", "NFM", "NFMArgs", "NFMMode", "DeviceGraph", "GraphLayout", "build_layout",
+__all__ = ["evaluation", "KGAT", "KGATArgs", "KGATMode", "NFM", "NFMArgs", "NFMMode", "DeviceGraph", "GraphLayout", "build_layout",
            "synthetic_ckg"]

@@ -286,6 +286,11 @@ class KGAT(nn.Module):
                 tables.append(x)
         return tables
 
+    def propagate(self) -> list[torch.Tensor]:
+        """The propagated tables [X0, H1, ..., HL] (no autograd state): PREDICT's first half,
+        computed once per evaluation by evaluation.evaluate / recommend_topk."""
+        return self._propagate()
+
     def _build_cf_embeddings(self) -> torch.Tensor:
         return torch.cat(self._propagate(), dim=1)
 

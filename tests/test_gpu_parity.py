@@ -561,3 +561,92 @@ def test_nfm_train_mode_dropout_runs(pkg):
     loss.backward()
     assert torch.isfinite(loss).item()
     assert all(torch.isfinite(p.grad).all().item() for p in m.parameters())
+
+
+def _dicts_from_golden(g):
+    train, test = {}, {}
+    for u, i in g["train_flat"]:
+        train.setdefault(int(u), []).append(int(i))
+    for u, i in g["test_flat"]:
+        test.setdefault(int(u), []).append(int(i))
+    for u in g["eval_users"]:
+        train.setdefault(int(u), [])
+    return train, test
+
+
+def _assert_metrics(got, g, scores_ref, train):
+    """Metrics equal the reference's except on rows whose own top-k boundary is a fp32 near-tie."""
+    users = g["eval_users"]
+    for k in (20, 40):
+        for m in ("precision", "recall", "ndcg"):
+            a, b = got[k][m], g[f"metrics/{k}/{m}"]
+            bad = ~np.isclose(a, b, rtol=1e-5, atol=1e-7, equal_nan=True)
+            for r in np.nonzero(bad)[0]:
+                row = scores_ref[r].copy()
+                row[train[int(users[r])]] = -np.inf
+                vals = np.sort(row)[::-1][:k + 1]
+                assert np.min(np.abs(np.diff(vals))) < 1e-5, (k, m, r, a[r], b[r])
+
+
+@pytest.mark.parametrize("case", KGAT_CASES)
+def test_rank_metrics_on_reference_scores(pkg, case):
+    """The reference's own score matrix through kgat_mask_rows/topk/rank_metrics == its metrics_at_k."""
+    ev = pkg.evaluation
+    g = golden("kgat_" + case)
+    train, test = _dicts_from_golden(g)
+    sc = torch.from_numpy(g["scores"].copy()).to(DEV)
+    got = ev.metrics_at_k(sc, train, test, g["eval_users"], np.arange(int(g["item_num"])), [20, 40])
+    _assert_metrics(got, g, g["scores"], train)
+    # in-place masking, as the reference does
+    for u, i in g["train_flat"][:50]:
+        r = np.nonzero(g["eval_users"] == u)[0]
+        if r.size:
+            assert sc[r[0], i].item() == float("-inf")
+
+
+@pytest.mark.parametrize("case", KGAT_CASES)
+def test_evaluate_vs_reference(pkg, case):
+    """main.py:70-130 driven through evaluation.evaluate (one propagation) == the reference's means."""
+    ev = pkg.evaluation
+    g = golden("kgat_" + case)
+    m = _refreshed_model(pkg, g)
+    train, test = _dicts_from_golden(g)
+    test = {int(u): test[int(u)] for u in g["eval_users"]}  # the reference iterates eval users in this order
+    scores, res = ev.evaluate(m, train, test, int(g["item_num"]), k_list=[20, 40], batch_size=64)
+    np.testing.assert_allclose(scores.numpy(), g["scores"], rtol=RTOL, atol=1e-5)
+    for k in (20, 40):
+        for name in ("precision", "recall", "ndcg"):
+            ref = float(np.mean(g[f"metrics/{k}/{name}"]))
+            assert abs(res[k][name] - ref) <= 2e-3 * max(1.0, abs(ref)), (k, name, res[k][name], ref)
+
+
+@pytest.mark.parametrize("rows,cols,k", [(3, 1, 1), (64, 1000, 20), (17, 5000, 100), (8, 100_000, 1024),
+                                         (33, 777, 777)])
+def test_topk_kernel_ties_and_inf(pkg, rows, cols, k):
+    ev = pkg.evaluation
+    rng = np.random.default_rng(rows * 7 + k)
+    x = rng.integers(-50, 50, size=(rows, cols)).astype(np.float32) / 8  # many exact ties
+    x[rng.random((rows, cols)) < 0.05] = -np.inf
+    x[rng.random((rows, cols)) < 0.01] = np.inf
+    idx, val = ev.topk(torch.from_numpy(x).to(DEV), k, values=True)
+    for r in range(rows):
+        order = np.lexsort((np.arange(cols), -x[r].astype(np.float64)))[:k]
+        np.testing.assert_array_equal(idx[r].cpu().numpy(), order)
+        np.testing.assert_array_equal(val[r].cpu().numpy(), x[r][order])
+
+
+def test_recommend_topk_matches_masked_torch_topk(pkg):
+    ev = pkg.evaluation
+    g = golden("kgat_L2_d64")
+    m = _refreshed_model(pkg, g)
+    train, _ = _dicts_from_golden(g)
+    users = list(range(int(g["user_num"])))
+    I = int(g["item_num"])
+    top = ev.recommend_topk(m, users, I, train, k=20, batch_size=32)
+    with torch.no_grad():
+        sc = m(torch.tensor(users, device=DEV), torch.arange(I, device=DEV), mode=pkg.KGATMode.PREDICT).cpu()
+    for u in users:
+        sc[u, train.get(u, [])] = -np.inf
+    ref = torch.topk(sc, 20, dim=1)
+    got_vals = torch.gather(sc, 1, top)
+    np.testing.assert_array_equal(got_vals.numpy(), ref.values.numpy())  # same scores at every rank

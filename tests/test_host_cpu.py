@@ -141,3 +141,11 @@ def test_nfm_init_matches_reference_rng():
     assert set(sd) == {k[5:] for k in g if k.startswith("init/")}
     for k, v in sd.items():
         np.testing.assert_array_equal(v.numpy(), g["init/" + k], err_msg=k)
+
+
+def test_eval_csr_helper_sorts_and_dedups():
+    ev = pkg.evaluation
+    ptr, idx = ev._csr([[5, 1, 5, 3], [], [2]], "cpu", unique=True)
+    assert ptr.tolist() == [0, 3, 3, 4] and idx.tolist() == [1, 3, 5, 2] and idx.dtype == torch.int32
+    ptr, idx = ev._csr([[], []], "cpu")
+    assert ptr.tolist() == [0, 0, 0] and idx.numel() == 1
