@@ -79,6 +79,9 @@ _SIGNATURES = {
                                             c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_slot_sum_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_row_softmax_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_gather_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "kgat_scatter_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
+    "kgat_add_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),
     "kgat_mask_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_f32, c_vp]),
     "kgat_topk_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "kgat_rank_metrics_f32": (ctypes.c_int, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),

@@ -159,6 +159,8 @@ __global__ __launch_bounds__(256) void bpr_bwd_kernel(kgat_tables T, int t, cons
     dup = __any(hit);
   }
   if (dup) return;
+  const int64_t drow = row_map ? static_cast<int64_t>(row_map[id]) : id;
+  if (drow < 0) return;  // row_map -1: a row this caller does not own (row-sharded mode); wave-uniform
   const float scale = grad_out[0] / static_cast<float>(batch);
   const float* tab = T.ptr[t];
   const int64_t ld = T.ld[t];
@@ -189,7 +191,6 @@ __global__ __launch_bounds__(256) void bpr_bwd_kernel(kgat_tables T, int t, cons
       }
     }
   }
-  const int64_t drow = row_map ? static_cast<int64_t>(row_map[id]) : id;
 #pragma unroll
   for (int cc = 0; cc < kCols; ++cc) {
     const int j = lane + 64 * cc;

@@ -81,6 +81,84 @@ extern "C" int kgat_adam_f32(float* p, const float* g, float* m, float* v, int64
   return KGAT_OK;
 }
 
+namespace kgat {
+
+// Row movers for the row-sharded mode: one 16-lane group per row, float4 per lane.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ src, int64_t lds,
+                                                          const int32_t* __restrict__ rows, int64_t n, int d,
+                                                          float* __restrict__ dst, int64_t ldd) {
+  const int64_t g = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (g >= n) return;
+  const int32_t r = rows[g];
+  for (int c = lane * 4; c < d; c += 64) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= 0) v = *reinterpret_cast<const float4*>(src + r * lds + c);
+    *reinterpret_cast<float4*>(dst + g * ldd + c) = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_rows_kernel(float* __restrict__ dst, int64_t ldd,
+                                                           const int32_t* __restrict__ rows, int64_t n, int d,
+                                                           const float* __restrict__ src, int64_t lds,
+                                                           int accumulate) {
+  const int64_t g = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (g >= n) return;
+  const int32_t r = rows[g];
+  if (r < 0) return;
+  for (int c = lane * 4; c < d; c += 64) {
+    float4 v = *reinterpret_cast<const float4*>(src + g * lds + c);
+    float4* o = reinterpret_cast<float4*>(dst + r * ldd + c);
+    if (accumulate) {
+      const float4 w = *o;
+      v = make_float4(w.x + v.x, w.y + v.y, w.z + v.z, w.w + v.w);
+    }
+    *o = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void add_kernel(float* __restrict__ y, const float* __restrict__ x, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) y[i] += x[i];
+}
+
+}  // namespace kgat
+
+static bool rows_args_ok(const void* a, int64_t lda, const void* b, int64_t ldb, int d) {
+  return a && b && d > 0 && (d & 3) == 0 && lda >= d && ldb >= d && (lda & 3) == 0 && (ldb & 3) == 0 &&
+         (reinterpret_cast<uintptr_t>(a) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0;
+}
+
+extern "C" int kgat_gather_rows_f32(const float* src, int64_t lds, const int32_t* rows, int64_t n, int32_t d,
+                                    float* dst, int64_t ldd, void* stream) {
+  if (!rows || n < 0 || !rows_args_ok(src, lds, dst, ldd, d)) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::gather_rows_kernel, dim3(kgat::blocks_for(n, 16, 1 << 30)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), src, lds, rows, n, d, dst, ldd);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_scatter_rows_f32(float* dst, int64_t ldd, const int32_t* rows, int64_t n, int32_t d,
+                                     const float* src, int64_t lds, int32_t accumulate, void* stream) {
+  if (!rows || n < 0 || !rows_args_ok(dst, ldd, src, lds, d)) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::scatter_rows_kernel, dim3(kgat::blocks_for(n, 16, 1 << 30)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dst, ldd, rows, n, d, src, lds, accumulate);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_add_f32(float* y, const float* x, int64_t n, void* stream) {
+  if (!y || !x || n < 0) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::add_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 8)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), y, x, n);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
 extern "C" int kgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst, void* stream) {
   if (!src || !idx || !dst || n < 0) return KGAT_ERR_INVALID;
   if (n == 0) return KGAT_OK;

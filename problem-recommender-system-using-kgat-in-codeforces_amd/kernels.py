@@ -67,6 +67,73 @@ def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, t
     return out
 
 
+def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    """Y (+)= B . X for a rectangular device CSR block B [out rows x X rows] (graph._DeviceCSR)."""
+    _req(X, "X", dim=2)
+    _req(out, "out", dim=2)
+    d = X.shape[1]
+    if out.shape[0] != csr.n_rows or out.shape[1] != d:
+        raise ValueError("out shape mismatch")
+    if csr.n_rows == 0:
+        return out
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=X.device)
+    _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
+              int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    return out
+
+
+def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row)."""
+    _req(src_map, "src_map", dtype=torch.int32, dim=1)
+    _req(Xc, "Xc", dim=2)
+    _req(out, "out", dim=2)
+    d = Xc.shape[1]
+    if out.shape[0] != csr.n_rows or out.shape[1] != d:
+        raise ValueError("out shape mismatch")
+    if csr.n_rows == 0:
+        return out
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    _lib.call("kgat_spmm_csr_masked_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc), None, 0,
+              out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    return out
+
+
+def gather_rows(src: torch.Tensor, rows: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = src[rows[i]] (rows int32, -1 => zeros)."""
+    _req(src, "src", dim=2)
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    n, d = rows.numel(), src.shape[1]
+    if out is None:
+        out = torch.empty(n, d, dtype=torch.float32, device=src.device)
+    _req(out, "out", dim=2)
+    _lib.call("kgat_gather_rows_f32", src.data_ptr(), _ld(src), rows.data_ptr(), n, d, out.data_ptr(), _ld(out),
+              stream_ptr(src.device))
+    return out
+
+
+def scatter_rows(dst: torch.Tensor, rows: torch.Tensor, src: torch.Tensor, accumulate: bool = True) -> None:
+    """dst[rows[i]] (+)= src[i] (rows int32 distinct, -1 skipped)."""
+    _req(dst, "dst", dim=2)
+    _req(src, "src", dim=2)
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    if src.shape[0] != rows.numel() or src.shape[1] != dst.shape[1]:
+        raise ValueError("scatter_rows shape mismatch")
+    _lib.call("kgat_scatter_rows_f32", dst.data_ptr(), _ld(dst), rows.data_ptr(), rows.numel(), dst.shape[1],
+              src.data_ptr(), _ld(src), int(accumulate), stream_ptr(dst.device))
+
+
+def add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """y += x (same shape, contiguous)."""
+    _req(y, "y")
+    _req(x, "x")
+    if y.shape != x.shape or not (y.is_contiguous() and x.is_contiguous()):
+        raise ValueError("add_: contiguous tensors of one shape")
+    _lib.call("kgat_add_f32", y.data_ptr(), x.data_ptr(), y.numel(), stream_ptr(y.device))
+    return y
+
+
 def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None = None,
                 transpose: bool = False) -> torch.Tensor:
     """Dense Y = A . X where X is zero outside a frontier: X[node] = Xc[src_map[node]] (src_map -1 => 0),

@@ -1,0 +1,122 @@
+"""One rank of the row-sharded parity check (launched by tests/test_gpu_sharded.py through
+``python -m torch.distributed.run --nproc-per-node 2``; every rank on cuda:0, gloo, host-staged).
+
+Every rank also runs the single-GPU KGAT on the GLOBAL batch (all ranks' pairs, rank order)
+and checks that the sharded model's loss, its shard of every gradient, the replicated
+gradients, the parameters after one Adam step of each optimiser and PREDICT scores agree.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tests.conftest import load_pkg  # noqa: E402
+
+# Gradients agree to fp32 summation order.  After an Adam step they are compared at 1e-4: the ring
+# sums A^T.dS in another order than one GPU, and Adam's eps turns that rounding on ~1e-9 gradients
+# into differences up to ~1e-5 of a step (a wrong update is ~lr = 1e-3 off).
+ATOL_GRAD, ATOL_PARAM = 1e-6, 1e-4
+FAILURES: list[str] = []
+
+
+def close(name, a, b, atol, rtol=1e-4):
+    """Record (never raise): every rank must reach every collective whatever the numbers say."""
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    if a.shape != b.shape or not torch.allclose(a, b, atol=atol, rtol=rtol):
+        diff = (a - b).abs().max().item() if a.shape == b.shape else float("nan")
+        FAILURES.append(f"{name}: shape {tuple(a.shape)} vs {tuple(b.shape)}, max |diff| {diff:.3e}")
+
+
+def main() -> None:
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    pkg = load_pkg()
+    graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+    sh = __import__(pkg.__name__ + ".sharded", fromlist=["sharded"])
+    U, E, inter, trip = graph.synthetic_ckg(30000, 240000, seed=5)
+    lay = graph.build_layout(U, E, inter, trip)
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                        message_dropout=[0.0, 0.0])
+    torch.manual_seed(11)
+    ref = pkg.KGAT(args)
+    ref.attach_graph(lay, "cuda")
+    comm = sh.Comm()
+    m = sh.RowShardedKGAT(args, lay, comm, "cuda")
+    m.load_full_state(ref.state_dict())
+    lo, hi = m.lo, m.hi
+    assert hi - lo > 0
+
+    # ---- CF step: each rank its own 64 pairs; the reference sees all of them
+    rng = np.random.default_rng(100)
+    n_items = int(inter[:, 1].max()) + 1
+    glob = [(rng.integers(0, U, 64), rng.integers(0, n_items, 64), rng.integers(0, n_items, 64))
+            for _ in range(world)]
+    mine = [torch.from_numpy(a).cuda() for a in glob[rank]]
+    allb = [torch.from_numpy(np.concatenate([g[i] for g in glob])).cuda() for i in range(3)]
+    ref.build_optimizer(1e-3, 1e-4)
+    m.build_optimizer(1e-3, 1e-4)
+    ref.train()
+    m.train()
+    lr = ref(*allb, mode=pkg.KGATMode.TRAIN_CF)
+    lr.backward()
+    ls = m(*mine, mode=pkg.KGATMode.TRAIN_CF)
+    ls.backward()
+    close("cf loss", ls, lr, 1e-6)
+    close("cf d table shard", m._user_entity_embedding_shard.grad, ref._user_entity_embedding.weight.grad[lo:hi],
+          ATOL_GRAD)
+    for a, b in zip(m._cf_weights(), ref._cf_weights()):
+        close("cf d aggregator", a.grad, b.grad, 1e-5)
+    ref.update_cf_weights()
+    m.update_cf_weights()
+    close("table after cf adam", m._user_entity_embedding_shard, ref._user_entity_embedding.weight[lo:hi],
+          ATOL_PARAM)
+    for a, b in zip(m._cf_weights(), ref._cf_weights()):
+        close("aggregator after cf adam", a, b, ATOL_PARAM)
+
+    # ---- KG step (from identical parameters again)
+    m.load_full_state(ref.state_dict())
+    heads_all = [rng.integers(0, U + E, 32) for _ in range(world)]
+    rels_all = [rng.integers(0, len(lay.rel_order), 32) for _ in range(world)]
+    pos_all = [rng.integers(0, U + E, 32) for _ in range(world)]
+    neg_all = [rng.integers(0, U + E, 32) for _ in range(world)]
+    kg_mine = [torch.from_numpy(x[rank]).cuda() for x in (heads_all, rels_all, pos_all, neg_all)]
+    kg_all = [torch.from_numpy(np.concatenate(x)).cuda() for x in (heads_all, rels_all, pos_all, neg_all)]
+    lr = ref(*kg_all, mode=pkg.KGATMode.TRAIN_KG)
+    lr.backward()
+    ls = m(*kg_mine, mode=pkg.KGATMode.TRAIN_KG)
+    ls.backward()
+    close("kg loss", ls, lr, 1e-6)
+    close("kg d table shard", m._user_entity_embedding_shard.grad, ref._user_entity_embedding.weight.grad[lo:hi],
+          ATOL_GRAD)
+    close("kg d relation", m._relation_embedding.weight.grad, ref._relation_embedding.weight.grad, ATOL_GRAD)
+    close("kg d trans", m._trans_matrix.grad, ref._trans_matrix.grad, ATOL_GRAD)
+    ref.update_kg_weights()
+    m.update_kg_weights()
+    close("table after kg adam", m._user_entity_embedding_shard, ref._user_entity_embedding.weight[lo:hi],
+          ATOL_PARAM)
+
+    # ---- PREDICT
+    m.load_full_state(ref.state_dict())
+    ref.eval()
+    m.eval()
+    users = torch.arange(0, 50, device="cuda")
+    items = torch.arange(0, 300, device="cuda")
+    with torch.no_grad():
+        close("scores", m(users, items, mode=pkg.KGATMode.PREDICT), ref(users, items, mode=pkg.KGATMode.PREDICT),
+              1e-5)
+    dist.barrier()
+    if FAILURES:
+        print(f"rank {rank}: " + "; ".join(FAILURES), flush=True)
+    else:
+        print(f"sharded parity ok: rank {rank}/{world} rows [{lo}, {hi})", flush=True)
+    dist.destroy_process_group()
+    sys.exit(1 if FAILURES else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -650,3 +650,24 @@ def test_recommend_topk_matches_masked_torch_topk(pkg):
     ref = torch.topk(sc, 20, dim=1)
     got_vals = torch.gather(sc, 1, top)
     np.testing.assert_array_equal(got_vals.numpy(), ref.values.numpy())  # same scores at every rank
+
+
+def test_bpr_bwd_row_map_skips_unowned_rows(pkg):
+    """row_map -1 (a row another shard owns) is skipped; mapped rows get the dense gradient."""
+    _, kernels = _mods(pkg)
+    torch.manual_seed(4)
+    n, d, B = 300, 32, 64
+    tab = torch.randn(n, d, device=DEV)
+    users = torch.randint(0, n, (B,), device=DEV)
+    pos = torch.randint(0, n, (B,), device=DEV)
+    neg = torch.randint(0, n, (B,), device=DEV)
+    loss, coef = kernels.bpr_fwd([tab], users, pos, neg, 1e-5)
+    gout = torch.ones(1, device=DEV)
+    dense = torch.zeros(n, d, device=DEV)
+    kernels.bpr_bwd([tab], 0, users, pos, neg, 1e-5, coef, gout, dense)
+    owned = torch.arange(n, device=DEV) % 3 == 0
+    row_map = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    row_map[owned] = torch.arange(int(owned.sum()), dtype=torch.int32, device=DEV)
+    comp = torch.zeros(int(owned.sum()), d, device=DEV)
+    kernels.bpr_bwd([tab], 0, users, pos, neg, 1e-5, coef, gout, comp, row_map=row_map)
+    torch.testing.assert_close(comp, dense[owned], rtol=0, atol=0)

@@ -1,0 +1,100 @@
+"""Row-sharded mode (sharded.py) on the GPU: world 1 in-process against KGAT, and world 2
+(two ranks on the one test GPU, gloo host-staged) through tests/sharded_worker.py."""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from tests.conftest import ROOT, load_pkg
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_pkg()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_sharded_world1_matches_kgat(pkg):
+    graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+    sh = __import__(pkg.__name__ + ".sharded", fromlist=["sharded"])
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    U, E, inter, trip = graph.synthetic_ckg(8000, 60000, seed=9)
+    lay = graph.build_layout(U, E, inter, trip)
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32, 16],
+                        message_dropout=[0.0, 0.0, 0.0])
+    torch.manual_seed(3)
+    ref = pkg.KGAT(args)
+    ref.attach_graph(lay, DEV)
+    m = sh.RowShardedKGAT(args, lay, sh.Comm(), DEV)
+    m.load_full_state(ref.state_dict())
+    rng = np.random.default_rng(1)
+    n_items = int(inter[:, 1].max()) + 1
+    b = [torch.from_numpy(x).to(DEV) for x in (rng.integers(0, U, 128), rng.integers(0, n_items, 128),
+                                                  rng.integers(0, n_items, 128))]
+    lr = ref(*b, mode=pkg.KGATMode.TRAIN_CF)
+    lr.backward()
+    ls = m(*b, mode=pkg.KGATMode.TRAIN_CF)
+    ls.backward()
+    assert abs(ls.item() - lr.item()) < 1e-6
+    np.testing.assert_allclose(m._user_entity_embedding_shard.grad.cpu().numpy(),
+                               ref._user_entity_embedding.weight.grad.cpu().numpy(), atol=1e-6, rtol=1e-4)
+    for a, w in zip(m._cf_weights(), ref._cf_weights()):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), w.grad.cpu().numpy(), atol=1e-5, rtol=1e-4)
+    ref.build_optimizer(1e-3, 1e-4)
+    m.build_optimizer(1e-3, 1e-4)
+    ref.update_cf_weights()
+    m.update_cf_weights()
+    np.testing.assert_allclose(m._user_entity_embedding_shard.detach().cpu().numpy(),
+                               ref._user_entity_embedding.weight.detach().cpu().numpy(), atol=2e-5)
+    # KG step on the same batch
+    kg = [torch.from_numpy(x).to(DEV) for x in (rng.integers(0, U + E, 64), rng.integers(0, len(lay.rel_order), 64),
+                                                   rng.integers(0, U + E, 64), rng.integers(0, U + E, 64))]
+    lr = ref(*kg, mode=pkg.KGATMode.TRAIN_KG)
+    lr.backward()
+    ls = m(*kg, mode=pkg.KGATMode.TRAIN_KG)
+    ls.backward()
+    assert abs(ls.item() - lr.item()) < 1e-6
+    np.testing.assert_allclose(m._user_entity_embedding_shard.grad.cpu().numpy(),
+                               ref._user_entity_embedding.weight.grad.cpu().numpy(), atol=1e-6, rtol=1e-4)
+    np.testing.assert_allclose(m._trans_matrix.grad.cpu().numpy(), ref._trans_matrix.grad.cpu().numpy(), atol=1e-6,
+                               rtol=1e-4)
+    ref.eval()
+    m.eval()
+    tabs_s, tabs_r = m.propagate(), ref.propagate()
+    for a, w in zip(tabs_s, tabs_r):
+        np.testing.assert_allclose(a.cpu().numpy(), w.cpu().numpy(), atol=1e-5, rtol=1e-4)
+    users, items = torch.arange(40, device=DEV), torch.arange(200, device=DEV)
+    with torch.no_grad():
+        np.testing.assert_allclose(m(users, items, mode=pkg.KGATMode.PREDICT).cpu().numpy(),
+                                   ref(users, items, mode=pkg.KGATMode.PREDICT).cpu().numpy(), atol=1e-5, rtol=1e-4)
+
+
+def test_sharded_world2_two_ranks_one_gpu():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "sharded_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / "sharded_world2.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert p.stdout.count("sharded parity ok") == 2, p.stdout[-2000:]

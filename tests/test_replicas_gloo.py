@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 import os
-import socket
+import tempfile
 
 import torch
 import torch.distributed as dist
@@ -11,16 +11,16 @@ import torch.multiprocessing as mp
 from tests.conftest import load_pkg
 
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _rendezvous() -> str:
+    """A file rendezvous: no TCP port to race for between concurrently started tests."""
+    fd, path = tempfile.mkstemp(prefix="kgat_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return "file://" + path
 
 
 def _worker(rank: int, world: int, port: int, q) -> None:
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         pkg = load_pkg()
         rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
@@ -45,7 +45,7 @@ def _worker(rank: int, world: int, port: int, q) -> None:
 def test_allreduce_and_broadcast_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
