@@ -1,0 +1,260 @@
+// a2 for the wide layers of C4/C5 (d_in or d_out of 256): the bi-interaction as
+// two library GEMMs plus fused HIP epilogues (src/model/KGAT/aggregator.py:57-65).
+//
+// At these widths the layer is MFMA-bound (4*d_in*d_out flop per row against
+// 4*(2*d_in + d_out) bytes) and a whole row of both products no longer fits a
+// wave's registers, so the contractions go to rocBLAS sgemm (fp32, MFMA, atomics
+// off => deterministic) and everything around them is ours:
+//   forward:  U = X+S, M = X*S                                   (um_kernel)
+//             P1 = U W1^T, P2 = M W2^T                           (rocBLAS)
+//             H = normalize(dropout(LReLU(P1+b1) + LReLU(P2+b2))) (epi_fwd_kernel,
+//             keeps P+b and the row norm as the backward's state)
+//   backward: dA, dB from H, dH, the norm, the signs of P+b       (epi_bwd_kernel)
+//             du = dA W1, dm = dB W2                             (rocBLAS, into dXd / dS)
+//             dXd = du + dm*S, dS = du + dm*X                    (dxs_kernel, in place)
+//             dW1 = dA^T U, dW2 = dB^T M, db = column sums        (rocBLAS gemm / gemv)
+// Dropout draws are the fused kernels' (one 64-bit hash per node, 16-column
+// group of 4 blocks), so both paths drop the same elements.
+#include <rocblas/rocblas.h>
+
+#include "common.hpp"
+
+namespace kgat {
+
+__device__ __forceinline__ bool gemm_keep(uint64_t seed, int64_t node, int col, int dout, uint32_t thr) {
+  const int groups = (dout / 16 + 3) / 4;
+  const int cb = col >> 4;
+  const uint64_t h = mix_hash64(seed, (static_cast<uint64_t>(node) * groups + (cb >> 2)) * 16 + (col & 15));
+  return static_cast<uint32_t>((h >> (16 * (cb & 3))) & 0xFFFFu) >= thr;
+}
+
+__device__ __forceinline__ uint32_t gemm_threshold(float p) {
+  const float t = p * 65536.f + 0.5f;
+  return t >= 65536.f ? 65536u : static_cast<uint32_t>(t);
+}
+
+__global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
+                                                 int64_t lds, float* __restrict__ U, float* __restrict__ M, int64_t n,
+                                                 int d) {
+  const int64_t total = n * (d / 4);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / (d / 4);
+    const int c = static_cast<int>(i % (d / 4)) * 4;
+    const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + c);
+    const float4 s = *reinterpret_cast<const float4*>(S + r * lds + c);
+    *reinterpret_cast<float4*>(U + r * d + c) = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
+    *reinterpret_cast<float4*>(M + r * d + c) = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
+  }
+}
+
+// one wave per row; P1/P2 [n, dout] in, P+b written back (the backward's sign source)
+__global__ __launch_bounds__(256) void epi_fwd_kernel(float* __restrict__ P1, float* __restrict__ P2,
+                                                      const float* __restrict__ b1, const float* __restrict__ b2,
+                                                      float* __restrict__ H, int64_t ldh, float* __restrict__ norm,
+                                                      int64_t n, int dout, float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = gemm_threshold(p);
+  float v[16];
+  float sq = 0.f;
+  int cnt = 0;
+  for (int c = lane; c < dout; c += 64, ++cnt) {
+    const float pa = P1[r * dout + c] + b1[c], pb = P2[r * dout + c] + b2[c];
+    P1[r * dout + c] = pa;
+    P2[r * dout + c] = pb;
+    float g = lrelu(pa) + lrelu(pb);
+    if (p > 0.f) g = gemm_keep(seed, r, c, dout, thr) ? g * scale : 0.f;
+    v[cnt] = g;
+    sq = fmaf(g, g, sq);
+  }
+  const float nrm = sqrtf(wave_sum(sq));
+  const float inv = 1.f / fmaxf(nrm, kNormEps);
+  cnt = 0;
+  for (int c = lane; c < dout; c += 64, ++cnt) H[r * ldh + c] = v[cnt] * inv;
+  if (lane == 0) norm[r] = nrm >= kNormEps ? nrm : -kNormEps;
+}
+
+// one wave per row: dA, dB written over the P+b state
+__global__ __launch_bounds__(256) void epi_bwd_kernel(float* __restrict__ P1, float* __restrict__ P2,
+                                                      const float* __restrict__ H, int64_t ldh,
+                                                      const float* __restrict__ norm, const float* __restrict__ dH,
+                                                      int64_t lddh, int64_t n, int dout, float p, uint64_t seed,
+                                                      const int32_t* __restrict__ key_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = gemm_threshold(p);
+  const int64_t key = key_rows ? static_cast<int64_t>(key_rows[r]) : r;
+  float dot = 0.f;
+  for (int c = lane; c < dout; c += 64) dot = fmaf(H[r * ldh + c], dH[r * lddh + c], dot);
+  dot = wave_sum(dot);
+  const float nr = norm[r];
+  const bool clamped = nr < 0.f;
+  const float inv = clamped ? 1.f / kNormEps : 1.f / nr;
+  const float proj = clamped ? 0.f : dot;
+  for (int c = lane; c < dout; c += 64) {
+    float dg = (dH[r * lddh + c] - H[r * ldh + c] * proj) * inv;
+    if (p > 0.f) dg = (key >= 0 && gemm_keep(seed, key, c, dout, thr)) ? dg * scale : 0.f;
+    if (key < 0) dg = 0.f;
+    const float pa = P1[r * dout + c], pb = P2[r * dout + c];
+    P1[r * dout + c] = pa > 0.f ? dg : dg * kLeakySlope;
+    P2[r * dout + c] = pb > 0.f ? dg : dg * kLeakySlope;
+  }
+}
+
+// in place: (du, dm) in (dXd, dS) -> dXd = du + dm*S, dS = du + dm*X
+__global__ __launch_bounds__(256) void dxs_kernel(float* __restrict__ dXd, int64_t lda, float* __restrict__ dS,
+                                                  int64_t ldb, const float* __restrict__ X, int64_t ldx,
+                                                  const float* __restrict__ S, int64_t lds, int64_t n, int d) {
+  const int64_t total = n * d;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / d;
+    const int c = static_cast<int>(i % d);
+    const float du = dXd[r * lda + c], dm = dS[r * ldb + c];
+    dXd[r * lda + c] = fmaf(dm, S[r * lds + c], du);
+    dS[r * ldb + c] = fmaf(dm, X[r * ldx + c], du);
+  }
+}
+
+__global__ void ones_kernel(float* __restrict__ o, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) o[i] = 1.f;
+}
+
+static rocblas_handle blas_handle(hipStream_t st, int* err) {
+  static rocblas_handle h[16] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
+    *err = KGAT_ERR_INVALID;
+    return nullptr;
+  }
+  if (h[dev] == nullptr) {
+    if (rocblas_create_handle(&h[dev]) != rocblas_status_success) {
+      *err = KGAT_ERR_INVALID;
+      return nullptr;
+    }
+    rocblas_set_atomics_mode(h[dev], rocblas_atomics_not_allowed);  // deterministic reductions
+  }
+  rocblas_set_stream(h[dev], st);
+  *err = 0;
+  return h[dev];
+}
+
+#define KGAT_BLAS(call)                                  \
+  do {                                                   \
+    if ((call) != rocblas_status_success) return KGAT_ERR_INVALID; \
+  } while (0)
+
+}  // namespace kgat
+
+static bool gemm_dims_ok(int32_t din, int32_t dout) {
+  return din >= 16 && dout >= 16 && din % 16 == 0 && dout % 16 == 0 && din <= 1024 && dout <= 1024;
+}
+
+extern "C" int64_t kgat_biinter_gemm_state_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {
+  if (n_rows < 0 || !gemm_dims_ok(d_in, d_out)) return -1;
+  return n_rows * 2 * static_cast<int64_t>(d_out) + n_rows;
+}
+
+extern "C" int64_t kgat_biinter_gemm_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {
+  if (n_rows < 0 || !gemm_dims_ok(d_in, d_out)) return -1;
+  return n_rows * 2 * static_cast<int64_t>(d_in) + n_rows;
+}
+
+extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                                         const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
+                                         int64_t n, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                                         float* state, float* work, int64_t work_floats, void* stream) {
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || !state || n < 0 || !gemm_dims_ok(d_in, d_out))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || (ldx & 3) || (lds & 3) || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  if (!work || work_floats < kgat_biinter_gemm_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* U = work;
+  float* M = work + n * d_in;
+  float* P1 = state;
+  float* P2 = state + n * d_out;
+  float* norm = state + 2 * n * d_out;
+  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * d_in / 4, 256, kgat::kCUs * 8)), dim3(256), 0, st, X,
+                     ldx, S, lds, U, M, n, d_in);
+  KGAT_LAUNCH_CHECK();
+  int err = 0;
+  rocblas_handle h = kgat::blas_handle(st, &err);
+  if (err) return err;
+  const float one = 1.f, zero = 0.f;
+  // row-major P[n, o] = U[n, k] W^T  <=>  column-major P^T[o, n] = W^T[o, k] ... (W row-major = W^T col-major)
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
+                          &one, W1, d_in, U, d_in, &zero, P1, d_out));
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
+                          &one, W2, d_in, M, d_in, &zero, P2, d_out));
+  hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh, norm, n, d_out,
+                     dropout_p, seed);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                         int64_t ldh, float* state, const float* dH, int64_t lddh, const float* W1,
+                                         const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
+                                         float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
+                                         int32_t d_out, float dropout_p, uint64_t seed, const int32_t* key_rows,
+                                         float* work, int64_t work_floats, void* stream) {
+  if (!X || !S || !H || !state || !dH || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n < 0 ||
+      !gemm_dims_ok(d_in, d_out))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || lddh < d_out || lddxd < d_in || ldds < d_in || (ldx & 3) ||
+      (lds & 3) || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return KGAT_ERR_INVALID;
+  if (!work || work_floats < kgat_biinter_gemm_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int err = 0;
+  rocblas_handle h = kgat::blas_handle(st, &err);
+  if (err) return err;
+  const float one = 1.f, zero = 0.f;
+  if (n == 0) {  // no rows: zero weight gradients
+    hipMemsetAsync(dW1, 0, sizeof(float) * d_in * d_out, st);
+    hipMemsetAsync(dW2, 0, sizeof(float) * d_in * d_out, st);
+    hipMemsetAsync(db1, 0, sizeof(float) * d_out, st);
+    hipMemsetAsync(db2, 0, sizeof(float) * d_out, st);
+    return static_cast<int>(hipGetLastError());
+  }
+  float* dA = state;
+  float* dB = state + n * d_out;
+  const float* norm = state + 2 * n * d_out;
+  float* U = work;
+  float* M = work + n * d_in;
+  float* ones = work + 2 * n * d_in;
+  hipLaunchKernelGGL(kgat::epi_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, dH, lddh, n,
+                     d_out, dropout_p, seed, key_rows);
+  KGAT_LAUNCH_CHECK();
+  // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
+                          W1, d_in, dA, d_out, &zero, dXd, static_cast<int>(lddxd)));
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
+                          W2, d_in, dB, d_out, &zero, dS, static_cast<int>(ldds)));
+  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * d_in / 4, 256, kgat::kCUs * 8)), dim3(256), 0, st, X,
+                     ldx, S, lds, U, M, n, d_in);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kgat::dxs_kernel, dim3(kgat::blocks_for(n * d_in, 256, kgat::kCUs * 8)), dim3(256), 0, st, dXd,
+                     lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
+  KGAT_LAUNCH_CHECK();
+  // dW = dA^T U  (row-major [o, n] x [n, k]): column-major C[k, o] = U^T-view[k, n] x dA-view[n, o]
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, d_in, d_out, static_cast<int>(n),
+                          &one, U, d_in, dA, d_out, &zero, dW1, d_in));
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, d_in, d_out, static_cast<int>(n),
+                          &one, M, d_in, dB, d_out, &zero, dW2, d_in));
+  hipLaunchKernelGGL(kgat::ones_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs)), dim3(256), 0, st, ones, n);
+  KGAT_LAUNCH_CHECK();
+  KGAT_BLAS(rocblas_sgemv(h, rocblas_operation_none, d_out, static_cast<int>(n), &one, dA, d_out, ones, 1, &zero, db1,
+                          1));
+  KGAT_BLAS(rocblas_sgemv(h, rocblas_operation_none, d_out, static_cast<int>(n), &one, dB, d_out, ones, 1, &zero, db2,
+                          1));
+  return KGAT_OK;
+}

@@ -171,18 +171,55 @@ def frontier_reset(rows: torch.Tensor, node_map: torch.Tensor) -> None:
     _lib.call("kgat_frontier_reset", rows.data_ptr(), rows.numel(), node_map.data_ptr(), stream_ptr(rows.device))
 
 
-class BiState:
-    """The forward's saved state for the backward (kgat_biinter_fwd_f32 norm_out / mask_out):
-    row norms and per-lane sign/keep bit words, indexed by node."""
+# (d_in, d_out) pairs the fused kernels of csrc/biinter.hip dispatch; others run the
+# rocBLAS + epilogue path of csrc/biinter_gemm.hip (kgat_biinter_*_gemm_f32).
+FUSED_SHAPES = {(16, 16), (32, 16), (32, 32), (64, 16), (64, 32), (64, 64), (128, 32), (128, 64), (128, 128),
+                (32, 64), (16, 32), (64, 128)}
 
-    def __init__(self, n: int, device):
-        self.norm = torch.empty(max(n, 1), dtype=torch.float32, device=device)
-        self.mask = torch.empty(max((n + 15) // 16, 1) * 64, dtype=torch.int64, device=device)
+
+def fused_supported(d_in: int, d_out: int) -> bool:
+    return (d_in, d_out) in FUSED_SHAPES
+
+
+class BiState:
+    """The forward's saved state for the backward, indexed by node.
+    fused shapes (kgat_biinter_fwd_f32 norm_out / mask_out): row norms + per-lane sign/keep words;
+    wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
+
+    def __init__(self, n: int, device, d_in: int = 64, d_out: int = 64):
+        self.n, self.d_in, self.d_out = n, d_in, d_out
+        self.kind = "fused" if fused_supported(d_in, d_out) else "gemm"
+        if self.kind == "fused":
+            self.norm = torch.empty(max((n + 15) // 16 * 16, 16), dtype=torch.float32, device=device)
+            self.mask = torch.empty(max((n + 15) // 16, 1) * 64, dtype=torch.int64, device=device)
+        else:
+            m = int(_lib.lib().kgat_biinter_gemm_state_floats(n, d_in, d_out))
+            if m < 0:
+                raise ValueError(f"unsupported bi-interaction shape {d_in}->{d_out}")
+            self.P = torch.empty(max(m, 1), dtype=torch.float32, device=device)
+
+    def gemm_views(self):
+        n, o = self.n, self.d_out
+        return self.P[:n * o].view(n, o), self.P[n * o:2 * n * o].view(n, o), self.P[2 * n * o:2 * n * o + n]
 
 
 def saved_state_supported(d_in: int, d_out: int) -> bool:
-    """Shapes whose backward runs from the saved state (see kgat_biinter_bwd_f32)."""
+    """Fused shapes whose backward runs from the saved state (see kgat_biinter_bwd_f32)."""
     return d_out <= 64 and d_in * d_out <= 4096
+
+
+def make_state(n: int, d_in: int, d_out: int, device) -> BiState | None:
+    """The state a training forward should keep for this layer (None: the backward recomputes)."""
+    if fused_supported(d_in, d_out):
+        return BiState(n, device, d_in, d_out) if saved_state_supported(d_in, d_out) else None
+    return BiState(n, device, d_in, d_out)
+
+
+def _gemm_work(n: int, d_in: int, d_out: int, device) -> torch.Tensor:
+    m = int(_lib.lib().kgat_biinter_gemm_work_floats(n, d_in, d_out))
+    if m < 0:
+        raise ValueError(f"unsupported bi-interaction shape {d_in}->{d_out}")
+    return torch.empty(max(m, 1), dtype=torch.float32, device=device)
 
 
 def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out=None,
@@ -199,7 +236,18 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
         raise ValueError("W must be contiguous")
     if out is None:
         out = torch.empty(n, dout, dtype=torch.float32, device=X.device)
-    if state is not None and (state.norm.numel() < n or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
+    if not fused_supported(din, dout):
+        st = state if state is not None else BiState(n, X.device, din, dout)
+        if st.kind != "gemm" or st.n != n:
+            raise ValueError("bi-interaction state does not match the layer")
+        work = _gemm_work(n, din, dout, X.device)
+        _lib.call("kgat_biinter_fwd_gemm_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(),
+                  b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout,
+                  float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), st.P.data_ptr(), work.data_ptr(),
+                  work.numel(), stream_ptr(X.device))
+        return out
+    if state is not None and (state.kind != "fused" or state.norm.numel() < n
+                              or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
         raise ValueError("bi-interaction state too small or d_out > 64")
     _lib.call("kgat_biinter_fwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
               W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout, float(dropout_p),
@@ -235,6 +283,9 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     dW2 = torch.empty_like(W2)
     db1 = torch.empty_like(b1)
     db2 = torch.empty_like(b2)
+    if not fused_supported(din, dout):
+        _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, dropout_p, seed, dXd, dS, dW1, db1, dW2, db2, rows, H, state)
+        return dXd, dS, dW1, db1, dW2, db2
     ws_n = int(_lib.lib().kgat_biinter_bwd_workspace(n, din, dout))
     if ws_n < 0:
         raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
@@ -248,6 +299,37 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
               float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
               rows.data_ptr() if rows is not None else None, src_rows, ws.data_ptr(), ws.numel(), stream_ptr(dev))
     return dXd, dS, dW1, db1, dW2, db2
+
+
+def _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, p, seed, dXd, dS, dW1, db1, dW2, db2, rows, H, state) -> None:
+    """Wide-layer backward (kgat_biinter_bwd_gemm_f32); frontier rows are gathered to a compact problem."""
+    src_rows, din = X.shape
+    dout = W1.shape[0]
+    dev = X.device
+    if H is None or state is None:  # no saved forward: recompute it
+        state = BiState(src_rows, dev, din, dout)
+        H = biinter_fwd(X, S, W1, b1, W2, b2, p, seed, state=state)
+    if state.kind != "gemm" or state.n != src_rows:
+        raise ValueError("bi-interaction state does not match the layer")
+    key = None
+    if rows is not None:
+        n = rows.numel()
+        P1, P2, norm = state.gemm_views()
+        Xc, Sc, Hc = gather_rows(X, rows), gather_rows(S, rows), gather_rows(H, rows)
+        comp = BiState(n, dev, din, dout)
+        c1, c2, cn = comp.gemm_views()
+        gather_rows(P1, rows, out=c1)
+        gather_rows(P2, rows, out=c2)
+        safe = rows.clamp_min(0)
+        _lib.call("kgat_gather_f32", norm.data_ptr(), safe.data_ptr(), n, cn.data_ptr(), stream_ptr(dev))
+        X, S, H, state, key = Xc, Sc, Hc, comp, rows
+    n = X.shape[0]
+    work = _gemm_work(n, din, dout, dev)
+    _lib.call("kgat_biinter_bwd_gemm_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
+              state.P.data_ptr(), dH.data_ptr(), _ld(dH), W1.data_ptr(), W2.data_ptr(), dXd.data_ptr(), _ld(dXd),
+              dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
+              float(p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), key.data_ptr() if key is not None else None,
+              work.data_ptr(), work.numel(), stream_ptr(dev))
 
 
 def make_tables(tables: list[torch.Tensor]) -> _lib.Tables:

@@ -112,8 +112,7 @@ class _CFLoss(torch.autograd.Function):
         for l in range(len(drops)):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             s = kernels.spmm(graph, x)
-            st = (kernels.BiState(x.shape[0], x.device)
-                  if kernels.saved_state_supported(W1.shape[1], W1.shape[0]) else None)
+            st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
             x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             sides.append(s)
             states.append(st)

@@ -148,7 +148,7 @@ def test_biinter_fwd_bwd_parity(pkg, din, dout):
     for got, want in ((dW1, w1.grad), (db1, bb1.grad), (dW2, w2.grad), (db2, bb2.grad)):
         np.testing.assert_allclose(got.cpu().numpy(), want.numpy(), rtol=1e-3, atol=1e-4)
     if kernels.saved_state_supported(din, dout):
-        st = kernels.BiState(n, DEV)
+        st = kernels.BiState(n, DEV, din, dout)
         H2 = kernels.biinter_fwd(*dv, state=st)
         assert torch.equal(H, H2)
         got = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], H=H2, state=st)
@@ -177,7 +177,7 @@ def test_biinter_saved_state_matches_recompute(pkg, din, dout):
     dHc = torch.zeros(320, dout, device=DEV)
     dHc[:300] = torch.randn(300, dout, device=DEV)
     for p in (0.0, 0.2):
-        st = kernels.BiState(n, DEV)
+        st = kernels.BiState(n, DEV, din, dout)
         H = kernels.biinter_fwd(*dv, dropout_p=p, seed=5, state=st)
         assert torch.equal(H, kernels.biinter_fwd(*dv, dropout_p=p, seed=5))
         norm = st.norm[:n].cpu()
@@ -302,15 +302,16 @@ def test_cf_step_dropout_train_mode_runs(pkg):
     m.update_cf_weights()
 
 
-@pytest.mark.parametrize("layers,batch", [([64, 32], 256), ([64, 32, 16], 512)])
-def test_cf_step_synthetic_hubs_vs_oracle(pkg, layers, batch):
+@pytest.mark.parametrize("dim,layers,batch", [(64, [64, 32], 256), (64, [64, 32, 16], 512), (256, [256, 128], 256)])
+def test_cf_step_synthetic_hubs_vs_oracle(pkg, dim, layers, batch):
     """Synthetic CKG with Zipf hub rows (long-row path in A and A^T), duplicate ids in the
     batch (users repeat, items collide with user rows): loss and every gradient vs the oracle."""
     graph_mod, _ = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(6000, 60000, seed=11)
     lay = graph_mod.build_layout(U, E, inter, trip)
     torch.manual_seed(2024)
-    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers))
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                              cf_embedding_dim=dim, kg_embedding_dim=dim))
     init = {k: v.clone() for k, v in m.state_dict().items() if not v.is_sparse}
     g = m.attach_graph(lay, DEV)
     assert g.A.n_long > 0 and g.AT.n_long > 0
@@ -671,3 +672,56 @@ def test_bpr_bwd_row_map_skips_unowned_rows(pkg):
     comp = torch.zeros(int(owned.sum()), d, device=DEV)
     kernels.bpr_bwd([tab], 0, users, pos, neg, 1e-5, coef, gout, comp, row_map=row_map)
     torch.testing.assert_close(comp, dense[owned], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("din,dout", [(256, 256), (256, 128), (128, 256), (96, 48)])
+def test_biinter_wide_gemm_path(pkg, din, dout):
+    """Shapes the fused kernels do not dispatch run rocBLAS GEMMs + HIP epilogues: forward and
+    backward vs a torch fp32 autograd reference, with dropout, clamped rows and frontier rows."""
+    _, kernels = _mods(pkg)
+    assert not kernels.fused_supported(din, dout)
+    torch.manual_seed(din + 3 * dout)
+    n, p = 2000 + 5, 0.2
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    X[10:20] = 0.0
+    S[10:20] = 0.0
+    W1, W2 = torch.randn(dout, din) * 0.1, torch.randn(dout, din) * 0.1
+    b1, b2 = torch.zeros(dout), torch.zeros(dout)  # zero rows => g = 0 => F.normalize's clamp
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    st = kernels.make_state(n, din, dout, DEV)
+    H = kernels.biinter_fwd(*dv, dropout_p=p, seed=9, state=st)
+    keep = (H.cpu() != 0).float()
+    keep[10:20] = 1.0  # zero rows: the mask is not visible there (g = 0 anyway)
+    assert abs((1 - keep[20:].mean().item()) - p) < 0.02
+    leaves = [t.clone().requires_grad_(True) for t in (X, S, W1, b1, W2, b2)]
+    x, s, w1, bb1, w2, bb2 = leaves
+    h = (torch.nn.functional.leaky_relu(torch.nn.functional.linear(x + s, w1, bb1), 0.01)
+         + torch.nn.functional.leaky_relu(torch.nn.functional.linear(x * s, w2, bb2), 0.01)) * keep / (1 - p)
+    ref = h / h.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    np.testing.assert_allclose(H.cpu().numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-5)
+    dH = torch.randn(n, dout)
+    dH[10:20] = 0.0  # keep the 1/eps gradient of clamped rows out of the comparison
+    ref.backward(dH)
+    got = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], dropout_p=p, seed=9, H=H, state=st)
+    want = (x.grad, s.grad, w1.grad, bb1.grad, w2.grad, bb2.grad)
+    for i, (a, b) in enumerate(zip(got, want)):
+        np.testing.assert_allclose(a.cpu().numpy(), b.numpy(), rtol=1e-3, atol=1e-5 if i < 2 else 1e-4,
+                                   err_msg=f"grad {i}")
+    # frontier rows (compact dH) == the dense backward restricted to those rows
+    F = torch.from_numpy(np.random.default_rng(3).choice(n, 100, replace=False))
+    rows = torch.cat([F, torch.full((12,), -1)]).int().to(DEV)
+    dHc = torch.zeros(112, dout)
+    dHc[:100] = torch.randn(100, dout)
+    dHd = torch.zeros(n, dout)
+    dHd[F] = dHc[:100]
+    st2 = kernels.make_state(n, din, dout, DEV)
+    H2 = kernels.biinter_fwd(*dv, dropout_p=p, seed=9, state=st2)
+    dense = kernels.biinter_bwd(dv[0], dv[1], dHd.to(DEV), *dv[2:], dropout_p=p, seed=9, H=H2, state=st2)
+    st3 = kernels.make_state(n, din, dout, DEV)
+    H3 = kernels.biinter_fwd(*dv, dropout_p=p, seed=9, state=st3)
+    comp = kernels.biinter_bwd(dv[0], dv[1], dHc.to(DEV), *dv[2:], dropout_p=p, seed=9, rows=rows, H=H3, state=st3)
+    Fd = F.to(DEV)
+    np.testing.assert_allclose(comp[0][:100].cpu().numpy(), dense[0][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(comp[1][:100].cpu().numpy(), dense[1][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
+    for a, b in zip(comp[2:], dense[2:]):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=1e-5)
