@@ -119,6 +119,9 @@ def dense_state(model) -> dict[str, np.ndarray]:
     return {k: v.detach().numpy().copy() for k, v in model.state_dict().items() if not v.is_sparse}
 
 
+CHECKPOINTS_ONLY = "--checkpoints" in sys.argv  # write only the *_ckpt.pth fixtures
+
+
 def make_kgat_case(name: str, users: int, problems: int, contests: int, tags: int, ratings: int,
                    dim: int, layers: list[int], cf_steps: int = 3, kg_steps: int = 2) -> None:
     rng = np.random.default_rng(SEED + len(name))
@@ -207,6 +210,11 @@ def make_kgat_case(name: str, users: int, problems: int, contests: int, tags: in
             rec[f"metrics/{k}/{m.value}"] = np.asarray(v, np.float64)
     rec["train_flat"] = np.array([(u, i) for u in train for i in train[u]], np.int64)
     rec["test_flat"] = np.array([(u, i) for u in test for i in test[u]], np.int64)
+    if name == "L2_d64":
+        # the reference's own checkpoint format (main.py:197-210) at the state the scores above came from
+        torch.save({"model_state_dict": model.state_dict()}, OUT / f"kgat_{name}_ckpt.pth")
+    if CHECKPOINTS_ONLY:
+        return
     np.savez_compressed(OUT / f"kgat_{name}.npz", **rec)
     print(f"kgat_{name}: N={n} E={len(heads)} nnz(A)={rec['A_val'].size} "
           f"-> {(OUT / f'kgat_{name}.npz').stat().st_size / 1e6:.2f} MB")
@@ -258,6 +266,9 @@ def make_nfm_case(name: str, users: int, problems: int, contests: int, tags: int
     with torch.no_grad():
         sc = model(x, mode=NFMMode.PREDICT)
     rec["pred_users"], rec["pred_scores"] = test_users.numpy(), sc.numpy()
+    torch.save({"model_state_dict": model.state_dict()}, OUT / f"nfm_{name}_ckpt.pth")  # NFM/main.py:186-198
+    if CHECKPOINTS_ONLY:
+        return
     np.savez_compressed(OUT / f"nfm_{name}.npz", **rec)
     print(f"nfm_{name}: F={users + entity_num} -> {(OUT / f'nfm_{name}.npz').stat().st_size / 1e6:.2f} MB")
 

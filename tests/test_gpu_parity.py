@@ -725,3 +725,41 @@ def test_biinter_wide_gemm_path(pkg, din, dout):
     np.testing.assert_allclose(comp[1][:100].cpu().numpy(), dense[1][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
     for a, b in zip(comp[2:], dense[2:]):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=1e-5)
+
+
+def test_reference_checkpoint_predict_and_round_trip(pkg, tmp_path):
+    """§8(f)4: a kgat.pth / nfm.pth written by the reference's save_model loads through its load_model
+    recipe (load_state_dict, eval) and PREDICT reproduces the scores the reference computed from that
+    state; our own checkpoint round-trips bit-exactly."""
+    from tests.conftest import GOLDEN
+    g = golden("kgat_L2_d64")
+    args = pkg.KGATArgs(user_num=int(g["user_num"]), entity_num=int(g["entity_num"]),
+                        relation_num=len(g["adjacency_relations"]), layer_size=[64, 32])
+    m = pkg.KGAT(args)
+    ck = torch.load(GOLDEN / "kgat_L2_d64_ckpt.pth", map_location="cpu", weights_only=True)
+    m.load_state_dict(ck["model_state_dict"])
+    m.eval()
+    m.to(DEV)
+    users = torch.from_numpy(g["eval_users"]).to(DEV)
+    items = torch.arange(int(g["item_num"]), device=DEV)
+    with torch.no_grad():
+        sc = m(users, items, mode=pkg.KGATMode.PREDICT)
+    np.testing.assert_allclose(sc.cpu().numpy(), g["scores"], rtol=RTOL, atol=1e-5)
+    torch.save({"model_state_dict": m.state_dict()}, tmp_path / "kgat.pth")
+    m2 = pkg.KGAT(args)
+    m2.load_state_dict(torch.load(tmp_path / "kgat.pth", map_location="cpu", weights_only=True)["model_state_dict"])
+    m2.eval()
+    m2.to(DEV)
+    with torch.no_grad():
+        assert torch.equal(m2(users, items, mode=pkg.KGATMode.PREDICT), sc)
+    gn = golden("nfm_h3_d64")
+    n = pkg.NFM(pkg.NFMArgs(user_num=int(gn["user_num"]), item_num=int(gn["item_num"]),
+                            entity_num=int(gn["entity_num"]), embedding_dim=int(gn["dim"]),
+                            hidden_dim=gn["hidden"].tolist()))
+    ckn = torch.load(GOLDEN / "nfm_h3_d64_ckpt.pth", map_location="cpu", weights_only=True)
+    n.load_state_dict(ckn["model_state_dict"])
+    n.eval()
+    n.to(DEV)
+    I = int(gn["item_num"])
+    x = _nfm_batch(gn, np.repeat(gn["pred_users"], I), np.tile(np.arange(I), len(gn["pred_users"]))).to(DEV)
+    np.testing.assert_allclose(n(x, mode=pkg.NFMMode.PREDICT).cpu().numpy(), gn["pred_scores"], rtol=RTOL, atol=1e-5)

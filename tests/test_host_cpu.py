@@ -149,3 +149,25 @@ def test_eval_csr_helper_sorts_and_dedups():
     assert ptr.tolist() == [0, 3, 3, 4] and idx.tolist() == [1, 3, 5, 2] and idx.dtype == torch.int32
     ptr, idx = ev._csr([[], []], "cpu")
     assert ptr.tolist() == [0, 0, 0] and idx.numel() == 1
+
+
+def test_reference_checkpoints_load_into_product_models():
+    """kgat.pth / nfm.pth in the reference's format (main.py:197-231, NFM/main.py:186-220) load with the
+    safe loader and match our state_dict keys and shapes (including the sparse attentive_matrix)."""
+    g = golden("kgat_L2_d64")
+    ck = torch.load(ROOT / "tests" / "golden" / "kgat_L2_d64_ckpt.pth", map_location="cpu", weights_only=True)
+    sd = ck["model_state_dict"]
+    m = pkg.KGAT(pkg.KGATArgs(user_num=int(g["user_num"]), entity_num=int(g["entity_num"]),
+                              relation_num=len(g["adjacency_relations"]), layer_size=[64, 32]))
+    own = m.state_dict()
+    assert set(sd) == set(own)
+    for k in sd:
+        assert sd[k].shape == own[k].shape and sd[k].is_sparse == own[k].is_sparse, k
+    m.load_state_dict(sd)
+    assert m.attentive_matrix.data._nnz() == sd["attentive_matrix"]._nnz()
+    gn = golden("nfm_h3_d64")
+    ckn = torch.load(ROOT / "tests" / "golden" / "nfm_h3_d64_ckpt.pth", map_location="cpu", weights_only=True)
+    n = pkg.NFM(pkg.NFMArgs(user_num=int(gn["user_num"]), item_num=int(gn["item_num"]),
+                            entity_num=int(gn["entity_num"]), embedding_dim=int(gn["dim"]),
+                            hidden_dim=gn["hidden"].tolist()))
+    n.load_state_dict(ckn["model_state_dict"])
