@@ -86,6 +86,9 @@ _SIGNATURES = {
     "kgat_biinter_bwd_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp,
                                                  c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                                  c_i32, c_f32, c_u64, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_sample_cf_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "kgat_sample_kg_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp,
+                                            c_vp]),
     "kgat_gather_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "kgat_scatter_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "kgat_add_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),

@@ -17,6 +17,8 @@
 // group of 4 blocks), so both paths drop the same elements.
 #include <rocblas/rocblas.h>
 
+#include <utility>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -219,11 +221,10 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
   if (err) return err;
   const float one = 1.f, zero = 0.f;
   if (n == 0) {  // no rows: zero weight gradients
-    hipMemsetAsync(dW1, 0, sizeof(float) * d_in * d_out, st);
-    hipMemsetAsync(dW2, 0, sizeof(float) * d_in * d_out, st);
-    hipMemsetAsync(db1, 0, sizeof(float) * d_out, st);
-    hipMemsetAsync(db2, 0, sizeof(float) * d_out, st);
-    return static_cast<int>(hipGetLastError());
+    for (auto [ptr, count] : {std::pair<float*, size_t>{dW1, size_t(d_in) * d_out}, {dW2, size_t(d_in) * d_out},
+                              {db1, size_t(d_out)}, {db2, size_t(d_out)}})
+      if (hipError_t e = hipMemsetAsync(ptr, 0, sizeof(float) * count, st); e != hipSuccess) return static_cast<int>(e);
+    return KGAT_OK;
   }
   float* dA = state;
   float* dB = state + n * d_out;
