@@ -31,6 +31,14 @@ class CSR(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("n", ctypes.c_int64), ("step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float)]
+
+
+KGAT_ADAM_MAX_TENSORS = 16
+
+
 class Tables(ctypes.Structure):
     """Mirror of ``kgat_tables``."""
 
@@ -89,6 +97,7 @@ _SIGNATURES = {
     "kgat_sample_cf_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "kgat_sample_kg_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp,
                                             c_vp]),
+    "kgat_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "kgat_scatter_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "kgat_add_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),

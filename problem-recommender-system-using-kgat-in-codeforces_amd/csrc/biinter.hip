@@ -553,7 +553,7 @@ __device__ __forceinline__ float img_at(const float* img, int row, int col) {
   return img[row * D + ((((col >> 2) ^ chunk_swz<D>(row))) << 2) + (col & 3)];
 }
 
-template <int DIN, int DOUT, bool FRONTIER, int EXP = 0>
+template <int DIN, int DOUT, bool FRONTIER>
 __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds, const float* __restrict__ H,
     int64_t ldh, const float* __restrict__ norm, const uint64_t* __restrict__ mask, const float* __restrict__ dH,
@@ -737,16 +737,11 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
 #pragma unroll
       for (int ib = 0; ib < NIB; ++ib) {
         floatx4 du = {0.f, 0.f, 0.f, 0.f}, dm = {0.f, 0.f, 0.f, 0.f};
-        if constexpr ((EXP & 2) == 0) {
 #pragma unroll
         for (int t = 0; t < KO; ++t) {
           const int k = q * KO + t;
           du = mfma16x4(dar[t], w1s[k * F::WLDB + ib * 16 + c], du);
           dm = mfma16x4(dbr[t], w2s[k * F::WLDB + ib * 16 + c], dm);
-        }
-        } else {
-          du[0] += dar[ib] * w1s[ib * 16 + c];
-          dm[0] += dbr[ib] * w2s[ib * 16 + c];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -768,7 +763,6 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
         u[i] = x[ib][i] + sv[ib][i];
         m[i] = x[ib][i] * sv[ib][i];
       }
-      if constexpr ((EXP & 1) == 0) {
 #pragma unroll
       for (int ob = 0; ob < NCB; ++ob)
 #pragma unroll
@@ -776,10 +770,6 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
           dw1[ob][ib] = mfma16x4(da[ob][s4], u[s4], dw1[ob][ib]);
           dw2[ob][ib] = mfma16x4(db[ob][s4], m[s4], dw2[ob][ib]);
         }
-      } else {
-        dw1[0][ib][0] += da[ib % NCB][0] * u[0];
-        dw2[0][ib][0] += db[ib % NCB][0] * m[0];
-      }
     }
   }
 
@@ -920,32 +910,15 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
   static bool attr_set = false;
   if (!attr_set) {
     for (const void* fn : {reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false>),
-                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, true>),
-                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 1>),
-                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 2>),
-                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, false, 3>)}) {
+                           reinterpret_cast<const void*>(&biinter_bwd_saved_kernel<DIN, DOUT, true>)}) {
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_bytes));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     attr_set = true;
   }
-  static int exp_mode = -1;
-  if (exp_mode < 0) {
-    const char* e = getenv("KGAT_BWD_EXP");  // timing experiments only (wrong results when set)
-    exp_mode = e ? atoi(e) : 0;
-  }
   if (rows != nullptr)
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, true>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
                        lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
-  else if (exp_mode == 1)
-    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 1>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
-                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
-  else if (exp_mode == 2)
-    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 2>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
-                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
-  else if (exp_mode == 3)
-    hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false, 3>), dim3(grid), dim3(256), lds_bytes, st, X, ldx,
-                       S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
   else
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
                        lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);

@@ -11,6 +11,16 @@ namespace kgat {
 //   v = v*b2 + ((1-b2) g) g     (mul_ then addcmul_)
 //   p = p + (-step_size) * (m / (sqrt(v)/bc2_sqrt + eps))
 // HBM-bound: 28 B per parameter (read p g m v, write p m v).
+// One element, each operation rounded on its own (no FMA contraction), so every
+// kernel below -- vector lanes and tails alike -- produces the same bits.
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float b2, float w2,
+                                          float step_size, float bc2s, float eps) {
+#pragma clang fp contract(off)
+  m = m + w1 * (g - m);
+  v = v * b2 + (w2 * g) * g;
+  p = p + (-step_size) * (m / (sqrtf(v) / bc2s + eps));
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    float step_size, float b1, float b2, float bc2s, float eps) {
@@ -22,9 +32,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   float4* v4 = reinterpret_cast<float4*>(v);
   const float4* g4 = reinterpret_cast<const float4*>(g);
   auto upd = [&](float& pp, float gg, float& mm, float& vv) {
-    mm = mm + w1 * (gg - mm);
-    vv = vv * b2 + (w2 * gg) * gg;
-    pp = pp + (-step_size) * (mm / (sqrtf(vv) / bc2s + eps));
+    adam_elem(pp, gg, mm, vv, w1, b2, w2, step_size, bc2s, eps);
   };
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = p4[i], mm = m4[i], vv = v4[i];
@@ -66,6 +74,84 @@ extern "C" const char* kgat_strerror(int status) {
 }
 
 extern "C" int kgat_version(void) { return 1; }
+
+namespace kgat {
+
+// Every tensor of one optimiser step in ONE launch: the tensor table travels in
+// the kernel arguments; block b works on chunk b of the concatenated float4
+// index space (tensor chosen by a scan of <= 16 chunk offsets).
+struct AdamTable {
+  kgat_adam_tensor t[KGAT_ADAM_MAX_TENSORS];
+  int64_t chunk_off[KGAT_ADAM_MAX_TENSORS + 1];  // first chunk of tensor i
+  int32_t count;
+};
+
+constexpr int kAdamChunk = 256 * 4 * 4;  // floats per block-iteration: 256 threads x float4 x 4
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps) {
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  const int64_t total = T.chunk_off[T.count];
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    int i = 0;
+    while (i + 1 < T.count && T.chunk_off[i + 1] <= c) ++i;
+    const kgat_adam_tensor& a = T.t[i];
+    const int64_t base = (c - T.chunk_off[i]) * kAdamChunk;
+    const float step_size = a.step_size, bc2s = a.bc2_sqrt;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
+      if (e + 4 <= a.n) {
+        float4 pp = *reinterpret_cast<float4*>(a.p + e), mm = *reinterpret_cast<float4*>(a.m + e);
+        float4 vv = *reinterpret_cast<float4*>(a.v + e);
+        const float4 gg = *reinterpret_cast<const float4*>(a.g + e);
+        float* P = &pp.x;
+        float* Mv = &mm.x;
+        float* V = &vv.x;
+        const float* G = &gg.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], V[k], w1, b2, w2, step_size, bc2s, eps);
+        *reinterpret_cast<float4*>(a.p + e) = pp;
+        *reinterpret_cast<float4*>(a.m + e) = mm;
+        *reinterpret_cast<float4*>(a.v + e) = vv;
+      } else {
+        for (int64_t k = e; k < a.n && k < e + 4; ++k) {
+          float pp = a.p[k], mm = a.m[k], vv = a.v[k];
+          adam_elem(pp, a.g[k], mm, vv, w1, b2, w2, step_size, bc2s, eps);
+          a.p[k] = pp;
+          a.m[k] = mm;
+          a.v[k] = vv;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace kgat
+
+extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
+                                   float eps, void* stream) {
+  if (!tensors || count < 1 || count > KGAT_ADAM_MAX_TENSORS) return KGAT_ERR_INVALID;
+  kgat::AdamTable T{};
+  T.count = count;
+  int64_t off = 0;
+  for (int i = 0; i < count; ++i) {
+    const kgat_adam_tensor& a = tensors[i];
+    if (!a.p || !a.g || !a.m || !a.v || a.n < 0) return KGAT_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(a.p) | reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.m) |
+         reinterpret_cast<uintptr_t>(a.v)) & 15)
+      return KGAT_ERR_INVALID;
+    T.t[i] = a;
+    T.chunk_off[i] = off;
+    off += (a.n + kgat::kAdamChunk - 1) / kgat::kAdamChunk;
+  }
+  T.chunk_off[count] = off;
+  if (off == 0) return KGAT_OK;
+  const int grid = static_cast<int>(off < kgat::kCUs * 8 ? off : kgat::kCUs * 8);
+  hipLaunchKernelGGL(kgat::adam_multi_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), T,
+                     beta1, beta2, eps);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
 
 extern "C" int kgat_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,
                              float beta2, float bc2_sqrt, float eps, void* stream) {

@@ -465,6 +465,21 @@ def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: flo
               beta2, bc2_sqrt, eps, stream_ptr(p.device))
 
 
+def adam_multi(items, beta1: float, beta2: float, eps: float) -> None:
+    """One launch per <= 16 tensors: items = [(p, g, m, v, step_size, bc2_sqrt), ...]."""
+    for i in range(0, len(items), _lib.KGAT_ADAM_MAX_TENSORS):
+        chunk = items[i:i + _lib.KGAT_ADAM_MAX_TENSORS]
+        arr = (_lib.AdamTensor * len(chunk))()
+        for a, (p, g, m, v, step_size, bc2s) in zip(arr, chunk):
+            for t, nm in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+                _req(t, nm)
+                if not t.is_contiguous():
+                    raise ValueError(f"{nm} must be contiguous")
+            a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+            a.n, a.step_size, a.bc2_sqrt = p.numel(), step_size, bc2s
+        _lib.call("kgat_adam_multi_f32", arr, len(chunk), beta1, beta2, eps, stream_ptr(chunk[0][0].device))
+
+
 def fill(t: torch.Tensor, value: float) -> torch.Tensor:
     _req(t, "t")
     if not t.is_contiguous():

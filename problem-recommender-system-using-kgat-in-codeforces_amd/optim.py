@@ -25,6 +25,8 @@ class FusedAdam:
 
     @torch.no_grad()
     def step(self) -> None:
+        """Every parameter with a gradient in one kgat_adam_multi_f32 launch (per 16 tensors)."""
+        items = []
         for p in self.params:
             g = p.grad
             if g is None:
@@ -40,8 +42,9 @@ class FusedAdam:
             t = st["step"]
             bc1 = 1.0 - self.beta1 ** t
             bc2_sqrt = math.sqrt(1.0 - self.beta2 ** t)
-            kernels.adam(p.data, g.contiguous(), st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, self.beta1,
-                         self.beta2, bc2_sqrt, self.eps)
+            items.append((p.data, g.contiguous(), st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, bc2_sqrt))
+        if items:
+            kernels.adam_multi(items, self.beta1, self.beta2, self.eps)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         for p in self.params:

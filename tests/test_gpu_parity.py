@@ -763,3 +763,22 @@ def test_reference_checkpoint_predict_and_round_trip(pkg, tmp_path):
     I = int(gn["item_num"])
     x = _nfm_batch(gn, np.repeat(gn["pred_users"], I), np.tile(np.arange(I), len(gn["pred_users"]))).to(DEV)
     np.testing.assert_allclose(n(x, mode=pkg.NFMMode.PREDICT).cpu().numpy(), gn["pred_scores"], rtol=RTOL, atol=1e-5)
+
+
+def test_adam_multi_matches_single_bit_exact(pkg):
+    _, kernels = _mods(pkg)
+    torch.manual_seed(8)
+    sizes = [1, 3, 4, 5, 1023, 4096, 4097, 300001] + [17] * 12  # > 16 tensors: two launches
+    single, multi = [], []
+    for n in sizes:
+        p, g = torch.randn(n, device=DEV), torch.randn(n, device=DEV) * 1e-3
+        m, v = torch.randn(n, device=DEV) * 1e-3, torch.rand(n, device=DEV) * 1e-6
+        single.append([t.clone() for t in (p, g, m, v)])
+        multi.append([t.clone() for t in (p, g, m, v)])
+    for k, (p, g, m, v) in enumerate(single):
+        kernels.adam(p, g, m, v, 1e-3 / (1 - 0.9 ** (k + 1)), 0.9, 0.999, (1 - 0.999 ** (k + 1)) ** 0.5, 1e-8)
+    kernels.adam_multi([(p, g, m, v, 1e-3 / (1 - 0.9 ** (k + 1)), (1 - 0.999 ** (k + 1)) ** 0.5)
+                        for k, (p, g, m, v) in enumerate(multi)], 0.9, 0.999, 1e-8)
+    for a, b in zip(single, multi):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
