@@ -98,6 +98,10 @@ _SIGNATURES = {
     "kgat_sample_kg_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp,
                                             c_vp]),
     "kgat_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp]),
+    "kgat_edge_logits_gemm_work_floats": (c_i64, [c_i64, c_i32]),
+    "kgat_edge_logits_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                 c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp,
+                                                 c_vp, c_i64, c_vp]),
     "kgat_gather_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "kgat_scatter_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "kgat_add_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp]),

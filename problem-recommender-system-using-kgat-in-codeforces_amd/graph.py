@@ -290,6 +290,9 @@ class RefreshPlan:
         local = np.arange(first_tile[-1], dtype=np.int64) - np.repeat(first_tile[:-1], cnt)
         tile_beg = np.r_[np.repeat(starts, cnt) + cls.TILE * local, E]
         p.rel_perm = torch.from_numpy(order.astype(np.int32)).to(dev)
+        # host copy of the relation runs of rel_perm (the wide-embedding GEMM scorer walks them)
+        p.seg_rel = np.ascontiguousarray(rs[starts], dtype=np.int32)
+        p.seg_beg = np.ascontiguousarray(np.r_[starts, E], dtype=np.int64)
         p.tile_rel = torch.from_numpy(np.repeat(rs[starts], cnt).astype(np.int32)).to(dev)
         p.tile_beg = torch.from_numpy(tile_beg.astype(np.int32)).to(dev)
         p.n_tiles = int(first_tile[-1])

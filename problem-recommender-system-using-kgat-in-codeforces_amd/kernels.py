@@ -37,6 +37,9 @@ def _ld(t: torch.Tensor) -> int:
 # on the launch stream around its kernels.
 SPMM_EVENTS: list | None = None
 
+# Edges per chunk of the wide-embedding GEMM edge scorer (scratch = 2 * chunk * d floats).
+EDGE_GEMM_CHUNK = 1 << 20
+
 
 def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, transpose: bool = False,
          accumulate: bool = False) -> torch.Tensor:
@@ -424,11 +427,24 @@ def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b
             raise ValueError("edge scorer weights must be contiguous")
     n_out = graph.nnz if plan.out_pos is not None else plan.n_edges
     out = torch.empty(max(n_out, 1), dtype=torch.float32, device=emb.device)
-    _lib.call("kgat_edge_logits_f32", emb.data_ptr(), _ld(emb), emb.shape[0], trans.data_ptr(), d, Wv.data_ptr(),
-              bv.data_ptr(), Wo.data_ptr(), bo.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), plan.tails.data_ptr(),
-              plan.weight.data_ptr(), plan.rel_perm.data_ptr(), plan.tile_rel.data_ptr(), plan.tile_beg.data_ptr(),
-              plan.n_tiles, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
-              plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(), stream_ptr(emb.device))
+    if d not in (16, 32, 64, 128):  # wide embeddings: GEMM path (csrc/attention_gemm.hip)
+        chunk = max(16, min(plan.n_edges, EDGE_GEMM_CHUNK))
+        work = torch.empty(int(_lib.lib().kgat_edge_logits_gemm_work_floats(chunk, d)), dtype=torch.float32,
+                           device=emb.device)
+        _lib.call("kgat_edge_logits_gemm_f32", emb.data_ptr(), _ld(emb), emb.shape[0], trans.data_ptr(), d,
+                  Wv.data_ptr(), bv.data_ptr(), Wo.data_ptr(), bo.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                  plan.tails.data_ptr(), plan.weight.data_ptr(), plan.rel_perm.data_ptr(), plan.n_edges,
+                  plan.seg_rel.ctypes.data, plan.seg_beg.ctypes.data, plan.seg_rel.size, float(dropout_p),
+                  ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+                  plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(), work.data_ptr(),
+                  work.numel(), stream_ptr(emb.device))
+    else:
+        _lib.call("kgat_edge_logits_f32", emb.data_ptr(), _ld(emb), emb.shape[0], trans.data_ptr(), d,
+                  Wv.data_ptr(), bv.data_ptr(), Wo.data_ptr(), bo.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                  plan.tails.data_ptr(), plan.weight.data_ptr(), plan.rel_perm.data_ptr(), plan.tile_rel.data_ptr(),
+                  plan.tile_beg.data_ptr(), plan.n_tiles, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+                  plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(),
+                  stream_ptr(emb.device))
     if plan.out_pos is None:
         slot_logits = torch.empty(max(graph.nnz, 1), dtype=torch.float32, device=emb.device)
         _lib.call("kgat_slot_sum_f32", plan.slot_ptr.data_ptr(), plan.slot_order.data_ptr(), graph.nnz,

@@ -782,3 +782,29 @@ def test_adam_multi_matches_single_bit_exact(pkg):
     for a, b in zip(single, multi):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("dim", [64, 256])
+def test_attention_refresh_synthetic_vs_oracle(pkg, dim):
+    """UPDATE_ATTENTION on a synthetic CKG vs the oracle: d=64 runs the fused MFMA scorer, d=256 (C5) the
+    rocBLAS GEMM scorer (csrc/attention_gemm.hip); several chunks and relation runs per chunk."""
+    graph_mod, kernels = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(3000, 24000, seed=21)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    torch.manual_seed(5)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[dim // 2],
+                              cf_embedding_dim=dim, kg_embedding_dim=dim))
+    params = {k: v.clone() for k, v in m.state_dict().items() if not v.is_sparse}
+    m.attach_graph(lay, DEV)
+    m.eval()
+    h, r, t = (torch.from_numpy(x).to(DEV) for x in (lay.heads, lay.rels, lay.tails))
+    old, kernels.EDGE_GEMM_CHUNK = kernels.EDGE_GEMM_CHUNK, 5000  # chunks end inside relation runs
+    try:
+        m(h, r, t, torch.tensor(lay.rel_order, device=DEV), mode=pkg.KGATMode.UPDATE_ATTENTION)
+    finally:
+        kernels.EDGE_GEMM_CHUNK = old
+    ref = K.refresh_attention(params, torch.from_numpy(lay.heads), torch.from_numpy(lay.rels),
+                              torch.from_numpy(lay.tails), lay.rel_order, U + E)
+    att = m.attentive_matrix.data.coalesce()
+    np.testing.assert_array_equal(att.indices().cpu().numpy(), ref.indices().numpy())
+    np.testing.assert_allclose(att.values().cpu().numpy(), ref.values().numpy(), rtol=1e-4, atol=1e-6)
