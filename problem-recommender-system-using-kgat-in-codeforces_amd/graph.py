@@ -257,6 +257,40 @@ class RefreshPlan:
         kh, kr, kt = self.key
         return (kh.shape == h.shape and torch.equal(kh, h) and torch.equal(kr, r) and torch.equal(kt, t))
 
+    def set_tiles(self, r: np.ndarray, t: np.ndarray, dev) -> None:
+        """Relation-sorted 16-edge tiles over this plan's edges (relation-major, then tail, so
+        neighbouring tiles share rows), plus the host copy of the relation runs."""
+        E = r.size
+        order = np.lexsort((t, r))
+        rs = r[order]
+        starts = np.flatnonzero(np.r_[True, rs[1:] != rs[:-1]]) if E else np.zeros(0, np.int64)
+        ends = np.r_[starts[1:], E]
+        cnt = (ends - starts + self.TILE - 1) // self.TILE
+        first_tile = np.zeros(cnt.size + 1, np.int64)
+        np.cumsum(cnt, out=first_tile[1:])
+        local = np.arange(first_tile[-1], dtype=np.int64) - np.repeat(first_tile[:-1], cnt)
+        tile_beg = np.r_[np.repeat(starts, cnt) + self.TILE * local, E]
+        self.rel_perm = torch.from_numpy(order.astype(np.int32)).to(dev)
+        self.tile_rel = torch.from_numpy(np.repeat(rs[starts], cnt).astype(np.int32)).to(dev)
+        self.tile_beg = torch.from_numpy(tile_beg.astype(np.int32)).to(dev)
+        self.n_tiles = int(first_tile[-1])
+        # host copy of the relation runs of rel_perm (the wide-embedding GEMM scorer walks them)
+        self.seg_rel = np.ascontiguousarray(rs[starts], dtype=np.int32)
+        self.seg_beg = np.ascontiguousarray(np.r_[starts, E], dtype=np.int64)
+
+    @classmethod
+    def for_edges(cls, tails: np.ndarray, rels: np.ndarray, weight: np.ndarray, out_pos: np.ndarray,
+                  dev) -> "RefreshPlan":
+        """A scoring plan over an arbitrary edge list: logit of edge i lands in out[out_pos[i]]."""
+        p = cls()
+        p.n_edges = int(tails.size)
+        p.tails = torch.from_numpy(np.ascontiguousarray(tails, np.int32)).to(dev)
+        p.weight = torch.from_numpy(np.ascontiguousarray(weight, np.float32)).to(dev)
+        p.set_tiles(np.asarray(rels, np.int64), np.asarray(tails, np.int64), dev)
+        p.out_pos = torch.from_numpy(np.ascontiguousarray(out_pos, np.int32)).to(dev)
+        p.slot_ptr = p.slot_order = None
+        return p
+
     @classmethod
     def build(cls, g: "DeviceGraph", h_d, r_d, t_d) -> "RefreshPlan | None":
         n = g.n_nodes
@@ -280,22 +314,7 @@ class RefreshPlan:
         p.n_edges = E
         p.tails = torch.from_numpy(t.astype(np.int32)).to(dev)
         p.weight = torch.from_numpy(degree_weights(h, t, r, n)).to(dev)
-        order = np.lexsort((t, r))  # relation-major, then tail (neighbouring tiles share rows)
-        rs = r[order]
-        starts = np.flatnonzero(np.r_[True, rs[1:] != rs[:-1]]) if E else np.zeros(0, np.int64)
-        ends = np.r_[starts[1:], E]
-        cnt = (ends - starts + cls.TILE - 1) // cls.TILE
-        first_tile = np.zeros(cnt.size + 1, np.int64)
-        np.cumsum(cnt, out=first_tile[1:])
-        local = np.arange(first_tile[-1], dtype=np.int64) - np.repeat(first_tile[:-1], cnt)
-        tile_beg = np.r_[np.repeat(starts, cnt) + cls.TILE * local, E]
-        p.rel_perm = torch.from_numpy(order.astype(np.int32)).to(dev)
-        # host copy of the relation runs of rel_perm (the wide-embedding GEMM scorer walks them)
-        p.seg_rel = np.ascontiguousarray(rs[starts], dtype=np.int32)
-        p.seg_beg = np.ascontiguousarray(np.r_[starts, E], dtype=np.int64)
-        p.tile_rel = torch.from_numpy(np.repeat(rs[starts], cnt).astype(np.int32)).to(dev)
-        p.tile_beg = torch.from_numpy(tile_beg.astype(np.int32)).to(dev)
-        p.n_tiles = int(first_tile[-1])
+        p.set_tiles(r, t, dev)
         if E == nnz:  # bijective: scores land directly in slot order
             p.out_pos = torch.from_numpy(slot.astype(np.int32)).to(dev)
             p.slot_ptr = p.slot_order = None

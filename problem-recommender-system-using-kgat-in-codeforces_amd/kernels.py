@@ -413,20 +413,11 @@ def transr_bwd(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out):
     return d_emb, d_rel, d_trans
 
 
-def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, dropout_p: float = 0.0,
-                seed: int = 0) -> torch.Tensor:
-    """Per-slot (bijective plans) or per-edge attention logits."""
-    for t, nm in ((emb, "emb"), (Wv, "Wv"), (Wo, "Wo")):
-        _req(t, nm, dim=2)
-    _req(trans, "trans", dim=3)
+def score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out: torch.Tensor, dropout_p: float = 0.0,
+                seed: int = 0) -> None:
+    """Edge scores of a plan: out[plan.out_pos[e]] (or out[e]) = logit of edge e; the fused MFMA
+    scorer for d <= 128, the chunked GEMM scorer above."""
     d = emb.shape[1]
-    if trans.shape[1:] != (d, d) or Wv.shape != (d, d) or Wo.shape != (d, d):
-        raise ValueError("edge scorer needs cf_embedding_dim == kg_embedding_dim (multi_head_attention.py:13-15)")
-    for t in (trans, Wv, Wo, bv, bo, ln_w, ln_b):
-        if not t.is_contiguous():
-            raise ValueError("edge scorer weights must be contiguous")
-    n_out = graph.nnz if plan.out_pos is not None else plan.n_edges
-    out = torch.empty(max(n_out, 1), dtype=torch.float32, device=emb.device)
     if d not in (16, 32, 64, 128):  # wide embeddings: GEMM path (csrc/attention_gemm.hip)
         chunk = max(16, min(plan.n_edges, EDGE_GEMM_CHUNK))
         work = torch.empty(int(_lib.lib().kgat_edge_logits_gemm_work_floats(chunk, d)), dtype=torch.float32,
@@ -445,6 +436,23 @@ def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b
                   plan.tile_beg.data_ptr(), plan.n_tiles, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
                   plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(),
                   stream_ptr(emb.device))
+
+
+def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, dropout_p: float = 0.0,
+                seed: int = 0) -> torch.Tensor:
+    """Per-slot (bijective plans) or per-edge attention logits."""
+    for t, nm in ((emb, "emb"), (Wv, "Wv"), (Wo, "Wo")):
+        _req(t, nm, dim=2)
+    _req(trans, "trans", dim=3)
+    d = emb.shape[1]
+    if trans.shape[1:] != (d, d) or Wv.shape != (d, d) or Wo.shape != (d, d):
+        raise ValueError("edge scorer needs cf_embedding_dim == kg_embedding_dim (multi_head_attention.py:13-15)")
+    for t in (trans, Wv, Wo, bv, bo, ln_w, ln_b):
+        if not t.is_contiguous():
+            raise ValueError("edge scorer weights must be contiguous")
+    n_out = graph.nnz if plan.out_pos is not None else plan.n_edges
+    out = torch.empty(max(n_out, 1), dtype=torch.float32, device=emb.device)
+    score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out, dropout_p, seed)
     if plan.out_pos is None:
         slot_logits = torch.empty(max(graph.nnz, 1), dtype=torch.float32, device=emb.device)
         _lib.call("kgat_slot_sum_f32", plan.slot_ptr.data_ptr(), plan.slot_order.data_ptr(), graph.nnz,

@@ -29,8 +29,10 @@ on device buffers; with a non-NCCL backend (gloo, used to run several ranks on
 one test GPU) buffers are staged through host memory.  All arithmetic is the
 HIP kernels of libkgat_hip.so.
 
-Not yet sharded: the attention refresh (UPDATE_ATTENTION) -- the layer-0 ring
-would carry the tail rows the edge scorer needs; see DESIGN.md.
+Attention refresh (UPDATE_ATTENTION): rank k scores the edges of its rows; the
+X0 shards travel the same ring and each arriving shard scores the local edges
+whose tail it holds; logits are soft-maxed over the local CSR rows and
+gathered back into the blocks and their transposes.
 """
 from __future__ import annotations
 
@@ -42,7 +44,8 @@ import torch.distributed as dist
 from torch import nn
 
 from . import kernels
-from .graph import GraphLayout, _DeviceCSR
+from . import _lib
+from .graph import GraphLayout, RefreshPlan, _DeviceCSR, degree_weights, stream_ptr
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
 from .optim import FusedAdam
 
@@ -133,15 +136,24 @@ class RowShard:
         lcol = col[e0:e1].astype(np.int64)
         lval = np.asarray(val[e0:e1], np.float32)
         sid = np.searchsorted(self.bounds, lcol, side="right") - 1
+        # the local CSR (rows lo..hi, global columns): attention logits are soft-maxed here, then
+        # gathered into the blocks (block_pos) and their transposes (block_t_pos)
+        self.local_rowptr = torch.from_numpy(np.ascontiguousarray(rowptr[lo:hi + 1] - rowptr[lo], np.int64)).to(device)
+        self.local_keys = lrow * int(rowptr.size - 1) + lcol  # row-major sorted (CSR order)
+        self.local_val = torch.from_numpy(lval.copy()).to(device)
+        self.block_pos, self.block_t_pos = [], []
         self.blocks, self.blocks_t, self.nnz = [], [], []
         for j in range(self.world):
             sel = sid == j
             r, c, v = lrow[sel], lcol[sel] - self.bounds[j], lval[sel]
+            pos = np.flatnonzero(sel).astype(np.int32)
             nj = int(self.sizes[j])
             rp = np.zeros(self.n + 1, np.int64)
             np.cumsum(np.bincount(r, minlength=self.n), out=rp[1:])
             self.blocks.append(_DeviceCSR(rp, c.astype(np.int32), torch.from_numpy(v.copy()).to(device), device))
             order = np.lexsort((r, c))
+            self.block_pos.append(torch.from_numpy(pos).to(device))
+            self.block_t_pos.append(torch.from_numpy(pos[order].copy()).to(device))
             rpt = np.zeros(nj + 1, np.int64)
             np.cumsum(np.bincount(c, minlength=nj), out=rpt[1:])
             self.blocks_t.append(_DeviceCSR(rpt, r[order].astype(np.int32),
@@ -149,10 +161,10 @@ class RowShard:
             self.nnz.append(int(sel.sum()))
 
 
-def ring_spmm(shard: RowShard, comm: Comm, X: torch.Tensor) -> torch.Tensor:
-    """S_k = sum_j A[k][j] . X_j with X_j arriving over the ring (all-gather pipelined with the SpMM)."""
+def ring_visit(shard: RowShard, comm: Comm, X: torch.Tensor, visit) -> None:
+    """Ring all-gather of the row shards X_j (k -> k+1): visit(j, X_j) runs on each shard while the
+    next one is in flight."""
     G, k, d = comm.world, comm.rank, X.shape[1]
-    S = torch.empty(shard.n, d, dtype=torch.float32, device=X.device)
     buf = X.contiguous()
     for s in range(G):
         j = (k - s) % G
@@ -160,10 +172,22 @@ def ring_spmm(shard: RowShard, comm: Comm, X: torch.Tensor) -> torch.Tensor:
         if s < G - 1:
             nxt = torch.empty(int(shard.sizes[(j - 1) % G]), d, dtype=torch.float32, device=X.device)
             pend = comm.exchange(buf, nxt)
-        kernels.spmm_block(shard.blocks[j], buf, S, accumulate=s > 0)
+        visit(j, buf)
         if pend is not None:
             pend.wait()
             buf = nxt
+
+
+def ring_spmm(shard: RowShard, comm: Comm, X: torch.Tensor) -> torch.Tensor:
+    """S_k = sum_j A[k][j] . X_j with X_j arriving over the ring (all-gather pipelined with the SpMM)."""
+    S = torch.empty(shard.n, X.shape[1], dtype=torch.float32, device=X.device)
+    first = [True]
+
+    def visit(j, buf):
+        kernels.spmm_block(shard.blocks[j], buf, S, accumulate=not first[0])
+        first[0] = False
+
+    ring_visit(shard, comm, X, visit)
     return S
 
 
@@ -414,6 +438,73 @@ class RowShardedKGAT(nn.Module):
         return _ShardedKGLoss.apply(ch, torch.from_numpy(r).to(dev), cp, cn, cfg, self._user_entity_embedding_shard,
                                     self._relation_embedding.weight, self._trans_matrix)
 
+    def _refresh_plan(self, h: np.ndarray, r: np.ndarray, t: np.ndarray):
+        """Per source shard j: a scoring plan over this rank's edges whose tail lies in shard j
+        (tails rebased into X_j), logits landing by local edge id; slot sums onto the local CSR."""
+        key = (h.size, h.tobytes()[:64], r.tobytes()[:64], t.tobytes()[:64], int(h.sum()), int(t.sum()))
+        cached = getattr(self, "_att_plan", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        sh, n, dev = self.shard, self._n_nodes, self._user_entity_embedding_shard.device
+        w = degree_weights(h, t, r, n)  # per-relation degrees over the whole graph (model.py:309-314)
+        sel = (h >= sh.lo) & (h < sh.hi)
+        hl, rl, tl, wl = h[sel] - sh.lo, r[sel], t[sel], w[sel]
+        keys = hl * n + tl
+        slot = np.searchsorted(sh.local_keys, keys)
+        ok = slot < sh.local_keys.size
+        ok[ok] &= sh.local_keys[slot[ok]] == keys[ok]
+        covered = np.zeros(sh.local_keys.size, bool)
+        covered[slot[ok]] = True
+        if not ok.all() or not covered.all():
+            raise NotImplementedError("row-sharded attention refresh needs the edge list of the sharded graph")
+        eid = np.arange(hl.size, dtype=np.int64)
+        sid = np.searchsorted(sh.bounds, tl, side="right") - 1
+        plans = []
+        for j in range(sh.world):
+            m = sid == j
+            plans.append(RefreshPlan.for_edges(tl[m] - sh.bounds[j], rl[m], wl[m], eid[m], dev)
+                         if m.any() else None)
+        so = np.argsort(slot, kind="stable")
+        slot_order = torch.from_numpy(so.astype(np.int32)).to(dev)
+        slot_ptr = torch.from_numpy(np.searchsorted(slot[so], np.arange(sh.local_keys.size + 1)).astype(np.int64)).to(dev)
+        plan = (plans, slot_ptr, slot_order, int(hl.size))
+        self._att_plan = (key, plan)
+        return plan
+
+    @torch.no_grad()
+    def _update_attention(self, heads, relations, tails, relation_indices) -> None:
+        """UPDATE_ATTENTION (model.py:318-366) on this rank's rows: X0 shards pass on the ring, each
+        scores the local edges whose tail it holds; softmax over the local rows; blocks refreshed."""
+        h, r, t = (torch.as_tensor(x).cpu().numpy().astype(np.int64) for x in (heads, relations, tails))
+        plans, slot_ptr, slot_order, n_edges = self._refresh_plan(h, r, t)
+        sh, dev = self.shard, self._user_entity_embedding_shard.device
+        mha = self._multi_head_attention
+        p = mha.dropout if self.training else 0.0
+        self._step += 1
+        seed = (self._step * 0x632BE5AB + 31 * self.comm.rank + 1) & ((1 << 62) - 1) if p > 0 else 0
+        W = [x.detach().contiguous() for x in (self._trans_matrix, mha._value_weight.weight, mha._value_weight.bias,
+                                                mha._output.weight, mha._output.bias, mha._layer_norm.weight,
+                                                mha._layer_norm.bias)]
+        logits = torch.empty(max(n_edges, 1), dtype=torch.float32, device=dev)
+
+        def visit(j, buf):
+            if plans[j] is not None:
+                kernels.score_edges(plans[j], buf, *W, logits, p, seed)
+
+        ring_visit(sh, self.comm, self._user_entity_embedding_shard.detach(), visit)
+        nnz = sh.local_keys.size
+        slot_logits = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+        st = stream_ptr(dev)
+        _lib.call("kgat_slot_sum_f32", slot_ptr.data_ptr(), slot_order.data_ptr(), nnz, logits.data_ptr(),
+                  slot_logits.data_ptr(), st)
+        _lib.call("kgat_row_softmax_f32", sh.local_rowptr.data_ptr(), sh.n, slot_logits.data_ptr(),
+                  sh.local_val.data_ptr(), st)
+        for j in range(sh.world):
+            for blk, pos in ((sh.blocks[j], sh.block_pos[j]), (sh.blocks_t[j], sh.block_t_pos[j])):
+                if pos.numel():
+                    _lib.call("kgat_gather_f32", sh.local_val.data_ptr(), pos.data_ptr(), pos.numel(),
+                              blk.val.data_ptr(), st)
+
     @torch.no_grad()
     def _calc_score(self, user_ids, item_ids) -> torch.Tensor:
         """[len(users), len(items)] -- identical on every rank (item ids index the table raw)."""
@@ -447,5 +538,6 @@ class RowShardedKGAT(nn.Module):
         if mode == KGATMode.PREDICT:
             return self._calc_score(*args)
         if mode == KGATMode.UPDATE_ATTENTION:
-            raise NotImplementedError("row-sharded attention refresh is not implemented yet (DESIGN.md §8)")
+            self._update_attention(*args)
+            return None
         raise ValueError(f"unknown mode {mode}")

@@ -100,10 +100,15 @@ def main() -> None:
     close("table after kg adam", m._user_entity_embedding_shard, ref._user_entity_embedding.weight[lo:hi],
           ATOL_PARAM)
 
-    # ---- PREDICT
+    # ---- UPDATE_ATTENTION (eval: MHA dropout off), then PREDICT on the refreshed graph
     m.load_full_state(ref.state_dict())
     ref.eval()
     m.eval()
+    att = [torch.from_numpy(x).cuda() for x in (lay.heads, lay.rels, lay.tails)] + [torch.tensor(lay.rel_order)]
+    ref(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    m(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    A = ref.graph().A
+    close("refreshed A rows", m.shard.local_val, A.val[int(lay.rowptr[lo]):int(lay.rowptr[hi])], 1e-6)
     users = torch.arange(0, 50, device="cuda")
     items = torch.arange(0, 300, device="cuda")
     with torch.no_grad():

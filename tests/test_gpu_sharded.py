@@ -78,6 +78,11 @@ def test_sharded_world1_matches_kgat(pkg):
                                rtol=1e-4)
     ref.eval()
     m.eval()
+    att = [torch.from_numpy(x).to(DEV) for x in (lay.heads, lay.rels, lay.tails)] + [torch.tensor(lay.rel_order)]
+    ref(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    m(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    np.testing.assert_allclose(m.shard.local_val.cpu().numpy(), ref.graph().A.val.cpu().numpy(), rtol=1e-4,
+                               atol=1e-6)
     tabs_s, tabs_r = m.propagate(), ref.propagate()
     for a, w in zip(tabs_s, tabs_r):
         np.testing.assert_allclose(a.cpu().numpy(), w.cpu().numpy(), atol=1e-5, rtol=1e-4)
