@@ -35,19 +35,41 @@ __device__ __forceinline__ uint32_t gemm_threshold(float p) {
   return t >= 65536.f ? 65536u : static_cast<uint32_t>(t);
 }
 
+// U = X+S, M = X*S with row pitch d+4; column d is 1 (so dA^T [U | 1] = [dW | db]), d+1..d+3 are 0
 __global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
                                                  int64_t lds, float* __restrict__ U, float* __restrict__ M, int64_t n,
                                                  int d) {
-  const int64_t total = n * (d / 4);
+  const int q = d / 4 + 1;  // float4 groups per padded row
+  const int64_t total = n * q;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int64_t ldu = d + 4;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int64_t r = i / (d / 4);
-    const int c = static_cast<int>(i % (d / 4)) * 4;
+    const int64_t r = i / q;
+    const int c = static_cast<int>(i % q) * 4;
+    if (c == d) {
+      const float4 e = make_float4(1.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(U + r * ldu + c) = e;
+      *reinterpret_cast<float4*>(M + r * ldu + c) = e;
+      continue;
+    }
     const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + c);
     const float4 s = *reinterpret_cast<const float4*>(S + r * lds + c);
-    *reinterpret_cast<float4*>(U + r * d + c) = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
-    *reinterpret_cast<float4*>(M + r * d + c) = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
+    *reinterpret_cast<float4*>(U + r * ldu + c) = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
+    *reinterpret_cast<float4*>(M + r * ldu + c) = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
   }
+}
+
+// [dW | db] = sum over row chunks of the slabs [nb][dout][d_in + 4], in chunk order
+__global__ __launch_bounds__(256) void wslab_reduce_kernel(const float* __restrict__ slabs, int nb, int din, int dout,
+                                                           float* __restrict__ dW, float* __restrict__ db) {
+  const int w = din + 4;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= dout * (din + 1)) return;
+  const int o = i / (din + 1), k = i % (din + 1);
+  float acc = 0.f;
+  for (int b = 0; b < nb; ++b) acc += slabs[static_cast<int64_t>(b) * dout * w + o * w + k];
+  if (k < din) dW[o * din + k] = acc;
+  else db[o] = acc;
 }
 
 // one wave per row; P1/P2 [n, dout] in, P+b written back (the backward's sign source)
@@ -123,10 +145,9 @@ __global__ __launch_bounds__(256) void dxs_kernel(float* __restrict__ dXd, int64
   }
 }
 
-__global__ void ones_kernel(float* __restrict__ o, int64_t n) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) o[i] = 1.f;
-}
+constexpr int64_t kGemmChunk = 65536;  // rows per split-K chunk of the weight-gradient GEMMs
+
+inline int64_t wslab_count(int64_t n) { return (n + kGemmChunk - 1) / kGemmChunk; }
 
 static rocblas_handle blas_handle(hipStream_t st, int* err) {
   static rocblas_handle h[16] = {};
@@ -165,7 +186,9 @@ extern "C" int64_t kgat_biinter_gemm_state_floats(int64_t n_rows, int32_t d_in, 
 
 extern "C" int64_t kgat_biinter_gemm_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {
   if (n_rows < 0 || !gemm_dims_ok(d_in, d_out)) return -1;
-  return n_rows * 2 * static_cast<int64_t>(d_in) + n_rows;
+  // U', M' [n, d_in + 4] + two sets of split-K slabs [chunks][d_out][d_in + 4]
+  return n_rows * 2 * static_cast<int64_t>(d_in + 4) +
+         2 * kgat::wslab_count(n_rows) * d_out * static_cast<int64_t>(d_in + 4) + 4;
 }
 
 extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
@@ -179,13 +202,14 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   if (n == 0) return KGAT_OK;
   if (!work || work_floats < kgat_biinter_gemm_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int ldu = d_in + 4;
   float* U = work;
-  float* M = work + n * d_in;
+  float* M = work + n * ldu;
   float* P1 = state;
   float* P2 = state + n * d_out;
   float* norm = state + 2 * n * d_out;
-  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * d_in / 4, 256, kgat::kCUs * 8)), dim3(256), 0, st, X,
-                     ldx, S, lds, U, M, n, d_in);
+  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
+                     st, X, ldx, S, lds, U, M, n, d_in);
   KGAT_LAUNCH_CHECK();
   int err = 0;
   rocblas_handle h = kgat::blas_handle(st, &err);
@@ -193,9 +217,9 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   const float one = 1.f, zero = 0.f;
   // row-major P[n, o] = U[n, k] W^T  <=>  column-major P^T[o, n] = W^T[o, k] ... (W row-major = W^T col-major)
   KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
-                          &one, W1, d_in, U, d_in, &zero, P1, d_out));
+                          &one, W1, d_in, U, ldu, &zero, P1, d_out));
   KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
-                          &one, W2, d_in, M, d_in, &zero, P2, d_out));
+                          &one, W2, d_in, M, ldu, &zero, P2, d_out));
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh, norm, n, d_out,
                      dropout_p, seed);
   KGAT_LAUNCH_CHECK();
@@ -229,9 +253,12 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
   float* dA = state;
   float* dB = state + n * d_out;
   const float* norm = state + 2 * n * d_out;
+  const int ldu = d_in + 4;
   float* U = work;
-  float* M = work + n * d_in;
-  float* ones = work + 2 * n * d_in;
+  float* M = work + n * ldu;
+  const int64_t nb = kgat::wslab_count(n);
+  float* slab1 = work + 2 * n * ldu;
+  float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   hipLaunchKernelGGL(kgat::epi_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, dH, lddh, n,
                      d_out, dropout_p, seed, key_rows);
   KGAT_LAUNCH_CHECK();
@@ -240,22 +267,31 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
                           W1, d_in, dA, d_out, &zero, dXd, static_cast<int>(lddxd)));
   KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
                           W2, d_in, dB, d_out, &zero, dS, static_cast<int>(ldds)));
-  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * d_in / 4, 256, kgat::kCUs * 8)), dim3(256), 0, st, X,
-                     ldx, S, lds, U, M, n, d_in);
+  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
+                     st, X, ldx, S, lds, U, M, n, d_in);
   KGAT_LAUNCH_CHECK();
   hipLaunchKernelGGL(kgat::dxs_kernel, dim3(kgat::blocks_for(n * d_in, 256, kgat::kCUs * 8)), dim3(256), 0, st, dXd,
                      lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
   KGAT_LAUNCH_CHECK();
-  // dW = dA^T U  (row-major [o, n] x [n, k]): column-major C[k, o] = U^T-view[k, n] x dA-view[n, o]
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, d_in, d_out, static_cast<int>(n),
-                          &one, U, d_in, dA, d_out, &zero, dW1, d_in));
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, d_in, d_out, static_cast<int>(n),
-                          &one, M, d_in, dB, d_out, &zero, dW2, d_in));
-  hipLaunchKernelGGL(kgat::ones_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs)), dim3(256), 0, st, ones, n);
-  KGAT_LAUNCH_CHECK();
-  KGAT_BLAS(rocblas_sgemv(h, rocblas_operation_none, d_out, static_cast<int>(n), &one, dA, d_out, ones, 1, &zero, db1,
-                          1));
-  KGAT_BLAS(rocblas_sgemv(h, rocblas_operation_none, d_out, static_cast<int>(n), &one, dB, d_out, ones, 1, &zero, db2,
-                          1));
+  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order)
+  //   column-major C_b[ldu, d_out] = U'_b-view[ldu, k] x dA_b-view^T[k, d_out]
+  const int64_t full = n / kgat::kGemmChunk, rest = n - full * kgat::kGemmChunk;
+  for (int mat = 0; mat < 2; ++mat) {
+    const float* Um = mat == 0 ? U : M;
+    const float* G = mat == 0 ? dA : dB;
+    float* sl = mat == 0 ? slab1 : slab2;
+    if (full > 0)
+      KGAT_BLAS(rocblas_sgemm_strided_batched(
+          h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(kgat::kGemmChunk), &one,
+          Um, ldu, kgat::kGemmChunk * ldu, G, d_out, kgat::kGemmChunk * d_out, &zero, sl, ldu,
+          static_cast<int64_t>(ldu) * d_out, static_cast<int>(full)));
+    if (rest > 0)
+      KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(rest),
+                              &one, Um + full * kgat::kGemmChunk * ldu, ldu, G + full * kgat::kGemmChunk * d_out, d_out,
+                              &zero, sl + full * ldu * static_cast<int64_t>(d_out), ldu));
+    hipLaunchKernelGGL(kgat::wslab_reduce_kernel, dim3((d_out * (d_in + 1) + 255) / 256), dim3(256), 0, st, sl,
+                       static_cast<int>(nb), d_in, d_out, mat == 0 ? dW1 : dW2, mat == 0 ? db1 : db2);
+    KGAT_LAUNCH_CHECK();
+  }
   return KGAT_OK;
 }

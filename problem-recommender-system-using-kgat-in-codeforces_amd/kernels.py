@@ -189,9 +189,13 @@ class BiState:
     fused shapes (kgat_biinter_fwd_f32 norm_out / mask_out): row norms + per-lane sign/keep words;
     wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
 
-    def __init__(self, n: int, device, d_in: int = 64, d_out: int = 64):
+    def __init__(self, n: int, device, d_in: int = 64, d_out: int = 64, kind: str | None = None):
         self.n, self.d_in, self.d_out = n, d_in, d_out
-        self.kind = "fused" if fused_supported(d_in, d_out) else "gemm"
+        if kind is None:
+            kind = "fused" if saved_state_supported(d_in, d_out) else "gemm"
+        if kind == "fused" and not saved_state_supported(d_in, d_out):
+            raise ValueError(f"no fused saved state for {d_in}->{d_out}")
+        self.kind = kind
         if self.kind == "fused":
             self.norm = torch.empty(max((n + 15) // 16 * 16, 16), dtype=torch.float32, device=device)
             self.mask = torch.empty(max((n + 15) // 16, 1) * 64, dtype=torch.int64, device=device)
@@ -211,10 +215,11 @@ def saved_state_supported(d_in: int, d_out: int) -> bool:
     return d_out <= 64 and d_in * d_out <= 4096
 
 
-def make_state(n: int, d_in: int, d_out: int, device) -> BiState | None:
-    """The state a training forward should keep for this layer (None: the backward recomputes)."""
-    if fused_supported(d_in, d_out):
-        return BiState(n, device, d_in, d_out) if saved_state_supported(d_in, d_out) else None
+def make_state(n: int, d_in: int, d_out: int, device) -> BiState:
+    """The state a training forward keeps for this layer's backward: the fused kernels' norm + sign
+    words where the saved-state backward exists (d_out <= 64, d_in*d_out <= 4096), else the GEMM
+    path's pre-activations -- e.g. C4's 128->128 layer, whose recomputing fused backward is 6x slower
+    than GEMMs on MI355X at 10M rows."""
     return BiState(n, device, d_in, d_out)
 
 
@@ -239,8 +244,8 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
         raise ValueError("W must be contiguous")
     if out is None:
         out = torch.empty(n, dout, dtype=torch.float32, device=X.device)
-    if not fused_supported(din, dout):
-        st = state if state is not None else BiState(n, X.device, din, dout)
+    if not fused_supported(din, dout) or (state is not None and state.kind == "gemm"):
+        st = state if state is not None else BiState(n, X.device, din, dout, kind="gemm")
         if st.kind != "gemm" or st.n != n:
             raise ValueError("bi-interaction state does not match the layer")
         work = _gemm_work(n, din, dout, X.device)
@@ -286,7 +291,7 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     dW2 = torch.empty_like(W2)
     db1 = torch.empty_like(b1)
     db2 = torch.empty_like(b2)
-    if not fused_supported(din, dout):
+    if not fused_supported(din, dout) or (state is not None and state.kind == "gemm"):
         _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, dropout_p, seed, dXd, dS, dW1, db1, dW2, db2, rows, H, state)
         return dXd, dS, dW1, db1, dW2, db2
     ws_n = int(_lib.lib().kgat_biinter_bwd_workspace(n, din, dout))
@@ -310,7 +315,7 @@ def _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, p, seed, dXd, dS, dW1, db1, dW2,
     dout = W1.shape[0]
     dev = X.device
     if H is None or state is None:  # no saved forward: recompute it
-        state = BiState(src_rows, dev, din, dout)
+        state = BiState(src_rows, dev, din, dout, kind="gemm")
         H = biinter_fwd(X, S, W1, b1, W2, b2, p, seed, state=state)
     if state.kind != "gemm" or state.n != src_rows:
         raise ValueError("bi-interaction state does not match the layer")
@@ -319,7 +324,7 @@ def _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, p, seed, dXd, dS, dW1, db1, dW2,
         n = rows.numel()
         P1, P2, norm = state.gemm_views()
         Xc, Sc, Hc = gather_rows(X, rows), gather_rows(S, rows), gather_rows(H, rows)
-        comp = BiState(n, dev, din, dout)
+        comp = BiState(n, dev, din, dout, kind="gemm")
         c1, c2, cn = comp.gemm_views()
         gather_rows(P1, rows, out=c1)
         gather_rows(P2, rows, out=c2)
