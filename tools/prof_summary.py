@@ -9,9 +9,10 @@ import sys
 def main() -> None:
     src, out, cmd = sys.argv[1], sys.argv[2], sys.argv[3]
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 12
+    cfg = sys.argv[5] if len(sys.argv) > 5 else "C2"
     rows = list(csv.DictReader(open(src)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    lines = [f"# rocprofv3 --kernel-trace --stats -- {cmd} (C2, 1x MI355X)",
+    lines = [f"# rocprofv3 --kernel-trace --stats -- {cmd} ({cfg}, 1x MI355X)",
              f"# {steps} CF steps profiled (warm-up + timed); avg per launch; per-step = total / {steps}", "",
              "| kernel | calls | avg us | us / step | % |", "|---|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
