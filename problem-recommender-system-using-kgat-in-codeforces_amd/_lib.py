@@ -113,7 +113,7 @@ _SIGNATURES = {
     "kgat_nfm_act_floats": (c_i64, [ctypes.POINTER(NFMNet), c_i64]),
     "kgat_nfm_fwd_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_nfm_loss_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),
-    "kgat_nfm_bwd_workspace": (c_i64, [ctypes.POINTER(NFMNet), c_i64]),
+    "kgat_nfm_bwd_workspace": (c_i64, [ctypes.POINTER(NFMNet), c_i64, c_i64]),
     "kgat_nfm_bwd_f32": (ctypes.c_int, [ctypes.POINTER(NFMNet), c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_f32,
                                         c_vp, c_i64, c_vp, c_vp, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp,
                                         c_i64, c_vp]),

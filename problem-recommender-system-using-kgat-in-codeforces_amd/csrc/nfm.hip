@@ -12,6 +12,8 @@
 // duplicate feature ids summed in entry order: deterministic, no atomics.
 #include <cmath>
 
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -54,78 +56,252 @@ __device__ __forceinline__ int64_t act_width(const NfmNet& N) {
   return w;
 }
 
-__global__ __launch_bounds__(256) void nfm_fwd_kernel(NfmNet N, const int64_t* __restrict__ rowptr,
-                                                      const int64_t* __restrict__ col, const float* __restrict__ val,
-                                                      int64_t rows, float* __restrict__ act, float* __restrict__ y) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+__device__ __forceinline__ void wave_lds_sync() {
+  // orders this wave's LDS writes before its later LDS reads of other lanes' data
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS plan of the forward (offsets / pitches in floats).  With `wlds` the hidden
+// weights sit in LDS zero-padded to [round16(dout)][round16(din) + 4] (+4: the 16
+// rows a B fragment reads land 4 banks apart) with round16(dout) biases; then one
+// 16 x P activation tile per wave.
+struct NfmLds {
+  int w_off[kNfmMaxLayers], w_pitch[kNfmMaxLayers], b_off[kNfmMaxLayers];
+  int tile_off, P, total;
+  bool wlds;
+};
+
+// Forward over tiles of 16 rows, one tile per wave.
+//  pooling: 16-lane groups each pool one row; the row pointers of all 16 rows
+//           and the first 16 entries of the group's 4 rows are loaded up front,
+//           then 4 entries' embedding rows at a time; lane cl of a group owns
+//           columns cl + 16k; z goes to the wave's LDS tile (zero-padded to a
+//           multiple of 16 columns), s and z to act;
+//  layers:  pre[16][dout] = h[16][din] W^T on v_mfma_f32_16x16x4_f32 -- lane l
+//           feeds A = h[l&15][k] and B = W[n][k] for k = k0 + 4(l>>4) + j, four
+//           MFMAs per 16-wide k step; bias, act store, ReLU and dropout fused on
+//           the accumulators, which overwrite the tile once the layer is done;
+//  head:    y = (x w + b) + W_out . h_L, a 16-lane reduction per row.
+// NC: dims <= 16 NC (column slots per pooling lane and output blocks per layer).
+// One hidden layer on a wave's 16-row tile: pre = h W^T + b (NB output blocks of 16,
+// blocks past dout read clamped weights and are dropped), act store, ReLU,
+// dropout; the result overwrites the tile.
+template <int NB, bool WLDS>
+__device__ __forceinline__ void nfm_layer(const NfmNet& N, const NfmLds& plan, const float* smem, float* tile, int l,
+                                          int64_t off, int64_t row0, int64_t rows, float* __restrict__ act, int64_t aw,
+                                          float scale) {
   const int lane = threadIdx.x & 63;
-  if (r >= rows) return;
-  const int d = N.dims[0];
-  const int64_t beg = rowptr[r], end = rowptr[r + 1];
-  float s[kNfmCols] = {0.f, 0.f, 0.f, 0.f}, q[kNfmCols] = {0.f, 0.f, 0.f, 0.f};
-  float wide = 0.f;
-  for (int64_t e = beg; e < end; ++e) {
-    const int64_t c = col[e];
-    const float x = val[e];
-    const float* v = N.V + c * N.ldv;
+  const int g = lane >> 4, cl = lane & 15;
+  const int P = plan.P;
+  const int din = N.dims[l], dout = N.dims[l + 1];
+  const int kpad = (din + 15) & ~15;
+  const int nblk = (dout + 15) >> 4;
+  floatx4 acc[NB];
 #pragma unroll
-    for (int cc = 0; cc < kNfmCols; ++cc) {
-      const int j = lane + 64 * cc;
-      if (j < d) {
-        const float t = x * v[j];
-        s[cc] += t;
-        q[cc] = fmaf(t, t, q[cc]);
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int wp = WLDS ? plan.w_pitch[l] : 0;
+  const float* wlds = WLDS ? smem + plan.w_off[l] + cl * wp + 4 * g : nullptr;
+  const float* a_row = tile + cl * P + 4 * g;
+  for (int k0 = 0; k0 < kpad; k0 += 16) {  // one A fragment feeds NB interleaved MFMA chains
+    const float4 a4 = *reinterpret_cast<const float4*>(a_row + k0);
+    float4 b4[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {  // every B fragment of the step read before the first MFMA
+      const int nbc = nb < nblk ? nb : nblk - 1;
+      if (WLDS) {
+        b4[nb] = *reinterpret_cast<const float4*>(wlds + nbc * 16 * wp + k0);
+      } else {
+        const int n = nbc * 16 + cl, kk = k0 + 4 * g;
+        const float* wr = N.W[l] + static_cast<int64_t>(n < dout ? n : 0) * din;
+        b4[nb].x = (n < dout && kk < din) ? wr[kk] : 0.f;
+        b4[nb].y = (n < dout && kk + 1 < din) ? wr[kk + 1] : 0.f;
+        b4[nb].z = (n < dout && kk + 2 < din) ? wr[kk + 2] : 0.f;
+        b4[nb].w = (n < dout && kk + 3 < din) ? wr[kk + 3] : 0.f;
       }
     }
-    if (lane == 0) wide = fmaf(x, N.w_lin[c], wide);
-  }
-  float h[kNfmCols];
-  float* ar = act ? act + r * act_width(N) : nullptr;
 #pragma unroll
-  for (int cc = 0; cc < kNfmCols; ++cc) {
-    const int j = lane + 64 * cc;
-    h[cc] = 0.5f * (s[cc] * s[cc] - q[cc]);
-    if (ar && j < d) {
-      ar[j] = s[cc];
-      ar[d + j] = h[cc];
+    for (int nb = 0; nb < NB; ++nb) {
+      acc[nb] = mfma16x4(a4.x, b4[nb].x, acc[nb]);
+      acc[nb] = mfma16x4(a4.y, b4[nb].y, acc[nb]);
+      acc[nb] = mfma16x4(a4.z, b4[nb].z, acc[nb]);
+      acc[nb] = mfma16x4(a4.w, b4[nb].w, acc[nb]);
     }
   }
+  wave_lds_sync();  // every lane has read the layer input
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    if (nb < nblk) {
+      const int n = nb * 16 + cl;
+      const float bias = WLDS ? smem[plan.b_off[l] + n] : (n < dout ? N.b[l][n] : 0.f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = g * 4 + i;
+        const int64_t r = row0 + m;
+        const float pre = acc[nb][i] + bias;
+        if (act && r < rows && n < dout) act[r * aw + off + n] = pre;
+        float h = fmaxf(pre, 0.f);
+        if (N.p > 0.f) h = nfm_keep(N, l, r, n) ? h * scale : 0.f;
+        tile[m * P + n] = n < dout ? h : 0.f;
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
+template <int NC, bool WLDS>
+__device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan, const float* smem, float* tile,
+                                             int64_t row0, const int64_t* __restrict__ rowptr,
+                                             const int64_t* __restrict__ col, const float* __restrict__ val,
+                                             int64_t rows, float* __restrict__ act, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, cl = lane & 15;
+  const int P = plan.P;
+  const int d = N.dims[0];
+  const int dpad = (d + 15) & ~15;
+  const int64_t aw = act_width(N);
+  // row pointers of the wave's 16 rows (lanes 0..16); rows past the end are empty
+  int rp = 0;  // entry offsets fit 32 bits (a batch holds < 2^31 entries)
+  if (lane <= 16) rp = static_cast<int>(rowptr[row0 + lane < rows ? row0 + lane : rows]);
+  int colk[NC];
+  float colm[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {  // this lane's pooling columns, clamped to the row (exact x*v*1 when inside)
+    colk[k] = cl + 16 * k < d ? cl + 16 * k : d - 1;
+    colm[k] = cl + 16 * k < d ? 1.f : 0.f;
+  }
+  // round rr pools row rr*4 + g; lane cl holds entry beg + cl (past the end: x = 0),
+  // and the next round's entries are loaded while this round's rows are fetched
+  int nbeg = __shfl(rp, g), nend = __shfl(rp, g + 1);
+  int nce = nend > nbeg ? static_cast<int>(col[nbeg + (cl < nend - nbeg ? cl : 0)]) : 0;
+  float nxe = cl < nend - nbeg ? val[nbeg + cl] : 0.f;
+#pragma unroll 1
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = rr * 4 + g;
+    const int64_t r = row0 + m;
+    const int beg = nbeg, end = nend;
+    const int ce = nce;
+    const float xe = nxe;
+    if (rr < 3) {
+      nbeg = __shfl(rp, m + 4);
+      nend = __shfl(rp, m + 5);
+      nce = nend > nbeg ? static_cast<int>(col[nbeg + (cl < nend - nbeg ? cl : 0)]) : 0;
+      nxe = cl < nend - nbeg ? val[nbeg + cl] : 0.f;
+    }
+    float s[NC], q[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s[k] = q[k] = 0.f;
+    float wd = 0.f;
+    for (int e0 = beg; e0 < end; e0 += 16) {
+      const int cnt = end - e0 < 16 ? end - e0 : 16;
+      int c_l = ce;
+      float x_l = xe;
+      if (e0 != beg) {  // rows of more than 16 entries
+        c_l = static_cast<int>(col[e0 + (cl < cnt ? cl : 0)]);
+        x_l = cl < cnt ? val[e0 + cl] : 0.f;
+      }
+      wd = fmaf(x_l, N.w_lin[c_l], wd);
+      constexpr int EB = NC <= 4 ? 8 : 4;     // entries whose loads are in flight together
+      for (int k0 = 0; k0 < cnt; k0 += EB) {  // summed in entry order
+        float xb[EB], vb[EB][NC];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          const int src = g * 16 + (k0 + u < 16 ? k0 + u : 15);
+          const uint32_t c = static_cast<uint32_t>(__shfl(c_l, src));
+          xb[u] = k0 + u < 16 ? __shfl(x_l, src) : 0.f;
+          const float* v = N.V + static_cast<uint64_t>(c) * static_cast<uint32_t>(N.ldv);
+#pragma unroll
+          for (int k = 0; k < NC; ++k) vb[u][k] = v[colk[k]];  // unconditional: columns clamped, masked below
+        }
+#pragma unroll
+        for (int u = 0; u < EB; ++u)
+#pragma unroll
+          for (int k = 0; k < NC; ++k) {
+            const float t = xb[u] * vb[u][k] * colm[k];
+            s[k] += t;
+            q[k] = fmaf(t, t, q[k]);
+          }
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) wd += __shfl_xor(wd, o);
+    if (cl == 0) tile[m * P + P - 1] = wd;  // the wide head waits in the tile's last pad column
+    float* ar = act && r < rows ? act + r * aw : nullptr;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int j = cl + 16 * k;
+      if (j < dpad) {
+        const float z = j < d ? 0.5f * (s[k] * s[k] - q[k]) : 0.f;
+        tile[m * P + j] = z;
+        if (ar && j < d) {
+          ar[j] = s[k];
+          ar[d + j] = z;
+        }
+      }
+    }
+  }
+  wave_lds_sync();
   int64_t off = 2 * d;
   const float scale = N.p > 0.f ? 1.f / (1.f - N.p) : 1.f;
   for (int l = 0; l < N.n_layers; ++l) {
-    const int din = N.dims[l], dout = N.dims[l + 1];
-    const float* W = N.W[l];
-    float nh[kNfmCols] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int cc = 0; cc < kNfmCols; ++cc) {
-      const int o = lane + 64 * cc;
-      float acc = 0.f;
-      for (int i = 0; i < din; ++i) {
-        const float hi = vget(h, i);
-        if (o < dout) acc = fmaf(W[static_cast<int64_t>(o) * din + i], hi, acc);
-      }
-      if (o < dout) {
-        const float pre = acc + N.b[l][o];
-        if (ar) ar[off + o] = pre;
-        float a = fmaxf(pre, 0.f);
-        if (N.p > 0.f) a = nfm_keep(N, l, r, o) ? a * scale : 0.f;
-        nh[cc] = a;
-      }
-    }
-#pragma unroll
-    for (int cc = 0; cc < kNfmCols; ++cc) h[cc] = nh[cc];
-    off += dout;
+    const int nblk = (N.dims[l + 1] + 15) >> 4;  // output blocks: a compile-time count per instance
+    if (nblk <= 1) nfm_layer<1, WLDS>(N, plan, smem, tile, l, off, row0, rows, act, aw, scale);
+    else if (nblk <= 2) nfm_layer<2, WLDS>(N, plan, smem, tile, l, off, row0, rows, act, aw, scale);
+    else if (nblk <= 4 || NC < 8) nfm_layer<(NC < 4 ? NC : 4), WLDS>(N, plan, smem, tile, l, off, row0, rows, act, aw, scale);
+    else if (nblk <= 8 || NC < 16) nfm_layer<(NC < 8 ? NC : 8), WLDS>(N, plan, smem, tile, l, off, row0, rows, act, aw, scale);
+    else nfm_layer<NC, WLDS>(N, plan, smem, tile, l, off, row0, rows, act, aw, scale);
+    off += N.dims[l + 1];
   }
   const int dl = N.dims[N.n_layers];
-  float deep = 0.f;
 #pragma unroll
-  for (int cc = 0; cc < kNfmCols; ++cc) {
-    const int j = lane + 64 * cc;
-    if (j < dl) deep = fmaf(N.W_out[j], h[cc], deep);
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = rr * 4 + g;
+    float deep = 0.f;
+    for (int j = cl; j < dl; j += 16) deep = fmaf(N.W_out[j], tile[m * P + j], deep);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) deep += __shfl_xor(deep, o);
+    const int64_t r = row0 + m;
+    if (cl == 0 && r < rows) y[r] = (tile[m * P + P - 1] + N.b_lin[0]) + deep;
   }
-  deep = wave_sum(deep);
-  if (lane == 0) y[r] = (wide + N.b_lin[0]) + deep;
+  wave_lds_sync();  // the tile is free for the wave's next rows
 }
+
+template <int NC, bool WLDS>
+__global__ __launch_bounds__(256, NC <= 4 ? 3 : NC <= 8 ? 2 : 1) void nfm_fwd_kernel(NfmNet N, NfmLds plan, const int64_t* __restrict__ rowptr,
+                                                      const int64_t* __restrict__ col, const float* __restrict__ val,
+                                                      int64_t rows, float* __restrict__ act, float* __restrict__ y) {
+  extern __shared__ float smem[];
+  const int wv = threadIdx.x >> 6;
+  if (WLDS) {  // stage the hidden layers once per block (8 loads in flight per thread)
+    for (int l = 0; l < N.n_layers; ++l) {
+      const int din = N.dims[l], dout = N.dims[l + 1], pitch = plan.w_pitch[l];
+      const int npad = (dout + 15) & ~15;
+      const int total = npad * pitch;
+      for (int t0 = threadIdx.x; t0 < total; t0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int t = t0 + u * 256;
+          const int n = t / pitch, k = t - n * pitch;
+          v[u] = (t < total && n < dout && k < din) ? N.W[l][static_cast<int64_t>(n) * din + k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t0 + u * 256 < total) smem[plan.w_off[l] + t0 + u * 256] = v[u];
+      }
+      for (int t = threadIdx.x; t < npad; t += 256) smem[plan.b_off[l] + t] = t < dout ? N.b[l][t] : 0.f;
+    }
+    __syncthreads();
+  }
+  float* tile = smem + plan.tile_off + wv * 16 * plan.P;
+  // persistent: the block walks 64-row groups (the staged weights serve them all)
+  for (int64_t grp = blockIdx.x; grp * 64 < rows; grp += gridDim.x) {
+    const int64_t row0 = grp * 64 + wv * 16;
+    if (row0 < rows) nfm_fwd_tile<NC, WLDS>(N, plan, smem, tile, row0, rowptr, col, val, rows, act, y);
+  }
+}
+
 
 // loss over B pairs (rows b and B+b); dy[row] = dL/dy (before the upstream scale)
 __global__ __launch_bounds__(256) void nfm_loss_kernel(const float* __restrict__ y, int batch, const float* __restrict__ W_out,
@@ -232,12 +408,15 @@ __device__ __forceinline__ float nfm_hin(const NfmNet& N, const float* ar, int l
 
 // Layer l < L: dW_l[o][i] = sum_r dpre_l[r][o] * hin_l[r][i], db_l[o] = sum_r dpre_l[r][o];
 // l == L (output head): dW_out[j] = sum_r g_r h_L[r][j] + lam W_out[j], db_lin = sum_r g_r.
-// Rows are summed in row order (deterministic); one thread per output element.
+// Split over 64-row chunks (blockIdx.y): one thread per output element sums its chunk's rows
+// in row order into part[chunk][t]; nfm_wgrad_reduce_kernel then adds the chunks in chunk
+// order -- deterministic, and every CU has work at training batch sizes.
+constexpr int kNfmRowChunk = 64;
+
 __global__ __launch_bounds__(256) void nfm_wgrad_kernel(NfmNet N, int l, const float* __restrict__ act, int64_t rows,
                                                         const float* __restrict__ dy, const float* __restrict__ gout,
-                                                        const float* __restrict__ dpre_ws, float lam,
-                                                        float* __restrict__ dWl, float* __restrict__ dbl,
-                                                        float* __restrict__ dW_out, float* __restrict__ db_lin) {
+                                                        const float* __restrict__ dpre_ws, int w,
+                                                        float* __restrict__ part) {
   const int L = N.n_layers;
   int64_t pre_off[kNfmMaxLayers], dp_off[kNfmMaxLayers];
   int64_t o1 = 2 * N.dims[0], o2 = 0;
@@ -250,84 +429,206 @@ __global__ __launch_bounds__(256) void nfm_wgrad_kernel(NfmNet N, int l, const f
   const int64_t aw = o1, hsum = o2;
   const float scale = N.p > 0.f ? 1.f / (1.f - N.p) : 1.f;
   const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= w) return;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kNfmRowChunk;
+  const int64_t r1 = r0 + kNfmRowChunk < rows ? r0 + kNfmRowChunk : rows;
+  float acc = 0.f;
   if (l < L) {
     const int din = N.dims[l], dout = N.dims[l + 1];
     if (t < dout * din) {
       const int o = t / din, i = t % din;
-      float acc = 0.f;
-      for (int64_t r = 0; r < rows; ++r)
+      for (int64_t r = r0; r < r1; ++r)
         acc = fmaf(dpre_ws[r * hsum + dp_off[l] + o], nfm_hin(N, act + r * aw, l, r, i, pre_off, scale), acc);
-      dWl[t] = acc;
-    } else if (t < dout * din + dout) {
+    } else {
       const int o = t - dout * din;
-      float acc = 0.f;
-      for (int64_t r = 0; r < rows; ++r) acc += dpre_ws[r * hsum + dp_off[l] + o];
-      dbl[o] = acc;
+      for (int64_t r = r0; r < r1; ++r) acc += dpre_ws[r * hsum + dp_off[l] + o];
     }
   } else {
     const int dl = N.dims[L];
     const float go = gout[0];
     if (t < dl) {
-      float acc = 0.f;
-      for (int64_t r = 0; r < rows; ++r) acc = fmaf(go * dy[r], nfm_hin(N, act + r * aw, L, r, t, pre_off, scale), acc);
-      dW_out[t] = acc + go * lam * N.W_out[t];
-    } else if (t == dl) {
-      float acc = 0.f;
-      for (int64_t r = 0; r < rows; ++r) acc += go * dy[r];
-      db_lin[0] = acc;
+      for (int64_t r = r0; r < r1; ++r) acc = fmaf(go * dy[r], nfm_hin(N, act + r * aw, L, r, t, pre_off, scale), acc);
+    } else {
+      for (int64_t r = r0; r < r1; ++r) acc += go * dy[r];
     }
+  }
+  part[static_cast<int64_t>(blockIdx.y) * w + t] = acc;
+}
+
+__global__ __launch_bounds__(256) void nfm_wgrad_reduce_kernel(NfmNet N, int l, const float* __restrict__ part,
+                                                               int nchunks, int w, const float* __restrict__ gout,
+                                                               float lam, float* __restrict__ dWl,
+                                                               float* __restrict__ dbl, float* __restrict__ dW_out,
+                                                               float* __restrict__ db_lin) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= w) return;
+  float acc = 0.f;
+  for (int k = 0; k < nchunks; ++k) acc += part[static_cast<int64_t>(k) * w + t];
+  const int L = N.n_layers;
+  if (l < L) {
+    const int n_w = N.dims[l] * N.dims[l + 1];
+    if (t < n_w) dWl[t] = acc;
+    else dbl[t - n_w] = acc;
+  } else {
+    const int dl = N.dims[L];
+    if (t < dl) dW_out[t] = acc + gout[0] * lam * N.W_out[t];
+    else db_lin[0] = acc;
   }
 }
 
 // Feature gradients: entry k (row rk, feature ck, value xk) contributes
 //   dV[ck]  += xk * (s_rk - xk V[ck]) * dz_rk        d z / d V through the pooling
 //   dw[ck]  += xk * g_rk                               the wide head
-// One wave per entry; the first entry of each feature id owns the feature row
-// and sums every entry of that id in entry order.  dV / dw are zero-filled.
-__global__ __launch_bounds__(256) void nfm_feat_kernel(NfmNet N, const int64_t* __restrict__ erow,
-                                                       const int64_t* __restrict__ col, const float* __restrict__ val,
-                                                       int64_t nnz, const float* __restrict__ act,
-                                                       const float* __restrict__ dz_ws, const float* __restrict__ dy,
-                                                       const float* __restrict__ gout, float* __restrict__ dV,
-                                                       int64_t lddv, float* __restrict__ dw) {
-  const int64_t k = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+// The entries are radix-sorted by feature id (stable: entry order kept within a
+// feature), and every run of equal ids is summed in entry order by exactly one
+// writer of its feature row -- deterministic, no atomics.  dV / dw are zero-filled.
+__global__ __launch_bounds__(256) void nfm_feat_keys_kernel(const int64_t* __restrict__ col, int64_t nnz,
+                                                            uint32_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (k >= nnz) return;
-  const int64_t c = col[k];
-  bool dup = false;
-  for (int64_t s0 = 0; s0 < k && !dup; s0 += 64) dup = __any(s0 + lane < k && col[s0 + lane] == c);
-  if (dup) return;
+  keys[k] = static_cast<uint32_t>(col[k]);
+  idx[k] = static_cast<uint32_t>(k);
+}
+
+// The sorted entries are cut into chunks of kFeatChunk; one wave per chunk walks
+// its runs ("pieces") in order, four entries' rows loaded at a time.  A piece
+// that is a whole run writes dV / dw itself; a piece of a run that crosses a
+// chunk edge leaves its partial sum in slot 0 (piece at the chunk start) or 1
+// (piece at the end) of its chunk, and nfm_feat_join_kernel has the chunk where
+// the run starts add those partials in chunk order.
+constexpr int kFeatChunk = 16;
+
+__global__ __launch_bounds__(256) void nfm_feat_piece_kernel(
+    NfmNet N, const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sidx, const int64_t* __restrict__ erow,
+    const float* __restrict__ val, int64_t nnz, const float* __restrict__ act, const float* __restrict__ dz_ws,
+    const float* __restrict__ dy, const float* __restrict__ gout, float* __restrict__ dV, int64_t lddv,
+    float* __restrict__ dw, float* __restrict__ slots) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t base = c * kFeatChunk;
+  if (base >= nnz) return;
+  const int cnt = nnz - base < kFeatChunk ? static_cast<int>(nnz - base) : kFeatChunk;
   const int d = N.dims[0];
-  int64_t aw = 2 * d;
-  for (int l = 0; l < N.n_layers; ++l) aw += N.dims[l + 1];
+  const int64_t aw = act_width(N);
   const float go = gout[0];
-  const float* vc = N.V + c * N.ldv;
-  float g[kNfmCols] = {0.f, 0.f, 0.f, 0.f};
+  uint32_t key_l = 0;
+  int64_t r_l = 0;
+  float x_l = 0.f;
+  if (lane < cnt) {
+    key_l = skey[base + lane];
+    const int64_t e = sidx[base + lane];
+    r_l = erow[e];
+    x_l = val[e];
+  }
+  const float gy_l = lane < cnt ? go * dy[r_l] : 0.f;
+  const bool prev_same = base > 0 && skey[base - 1] == __shfl(key_l, 0);
+  const bool next_same = base + cnt < nnz && skey[base + cnt] == __shfl(key_l, cnt - 1);
+  const int64_t slot_w = d + 1;
+  float g[kNfmCols] = {0.f, 0.f, 0.f, 0.f}, vcur[kNfmCols] = {0.f, 0.f, 0.f, 0.f};
   float gw = 0.f;
-  for (int64_t s0 = k; s0 < nnz; s0 += 64) {
-    unsigned long long mask = __ballot(s0 + lane < nnz && col[s0 + lane] == c);
-    while (mask) {
-      const int bit = __ffsll(static_cast<long long>(mask)) - 1;
-      mask &= mask - 1;
-      const int64_t e = s0 + bit;
-      const int64_t r = erow[e];
-      const float x = val[e];
-      const float* sr = act + r * aw;
-      const float* dzr = dz_ws + r * d;
+  int ps = 0;
+  for (int j0 = 0; j0 < cnt; j0 += 4) {
+    float sr[4][kNfmCols], dz[4][kNfmCols], vv[4][kNfmCols];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u < cnt ? j0 + u : cnt - 1;
+      const int64_t r = __shfl(r_l, j);
+      const uint32_t k = __shfl(key_l, j);
 #pragma unroll
       for (int cc = 0; cc < kNfmCols; ++cc) {
-        const int j = lane + 64 * cc;
-        if (j < d) g[cc] = fmaf(x * (sr[j] - x * vc[j]), dzr[j], g[cc]);
+        const int col = lane + 64 * cc;
+        const bool in = col < d;
+        sr[u][cc] = in ? act[r * aw + col] : 0.f;
+        dz[u][cc] = in ? dz_ws[r * d + col] : 0.f;
+        vv[u][cc] = in ? N.V[static_cast<int64_t>(k) * N.ldv + col] : 0.f;
       }
-      gw = fmaf(x, go * dy[r], gw);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u;
+      if (j >= cnt) break;
+      const uint32_t k = __shfl(key_l, j);
+      if (j == ps) {
+#pragma unroll
+        for (int cc = 0; cc < kNfmCols; ++cc) vcur[cc] = vv[u][cc];
+      }
+      const float x = __shfl(x_l, j);
+#pragma unroll
+      for (int cc = 0; cc < kNfmCols; ++cc) g[cc] = fmaf(x * (sr[u][cc] - x * vcur[cc]), dz[u][cc], g[cc]);
+      gw = fmaf(x, __shfl(gy_l, j), gw);
+      const bool last = j == cnt - 1 || __shfl(key_l, j + 1 < cnt ? j + 1 : j) != k;
+      if (last) {
+        const bool cont_prev = ps == 0 && prev_same;
+        const bool cont_next = j == cnt - 1 && next_same;
+        float* dst;
+        if (!cont_prev && !cont_next) {  // a whole run: this wave owns feature k
+          dst = dV + static_cast<int64_t>(k) * lddv;
+#pragma unroll
+          for (int cc = 0; cc < kNfmCols; ++cc)
+            if (lane + 64 * cc < d) dst[lane + 64 * cc] += g[cc];
+          if (lane == 0) dw[k] += gw;
+        } else {
+          dst = slots + (c * 2 + (ps == 0 ? 0 : 1)) * slot_w;
+#pragma unroll
+          for (int cc = 0; cc < kNfmCols; ++cc)
+            if (lane + 64 * cc < d) dst[lane + 64 * cc] = g[cc];
+          if (lane == 0) dst[d] = gw;
+        }
+#pragma unroll
+        for (int cc = 0; cc < kNfmCols; ++cc) g[cc] = 0.f;
+        gw = 0.f;
+        ps = j + 1;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void nfm_feat_join_kernel(const uint32_t* __restrict__ skey, int64_t nnz, int d,
+                                                            const float* __restrict__ slots, float* __restrict__ dV,
+                                                            int64_t lddv, float* __restrict__ dw) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t base = c * kFeatChunk, cend = base + kFeatChunk;
+  if (cend >= nnz) return;
+  const uint32_t k = skey[cend - 1];
+  if (skey[cend] != k) return;                              // no run crosses this chunk's end
+  const bool piece_at_start = skey[base] == k;
+  if (piece_at_start && base > 0 && skey[base - 1] == k) return;  // the run started in an earlier chunk
+  const int64_t slot_w = d + 1;
+  float acc[kNfmCols];
+  const float* src = slots + (c * 2 + (piece_at_start ? 0 : 1)) * slot_w;
+#pragma unroll
+  for (int cc = 0; cc < kNfmCols; ++cc) acc[cc] = lane + 64 * cc < d ? src[lane + 64 * cc] : 0.f;
+  float aw = src[d];
+  const int64_t nch = (nnz + kFeatChunk - 1) / kFeatChunk;
+  bool more = true;
+  for (int64_t c2 = c + 1; more; c2 += 8) {  // later chunks: the run's piece sits at their start
+    float v[8][kNfmCols], vw[8];              // 8 chunks' loads in flight, added in chunk order
+    bool cont[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t cu = c2 + u;
+      const bool ok = cu < nch;
+      const float* p = slots + (ok ? cu : c2) * 2 * slot_w;
+#pragma unroll
+      for (int cc = 0; cc < kNfmCols; ++cc) v[u][cc] = lane + 64 * cc < d ? p[lane + 64 * cc] : 0.f;
+      vw[u] = p[d];
+      const int64_t e2 = (cu + 1) * kFeatChunk;
+      cont[u] = ok && e2 < nnz && skey[e2 - 1] == k && skey[e2] == k;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (!more) break;
+#pragma unroll
+      for (int cc = 0; cc < kNfmCols; ++cc) acc[cc] += v[u][cc];
+      aw += vw[u];
+      more = cont[u];
     }
   }
 #pragma unroll
-  for (int cc = 0; cc < kNfmCols; ++cc) {
-    const int j = lane + 64 * cc;
-    if (j < d) dV[c * lddv + j] += g[cc];
-  }
-  if (lane == 0) dw[c] += gw;
+  for (int cc = 0; cc < kNfmCols; ++cc)
+    if (lane + 64 * cc < d) dV[static_cast<int64_t>(k) * lddv + lane + 64 * cc] += acc[cc];
+  if (lane == 0) dw[k] += aw;
 }
 
 __global__ __launch_bounds__(256) void rowptr_kernel(const int64_t* __restrict__ rows_sorted, int64_t nnz,
@@ -395,8 +696,41 @@ extern "C" int kgat_nfm_fwd_f32(const kgat_nfm* net, const int64_t* rowptr, cons
   const kgat::NfmNet N = to_net(net);
   if (int e = kgat::check_net(N)) return e;
   if (rows == 0) return KGAT_OK;
-  hipLaunchKernelGGL(kgat::nfm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), N,
-                     rowptr, col, val, rows, act, y);
+  int dmax = 16;
+  for (int l = 0; l <= N.n_layers; ++l) dmax = N.dims[l] > dmax ? N.dims[l] : dmax;
+  kgat::NfmLds plan{};
+  plan.P = ((dmax + 15) & ~15) + 4;  // tile pitch: rows 4 banks apart
+  int o = 0;
+  for (int l = 0; l < N.n_layers; ++l) {
+    plan.w_off[l] = o;
+    plan.w_pitch[l] = ((N.dims[l] + 15) & ~15) + 4;
+    o += ((N.dims[l + 1] + 15) & ~15) * plan.w_pitch[l];
+    plan.b_off[l] = o;
+    o += (N.dims[l + 1] + 15) & ~15;
+  }
+  plan.wlds = o <= 12288;  // <= 48 KB of weights: 2-3 blocks per CU beside the tiles
+  plan.tile_off = plan.wlds ? o : 0;
+  plan.total = plan.tile_off + 4 * 16 * plan.P;
+  const size_t lds = sizeof(float) * static_cast<size_t>(plan.total);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nc = dmax <= 64 ? 4 : dmax <= 128 ? 8 : 16;
+  using Fn = void (*)(kgat::NfmNet, kgat::NfmLds, const int64_t*, const int64_t*, const float*, int64_t, float*, float*);
+  Fn fn = nc == 4    ? (plan.wlds ? kgat::nfm_fwd_kernel<4, true> : kgat::nfm_fwd_kernel<4, false>)
+          : nc == 8  ? (plan.wlds ? kgat::nfm_fwd_kernel<8, true> : kgat::nfm_fwd_kernel<8, false>)
+                     : (plan.wlds ? kgat::nfm_fwd_kernel<16, true> : kgat::nfm_fwd_kernel<16, false>);
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  int per_cu = 0;  // persistent grid: as many blocks as fit at once
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), 256, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t groups = (rows + 63) / 64;
+  const int64_t cap = static_cast<int64_t>(per_cu) * kgat::kCUs;
+  const dim3 grid(static_cast<unsigned>(groups < cap ? groups : cap));
+  hipLaunchKernelGGL(fn, grid, dim3(256), lds, st, N, plan, rowptr, col, val, rows, act, y);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -410,10 +744,48 @@ extern "C" int kgat_nfm_loss_f32(const kgat_nfm* net, const float* y, int32_t ba
   return KGAT_OK;
 }
 
-extern "C" int64_t kgat_nfm_bwd_workspace(const kgat_nfm* net, int64_t rows) {
+static int64_t nfm_wgrad_width(const kgat_nfm* net) {
+  int64_t w = net->dims[net->n_layers] + 1;
+  for (int l = 0; l < net->n_layers; ++l) {
+    const int64_t wl = static_cast<int64_t>(net->dims[l]) * net->dims[l + 1] + net->dims[l + 1];
+    if (wl > w) w = wl;
+  }
+  return w;
+}
+
+// workspace: dpre [rows][sum dims[1..L]] | dz [rows][d] | weight-gradient chunk
+// partials | run-piece partials [2 per 16 sorted entries][d + 1] | the feature sort: keys/idx in and out (4 nnz uint32) | radix-sort scratch
+struct NfmBwdWs {
+  int64_t dpre, dz, part, slots, sort, scratch, total;  // offsets in floats
+  size_t scratch_bytes;
+};
+
+static int nfm_bwd_ws(const kgat_nfm* net, int64_t rows, int64_t nnz, NfmBwdWs* w) {
   int64_t h = 0;
   for (int l = 0; l < net->n_layers; ++l) h += net->dims[l + 1];
-  return rows * (h + net->dims[0]);
+  const int64_t chunks = (rows + kgat::kNfmRowChunk - 1) / kgat::kNfmRowChunk;
+  w->dpre = 0;
+  w->dz = rows * h;
+  w->part = w->dz + rows * net->dims[0];
+  w->slots = w->part + chunks * nfm_wgrad_width(net);
+  w->sort = w->slots + 2 * ((nnz + kgat::kFeatChunk - 1) / kgat::kFeatChunk) * (net->dims[0] + 1);
+  w->scratch_bytes = 0;
+  if (nnz > 0) {
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
+        nullptr, w->scratch_bytes, static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr),
+        static_cast<const uint32_t*>(nullptr), static_cast<uint32_t*>(nullptr), static_cast<int>(nnz), 0, 32);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  w->scratch = (w->sort + 4 * nnz + 63) & ~static_cast<int64_t>(63);  // 256-byte aligned
+  w->total = w->scratch + static_cast<int64_t>((w->scratch_bytes + 3) / 4);
+  return KGAT_OK;
+}
+
+extern "C" int64_t kgat_nfm_bwd_workspace(const kgat_nfm* net, int64_t rows, int64_t nnz) {
+  if (!net || rows < 0 || nnz < 0 || nnz > INT32_MAX) return -1;
+  NfmBwdWs w;
+  if (nfm_bwd_ws(net, rows, nnz, &w) != KGAT_OK) return -1;
+  return w.total;
 }
 
 extern "C" int kgat_nfm_bwd_f32(const kgat_nfm* net, const int64_t* erow, const int64_t* col, const float* val,
@@ -426,26 +798,47 @@ extern "C" int kgat_nfm_bwd_f32(const kgat_nfm* net, const int64_t* erow, const 
   const kgat::NfmNet N = to_net(net);
   if (int e = kgat::check_net(N)) return e;
   if (N.n_layers > 0 && (!dW || !db)) return KGAT_ERR_INVALID;
-  if (workspace_floats < kgat_nfm_bwd_workspace(net, rows)) return KGAT_ERR_WORKSPACE;
+  if (nnz > INT32_MAX || (nnz > 0 && (!erow || !col || !val))) return KGAT_ERR_INVALID;
+  NfmBwdWs ws;
+  if (int e = nfm_bwd_ws(net, rows, nnz, &ws)) return e;
+  if (workspace_floats < ws.total) return KGAT_ERR_WORKSPACE;
   if (rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int64_t hsum = 0;
-  for (int l = 0; l < N.n_layers; ++l) hsum += N.dims[l + 1];
-  float* dpre = workspace;
-  float* dz = workspace + rows * hsum;
+  float* dpre = workspace + ws.dpre;
+  float* dz = workspace + ws.dz;
+  float* part = workspace + ws.part;
+  const int nchunks = static_cast<int>((rows + kgat::kNfmRowChunk - 1) / kgat::kNfmRowChunk);
   hipLaunchKernelGGL(kgat::nfm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, N, act, rows, dy, grad_out, dpre, dz);
   KGAT_LAUNCH_CHECK();
-  for (int l = 0; l <= N.n_layers; ++l) {  // one launch per layer + the output head
+  for (int l = 0; l <= N.n_layers; ++l) {  // per layer + the output head: chunk partials, then their ordered sum
     const int w = l < N.n_layers ? N.dims[l] * N.dims[l + 1] + N.dims[l + 1] : N.dims[N.n_layers] + 1;
     float* wl = l < N.n_layers ? dW[l] : nullptr;
     float* bl = l < N.n_layers ? db[l] : nullptr;
-    hipLaunchKernelGGL(kgat::nfm_wgrad_kernel, dim3((w + 255) / 256), dim3(256), 0, st, N, l, act, rows, dy, grad_out,
-                       dpre, lam, wl, bl, dW_out, db_lin);
+    hipLaunchKernelGGL(kgat::nfm_wgrad_kernel, dim3((w + 255) / 256, nchunks), dim3(256), 0, st, N, l, act, rows, dy,
+                       grad_out, dpre, w, part);
+    KGAT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kgat::nfm_wgrad_reduce_kernel, dim3((w + 255) / 256), dim3(256), 0, st, N, l, part, nchunks, w,
+                       grad_out, lam, wl, bl, dW_out, db_lin);
     KGAT_LAUNCH_CHECK();
   }
   if (nnz > 0) {
-    hipLaunchKernelGGL(kgat::nfm_feat_kernel, dim3((nnz + 3) / 4), dim3(256), 0, st, N, erow, col, val, nnz, act, dz, dy,
-                       grad_out, dV, ld_dv, dw_lin);
+    uint32_t* keys = reinterpret_cast<uint32_t*>(workspace + ws.sort);
+    uint32_t* idx = keys + nnz;
+    uint32_t* skey = idx + nnz;
+    uint32_t* sidx = skey + nnz;
+    hipLaunchKernelGGL(kgat::nfm_feat_keys_kernel, dim3((nnz + 255) / 256), dim3(256), 0, st, col, nnz, keys, idx);
+    KGAT_LAUNCH_CHECK();
+    size_t bytes = ws.scratch_bytes;
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(workspace + ws.scratch, bytes, keys, skey, idx, sidx,
+                                                            static_cast<int>(nnz), 0, 32, st);
+    if (e != hipSuccess) return static_cast<int>(e);
+    const int64_t fchunks = (nnz + kgat::kFeatChunk - 1) / kgat::kFeatChunk;
+    float* slots = workspace + ws.slots;
+    hipLaunchKernelGGL(kgat::nfm_feat_piece_kernel, dim3((fchunks + 3) / 4), dim3(256), 0, st, N, skey, sidx, erow, val,
+                       nnz, act, dz, dy, grad_out, dV, ld_dv, dw_lin, slots);
+    KGAT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(kgat::nfm_feat_join_kernel, dim3((fchunks + 3) / 4), dim3(256), 0, st, skey, nnz, N.dims[0],
+                       slots, dV, ld_dv, dw_lin);
     KGAT_LAUNCH_CHECK();
   }
   return KGAT_OK;

@@ -55,7 +55,8 @@ def _csr(x: torch.Tensor, row_offset: int = 0):
         raise ValueError("NFM feature batches are sparse COO tensors (NFM/preprocess.py:290-356)")
     x = x.coalesce()
     idx = x.indices()
-    return idx[0] + row_offset, idx[1].contiguous(), x.values().to(torch.float32).contiguous()
+    rows = idx[0] + row_offset if row_offset else idx[0]
+    return rows, idx[1].contiguous(), x.values().to(torch.float32).contiguous()
 
 
 class _NFMLoss(torch.autograd.Function):
@@ -94,7 +95,7 @@ class _NFMLoss(torch.autograd.Function):
         dbs = [torch.empty_like(hidden[2 * l + 1]) for l in range(L)]
         pw = (ctypes.c_void_p * max(1, L))(*[t.data_ptr() for t in dWs])
         pb = (ctypes.c_void_p * max(1, L))(*[t.data_ptr() for t in dbs])
-        ws = torch.empty(max(1, int(_lib.lib().kgat_nfm_bwd_workspace(ctypes.byref(net), n_rows))),
+        ws = torch.empty(max(1, int(_lib.lib().kgat_nfm_bwd_workspace(ctypes.byref(net), n_rows, cols.numel()))),
                          dtype=torch.float32, device=dev)
         _lib.call("kgat_nfm_bwd_f32", ctypes.byref(net), rows.data_ptr(), cols.data_ptr(), vals.data_ptr(),
                   cols.numel(), n_rows, act.data_ptr(), dy.data_ptr(), gout.data_ptr(), float(model._loss_lambda),

@@ -552,6 +552,53 @@ def test_nfm_train_steps_vs_reference(pkg):
     np.testing.assert_allclose(sc, g["pred_scores"], rtol=RTOL, atol=1e-5)
 
 
+def _skewed_nfm_batch(rng, rows, U, F):
+    """Rows of one user (from 5: runs of ~rows/5 equal feature ids), one item, three of
+    eight shared tags and a real-valued rating feature: long runs cross the backward's
+    16-entry chunks of the feature-sorted entries."""
+    r_idx, c_idx, vals = [], [], []
+    for r in range(rows):
+        feats = [int(rng.integers(0, 5)), int(U + rng.integers(0, 50))]
+        feats += [int(U + 50 + t) for t in rng.choice(8, 3, replace=False)]
+        vs = [1.0] * 5
+        feats.append(F - 1)
+        vs.append(float(rng.uniform(0.2, 1.0)))
+        r_idx += [r] * len(feats)
+        c_idx += feats
+        vals += vs
+    return torch.sparse_coo_tensor(torch.tensor([r_idx, c_idx]), torch.tensor(vals, dtype=torch.float32), (rows, F))
+
+
+@pytest.mark.parametrize("dim,hidden", [(64, [64, 32, 16]), (128, [128, 64]), (200, [96]), (32, [])])
+def test_nfm_shapes_and_long_runs_vs_oracle(pkg, dim, hidden):
+    """NFM loss, every gradient and PREDICT scores vs the oracle (NFM/model.py:73-129) for the
+    LDS-staged (d=64), global-weight (d=128, 200) and no-hidden-layer forwards, with feature
+    runs far longer than a backward chunk."""
+    rng = np.random.default_rng(dim)
+    torch.manual_seed(dim)
+    U, E = 40, 120
+    m = pkg.NFM(pkg.NFMArgs(user_num=U, item_num=60, entity_num=E, embedding_dim=dim, hidden_dim=hidden,
+                            message_dropout=[0.1] * len(hidden))).to(DEV)
+    m.eval()
+    F = U + E
+    xp = _skewed_nfm_batch(rng, 700, U, F)
+    xn = _skewed_nfm_batch(rng, 700, U, F)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
+    ref = K.nfm_loss(params, xp, xn, lam=1e-5)
+    ref.backward()
+    loss = m(xp.to(DEV), xn.to(DEV), mode=pkg.NFMMode.TRAIN)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5)
+    for k, prm in m.named_parameters():
+        want = params[k].grad.numpy()
+        np.testing.assert_allclose(prm.grad.cpu().numpy(), want, rtol=1e-3, atol=1e-6 + 1e-4 * np.abs(want).max(),
+                                   err_msg=k)
+    with torch.no_grad():
+        sc = m(xp.to(DEV), mode=pkg.NFMMode.PREDICT).cpu().numpy()
+        want = K.nfm_score({k: v.detach() for k, v in params.items()}, xp).numpy()
+    np.testing.assert_allclose(sc, want, rtol=RTOL, atol=1e-5)
+
+
 def test_nfm_train_mode_dropout_runs(pkg):
     g = golden("nfm_h3_d64")
     m = _nfm_from_golden(pkg, g)

@@ -59,16 +59,24 @@ def main():
         print(json.dumps(r), flush=True)
         out.append(r)
 
+    def want(sec):
+        return not args.only or sec in args.only.split(",")
+
     torch.manual_seed(0)
-    for d in (64, 32):
-        if args.only and "spmm" not in args.only:
-            break
+    for d in (64, 32) if want("spmm") else ():
         X = torch.randn(n, d, device=dev)
         Y = torch.empty(n, d, device=dev)
         byt = 8 * (n + 1) + nnz * (8 + 4 * d) + 4 * n * d
         rec(f"spmm_fwd_d{d}", timeit(lambda: K.spmm(g, X, out=Y), args.reps), byt)
         rec(f"spmm_T_acc_d{d}", timeit(lambda: K.spmm(g, X, out=Y, transpose=True, accumulate=True), args.reps),
             byt + 4 * n * d)
+    if want("graph"):
+        graph_section(args, K, g, U, E, n, dev, rec)
+    if want("nfm"):
+        nfm_section(args, dev, rec)
+
+
+def graph_section(args, K, g, U, E, n, dev, rec):
     B = 256
     rng = np.random.default_rng(0)
     users = torch.from_numpy(rng.integers(0, U, B)).to(dev)
@@ -108,6 +116,40 @@ def main():
     rec("adam_table", timeit(lambda: K.adam(p, gg, m, v, 1e-3, 0.9, 0.999, 0.03, 1e-8), args.reps), 28 * p.numel())
     tables = [torch.randn(n, 64, device=dev), torch.randn(n, 64, device=dev), torch.randn(n, 32, device=dev)]
     rec("bpr_fwd", timeit(lambda: K.bpr_fwd(tables, users, pos, neg, 1e-5), args.reps))
+
+
+def nfm_section(args, dev, rec):
+    # NFM at the reference's evaluation scale: 64 users x 9,600 items = 614,400
+    # rows of ~5.3 one-hot features (user, item, contest, tags, rating) over F = 500 + 11,600 features
+    pkg = importlib.import_module(PKG)
+    U_, I_, Ent = 500, 9600, 11600
+    torch.manual_seed(0)
+    nfm = pkg.NFM(pkg.NFMArgs(user_num=U_, item_num=I_, entity_num=Ent, embedding_dim=64, hidden_dim=[64, 32, 16]))
+    nfm.to(dev)
+    nfm.eval()
+    rows_n = 64 * I_
+    r_idx = torch.arange(rows_n, device=dev)
+    feats = [r_idx // I_ % U_, U_ + r_idx % I_, U_ + I_ + (r_idx % I_) % 1900,
+             U_ + I_ + 1900 + (r_idx % I_) % 37, U_ + I_ + 1937 + (r_idx % I_) % 28]
+    idx = torch.stack([torch.cat([r_idx] * 5), torch.cat(feats)])
+    x = torch.sparse_coo_tensor(idx, torch.ones(idx.shape[1], device=dev), (rows_n, U_ + Ent)).coalesce()
+    with torch.no_grad():
+        rec("nfm_predict_614k_rows", timeit(lambda: nfm(x, mode=pkg.NFMMode.PREDICT), args.reps))
+    nfm.train()
+    nfm.build_optimizer(1e-3)
+    xb = torch.sparse_coo_tensor(idx[:, :0], torch.ones(0, device=dev), (1024, U_ + Ent))
+    sel = torch.cat([torch.arange(1024, device=dev) + k * rows_n for k in range(5)])
+    xb = torch.sparse_coo_tensor(torch.stack([idx[0, sel] % 1024, idx[1, sel]]), torch.ones(sel.numel(), device=dev),
+                                 (1024, U_ + Ent)).coalesce()
+    xn = torch.sparse_coo_tensor(torch.stack([idx[0, sel] % 1024, (idx[1, sel] + 7) % (U_ + Ent)]),
+                                 torch.ones(sel.numel(), device=dev), (1024, U_ + Ent)).coalesce()
+
+    def nfm_step():
+        loss = nfm(xb, xn, mode=pkg.NFMMode.TRAIN)
+        loss.backward()
+        nfm.update_weights()
+
+    rec("nfm_train_step_b1024", timeit(nfm_step, args.reps))
 
 
 if __name__ == "__main__":
