@@ -265,6 +265,33 @@ class AdamOracle:
 # --------------------------------------------------------------------------
 # a10/a11: NFM (src/model/NFM/model.py:73-129, hidden_layer.py:31-35)
 # --------------------------------------------------------------------------
+def nfm_feature_matrix(item_num: int, entity_num: int, feature_heads, feature_tails) -> sp.csr_matrix:
+    """Item one-hots plus the tails of problem-headed triplets, duplicates summed
+    (src/model/NFM/preprocess.py:166-183: coo_matrix(...).tocsr())."""
+    rows = list(range(item_num)) + [int(h) for h in feature_heads]
+    cols = list(range(item_num)) + [int(t) for t in feature_tails]
+    return sp.coo_matrix(([1] * len(rows), (rows, cols)), shape=(item_num, entity_num)).tocsr()
+
+
+def nfm_train_feature_batch(user_num: int, feature: sp.csr_matrix, users, items) -> torch.Tensor:
+    """sp.hstack([user one-hots, feature rows]) as a torch COO (NFM/preprocess.py:284-307, 336-356)."""
+    user_matrix = sp.identity(user_num).tocsr()
+    coo = sp.hstack([user_matrix[np.asarray(users)], feature[np.asarray(items)]]).tocoo()
+    return torch.sparse_coo_tensor(torch.LongTensor(np.vstack((coo.row, coo.col))), torch.FloatTensor(coo.data),
+                                   torch.Size(coo.shape))
+
+
+def nfm_test_feature_batch(user_num: int, feature: sp.csr_matrix, batch_user_ids) -> torch.Tensor:
+    """Users x all items (NFM/preprocess.py:309-334)."""
+    item_num = feature.shape[0]
+    row_num = len(batch_user_ids) * item_num
+    user_cols = np.repeat(np.asarray(batch_user_ids), item_num)
+    um = sp.coo_matrix(([1] * row_num, (list(range(row_num)), user_cols)), shape=(row_num, user_num)).tocsr()
+    coo = sp.hstack([um, sp.vstack([feature] * len(batch_user_ids))]).tocoo()
+    return torch.sparse_coo_tensor(torch.LongTensor(np.vstack((coo.row, coo.col))), torch.FloatTensor(coo.data),
+                                   torch.Size(coo.shape))
+
+
 def nfm_score(params: dict, x: torch.Tensor) -> torch.Tensor:
     V = params["_feature_embedding"]
     xv = torch.sparse.mm(x, V)

@@ -8,7 +8,7 @@ name is not a Python identifier).
 from .graph import DeviceGraph, GraphLayout, build_layout, synthetic_ckg  # noqa: F401
 from . import evaluation  # noqa: F401
 from .model import KGAT, KGATArgs, KGATMode  # noqa: F401
-from .nfm import NFM, NFMArgs, NFMMode  # noqa: F401
+from .nfm import NFM, NFMArgs, NFMBatch, NFMBatcher, NFMMode  # noqa: F401
 
-__all__ = ["evaluation", "KGAT", "KGATArgs", "KGATMode", "NFM", "NFMArgs", "NFMMode", "DeviceGraph", "GraphLayout", "build_layout",
+__all__ = ["evaluation", "KGAT", "KGATArgs", "KGATMode", "NFM", "NFMArgs", "NFMBatch", "NFMBatcher", "NFMMode", "DeviceGraph", "GraphLayout", "build_layout",
            "synthetic_ckg"]

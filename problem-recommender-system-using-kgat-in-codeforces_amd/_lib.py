@@ -95,6 +95,10 @@ _SIGNATURES = {
                                                  c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                                  c_i32, c_f32, c_u64, c_vp, c_vp, c_i64, c_vp]),
     "kgat_sample_cf_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    "kgat_nfm_batch_work_bytes": (c_i64, [c_i64]),
+    "kgat_nfm_batch_rowptr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_nfm_batch_fill": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp]),
     "kgat_sample_kg_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp,
                                             c_vp]),
     "kgat_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp]),

@@ -15,6 +15,7 @@ from dataclasses import dataclass, field
 from enum import IntEnum
 from typing import Any
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -49,8 +50,27 @@ class HiddenLayer(nn.Module):
         nn.init.xavier_uniform_(self._linear.weight)
 
 
-def _csr(x: torch.Tensor, row_offset: int = 0):
+@dataclass
+class NFMBatch:
+    """A feature batch already in the HIP path's layout (NFMBatcher's output): the
+    COO row / column / value of every entry, rows sorted and columns ascending
+    within a row, plus CSR row pointers.  ``NFM.forward`` takes it wherever the
+    reference takes a sparse COO tensor; ``to_sparse_coo`` gives that tensor."""
+    rows: torch.Tensor
+    cols: torch.Tensor
+    vals: torch.Tensor
+    rowptr: torch.Tensor
+    shape: tuple[int, int]
+
+    def to_sparse_coo(self) -> torch.Tensor:
+        x = torch.sparse_coo_tensor(torch.stack([self.rows, self.cols]), self.vals, self.shape)
+        return x._coalesced_(True)
+
+
+def _csr(x, row_offset: int = 0):
     """(rows int64, cols int64, vals fp32) of a sparse COO batch, row-sorted."""
+    if isinstance(x, NFMBatch):
+        return (x.rows + row_offset if row_offset else x.rows), x.cols, x.vals
     if not x.is_sparse:
         raise ValueError("NFM feature batches are sparse COO tensors (NFM/preprocess.py:290-356)")
     x = x.coalesce()
@@ -166,10 +186,16 @@ class NFM(nn.Module):
 
     def _calc_score(self, feature_values: torch.Tensor) -> torch.Tensor:
         dev = self._feature_embedding.device
-        rows, cols, vals = _csr(feature_values.to(dev))
+        if isinstance(feature_values, NFMBatch):
+            rows, cols, vals = _csr(feature_values)
+            rowptr = feature_values.rowptr
+        else:
+            rows, cols, vals = _csr(feature_values.to(dev))
+            rowptr = None
         n_rows = feature_values.shape[0]
         net = self._net(self.training)
-        rowptr = self._rowptr(rows, n_rows)
+        if rowptr is None:
+            rowptr = self._rowptr(rows, n_rows)
         y = torch.empty(n_rows, dtype=torch.float32, device=dev)
         with torch.no_grad():
             _lib.call("kgat_nfm_fwd_f32", ctypes.byref(net), rowptr.data_ptr(), cols.data_ptr(), vals.data_ptr(),
@@ -181,8 +207,10 @@ class NFM(nn.Module):
         B = positive_feature_values.shape[0]
         if negative_feature_values.shape[0] != B:
             raise ValueError("positive and negative batches must have the same number of rows")
-        rp, cp, vp = _csr(positive_feature_values.to(dev))
-        rn, cn, vn = _csr(negative_feature_values.to(dev), row_offset=B)
+        rp, cp, vp = _csr(positive_feature_values if isinstance(positive_feature_values, NFMBatch)
+                          else positive_feature_values.to(dev))
+        rn, cn, vn = _csr(negative_feature_values if isinstance(negative_feature_values, NFMBatch)
+                          else negative_feature_values.to(dev), row_offset=B)
         rows, cols, vals = torch.cat([rp, rn]), torch.cat([cp, cn]), torch.cat([vp, vn])
         return _NFMLoss.apply(rows, cols, vals, B, self, self._feature_embedding, self._linear.weight,
                               self._linear.bias, self._output_layer.weight, *self._hidden_params())
@@ -200,3 +228,82 @@ class NFM(nn.Module):
         if mode == NFMMode.PREDICT:
             return self._calc_score(*args)
         raise ValueError(f"unknown mode {mode}")
+
+
+class NFMBatcher:
+    """NFM batch generation (NFM/preprocess.py:150-356) with the feature rows built on the device.
+
+    The item feature matrix is the reference's ``_get_user_and_feature_matrices``
+    (preprocess.py:150-193): each item's one-hot plus the tails of the KG triplets
+    whose head is that problem, duplicates summed, over entity_num columns.
+    ``generate_train_batch`` draws (users, positive, negative) with the native CF
+    sampler (sampler.BatchSampler, the same draws as preprocess.py:195-270) and
+    returns two ``NFMBatch``; ``generate_test_batch(user_ids)`` is the users x all
+    items grid of preprocess.py:309-334.  Rows come from kgat_nfm_batch_rowptr /
+    kgat_nfm_batch_fill (csrc/nfm_batch.hip)."""
+
+    def __init__(self, user_num: int, item_num: int, entity_num: int, feature_heads, feature_tails,
+                 interaction_dict, device, train_batch_size: int = 1024, seed: int = 2024):
+        from .sampler import BatchSampler
+
+        self.user_num, self.item_num, self.entity_num = int(user_num), int(item_num), int(entity_num)
+        self.device = torch.device(device)
+        h = np.concatenate([np.arange(self.item_num, dtype=np.int64), np.asarray(feature_heads, np.int64)])
+        t = np.concatenate([np.arange(self.item_num, dtype=np.int64), np.asarray(feature_tails, np.int64)])
+        if h.size and (h.min() < 0 or h.max() >= self.item_num or t.min() < 0 or t.max() >= self.entity_num):
+            raise IndexError("feature triplets must have problem heads < item_num and tails < entity_num")
+        key = h * self.entity_num + t
+        uniq, counts = np.unique(key, return_counts=True)  # coo -> csr sums duplicates
+        rows, cols = uniq // self.entity_num, uniq % self.entity_num
+        rowptr = np.zeros(self.item_num + 1, np.int64)
+        np.cumsum(np.bincount(rows, minlength=self.item_num), out=rowptr[1:])
+        self.feature_rowptr = torch.from_numpy(rowptr).to(self.device)
+        self.feature_col = torch.from_numpy(cols.astype(np.int64)).to(self.device)
+        self.feature_val = torch.from_numpy(counts.astype(np.float32)).to(self.device)
+        self._sampler = BatchSampler(interaction_dict, self.item_num, np.zeros(0, np.int64), np.zeros(0, np.int64),
+                                     np.zeros(0, np.int64), max(1, self.user_num + self.entity_num),
+                                     cf_batch_size=train_batch_size, seed=seed)
+
+    @property
+    def n_features(self) -> int:
+        return self.user_num + self.entity_num
+
+    def build(self, users: torch.Tensor, items: torch.Tensor | None = None) -> NFMBatch:
+        """Rows (users[r], items[r]); items None: every user of ``users`` x every item."""
+        dev = self.device
+        users = torch.as_tensor(users, dtype=torch.int64).to(dev).contiguous()
+        if users.numel() and (int(users.min()) < 0 or int(users.max()) >= self.user_num):
+            raise IndexError("user id out of range")
+        if items is not None:
+            items = torch.as_tensor(items, dtype=torch.int64).to(dev).contiguous()
+            if items.shape != users.shape:
+                raise ValueError("users and items must have the same length")
+            if items.numel() and (int(items.min()) < 0 or int(items.max()) >= self.item_num):
+                raise IndexError("item id out of range")
+            n_rows = items.numel()
+        else:
+            n_rows = users.numel() * self.item_num
+        lib = _lib.lib()
+        rowptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+        work = torch.empty(max(1, int(lib.kgat_nfm_batch_work_bytes(n_rows))), dtype=torch.uint8, device=dev)
+        st = stream_ptr(dev)
+        ip = items.data_ptr() if items is not None else None
+        _lib.call("kgat_nfm_batch_rowptr", users.data_ptr(), ip, n_rows, self.item_num, self.feature_rowptr.data_ptr(),
+                  rowptr.data_ptr(), work.data_ptr(), work.numel(), st)
+        nnz = int(rowptr[-1].item())
+        rows = torch.empty(nnz, dtype=torch.int64, device=dev)
+        cols = torch.empty(nnz, dtype=torch.int64, device=dev)
+        vals = torch.empty(nnz, dtype=torch.float32, device=dev)
+        _lib.call("kgat_nfm_batch_fill", users.data_ptr(), ip, n_rows, self.item_num, self.user_num,
+                  self.feature_rowptr.data_ptr(), self.feature_col.data_ptr(), self.feature_val.data_ptr(),
+                  rowptr.data_ptr(), rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), st)
+        return NFMBatch(rows, cols, vals, rowptr, (n_rows, self.n_features))
+
+    def generate_train_batch(self) -> tuple[NFMBatch, NFMBatch]:
+        """(positive, negative) feature batches (preprocess.py:284-307)."""
+        users, pos, neg = self._sampler.generate_cf_batch()
+        return self.build(users, pos), self.build(users, neg)
+
+    def generate_test_batch(self, batch_user_ids) -> NFMBatch:
+        """Users x all items, row u * item_num + i (preprocess.py:309-334)."""
+        return self.build(torch.as_tensor(batch_user_ids, dtype=torch.int64))

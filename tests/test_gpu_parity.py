@@ -599,6 +599,53 @@ def test_nfm_shapes_and_long_runs_vs_oracle(pkg, dim, hidden):
     np.testing.assert_allclose(sc, want, rtol=RTOL, atol=1e-5)
 
 
+def test_nfm_batcher_vs_reference_batches(pkg):
+    """§8(f)2: NFMBatcher's device-built feature batches equal the reference's scipy construction
+    (NFM/preprocess.py:150-193 feature matrix, 284-307 train rows, 309-334 test grid), entry for
+    entry after coalescing, and score / train identically to the COO input."""
+    rng = np.random.default_rng(5)
+    U, I, E = 30, 40, 90
+    heads = rng.integers(0, I, 150)
+    tails = rng.integers(I, E, 150)  # duplicates included: summed like coo -> csr
+    inter = {u: sorted(rng.choice(I, 5, replace=False).tolist()) for u in range(U)}
+    b = pkg.NFMBatcher(U, I, E, heads, tails, inter, DEV, train_batch_size=16)
+    feat = K.nfm_feature_matrix(I, E, heads, tails)
+
+    def same(got, want):
+        want = want.coalesce()
+        assert got.shape == tuple(want.shape)
+        np.testing.assert_array_equal(torch.stack([got.rows, got.cols]).cpu().numpy(), want.indices().numpy())
+        np.testing.assert_array_equal(got.vals.cpu().numpy(), want.values().numpy())
+        rp = np.searchsorted(want.indices()[0].numpy(), np.arange(got.shape[0] + 1))
+        np.testing.assert_array_equal(got.rowptr.cpu().numpy(), rp)
+
+    users, items = rng.integers(0, U, 50), rng.integers(0, I, 50)
+    xb = b.build(torch.from_numpy(users), torch.from_numpy(items))
+    same(xb, K.nfm_train_feature_batch(U, feat, users, items))
+    grid = b.generate_test_batch([3, 7, 0])
+    same(grid, K.nfm_test_feature_batch(U, feat, [3, 7, 0]))
+    assert b.build(torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64)).rows.numel() == 0
+    with pytest.raises(IndexError):
+        b.build(torch.tensor([U]), torch.tensor([0]))
+
+    pos, neg = b.generate_train_batch()
+    for r in range(pos.shape[0]):  # row r: user column, then the item's one-hot at user_num + item
+        beg = int(pos.rowptr[r])
+        u, it = int(pos.cols[beg]), int(pos.cols[beg + 1]) - U
+        assert it in inter[u]
+        nb = int(neg.rowptr[r])
+        assert int(neg.cols[nb]) == u and int(neg.cols[nb + 1]) - U not in inter[u]
+    torch.manual_seed(1)
+    m = pkg.NFM(pkg.NFMArgs(user_num=U, item_num=I, entity_num=E)).to(DEV)
+    m.eval()
+    with torch.no_grad():
+        np.testing.assert_array_equal(m(grid, mode=pkg.NFMMode.PREDICT).cpu().numpy(),
+                                      m(grid.to_sparse_coo(), mode=pkg.NFMMode.PREDICT).cpu().numpy())
+    l1 = m(pos, neg, mode=pkg.NFMMode.TRAIN)
+    l2 = m(pos.to_sparse_coo(), neg.to_sparse_coo(), mode=pkg.NFMMode.TRAIN)
+    assert l1.item() == l2.item()
+
+
 def test_nfm_train_mode_dropout_runs(pkg):
     g = golden("nfm_h3_d64")
     m = _nfm_from_golden(pkg, g)

@@ -171,3 +171,20 @@ def test_reference_checkpoints_load_into_product_models():
                             entity_num=int(gn["entity_num"]), embedding_dim=int(gn["dim"]),
                             hidden_dim=gn["hidden"].tolist()))
     n.load_state_dict(ckn["model_state_dict"])
+
+
+def test_nfm_feature_matrix_matches_reference_construction():
+    """NFMBatcher's item feature CSR (built on the host, NFM/preprocess.py:150-193) equals the
+    reference's coo_matrix(...).tocsr(): item one-hots plus problem-headed triplet tails, duplicates summed."""
+    rng = np.random.default_rng(3)
+    I, E = 25, 70
+    heads, tails = rng.integers(0, I, 120), rng.integers(I, E, 120)
+    b = pkg.NFMBatcher(10, I, E, heads, tails, {0: [1, 2]}, "cpu")
+    want = K.nfm_feature_matrix(I, E, heads, tails)
+    want.sum_duplicates()
+    want.sort_indices()
+    np.testing.assert_array_equal(b.feature_rowptr.numpy(), want.indptr)
+    np.testing.assert_array_equal(b.feature_col.numpy(), want.indices)
+    np.testing.assert_array_equal(b.feature_val.numpy(), want.data.astype(np.float32))
+    with pytest.raises(IndexError):
+        pkg.NFMBatcher(10, I, E, [I], [I], {0: [1]}, "cpu")

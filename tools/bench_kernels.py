@@ -150,6 +150,15 @@ def nfm_section(args, dev, rec):
         nfm.update_weights()
 
     rec("nfm_train_step_b1024", timeit(nfm_step, args.reps))
+    # batch generation (NFM/preprocess.py:284-334): features = item one-hot + 4 KG tails per item
+    rng = np.random.default_rng(0)
+    fh = np.repeat(np.arange(I_), 4)
+    ft = np.concatenate([[I_ + (i % 1900), I_ + 1900 + i % 37, I_ + 1937 + i % 28, I_ + 1965 + i % 5]
+                         for i in range(I_)])
+    inter = {u: rng.choice(I_, 40, replace=False).tolist() for u in range(U_)}
+    batcher = pkg.NFMBatcher(U_, I_, Ent, fh, ft, inter, dev, train_batch_size=1024)
+    rec("nfm_test_batch_64users", timeit(lambda: batcher.generate_test_batch(list(range(64))), args.reps))
+    rec("nfm_train_batch_b1024", timeit(batcher.generate_train_batch, args.reps))
 
 
 if __name__ == "__main__":
