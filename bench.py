@@ -8,8 +8,10 @@ batch, backward through every layer, dense Adam on the whole model -- in
 train mode (dropout on), inputs resident in HBM before timing starts.
 
 value = CKG layer-edges per second of the whole job = n_gpus * E * L / t_step
-(weak scaling: every rank runs full propagation for its own batch; for N > 1
-the gradients are all-reduced over RCCL each step, data-parallel replicas).
+(weak scaling: every rank runs full propagation for its own batch; for N > 1,
+data-parallel replicas: the table gradient is reduce-scattered by row blocks
+over RCCL, each rank runs Adam on its own rows and the rows are all-gathered
+back -- replicas.ShardedGradSync; small gradients in one flat all-reduce).
 Also reported: BPR pairs/s = 256 * n_gpus / t_step, forward-propagation
 edges/s, the roofline of the dominant kernel (the SpMM gather, timed live
 with HIP events on its launch stream) and the CPU baseline (the oracle's
@@ -151,12 +153,15 @@ def main() -> None:
         batches.append([torch.from_numpy(x.astype(np.int64)).to(dev)
                         for x in (u, su[k, 1], rng.integers(0, n_items, B))])
     params = [p for p in model.parameters() if not p.is_sparse and p.requires_grad]
+    sync = replicas.ShardedGradSync(params)
 
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
-        replicas.allreduce_gradients(params)  # RCCL over xGMI; no-op at N=1
-        model.update_cf_weights()
+        # RCCL over xGMI (no-op at N=1): table gradient reduce-scattered by row blocks, Adam on the
+        # owned rows, updated rows all-gathered; small gradients in one flat all-reduce
+        model.update_cf_weights(row_ranges=sync.reduce())
+        sync.gather()
         return loss
 
     for i in range(args.warmup):

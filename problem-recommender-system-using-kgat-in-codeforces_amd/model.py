@@ -348,12 +348,13 @@ class KGAT(nn.Module):
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 
-    def update_cf_weights(self) -> None:
-        self._cf_optimizer.step()
+    def update_cf_weights(self, row_ranges: dict | None = None) -> None:
+        """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all."""
+        self._cf_optimizer.step(row_ranges)
         self._cf_optimizer.zero_grad()
 
-    def update_kg_weights(self) -> None:
-        self._kg_optimizer.step()
+    def update_kg_weights(self, row_ranges: dict | None = None) -> None:
+        self._kg_optimizer.step(row_ranges)
         self._kg_optimizer.zero_grad()
 
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:

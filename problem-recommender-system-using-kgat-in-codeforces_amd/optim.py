@@ -24,8 +24,12 @@ class FusedAdam:
         self.state: dict[int, dict] = {}
 
     @torch.no_grad()
-    def step(self) -> None:
-        """Every parameter with a gradient in one kgat_adam_multi_f32 launch (per 16 tensors)."""
+    def step(self, row_ranges: dict | None = None) -> None:
+        """Every parameter with a gradient in one kgat_adam_multi_f32 launch (per 16 tensors).
+
+        ``row_ranges`` {id(param): [(r0, r1), ...]} restricts a parameter's update to those
+        row ranges, each with its own optimizer state (replicas.ShardedGradSync: every rank
+        steps only the table rows it owns; the arithmetic per element is unchanged)."""
         items = []
         for p in self.params:
             g = p.grad
@@ -33,16 +37,21 @@ class FusedAdam:
                 continue
             if p.is_sparse or g.is_sparse:
                 raise RuntimeError("FusedAdam: sparse parameters/gradients are not supported")
-            st = self.state.get(id(p))
-            if st is None:
-                st = {"step": 0, "exp_avg": kernels.zeros(p.shape, p.device),
-                      "exp_avg_sq": kernels.zeros(p.shape, p.device)}
-                self.state[id(p)] = st
-            st["step"] += 1
-            t = st["step"]
-            bc1 = 1.0 - self.beta1 ** t
-            bc2_sqrt = math.sqrt(1.0 - self.beta2 ** t)
-            items.append((p.data, g.contiguous(), st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, bc2_sqrt))
+            g = g.contiguous()
+            ranges = row_ranges.get(id(p)) if row_ranges else None
+            views = [(id(p), p.data, g)] if ranges is None else \
+                [((id(p), r0, r1), p.data[r0:r1], g[r0:r1]) for r0, r1 in ranges if r1 > r0]
+            for key, pv, gv in views:
+                st = self.state.get(key)
+                if st is None:
+                    st = {"step": 0, "exp_avg": kernels.zeros(pv.shape, p.device),
+                          "exp_avg_sq": kernels.zeros(pv.shape, p.device)}
+                    self.state[key] = st
+                st["step"] += 1
+                t = st["step"]
+                bc1 = 1.0 - self.beta1 ** t
+                bc2_sqrt = math.sqrt(1.0 - self.beta2 ** t)
+                items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, bc2_sqrt))
         if items:
             kernels.adam_multi(items, self.beta1, self.beta2, self.eps)
 

@@ -8,6 +8,14 @@ shape: the [N, d] table gradient is one large all-reduce on its own; the many
 small aggregator / relation / trans gradients are coalesced into one flat
 bucket so they cost a single ring instead of one launch each.
 
+``ShardedGradSync`` is the bandwidth-lean form used by bench.py: the big
+row-major gradients (the [N, d] table) are reduce-scattered by row blocks
+instead of all-reduced, every rank runs Adam on the rows it owns only (1/G of
+the optimizer traffic, 1/G of its state), and the updated rows are
+all-gathered back -- the same bytes on the wire as one all-reduce, with the
+dense Adam pass cut G-fold.  Per element the arithmetic is the all-reduce
+path's (mean gradient, same Adam), so replicas stay identical.
+
 Works with any torch.distributed backend: ``nccl`` (= RCCL on ROCm) on the
 GPU box, ``gloo`` for the CPU tests.
 """
@@ -55,3 +63,88 @@ def allreduce_gradients(params, average: bool = True) -> None:
             k = g.numel()
             g.copy_(flat[off:off + k].view_as(g))
             off += k
+
+
+def _rank() -> int:
+    return dist.get_rank() if world() > 1 else 0
+
+
+def _is_nccl() -> bool:
+    return dist.get_backend() == "nccl"
+
+
+class ShardedGradSync:
+    """Reduce-scatter / own-rows Adam / all-gather for the big gradients (ZeRO-1 on rows).
+
+    ``reduce()`` after ``loss.backward()``: every big gradient [R, ...] is split into G
+    row blocks of s = R // G rows; rank k receives the mean of block k (in place,
+    RCCL reduce-scatter) and the R - G*s tail rows are all-reduced.  Small gradients
+    go through one flat all-reduce as in allreduce_gradients.  Returns the row
+    ranges for ``FusedAdam.step(row_ranges=...)`` (own block + tail).  ``gather()``
+    after the optimizer step all-gathers the owned blocks of the parameters."""
+
+    def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES):
+        self.params = list(params)
+        self.big_bytes = int(big_bytes)
+        self._big: list[tuple[torch.Tensor, int, int]] = []
+
+    def reduce(self) -> dict | None:
+        n = world()
+        self._big = []
+        if n == 1:
+            return None
+        rank = _rank()
+        ranges: dict = {}
+        small = []
+        for p in self.params:
+            g = p.grad
+            if g is None:
+                continue
+            if g.dim() >= 1 and g.shape[0] >= n and g.numel() * g.element_size() > self.big_bytes \
+                    and g.is_contiguous() and p.data.is_contiguous():
+                rows = g.shape[0]
+                s = rows // n
+                main = s * n
+                own = g[rank * s:(rank + 1) * s]
+                if _is_nccl():
+                    dist.reduce_scatter_tensor(own, g[:main])  # in place: recv = send + rank * s rows
+                else:  # gloo has no reduce-scatter: the same sums, all ranks
+                    dist.all_reduce(g[:main])
+                own.div_(n)
+                rr = [(rank * s, (rank + 1) * s)]
+                if main < rows:
+                    tail = g[main:]
+                    dist.all_reduce(tail)
+                    tail.div_(n)
+                    rr.append((main, rows))
+                ranges[id(p)] = rr
+                self._big.append((p, s, main))
+            else:
+                small.append(g)
+        if small:
+            flat = torch.cat([g.reshape(-1) for g in small])
+            dist.all_reduce(flat)
+            flat.div_(n)
+            off = 0
+            for g in small:
+                k = g.numel()
+                g.copy_(flat[off:off + k].view_as(g))
+                off += k
+        return ranges
+
+    @torch.no_grad()
+    def gather(self) -> None:
+        n = world()
+        if n == 1:
+            return
+        rank = _rank()
+        for p, s, main in self._big:
+            full = p.data[:main]
+            own = full[rank * s:(rank + 1) * s]
+            if _is_nccl():
+                dist.all_gather_into_tensor(full, own)  # in place: send = recv + rank * s rows
+            else:
+                parts = list(full.split(s))
+                dist.all_gather(parts, own.clone())
+                # gloo fills the views of `full` in place
+        self._big = []

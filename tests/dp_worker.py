@@ -1,0 +1,73 @@
+"""One rank of the data-parallel replica check (launched by tests/test_gpu_sharded.py through
+``python -m torch.distributed.run --nproc-per-node 2``; both ranks on cuda:0, gloo).
+
+Two replica sets train side by side on the same rank-dependent batches with rank-dependent dropout:
+(A) replicas.allreduce_gradients + every rank's full Adam, and (B) replicas.ShardedGradSync --
+row-block gradient exchange, Adam on the owned rows, all-gather.  With two ranks every sum has two
+operands, so (A) and (B) must agree bit for bit, and each path's replicas must stay identical.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tests.conftest import load_pkg  # noqa: E402
+
+
+def main() -> None:
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    pkg = load_pkg()
+    graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+    rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
+    U, E, inter, trip = graph.synthetic_ckg(20001, 160000, seed=9)  # odd row count: a tail row
+    lay = graph.build_layout(U, E, inter, trip)
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                        message_dropout=[0.1, 0.1])
+    models = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        m = pkg.KGAT(args)
+        m.attach_graph(lay, "cuda")
+        rep.broadcast_parameters(m)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        models.append(m)
+    rng = np.random.default_rng(40 + rank)
+    failures = []
+    for step in range(3):
+        b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
+                                                  rng.integers(0, E // 10, 64))]
+        for k, m in enumerate(models):
+            torch.manual_seed(1000 * step + rank)  # same dropout for both paths, per rank
+            loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
+            loss.backward()
+            params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
+            if k == 0:
+                rep.allreduce_gradients(params)
+                m.update_cf_weights()
+            else:
+                sync = rep.ShardedGradSync(params)
+                m.update_cf_weights(row_ranges=sync.reduce())
+                sync.gather()
+    for (na, pa), (nb, pb) in zip(models[0].named_parameters(), models[1].named_parameters()):
+        if pa.is_sparse:
+            continue
+        if not torch.equal(pa.data, pb.data):
+            failures.append(f"{na}: max |diff| {(pa.data - pb.data).abs().max().item():.3e}")
+        other = pa.data.clone()
+        dist.broadcast(other, 0)
+        if not torch.equal(other, pa.data):
+            failures.append(f"{na}: replicas diverged")
+    print(f"rank {rank}: {'OK' if not failures else failures}", flush=True)
+    dist.destroy_process_group()
+    sys.exit(1 if failures else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -103,3 +103,17 @@ def test_sharded_world2_two_ranks_one_gpu():
     log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert p.stdout.count("sharded parity ok") == 2, p.stdout[-2000:]
+
+
+def test_dp_sharded_grad_sync_world2_matches_allreduce():
+    """replicas.ShardedGradSync (row-block exchange, owned-row Adam, all-gather) vs all-reduce + full
+    Adam over 3 CF steps on two ranks (tests/dp_worker.py): bit-identical parameters, identical replicas."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / "dp_world2.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])

@@ -56,3 +56,47 @@ def test_allreduce_and_broadcast_world2():
     assert all(r[1] for r in res), "gradients not averaged"
     assert torch.equal(res[0][2], res[1][2]), "replicas did not start from the same weights"
     assert all(r[3] for r in res)
+
+
+def _sharded_worker(rank: int, world: int, port: str, q) -> None:
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
+    try:
+        pkg = load_pkg()
+        rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
+        table = torch.nn.Parameter(torch.zeros(11, 4))   # 11 rows over 2 ranks: blocks of 5 + 1 tail row
+        small = torch.nn.Parameter(torch.zeros(3))
+        g = torch.arange(44, dtype=torch.float32).view(11, 4) * (rank + 1)
+        table.grad, small.grad = g.clone(), torch.full((3,), float(rank + 1))
+        sync = rep.ShardedGradSync([table, small], big_bytes=64)
+        ranges = sync.reduce()
+        r0, r1 = 5 * rank, 5 * rank + 5
+        mean = torch.arange(44, dtype=torch.float32).view(11, 4) * 1.5
+        ok = ranges == {id(table): [(r0, r1), (10, 11)]}
+        ok &= torch.equal(table.grad[r0:r1], mean[r0:r1]) and torch.equal(table.grad[10:], mean[10:])
+        ok &= torch.equal(small.grad, torch.full((3,), 1.5))
+        # the optimizer touches only the owned rows (+ the replicated tail) ...
+        with torch.no_grad():
+            table.data[r0:r1] = rank + 7.0
+            table.data[10:] = 3.0
+        sync.gather()  # ... and the gather makes every replica whole again
+        want = torch.cat([torch.full((5, 4), 7.0), torch.full((5, 4), 8.0), torch.full((1, 4), 3.0)])
+        q.put((rank, bool(ok), torch.equal(table.data, want)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_grad_sync_world2():
+    """replicas.ShardedGradSync: row-block reduce-scatter (gloo: all-reduce) of the big gradient,
+    tail rows and small gradients all-reduced, the row ranges the optimizer steps, the all-gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _rendezvous()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] for r in res), res
+    assert all(r[2] for r in res), res
