@@ -153,7 +153,7 @@ def main() -> None:
         batches.append([torch.from_numpy(x.astype(np.int64)).to(dev)
                         for x in (u, su[k, 1], rng.integers(0, n_items, B))])
     params = [p for p in model.parameters() if not p.is_sparse and p.requires_grad]
-    sync = replicas.ShardedGradSync(params)
+    sync = replicas.ShardedGradSync(params).attach(model)  # table-gradient exchange overlapped with its blocks
 
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)

@@ -160,7 +160,8 @@ class _DeviceCSR:
 
     def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: torch.Tensor, device):
         self.n_rows = rowptr.size - 1
-        self.rowptr = torch.from_numpy(np.ascontiguousarray(rowptr, np.int64)).to(device)
+        self.rowptr_host = np.ascontiguousarray(rowptr, np.int64)
+        self.rowptr = torch.from_numpy(self.rowptr_host).to(device)
         self.col = torch.from_numpy(np.ascontiguousarray(col, np.int32)).to(device)
         self.val = val
         lr, off, sr, sb = long_row_plan(rowptr)
@@ -174,6 +175,28 @@ class _DeviceCSR:
     def descriptor(self) -> _lib.CSR:
         return _lib.CSR(self.rowptr.data_ptr(), self.col.data_ptr(), self.val.data_ptr(), self.n_rows,
                         self.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
+                        self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
+                        LONG_THRESHOLD)
+
+
+class _CSRRowView:
+    """Rows [r0, r1) of a _DeviceCSR, sharing its device arrays (values stay live across
+    refreshes): the descriptor points at rowptr + r0 -- row pointers are absolute
+    offsets into col / val -- with a long-row plan of its own rows."""
+
+    def __init__(self, base: _DeviceCSR, r0: int, r1: int, device):
+        self.base, self.r0, self.n_rows = base, int(r0), int(r1) - int(r0)
+        lr, off, sr, sb = long_row_plan(base.rowptr_host[r0:r1 + 1])
+        self.long_rows = torch.from_numpy(lr).to(device)
+        self.long_seg_off = torch.from_numpy(off).to(device)
+        self.seg_row = torch.from_numpy(sr).to(device)
+        self.seg_beg = torch.from_numpy(sb).to(device)
+        self.n_long, self.n_seg = int(lr.size), int(sr.size)
+
+    def descriptor(self) -> _lib.CSR:
+        b = self.base
+        return _lib.CSR(b.rowptr.data_ptr() + 8 * self.r0, b.col.data_ptr(), b.val.data_ptr(), self.n_rows,
+                        b.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
                         self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
                         LONG_THRESHOLD)
 
@@ -211,6 +234,15 @@ class DeviceGraph:
     @property
     def nnz(self) -> int:
         return int(self.A.col.numel())
+
+    def transpose_row_blocks(self, bounds) -> list[_CSRRowView]:
+        """Row-block views of A^T for ``bounds`` [(r0, r1), ...] (cached per bounds)."""
+        key = tuple((int(a), int(b)) for a, b in bounds)
+        cache = getattr(self, "_at_blocks", {})
+        if key not in cache:
+            cache[key] = [_CSRRowView(self.AT, a, b, self.device) for a, b in key]
+            self._at_blocks = cache
+        return cache[key]
 
     def refresh_transpose(self) -> None:
         """valT = val[perm_t] after A's values changed (one gather kernel)."""

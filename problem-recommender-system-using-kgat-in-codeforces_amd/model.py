@@ -100,13 +100,15 @@ class _CFLoss(torch.autograd.Function):
     (kgat_spmm_csr_masked_f32; equal to the dense product).  Then for
     l = L-2..0 densely:
         (dXd, dS_l, dW) = biinter_bwd(...)   (kgat_biinter_bwd_f32)
-        dX_l = dXd + A^T . dS_l              (spmm on the transposed CSR, accumulate)
-        dX_l += scatter(dBPR_l)              (kgat_bpr_bwd_f32)
+        dXd += scatter(dBPR_l)               (kgat_bpr_bwd_f32)
+        dX_l = dXd + A^T . dS_l              (spmm on the transposed CSR, accumulate;
+                                              for l = 0 optionally by row blocks, see
+                                              replicas.ShardedGradSync.attach)
     """
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg = cfg
+        graph, drops, seeds, reg, _hook = cfg
         tables, sides, states = [X0], [], []
         x = X0
         for l in range(len(drops)):
@@ -126,7 +128,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg = ctx.cfg
+        graph, drops, seeds, reg, hook = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -148,8 +150,15 @@ class _CFLoss(torch.autograd.Function):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],
                                                               seeds[l], **_saved(tables, states, l))
-            kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
             kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXd)
+            if l == 0 and hook is not None:
+                # the table gradient by row blocks: each block's exchange (replicas.ShardedGradSync)
+                # starts while the next block's A^T . dS is computed
+                for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
+                    kernels.spmm_block(view, dS, dXd[view.r0:view.r0 + view.n_rows], accumulate=True)
+                    hook.block_ready(k, dXd)
+            else:
+                kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
             wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
             dX = dXd
         ctx.tables = ctx.sides = ctx.states = None
@@ -297,7 +306,7 @@ class KGAT(nn.Module):
     def _calc_cf_loss(self, user_ids, positive_item_ids, negative_item_ids) -> torch.Tensor:
         g = self.graph()
         drops, seeds = self._dropouts()
-        cfg = (g, drops, seeds, float(self._regularization_params[0]))
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None))
         ids = [t.to(g.device).long().contiguous() for t in (user_ids, positive_item_ids, negative_item_ids)]
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 

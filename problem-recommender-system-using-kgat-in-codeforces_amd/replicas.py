@@ -87,6 +87,38 @@ class ShardedGradSync:
         self.params = list(params)
         self.big_bytes = int(big_bytes)
         self._big: list[tuple[torch.Tensor, int, int]] = []
+        self._table = None
+        self.bounds: list[tuple[int, int]] = []
+        self._early = None  # (gradient tensor, [work handles]) of the hooked table gradient
+
+    def attach(self, model) -> "ShardedGradSync":
+        """Overlap the table gradient's exchange with its computation: the CF backward then
+        computes the table's A^T . dS in the G row blocks of this rank layout (+ the tail)
+        and calls ``block_ready`` after each, which starts block k's reduction to rank k
+        (RCCL, async) while block k+1 is computed.  No-op on one rank."""
+        n = world()
+        if n == 1:
+            return self
+        table = model._user_entity_embedding.weight
+        rows = table.shape[0]
+        s = rows // n
+        if s == 0:
+            return self
+        self._table = table
+        self.bounds = [(k * s, (k + 1) * s) for k in range(n)] + ([(s * n, rows)] if s * n < rows else [])
+        model._table_grad_hook = self
+        return self
+
+    def block_ready(self, k: int, grad: torch.Tensor) -> None:
+        n = world()
+        if self._early is None or self._early[0] is not grad:
+            self._early = (grad, [])
+        r0, r1 = self.bounds[k]
+        view = grad[r0:r1]
+        if k < n and _is_nccl():
+            self._early[1].append(dist.reduce(view, dst=k, async_op=True))
+        else:  # the tail rows (every rank steps them), and gloo (no CUDA reduce): all-reduce
+            self._early[1].append(dist.all_reduce(view, async_op=True))
 
     def reduce(self) -> dict | None:
         n = world()
@@ -96,9 +128,25 @@ class ShardedGradSync:
         rank = _rank()
         ranges: dict = {}
         small = []
+        early, self._early = self._early, None
         for p in self.params:
             g = p.grad
             if g is None:
+                continue
+            if early is not None and p is self._table and len(early[1]) == len(self.bounds):
+                for w in early[1]:
+                    w.wait()
+                if g.data_ptr() != early[0].data_ptr():  # autograd kept a copy: take the reduced tensor
+                    g.copy_(early[0])
+                s = self.bounds[0][1]
+                main = s * n
+                g[rank * s:(rank + 1) * s].div_(n)
+                rr = [(rank * s, (rank + 1) * s)]
+                if main < g.shape[0]:
+                    g[main:].div_(n)
+                    rr.append((main, g.shape[0]))
+                ranges[id(p)] = rr
+                self._big.append((p, s, main))
                 continue
             if g.dim() >= 1 and g.shape[0] >= n and g.numel() * g.element_size() > self.big_bytes \
                     and g.is_contiguous() and p.data.is_contiguous():

@@ -1,10 +1,12 @@
 """One rank of the data-parallel replica check (launched by tests/test_gpu_sharded.py through
 ``python -m torch.distributed.run --nproc-per-node 2``; both ranks on cuda:0, gloo).
 
-Two replica sets train side by side on the same rank-dependent batches with rank-dependent dropout:
-(A) replicas.allreduce_gradients + every rank's full Adam, and (B) replicas.ShardedGradSync --
-row-block gradient exchange, Adam on the owned rows, all-gather.  With two ranks every sum has two
-operands, so (A) and (B) must agree bit for bit, and each path's replicas must stay identical.
+Three replica sets train side by side on the same rank-dependent batches with rank-dependent dropout:
+(A) replicas.allreduce_gradients + every rank's full Adam, (B) replicas.ShardedGradSync -- row-block
+gradient exchange, Adam on the owned rows, all-gather -- and (C) the same sync attached to the model,
+so the table gradient's blocks are exchanged while the backward computes the next block.  With two
+ranks every sum has two operands, so all three must agree bit for bit, and each path's replicas must
+stay identical.
 """
 from __future__ import annotations
 
@@ -30,7 +32,7 @@ def main() -> None:
     args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
                         message_dropout=[0.1, 0.1])
     models = []
-    for _ in range(2):
+    for _ in range(3):
         torch.manual_seed(3)
         m = pkg.KGAT(args)
         m.attach_graph(lay, "cuda")
@@ -40,11 +42,17 @@ def main() -> None:
         models.append(m)
     rng = np.random.default_rng(40 + rank)
     failures = []
+    syncs = [None, None, None]
     for step in range(3):
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
         for k, m in enumerate(models):
-            torch.manual_seed(1000 * step + rank)  # same dropout for both paths, per rank
+            torch.manual_seed(1000 * step + rank)  # same dropout for every path, per rank
+            if k and syncs[k] is None:
+                params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
+                syncs[k] = rep.ShardedGradSync(params)
+                if k == 2:
+                    syncs[k].attach(m)
             loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
             loss.backward()
             params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
@@ -52,14 +60,15 @@ def main() -> None:
                 rep.allreduce_gradients(params)
                 m.update_cf_weights()
             else:
-                sync = rep.ShardedGradSync(params)
-                m.update_cf_weights(row_ranges=sync.reduce())
-                sync.gather()
-    for (na, pa), (nb, pb) in zip(models[0].named_parameters(), models[1].named_parameters()):
+                m.update_cf_weights(row_ranges=syncs[k].reduce())
+                syncs[k].gather()
+    for (na, pa), (_, pb), (_, pc) in zip(models[0].named_parameters(), models[1].named_parameters(),
+                                          models[2].named_parameters()):
         if pa.is_sparse:
             continue
-        if not torch.equal(pa.data, pb.data):
-            failures.append(f"{na}: max |diff| {(pa.data - pb.data).abs().max().item():.3e}")
+        for tag, other_m in (("B", pb), ("C", pc)):
+            if not torch.equal(pa.data, other_m.data):
+                failures.append(f"{tag} {na}: max |diff| {(pa.data - other_m.data).abs().max().item():.3e}")
         other = pa.data.clone()
         dist.broadcast(other, 0)
         if not torch.equal(other, pa.data):
