@@ -189,7 +189,8 @@ def main() -> None:
 
     # dominant kernel: the forward SpMM gather A . X (d = embed dim), timed over the timed region
     fwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if not tr and not acc]
-    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr]
+    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc != "masked"]
+    masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc == "masked"]
     n, nnz = layout.n_nodes, layout.nnz
     d0 = cfg["dim"]
     fwd_d0 = [t for t, d in fwd if d == d0]
@@ -225,6 +226,7 @@ def main() -> None:
         "final_loss": final_loss,
         "spmm": {"fwd_launches": len(fwd), "bwd_launches": len(bwd), "fwd_avg_ms": avg_ms,
                  "bwd_avg_ms": float(np.mean([t for t, _ in bwd])) if bwd else None,
+                 "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / args.steps,
                  "fwd_spmm_ms_per_step": t_prop,
                  "fwd_spmm_layer_edges_per_s": nnz * L / (t_prop * 1e-3)},
         "roofline": {"bound": "hbm", "kernel": f"spmm_main_kernel<{d0}> (+fixup), forward A.X0",

@@ -83,6 +83,28 @@ int kgat_spmm_csr_masked_f32(const kgat_csr *A, const int32_t *src_map, const fl
                              const float *Yc_init, int64_t ldyc, float *Y, int64_t ldy, int32_t d,
                              float *workspace, int64_t workspace_floats, void *stream);
 
+/* The masked product of the backward's hop chain (layers below the last, whose
+ * upstream gradient is nonzero only on the rows the previous A^T product
+ * reached -- model.py:124-140's autograd through aggregator.py:54):
+ * as kgat_spmm_csr_masked_f32, plus
+ *   yc_row0: A is a row-block view whose local row r is global row yc_row0 + r
+ *            (Yc_init is looked up through src_map[yc_row0 + r]);
+ *   row_hit (nullable, int32 [n_rows]): zeroed, then 1 for every output row
+ *            that gathered at least one frontier edge or has a Yc_init row,
+ *            i.e. a superset of the rows of Y that can be nonzero. */
+int kgat_spmm_csr_masked_ex_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                const float *Yc_init, int64_t ldyc, int64_t yc_row0, float *Y, int64_t ldy,
+                                int32_t d, int32_t *row_hit, float *workspace, int64_t workspace_floats,
+                                void *stream);
+
+/* The next hop set from row_hit (int32 [n], 0/1): node_map[i] = position of i
+ * among the flagged nodes (ascending node order) or -1, rows[0..count) = the
+ * flagged nodes, *count (device int32) = their number.  work: scan scratch of
+ * kgat_hop_compact_work_bytes(n) bytes. */
+int64_t kgat_hop_compact_work_bytes(int64_t n);
+int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *rows, int32_t *count, void *work,
+                     int64_t work_bytes, void *stream);
+
 /* a2 -- bi-interaction aggregator forward, fused:
  *   H = normalize(dropout(LReLU(W1 (X+S) + b1) + LReLU(W2 (X*S) + b2)))
  * Replaces src/model/KGAT/aggregator.py:57-65.  W1/W2 are nn.Linear weights

@@ -26,6 +26,8 @@
 // 0, so the result equals the dense product with zero rows.
 #include "common.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 namespace kgat {
 
 enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2 };
@@ -39,6 +41,8 @@ struct SpmmIo {
   const int32_t* src_map; // masked: node -> compact row or -1
   const float* Yc;        // masked: compact init rows (nullable)
   int64_t ldyc;
+  int32_t* row_hit;       // masked: set to 1 for every output row that gathered an edge or has a Yc row (nullable)
+  int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
 };
 
 template <int D>
@@ -68,7 +72,7 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
 template <int D, bool MASKED>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
-                                             int gl, float4& acc) {
+                                             int gl, float4& acc, bool& any) {
   constexpr int L = SpmmShape<D>::kLanes;
   const float4* X4 = reinterpret_cast<const float4*>(io.X);
   const int64_t ldx4 = io.ldx / 4;
@@ -85,6 +89,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       // only frontier sources gather (usually none in a chunk); skipped edges
       // add an exact 0, so edge order is preserved among the ones that do
       uint64_t hit = (__ballot(gl < n && mc >= 0) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
+      any |= hit != 0;
       while (hit) {
         const int j = __ffsll(static_cast<long long>(hit)) - 1;
         hit &= hit - 1;
@@ -119,19 +124,21 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
 
 // Final write of one output row segment (lane gl) in the three modes.
 template <int MODE>
-__device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int gl, float4 acc) {
+__device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int gl, float4 acc, bool any = false) {
   float4* y = reinterpret_cast<float4*>(io.Y + row * io.ldy) + gl;
   if (MODE == kAccumulate) {
     const float4 o = *y;
     acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
   } else if (MODE == kMasked) {
     if (io.Yc != nullptr) {
-      const int m = io.src_map[row];
+      const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
         const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
         acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+        any = true;
       }
     }
+    if (io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
   *y = acc;
 }
@@ -154,11 +161,14 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     const int64_t row_end = A.rowptr[row + 1];
     const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
     // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
     for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
       const int64_t ce = cb + L < end ? cb + L : end;
-      gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc);
+      gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any);
     }
+    // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
+    if (MASKED && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
 #pragma unroll
     for (int o = L; o < kWave; o <<= 1) {
       acc.x += __shfl_xor(acc.x, o);
@@ -179,8 +189,9 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc);
-    store_row<MODE>(io, r, gl, acc);
+    bool any = false;
+    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any);
+    store_row<MODE>(io, r, gl, acc, any);
   }
 }
 
@@ -239,6 +250,25 @@ static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) 
 
 static bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
 
+// Hop set from the masked product's row flags: pos = exclusive scan of hit
+// (already in node_map); a flagged node keeps its position and is listed in
+// rows[pos], an unflagged one gets -1.  Thread i alone rewrites node_map[i],
+// so the last thread can read its own scan value for the count first.
+__global__ __launch_bounds__(256) void hop_finish_kernel(const int32_t* __restrict__ hit, int64_t n,
+                                                         int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
+                                                         int32_t* __restrict__ count) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t pos = node_map[i];
+  const bool h = hit[i] != 0;
+  if (i == n - 1) *count = pos + (h ? 1 : 0);
+  if (h) {
+    rows[pos] = static_cast<int32_t>(i);
+  } else {
+    node_map[i] = -1;
+  }
+}
+
 }  // namespace kgat
 
 extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx, float* Y, int64_t ldy,
@@ -250,22 +280,58 @@ extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx,
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0};
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return accumulate ? dispatch<kAccumulate>(*A, io, d, st) : dispatch<kOverwrite>(*A, io, d, st);
 }
 
-extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
-                                        const float* Yc_init, int64_t ldyc, float* Y, int64_t ldy, int32_t d,
-                                        float* workspace, int64_t workspace_floats, void* stream) {
+extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
+                                           const float* Yc_init, int64_t ldyc, int64_t yc_row0, float* Y, int64_t ldy,
+                                           int32_t d, int32_t* row_hit, float* workspace, int64_t workspace_floats,
+                                           void* stream) {
   using namespace kgat;
-  if (!A || !src_map || !Xc || !Y || A->n_rows < 0 || ldxc < d || ldy < d || (ldxc & 3) || (ldy & 3))
+  if (!A || !src_map || !Xc || !Y || A->n_rows < 0 || ldxc < d || ldy < d || (ldxc & 3) || (ldy & 3) || yc_row0 < 0)
     return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(Y) || (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
     return KGAT_ERR_INVALID;
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc};
-  return dispatch<kMasked>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (row_hit != nullptr &&
+      hipMemsetAsync(row_hit, 0, static_cast<size_t>(A->n_rows) * sizeof(int32_t), st) != hipSuccess)
+    return KGAT_ERR_INVALID;
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0};
+  return dispatch<kMasked>(*A, io, d, st);
+}
+
+extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
+                                        const float* Yc_init, int64_t ldyc, float* Y, int64_t ldy, int32_t d,
+                                        float* workspace, int64_t workspace_floats, void* stream) {
+  return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, workspace,
+                                     workspace_floats, stream);
+}
+
+extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {
+  if (n < 0 || n > INT32_MAX) return -1;
+  size_t bytes = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, static_cast<const int32_t*>(nullptr),
+                                       static_cast<int32_t*>(nullptr), static_cast<int>(n)) != hipSuccess)
+    return -1;
+  return static_cast<int64_t>(bytes > 0 ? bytes : 1);
+}
+
+extern "C" int kgat_hop_compact(const int32_t* hit, int64_t n, int32_t* node_map, int32_t* rows, int32_t* count,
+                                void* work, int64_t work_bytes, void* stream) {
+  if (!hit || !node_map || !rows || !count || n < 0 || n > INT32_MAX) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return hipMemsetAsync(count, 0, sizeof(int32_t), st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  const int64_t need = kgat_hop_compact_work_bytes(n);
+  if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
+  size_t bytes = static_cast<size_t>(need);
+  const hipError_t e = hipcub::DeviceScan::ExclusiveSum(work, bytes, hit, node_map, static_cast<int>(n), st);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(kgat::hop_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, hit, n, node_map, rows, count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }

@@ -235,6 +235,24 @@ class DeviceGraph:
     def nnz(self) -> int:
         return int(self.A.col.numel())
 
+    def hop_buffers(self):
+        """Scratch of the backward's hop chain (kernels.hop_compact): row flags, node -> hop
+        position map, hop rows, device count, scan work (allocated once)."""
+        hb = getattr(self, "_hop", None)
+        if hb is None:
+            n = self.n_nodes
+            work = int(_lib.lib().kgat_hop_compact_work_bytes(n))
+            if work < 0:
+                raise ValueError("graph too large for the hop compaction")
+            hb = (torch.zeros(n, dtype=torch.int32, device=self.device),
+                  torch.full((n,), -1, dtype=torch.int32, device=self.device),
+                  torch.empty(max(n, 1), dtype=torch.int32, device=self.device),
+                  torch.zeros(1, dtype=torch.int32, device=self.device),
+                  torch.empty(work, dtype=torch.uint8, device=self.device),
+                  torch.zeros(1, dtype=torch.int32, pin_memory=True))
+            self._hop = hb
+        return hb
+
     def transpose_row_blocks(self, bounds) -> list[_CSRRowView]:
         """Row-block views of A^T for ``bounds`` [(r0, r1), ...] (cached per bounds)."""
         key = tuple((int(a), int(b)) for a, b in bounds)

@@ -86,20 +86,27 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
     return out
 
 
-def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row)."""
+def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor,
+                      Yc_init: torch.Tensor | None = None, row0: int = 0) -> torch.Tensor:
+    """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row); with Yc_init,
+    local row r also gets Yc_init[src_map[row0 + r]] (B = rows [row0, ...) of a square matrix)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     _req(out, "out", dim=2)
     d = Xc.shape[1]
     if out.shape[0] != csr.n_rows or out.shape[1] != d:
         raise ValueError("out shape mismatch")
+    if Yc_init is not None:
+        _req(Yc_init, "Yc_init", dim=2)
+        if Yc_init.shape[1] != d or row0 < 0 or row0 + csr.n_rows > src_map.numel():
+            raise ValueError("Yc_init width / row0 mismatch")
     if csr.n_rows == 0:
         return out
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
-    _lib.call("kgat_spmm_csr_masked_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc), None, 0,
-              out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
+              int(row0), out.data_ptr(), _ld(out), d, None, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     return out
 
 
@@ -138,9 +145,10 @@ def add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 
 def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None = None,
-                transpose: bool = False) -> torch.Tensor:
+                transpose: bool = False, row_hit: torch.Tensor | None = None) -> torch.Tensor:
     """Dense Y = A . X where X is zero outside a frontier: X[node] = Xc[src_map[node]] (src_map -1 => 0),
-    plus Yc_init[src_map[r]] on frontier rows.  Returns a new dense [N, d] tensor."""
+    plus Yc_init[src_map[r]] on frontier rows.  Returns a new dense [N, d] tensor.  With ``row_hit``
+    (int32 [N]) the rows of Y that can be nonzero are flagged 1 (the next hop set, see hop_compact)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     if src_map.numel() != graph.n_nodes:
@@ -150,14 +158,40 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
         _req(Yc_init, "Yc_init", dim=2)
         if Yc_init.shape[1] != d:
             raise ValueError("Yc_init width mismatch")
+    if row_hit is not None:
+        _req(row_hit, "row_hit", dtype=torch.int32, dim=1)
+        if row_hit.numel() != graph.n_nodes:
+            raise ValueError("row_hit must cover every node")
     out = torch.empty(graph.n_nodes, d, dtype=torch.float32, device=Xc.device)
     csr = graph.AT if transpose else graph.A
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
-    _lib.call("kgat_spmm_csr_masked_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
-              out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0, 0,
+              out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None, ws.data_ptr(),
+              ws.numel(), stream_ptr(Xc.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, transpose, "masked"))
     return out
+
+
+def hop_compact(graph: DeviceGraph):
+    """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked: returns
+    (rows int32 [n] ascending, node_map int32 [N] node -> position or -1, n).  Reads the count
+    back to the host (one stream sync)."""
+    hit, node_map, rows, count, work, host = graph.hop_buffers()
+    dev = hit.device
+    _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
+              count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
+    host.copy_(count, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    n = int(host.item())
+    return rows[:n], node_map, n
 
 
 def frontier_build(users, pos, neg, node_map: torch.Tensor):

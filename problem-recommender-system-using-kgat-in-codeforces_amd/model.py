@@ -81,6 +81,11 @@ class MultiHeadAttention(nn.Module):
             nn.init.xavier_uniform_(lin.weight)
 
 
+# The backward's hop chain runs a layer on its hop set while that set holds at most this
+# fraction of the nodes (beyond it the dense kernels stream the rows faster).
+HOP_DENSE_FRACTION = 0.4
+
+
 def _saved(tables, states, l) -> dict:
     """Layer l's forward output + saved state for the backward (none: it recomputes)."""
     return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
@@ -97,8 +102,13 @@ class _CFLoss(torch.autograd.Function):
     distinct batch rows F (<= 3B, model.py:189-191 gathers nothing else), so
       dH_L[F] = scatter(dBPR) (compact), (dXd, dS, dW) = biinter_bwd on F rows,
       dX_{L-1} = dXd + A^T . dS  with the A^T gather restricted to F
-    (kgat_spmm_csr_masked_f32; equal to the dense product).  Then for
-    l = L-2..0 densely:
+    (kgat_spmm_csr_masked_ex_f32; equal to the dense product).  That product
+    also flags the rows it reached: dX_{L-1} is zero outside F + N(F), the
+    next "hop set".  Each lower layer runs the same way on its hop set
+    (kgat_hop_compact lists it; compact biinter_bwd; masked A^T product that
+    flags the next hop) while the set holds <= HOP_DENSE_FRACTION of the
+    nodes -- at C2 the layer-0 hop set is 1.7 % of the rows but 35 % of the
+    edges.  Once a hop set is larger, the remaining layers l run densely:
         (dXd, dS_l, dW) = biinter_bwd(...)   (kgat_biinter_bwd_f32)
         dXd += scatter(dBPR_l)               (kgat_bpr_bwd_f32)
         dX_l = dXd + A^T . dS_l              (spmm on the transposed CSR, accumulate;
@@ -133,7 +143,9 @@ class _CFLoss(torch.autograd.Function):
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
         L = len(drops)
+        n_nodes = graph.n_nodes
         wgrads: list[torch.Tensor | None] = [None] * (4 * L)
+        hit = graph.hop_buffers()[0] if L > 1 else None
         # ---- last layer on the batch frontier
         rows, _count = kernels.frontier_build(users, pos, neg, graph.node_map)
         dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)
@@ -141,13 +153,37 @@ class _CFLoss(torch.autograd.Function):
         l = L - 1
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
-        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True)
+        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True, row_hit=hit)
         kernels.frontier_reset(rows, graph.node_map)
         kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
         wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
-        # ---- remaining layers densely
+        # ---- remaining layers: on the hop set while it stays small, then densely
+        sparse = hit is not None
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
+            if sparse:
+                hrows, hmap, n_hop = kernels.hop_compact(graph)
+                sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
+            if sparse:
+                # dX is zero outside the hop set: the bi-interaction backward runs on its rows
+                # only and the A^T product gathers from them only (kgat_spmm_csr_masked_ex_f32);
+                # per row and per output element the arithmetic and order are the dense path's
+                dHc = kernels.gather_rows(dX, hrows)
+                dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,
+                                                                    drops[l], seeds[l], rows=hrows,
+                                                                    **_saved(tables, states, l))
+                kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
+                if l == 0 and hook is not None:
+                    dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
+                    for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
+                        kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
+                                                  Yc_init=dXdc, row0=view.r0)
+                        hook.block_ready(k, dX)
+                else:
+                    dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True,
+                                             row_hit=hit if l > 0 else None)
+                wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
+                continue
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],
                                                               seeds[l], **_saved(tables, states, l))
             kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXd)

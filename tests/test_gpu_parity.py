@@ -381,6 +381,90 @@ def test_spmm_masked_matches_dense(pkg, d):
         np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
 
 
+def test_spmm_masked_row_hit_hop_compact_and_row_blocks(pkg):
+    """The hop chain's pieces: row_hit flags exactly the rows that gathered a frontier edge or
+    carry a Yc row (long hub rows included), kgat_hop_compact lists them ascending with their
+    map, and row-block views with yc_row0 reproduce the whole masked product bit for bit."""
+    graph_mod, kernels = _mods(pkg)
+    rng = np.random.default_rng(3)
+    n, d = 5000, 64
+    h = np.concatenate([rng.integers(0, n, 20000), np.repeat(rng.integers(0, n, 5), 1200)])
+    t = rng.integers(0, n, h.size)
+    rowptr, col, val = graph_mod.csr_from_coo(n, np.concatenate([h, t]), np.concatenate([t, h]),
+                                              rng.random(2 * h.size).astype(np.float32))
+    lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
+                                tails=np.zeros(0, np.int64), edge_vals=np.zeros(0, np.float32), rowptr=rowptr,
+                                col=col, val=val, slot=np.zeros(0, np.int64))
+    g = graph_mod.DeviceGraph(lay, DEV)
+    assert g.AT.n_long > 0
+    F = rng.choice(n, 120, replace=False)
+    node_map = np.full(n, -1, np.int32)
+    node_map[F] = np.arange(F.size)
+    Xc, Yc = torch.randn(F.size, d, device=DEV), torch.randn(F.size, d, device=DEV)
+    hit = g.hop_buffers()[0]
+    hit.fill_(7)  # stale flags must be cleared by the call
+    nm = torch.from_numpy(node_map).to(DEV)
+    out = kernels.spmm_masked(g, nm, Xc, Yc_init=Yc, transpose=True, row_hit=hit)
+    # expected flags: rows r of A^T with an edge into F, or r in F
+    rt = g.AT.rowptr_host
+    colt = g.AT.col.cpu().numpy()
+    inF = np.zeros(n, bool)
+    inF[F] = True
+    want = np.zeros(n, bool)
+    want[np.repeat(np.arange(n), np.diff(rt))[inF[colt]]] = True
+    want |= inF
+    np.testing.assert_array_equal(hit.cpu().numpy().astype(bool), want)
+    hrows, hmap, cnt = kernels.hop_compact(g)
+    assert cnt == int(want.sum())
+    np.testing.assert_array_equal(hrows.cpu().numpy(), np.nonzero(want)[0])
+    m = hmap.cpu().numpy()
+    np.testing.assert_array_equal(m[want], np.arange(cnt))
+    assert np.all(m[~want] == -1)
+    # rows outside the hop set are exactly zero
+    assert float(out[torch.from_numpy(~want).to(DEV)].abs().max()) == 0.0
+    # row-block views (yc_row0) give the same bits
+    bounds = [(0, 1700), (1700, 3333), (3333, n)]
+    blk = torch.empty_like(out)
+    for v in g.transpose_row_blocks(bounds):
+        kernels.spmm_block_masked(v, nm, Xc, blk[v.r0:v.r0 + v.n_rows], Yc_init=Yc, row0=v.r0)
+    assert torch.equal(blk, out)
+
+
+@pytest.mark.parametrize("layers", [[64, 32], [64, 32, 16]])
+def test_cf_hop_chain_matches_dense_backward(pkg, layers):
+    """The hop-chain backward (lower layers on their hop sets) against the dense backward of the
+    same model and batch: the table gradient bit for bit (same per-row arithmetic and order),
+    the aggregator weight gradients within fp32 summation-order tolerance."""
+    graph_mod, _ = _mods(pkg)
+    model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    torch.manual_seed(2024)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                              message_dropout=[0.1] * len(layers)))
+    m.attach_graph(lay, DEV)
+    m.train()
+    rng = np.random.default_rng(4)
+    ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+    grads = {}
+    old = model_mod.HOP_DENSE_FRACTION
+    try:
+        for frac in (1.0, 0.0):
+            model_mod.HOP_DENSE_FRACTION = frac
+            for p in m.parameters():
+                p.grad = None
+            torch.manual_seed(123)  # same dropout seeds for both runs
+            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            grads[frac] = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    finally:
+        model_mod.HOP_DENSE_FRACTION = old
+    sp, de = grads[1.0], grads[0.0]
+    assert sp.keys() == de.keys()
+    assert torch.equal(sp["_user_entity_embedding.weight"], de["_user_entity_embedding.weight"])
+    for k in sp:
+        np.testing.assert_allclose(sp[k].cpu().numpy(), de[k].cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=k)
+
+
 def test_biinter_bwd_rows_matches_dense(pkg):
     _, kernels = _mods(pkg)
     torch.manual_seed(9)
