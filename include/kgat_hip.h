@@ -140,6 +140,19 @@ int kgat_biinter_bwd_f32(const float *X, int64_t ldx, const float *S, int64_t ld
                          float dropout_p, uint64_t seed, const int32_t *rows, int64_t src_rows,
                          float *workspace, int64_t workspace_floats, void *stream);
 
+/* a2 backward on a hop set of the backward chain (see kgat_hop_compact): rows /
+ * count are that call's outputs (count stays on the device; n_max bounds it),
+ * dH is indexed by node like X (the dense output of the previous masked
+ * product), dXd / dS are compact (row i <-> node rows[i], n_max rows
+ * allocated).  Saved forward state only (H, norm, mask; d_out <= 64 and
+ * d_in * d_out <= 4096).  Per row the arithmetic is kgat_biinter_bwd_f32's. */
+int kgat_biinter_bwd_hop_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H, int64_t ldh,
+                             const float *norm, const uint64_t *mask, const float *dH, int64_t lddh,
+                             const float *W1, const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds,
+                             float *dW1, float *db1, float *dW2, float *db2, const int32_t *rows,
+                             const int32_t *count, int64_t n_max, int64_t src_rows, int32_t d_in, int32_t d_out,
+                             float dropout_p, float *workspace, int64_t workspace_floats, void *stream);
+
 /* a2 for the wide layers of C4/C5 (any d_in, d_out multiple of 16 up to 1024; used
  * where the fused kernels above do not dispatch, e.g. 256): two rocBLAS sgemm per
  * direction (atomics off: deterministic) around fused HIP epilogues, same

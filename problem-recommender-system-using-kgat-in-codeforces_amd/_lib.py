@@ -73,6 +73,9 @@ _SIGNATURES = {
                                                    c_i64, c_i32, c_vp, c_vp, c_i64, c_vp]),
     "kgat_hop_compact_work_bytes": (c_i64, [c_i64]),
     "kgat_hop_compact": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_biinter_bwd_hop_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                                c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp]),
     "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                             c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32,

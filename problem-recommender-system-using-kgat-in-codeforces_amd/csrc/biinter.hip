@@ -559,9 +559,14 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     int64_t ldh, const float* __restrict__ norm, const uint64_t* __restrict__ mask, const float* __restrict__ dH,
     int64_t lddh, const float* __restrict__ W1, const float* __restrict__ W2, float* __restrict__ dXd,
     int64_t lddxd, float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p,
-    const int32_t* __restrict__ rows, int64_t n_src) {
+    const int32_t* __restrict__ rows, int64_t n_src, const int32_t* __restrict__ n_dev, int dh_by_node) {
   using B = BiShape<DIN, DOUT>;
   using F = SavedBwd<DIN, DOUT>;
+  // hop mode: the row count is produced on the device (kgat_hop_compact); n is its bound
+  if (n_dev != nullptr) {
+    const int64_t nd = *n_dev;
+    n = nd < n ? nd : n;
+  }
   constexpr int NCB = B::NCB, NIB = B::NIB, KO = B::KO;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w1s = smem;
@@ -615,10 +620,11 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
       return row < lim ? r0 + row : -1;
     };
     auto crow_of = [&](int row) -> int64_t { return row < lim ? r0 + row : -1; };
+    auto dh_of = [&](int row) -> int64_t { return dh_by_node ? node_of(row) : crow_of(row); };
     dma_rows<DIN>(ix, X, ldx, lane, node_of);
     dma_rows<DIN>(is, S, lds, lane, node_of);
     dma_rows<DOUT>(ih, H, ldh, lane, node_of);
-    dma_rows<DOUT>(ig, dH, lddh, lane, crow_of);
+    dma_rows<DOUT>(ig, dH, lddh, lane, dh_of);
     {
       const int64_t nn = node_of(lane & 15);
       dma4(norm + (nn >= 0 ? nn : 0), inorm);
@@ -900,7 +906,7 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
                         const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
                         const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, int64_t n, float p,
                         const int32_t* rows, int64_t n_src, float* ws, int64_t ws_floats, int* nslab,
-                        hipStream_t st) {
+                        hipStream_t st, const int32_t* n_dev = nullptr, int dh_by_node = 0) {
   using F = SavedBwd<DIN, DOUT>;
   const int width = 2 * DOUT * DIN + 2 * DOUT;
   const int grid = saved_grid<DIN, DOUT>(n);
@@ -918,12 +924,37 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
   }
   if (rows != nullptr)
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, true>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
-                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src,
+                       n_dev, dh_by_node);
   else
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
-                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src);
+                       lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src,
+                       nullptr, 0);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
+}
+
+// Hop-chain backward: rows / count from kgat_hop_compact (count on the device,
+// n_max its bound), dH indexed by node, dXd / dS compact.  Saved state only.
+template <int DIN, int DOUT>
+static int launch_hop(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H, int64_t ldh,
+                      const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
+                      const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
+                      float* dW2, float* db2, int64_t n_max, float p, const int32_t* rows, const int32_t* n_dev,
+                      int64_t src_rows, float* ws, int64_t ws_floats, hipStream_t st) {
+  if constexpr (!SavedBwd<DIN, DOUT>::kOk) {
+    return KGAT_ERR_UNSUPPORTED_DIM;
+  } else {
+    const int width = 2 * DOUT * DIN + 2 * DOUT;
+    int nslab = 0;
+    if (int e = launch_saved<DIN, DOUT>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds,
+                                        n_max, p, rows, src_rows, ws, ws_floats, &nslab, st, n_dev, 1))
+      return e;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, nslab, width, dW1, dW2,
+                       db1, db2, DIN, DOUT);
+    KGAT_LAUNCH_CHECK();
+    return KGAT_OK;
+  }
 }
 
 template <int DIN, int DOUT>
@@ -1044,4 +1075,26 @@ extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S,
                          n_rows, dropout_p, seed, rows, src_rows, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_BWD_CALL)
 #undef KGAT_BWD_CALL
+}
+
+extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                        int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
+                                        int64_t lddh, const float* W1, const float* W2, float* dXd, int64_t lddxd,
+                                        float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2,
+                                        const int32_t* rows, const int32_t* count, int64_t n_max, int64_t src_rows,
+                                        int32_t d_in, int32_t d_out, float dropout_p, float* workspace,
+                                        int64_t workspace_floats, void* stream) {
+  if (!X || !S || !H || !norm || !mask || !dH || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 ||
+      !rows || !count || n_max < 0 || src_rows < 0)
+    return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || lddh < d_out || lddxd < d_in || ldds < d_in || ldh < d_out) return KGAT_ERR_INVALID;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_HOP_CALL(a, b)                                                                                       \
+  kgat::launch_hop<a, b>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, dW1, db1, dW2, \
+                         db2, n_max, dropout_p, rows, count, src_rows, workspace, workspace_floats, st)
+  KGAT_BI_DISPATCH(KGAT_HOP_CALL)
+#undef KGAT_HOP_CALL
 }

@@ -180,18 +180,54 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     return out
 
 
-def hop_compact(graph: DeviceGraph):
-    """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked: returns
-    (rows int32 [n] ascending, node_map int32 [N] node -> position or -1, n).  Reads the count
-    back to the host (one stream sync)."""
+def hop_compact(graph: DeviceGraph, sync: bool = False):
+    """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked.
+
+    Returns (rows int32 [N] -- the first n entries are the hop set, ascending --, node_map
+    int32 [N] node -> position or -1, count int32 [1] on the device, n).  With ``sync`` the
+    count is read back (one stream sync) and rows is cut to n; otherwise n is None and
+    consumers read the count on the device (biinter_bwd_hop)."""
     hit, node_map, rows, count, work, host = graph.hop_buffers()
     dev = hit.device
     _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
               count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
+    if not sync:
+        return rows, node_map, count, None
     host.copy_(count, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
     n = int(host.item())
-    return rows[:n], node_map, n
+    return rows[:n], node_map, count, n
+
+
+def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int):
+    """Saved-state bi-interaction backward on a hop set whose size is only known on the device:
+    rows / count from hop_compact, dH indexed by node ([N, d_out], the previous masked product's
+    output).  Returns compact (dXd, dS) with ``out_rows`` rows allocated (the first count are
+    valid) and (dW1, db1, dW2, db2)."""
+    src_rows, din = X.shape
+    dout = W1.shape[0]
+    for t, nm in ((X, "X"), (S, "S"), (dH, "dH"), (H, "H")):
+        _req(t, nm, dim=2)
+    if dH.shape != (src_rows, dout) or H.shape != (src_rows, dout) or S.shape != X.shape:
+        raise ValueError("hop backward shape mismatch")
+    if state is None or state.kind != "fused" or not saved_state_supported(din, dout):
+        raise ValueError("hop backward needs the fused saved state")
+    if out_rows < 1 or rows.numel() < out_rows:
+        raise ValueError("hop rows buffer too small")
+    dev = X.device
+    dXd = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
+    dS = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
+    dW1, dW2 = torch.empty_like(W1), torch.empty_like(W2)
+    db1 = torch.empty(dout, dtype=torch.float32, device=dev)
+    db2 = torch.empty(dout, dtype=torch.float32, device=dev)
+    ws_n = int(_lib.lib().kgat_biinter_bwd_workspace(out_rows, din, dout))
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
+    _lib.call("kgat_biinter_bwd_hop_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
+              state.norm.data_ptr(), state.mask.data_ptr(), dH.data_ptr(), _ld(dH), W1.data_ptr(), W2.data_ptr(),
+              dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(),
+              db2.data_ptr(), rows.data_ptr(), count.data_ptr(), out_rows, src_rows, din, dout, float(dropout_p),
+              ws.data_ptr(), ws.numel(), stream_ptr(dev))
+    return dXd, dS, dW1, db1, dW2, db2
 
 
 def frontier_build(users, pos, neg, node_map: torch.Tensor):

@@ -86,6 +86,24 @@ class MultiHeadAttention(nn.Module):
 HOP_DENSE_FRACTION = 0.4
 
 
+def _hop_estimate(graph, l: int):
+    """Layer l's hop-set size at the previous step (None before the first is known)."""
+    ent = getattr(graph, "_hop_est", {}).get(l)
+    if ent is None or not ent[1].query():
+        return None
+    return int(ent[0].item())
+
+
+def _hop_record(graph, l: int, count: torch.Tensor) -> None:
+    """Copy layer l's device-side hop count to pinned memory for the next step's choice."""
+    est = graph.__dict__.setdefault("_hop_est", {})
+    ent = est.get(l)
+    if ent is None:
+        ent = est[l] = (torch.zeros(1, dtype=torch.int32, pin_memory=True), torch.cuda.Event())
+    ent[0].copy_(count, non_blocking=True)
+    ent[1].record()
+
+
 def _saved(tables, states, l) -> dict:
     """Layer l's forward output + saved state for the backward (none: it recomputes)."""
     return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
@@ -158,20 +176,33 @@ class _CFLoss(torch.autograd.Function):
         kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
         wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
         # ---- remaining layers: on the hop set while it stays small, then densely
-        sparse = hit is not None
+        sparse = hit is not None and HOP_DENSE_FRACTION > 0
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
-            if sparse:
-                hrows, hmap, n_hop = kernels.hop_compact(graph)
+            fused = states[l] is not None and states[l].kind == "fused"
+            if sparse and fused:
+                # hop size stays on the device (no host sync); the sparse/dense choice uses the
+                # size this layer's hop set had at the previous step
+                est = _hop_estimate(graph, l)
+                sparse = est is None or est <= HOP_DENSE_FRACTION * n_nodes
+                if sparse:
+                    hrows, hmap, hcount, _ = kernels.hop_compact(graph)
+                    _hop_record(graph, l, hcount)
+            elif sparse:
+                hrows, hmap, hcount, n_hop = kernels.hop_compact(graph, sync=True)
                 sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
             if sparse:
                 # dX is zero outside the hop set: the bi-interaction backward runs on its rows
                 # only and the A^T product gathers from them only (kgat_spmm_csr_masked_ex_f32);
                 # per row and per output element the arithmetic and order are the dense path's
-                dHc = kernels.gather_rows(dX, hrows)
-                dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,
-                                                                    drops[l], seeds[l], rows=hrows,
-                                                                    **_saved(tables, states, l))
+                if fused:
+                    dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd_hop(
+                        tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], n_nodes)
+                else:
+                    dHc = kernels.gather_rows(dX, hrows)
+                    dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,
+                                                                        drops[l], seeds[l], rows=hrows,
+                                                                        **_saved(tables, states, l))
                 kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
                 if l == 0 and hook is not None:
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)

@@ -414,7 +414,7 @@ def test_spmm_masked_row_hit_hop_compact_and_row_blocks(pkg):
     want[np.repeat(np.arange(n), np.diff(rt))[inF[colt]]] = True
     want |= inF
     np.testing.assert_array_equal(hit.cpu().numpy().astype(bool), want)
-    hrows, hmap, cnt = kernels.hop_compact(g)
+    hrows, hmap, _, cnt = kernels.hop_compact(g, sync=True)
     assert cnt == int(want.sum())
     np.testing.assert_array_equal(hrows.cpu().numpy(), np.nonzero(want)[0])
     m = hmap.cpu().numpy()
