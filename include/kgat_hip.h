@@ -91,11 +91,16 @@ int kgat_spmm_csr_masked_f32(const kgat_csr *A, const int32_t *src_map, const fl
  *            (Yc_init is looked up through src_map[yc_row0 + r]);
  *   row_hit (nullable, int32 [n_rows]): zeroed, then 1 for every output row
  *            that gathered at least one frontier edge or has a Yc_init row,
- *            i.e. a superset of the rows of Y that can be nonzero. */
+ *            i.e. a superset of the rows of Y that can be nonzero;
+ *   src_bits (nullable): kgat_map_bits(src_map) -- the membership test reads
+ *            one bit per edge instead of a map entry. */
 int kgat_spmm_csr_masked_ex_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
                                 const float *Yc_init, int64_t ldyc, int64_t yc_row0, float *Y, int64_t ldy,
-                                int32_t d, int32_t *row_hit, float *workspace, int64_t workspace_floats,
-                                void *stream);
+                                int32_t d, int32_t *row_hit, const uint32_t *src_bits, float *workspace,
+                                int64_t workspace_floats, void *stream);
+
+/* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
+int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 
 /* The next hop set from row_hit (int32 [n], 0/1): node_map[i] = position of i
  * among the flagged nodes (ascending node order) or -1, rows[0..count) = the
@@ -120,6 +125,18 @@ int kgat_biinter_fwd_f32(const float *X, int64_t ldx, const float *S, int64_t ld
                          const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
                          int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
                          float *norm_out, uint64_t *mask_out, void *stream);
+
+/* a1 + a2 forward of one layer in one pass (aggregator.py:54-65):
+ *   S = A . X (written: the backward reads it), H = bi-interaction(X, S)
+ * with kgat_biinter_fwd_f32's saved state (norm_out / mask_out, both or
+ * neither).  Bit-identical to kgat_spmm_csr_f32 followed by
+ * kgat_biinter_fwd_f32.  A square (n_rows = rows of X); d_in in {16, 32, 64},
+ * d_out <= d_in; workspace: n_seg * d_in floats (long-row partials). */
+int kgat_spmm_biinter_fwd_f32(const kgat_csr *A, const float *X, int64_t ldx, float *S, int64_t lds,
+                              const float *W1, const float *b1, const float *W2, const float *b2, float *H,
+                              int64_t ldh, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                              float *norm_out, uint64_t *mask_out, float *workspace, int64_t workspace_floats,
+                              void *stream);
 
 /* Workspace (floats) kgat_biinter_bwd_f32 needs for its weight-gradient slabs. */
 int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int32_t d_out);

@@ -14,6 +14,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "spmm_core.hpp"
 
 namespace kgat {
 
@@ -105,6 +106,67 @@ __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const floa
   }
 }
 
+// The forward epilogue of one 16-row sub-tile st: u = X+S and m = X*S in the
+// A-operand layout (lane (q, c): row c, k in [q*KQ, (q+1)*KQ)), W staged in
+// LDS.  Writes H, the row norms and the per-lane state word.  Shared by
+// biinter_fwd_kernel and spmm_bi_fwd_kernel, so both produce the same bits.
+template <int DIN, int DOUT>
+__device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const float (&m)[DIN / 4], int64_t st,
+                                               int lane, const float* w1s, const float* w2s,
+                                               const float (&bias1)[DOUT / 16], const float (&bias2)[DOUT / 16],
+                                               float p, float scale, uint32_t thr, uint64_t seed,
+                                               float* __restrict__ H, int64_t ldh, int64_t n,
+                                               float* __restrict__ norm_out, uint64_t* __restrict__ mask_out) {
+  using B = BiShape<DIN, DOUT>;
+  const int q = lane >> 4, c = lane & 15;
+  const int64_t r0 = st * 16;
+  float g[B::NCB][4];
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
+  uint64_t word = 0;  // saved state: 3 bits per (cb, i) -- pre_sum > 0, pre_mul > 0, kept
+  constexpr int NG = (B::NCB + 3) / 4;
+  uint64_t dh_[4][NG];
+  if (p > 0.f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, r0 + q * 4 + i, gi, c);
+  }
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    floatx4 acc1, acc2;
+    __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
+    bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pa = acc1[i] + bias1[cb], pb = acc2[i] + bias2[cb];
+      float v = lrelu(pa) + lrelu(pb);
+      bool keep = true;
+      if (p > 0.f) {
+        keep = bi_drop_keep(dh_[i][cb / 4], cb, thr);
+        v = keep ? v * scale : 0.f;
+      }
+      if (B::NCB * 12 <= 64)
+        word |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << ((cb * 4 + i) * 3);
+      g[cb][i] = v;
+      sq[i] = fmaf(v, v, sq[i]);
+    }
+  }
+  if (mask_out != nullptr) mask_out[st * 64 + lane] = word;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float nrm = sqrtf(sum16(sq[i]));
+    const float inv = 1.f / fmaxf(nrm, kNormEps);
+    const int64_t row = r0 + q * 4 + i;
+    if (row < n) {
+      float* h = H + row * ldh + c;
+#pragma unroll
+      for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] * inv;
+      // saved norm; negative = the clamp was active (F.normalize's eps)
+      if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
+    }
+  }
+}
+
 template <int DIN, int DOUT>
 __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
@@ -137,7 +199,6 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
   load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
   load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
   for (; st < nsub; st += stride) {
-    const int64_t r0 = st * 16;
     float u[B::KQ], m[B::KQ];
 #pragma unroll
     for (int t = 0; t < B::KQ; ++t) {
@@ -148,51 +209,103 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
       load_rows<DIN>(X, ldx, (st + stride) * 16 + c, n, q, nx);
       load_rows<DIN>(S, lds, (st + stride) * 16 + c, n, q, ns);
     }
-    float g[B::NCB][4];
-    float sq[4] = {0.f, 0.f, 0.f, 0.f};
-    uint64_t word = 0;  // saved state: 3 bits per (cb, i) -- pre_sum > 0, pre_mul > 0, kept
-    constexpr int NG = (B::NCB + 3) / 4;
-    uint64_t dh_[4][NG];
-    if (p > 0.f) {
+    bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
+                              mask_out);
+  }
+}
+
+// Propagation + bi-interaction forward in one pass (aggregator.py:54-65):
+// a wave owns a 16-row sub-tile; its 64/(DIN/4) lane groups gather the
+// sub-tile's S rows (the a1 edge walk of spmm_core.hpp, same order as
+// spmm_main_kernel), store them (saved for the backward) and transpose them
+// through a per-wave LDS tile into the MFMA operand layout; then the
+// sub-tile's epilogue runs as in biinter_fwd_kernel.  Rows longer than
+// long_threshold were produced beforehand by the segment + fix-up passes and
+// are read back from S.  S never makes a second trip through HBM and the
+// MFMA work of one wave overlaps the gathers of the others.
+template <int DIN>
+struct FusedFwdShape {
+  static constexpr int kWaves = 8;                     // 512-thread blocks share one W copy
+  static constexpr int kTile = 16 * (DIN + 4);         // floats of a wave's S tile
+};
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(512) void spmm_bi_fwd_kernel(kgat_csr A, const float* __restrict__ X, int64_t ldx,
+                                                          float* __restrict__ S, int64_t lds,
+                                                          const float* __restrict__ W1, const float* __restrict__ b1,
+                                                          const float* __restrict__ W2, const float* __restrict__ b2,
+                                                          float* __restrict__ H, int64_t ldh, float p, uint64_t seed,
+                                                          float* __restrict__ norm_out,
+                                                          uint64_t* __restrict__ mask_out) {
+  using B = BiShape<DIN, DOUT>;
+  using SS = SpmmShape<DIN>;
+  using FS = FusedFwdShape<DIN>;
+  constexpr int L = SS::kLanes, G = SS::kGroups;
+  __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD + FS::kWaves * FS::kTile];
+  float* w1s = smem;
+  float* w2s = smem + DOUT * B::WLD;
+  stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  const int g = lane / L, gl = lane % L, base = g * L;
+  float* tile = smem + 2 * DOUT * B::WLD + wave * FS::kTile;
+  float bias1[B::NCB], bias2[B::NCB];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    bias1[cb] = b1[cb * 16 + c];
+    bias2[cb] = b2[cb * 16 + c];
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = bi_drop_threshold(p);
+  const int64_t n = A.n_rows;
+  const int64_t nsub = (n + 15) / 16;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * FS::kWaves;
+  const SpmmIo io{X, ldx, S, lds, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr};
+  for (int64_t st = static_cast<int64_t>(blockIdx.x) * FS::kWaves + wave; st < nsub; st += stride) {
+    const int64_t r0 = st * 16;
+    // the sub-tile's own X rows, in the operand layout (issued before the gathers)
+    float xv[B::KQ];
+    load_rows<DIN>(X, ldx, r0 + c, n, q, xv);
 #pragma unroll
-        for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, r0 + q * 4 + i, gi, c);
-    }
-#pragma unroll
-    for (int cb = 0; cb < B::NCB; ++cb) {
-      floatx4 acc1, acc2;
-      __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
-      bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float pa = acc1[i] + bias1[cb], pb = acc2[i] + bias2[cb];
-        float v = lrelu(pa) + lrelu(pb);
-        bool keep = true;
-        if (p > 0.f) {
-          keep = bi_drop_keep(dh_[i][cb / 4], cb, thr);
-          v = keep ? v * scale : 0.f;
+    for (int k = 0; k < 16 / G; ++k) {
+      const int lr = g + k * G;
+      const int64_t r = r0 + lr;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < n) {
+        const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+        float4* srow = reinterpret_cast<float4*>(S + r * lds) + gl;
+        if (end - beg > A.long_threshold) {
+          acc = *srow;  // long row: the fix-up pass wrote it
+        } else {
+          bool any = false;
+          gather_edges<DIN, false>(A, io, beg, end, base, gl, acc, any);
+          *srow = acc;
         }
-        if (B::NCB * 12 <= 64)
-          word |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << ((cb * 4 + i) * 3);
-        g[cb][i] = v;
-        sq[i] = fmaf(v, v, sq[i]);
+      }
+      *reinterpret_cast<float4*>(tile + lr * (DIN + 4) + gl * 4) = acc;
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+    float u[B::KQ], m[B::KQ];
+    {
+      const float* sr = tile + c * (DIN + 4) + q * B::KQ;
+#pragma unroll
+      for (int t = 0; t < B::KQ; t += 4) {
+        const float4 sv = *reinterpret_cast<const float4*>(sr + t);
+        u[t] = xv[t] + sv.x;
+        m[t] = xv[t] * sv.x;
+        u[t + 1] = xv[t + 1] + sv.y;
+        m[t + 1] = xv[t + 1] * sv.y;
+        u[t + 2] = xv[t + 2] + sv.z;
+        m[t + 2] = xv[t + 2] * sv.z;
+        u[t + 3] = xv[t + 3] + sv.w;
+        m[t + 3] = xv[t + 3] * sv.w;
       }
     }
-    if (mask_out != nullptr) mask_out[st * 64 + lane] = word;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float nrm = sqrtf(sum16(sq[i]));
-      const float inv = 1.f / fmaxf(nrm, kNormEps);
-      const int64_t row = r0 + q * 4 + i;
-      if (row < n) {
-        float* h = H + row * ldh + c;
-#pragma unroll
-        for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] * inv;
-        // saved norm; negative = the clamp was active (F.normalize's eps)
-        if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
-      }
-    }
+    __builtin_amdgcn_wave_barrier();  // tile reads done before the next sub-tile overwrites it
+    bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
+                              mask_out);
   }
 }
 
@@ -874,6 +987,20 @@ static int launch_bwd_kernel(int grid, const float* X, int64_t ldx, const float*
 }
 
 template <int DIN, int DOUT>
+static int launch_spmm_fwd(const kgat_csr& A, const float* X, int64_t ldx, float* S, int64_t lds, const float* W1,
+                           const float* b1, const float* W2, const float* b2, float* H, int64_t ldh, float p,
+                           uint64_t seed, float* norm, uint64_t* mask, float* ws, hipStream_t st) {
+  const SpmmIo io{X, ldx, S, lds, ws, nullptr, nullptr, 0, nullptr, 0, nullptr};
+  if (int e = spmm_long_rows(A, io, DIN, st)) return e;
+  const int64_t nsub = (A.n_rows + 15) / 16;
+  const int grid = blocks_for(nsub, FusedFwdShape<DIN>::kWaves, kCUs * 16);
+  hipLaunchKernelGGL((spmm_bi_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(64 * FusedFwdShape<DIN>::kWaves), 0, st, A, X,
+                     ldx, S, lds, W1, b1, W2, b2, H, ldh, p, seed, norm, mask);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
                       float* norm, uint64_t* mask, hipStream_t st) {
@@ -1097,4 +1224,34 @@ extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float
                          db2, n_max, dropout_p, rows, count, src_rows, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_HOP_CALL)
 #undef KGAT_HOP_CALL
+}
+
+extern "C" int kgat_spmm_biinter_fwd_f32(const kgat_csr* A, const float* X, int64_t ldx, float* S, int64_t lds,
+                                         const float* W1, const float* b1, const float* W2, const float* b2, float* H,
+                                         int64_t ldh, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                                         float* norm_out, uint64_t* mask_out, float* workspace,
+                                         int64_t workspace_floats, void* stream) {
+  if (!A || !X || !S || !W1 || !b1 || !W2 || !b2 || !H || A->n_rows < 0) return KGAT_ERR_INVALID;
+  if ((norm_out == nullptr) != (mask_out == nullptr) || d_out > 64) return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out) return KGAT_ERR_INVALID;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d_in))
+    return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_SPMM_FWD_CALL(a, b) \
+  kgat::launch_spmm_fwd<a, b>(*A, X, ldx, S, lds, W1, b1, W2, b2, H, ldh, dropout_p, seed, norm_out, mask_out, \
+                              workspace, st)
+  switch (d_in * 1000 + d_out) {
+    case 64064: return KGAT_SPMM_FWD_CALL(64, 64);
+    case 64032: return KGAT_SPMM_FWD_CALL(64, 32);
+    case 64016: return KGAT_SPMM_FWD_CALL(64, 16);
+    case 32032: return KGAT_SPMM_FWD_CALL(32, 32);
+    case 32016: return KGAT_SPMM_FWD_CALL(32, 16);
+    case 16016: return KGAT_SPMM_FWD_CALL(16, 16);
+    default: return KGAT_ERR_UNSUPPORTED_DIM;
+  }
+#undef KGAT_SPMM_FWD_CALL
 }

@@ -25,102 +25,11 @@
 // from a compact Yc through the same map.  Skipped edges contribute exactly
 // 0, so the result equals the dense product with zero rows.
 #include "common.hpp"
+#include "spmm_core.hpp"
 
 #include <hipcub/hipcub.hpp>
 
 namespace kgat {
-
-enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2 };
-
-struct SpmmIo {
-  const float* X;         // source rows (dense) or compact source rows (masked)
-  int64_t ldx;
-  float* Y;
-  int64_t ldy;
-  float* part;            // [n_seg][D] long-row segment partials
-  const int32_t* src_map; // masked: node -> compact row or -1
-  const float* Yc;        // masked: compact init rows (nullable)
-  int64_t ldyc;
-  int32_t* row_hit;       // masked: set to 1 for every output row that gathered an edge or has a Yc row (nullable)
-  int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
-};
-
-template <int D>
-struct SpmmShape {
-  static constexpr int kLanes = D / 4;            // float4 lanes per row
-  static constexpr int kGroups = kWave / kLanes;  // rows in flight per wave
-  static constexpr int kRowsPerGroup = 4;
-  static constexpr int kRowsPerWave = kGroups * kRowsPerGroup;
-  static constexpr int kRowsPerBlock = kRowsPerWave * 4;  // 256-thread blocks
-};
-
-__device__ __forceinline__ void fma4(float v, const float4& x, float4& acc) {
-  acc.x = fmaf(v, x.x, acc.x);
-  acc.y = fmaf(v, x.y, acc.y);
-  acc.z = fmaf(v, x.z, acc.z);
-  acc.w = fmaf(v, x.w, acc.w);
-}
-
-__device__ __forceinline__ void add4(float4& a, const float4& b) {
-  a.x += b.x;
-  a.y += b.y;
-  a.z += b.z;
-  a.w += b.w;
-}
-
-// Accumulate edges [beg, end) of one row into acc.  All lanes of the group
-// (base .. base+kLanes-1) run this with identical bounds (group-uniform).
-template <int D, bool MASKED>
-__device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
-                                             int gl, float4& acc, bool& any) {
-  constexpr int L = SpmmShape<D>::kLanes;
-  const float4* X4 = reinterpret_cast<const float4*>(io.X);
-  const int64_t ldx4 = io.ldx / 4;
-  for (int64_t cb = beg; cb < end; cb += L) {
-    const int n = static_cast<int>(end - cb < L ? end - cb : L);
-    int mc = 0;
-    float mv = 0.f;
-    if (gl < n) {
-      mc = A.col[cb + gl];
-      mv = A.val[cb + gl];
-      if (MASKED) mc = io.src_map[mc];
-    }
-    if (MASKED) {
-      // only frontier sources gather (usually none in a chunk); skipped edges
-      // add an exact 0, so edge order is preserved among the ones that do
-      uint64_t hit = (__ballot(gl < n && mc >= 0) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
-      any |= hit != 0;
-      while (hit) {
-        const int j = __ffsll(static_cast<long long>(hit)) - 1;
-        hit &= hit - 1;
-        const int c = __shfl(mc, base + j);
-        const float v = __shfl(mv, base + j);
-        fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
-      }
-      continue;
-    }
-    int j = 0;
-    for (; j + 4 <= n; j += 4) {
-      const int c0 = __shfl(mc, base + j), c1 = __shfl(mc, base + j + 1);
-      const int c2 = __shfl(mc, base + j + 2), c3 = __shfl(mc, base + j + 3);
-      const float v0 = __shfl(mv, base + j), v1 = __shfl(mv, base + j + 1);
-      const float v2 = __shfl(mv, base + j + 2), v3 = __shfl(mv, base + j + 3);
-      const float4 x0 = X4[static_cast<int64_t>(c0) * ldx4 + gl];
-      const float4 x1 = X4[static_cast<int64_t>(c1) * ldx4 + gl];
-      const float4 x2 = X4[static_cast<int64_t>(c2) * ldx4 + gl];
-      const float4 x3 = X4[static_cast<int64_t>(c3) * ldx4 + gl];
-      fma4(v0, x0, acc);
-      fma4(v1, x1, acc);
-      fma4(v2, x2, acc);
-      fma4(v3, x3, acc);
-    }
-    for (; j < n; ++j) {
-      const int c = __shfl(mc, base + j);
-      const float v = __shfl(mv, base + j);
-      fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
-    }
-  }
-}
 
 // Final write of one output row segment (lane gl) in the three modes.
 template <int MODE>
@@ -236,6 +145,30 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   return KGAT_OK;
 }
 
+// Only the long rows: segment partials + fix-up, writing Y's long rows (the
+// fused propagation + bi-interaction forward reads them back).
+template <int D>
+static int launch_long(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
+  if (A.n_long == 0) return KGAT_OK;
+  const int seg_blocks = (A.n_seg + 3) / 4;
+  hipLaunchKernelGGL((spmm_main_kernel<D, kOverwrite>), dim3(seg_blocks), dim3(256), 0, st, A, io, seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL((spmm_fixup_kernel<D, kOverwrite>), dim3(A.n_long), dim3(256), 0, st, A, io);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+int spmm_long_rows(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) {
+  switch (d) {
+    case 16: return launch_long<16>(A, io, st);
+    case 32: return launch_long<32>(A, io, st);
+    case 64: return launch_long<64>(A, io, st);
+    case 128: return launch_long<128>(A, io, st);
+    case 256: return launch_long<256>(A, io, st);
+    default: return KGAT_ERR_UNSUPPORTED_DIM;
+  }
+}
+
 template <int MODE>
 static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) {
   switch (d) {
@@ -249,6 +182,14 @@ static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) 
 }
 
 static bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
+
+// Frontier bitmap from a node map: bit i of the (64-bit) word i/64 = map[i] >= 0.
+__global__ __launch_bounds__(256) void map_bits_kernel(const int32_t* __restrict__ node_map, int64_t n,
+                                                       uint64_t* __restrict__ bits) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t b = __ballot(i < n && node_map[i] >= 0);
+  if ((threadIdx.x & 63) == 0 && i < n) bits[i >> 6] = b;
+}
 
 // Hop set from the masked product's row flags: pos = exclusive scan of hit
 // (already in node_map); a flagged node keeps its position and is listed in
@@ -280,15 +221,15 @@ extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx,
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0};
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return accumulate ? dispatch<kAccumulate>(*A, io, d, st) : dispatch<kOverwrite>(*A, io, d, st);
 }
 
 extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
                                            const float* Yc_init, int64_t ldyc, int64_t yc_row0, float* Y, int64_t ldy,
-                                           int32_t d, int32_t* row_hit, float* workspace, int64_t workspace_floats,
-                                           void* stream) {
+                                           int32_t d, int32_t* row_hit, const uint32_t* src_bits, float* workspace,
+                                           int64_t workspace_floats, void* stream) {
   using namespace kgat;
   if (!A || !src_map || !Xc || !Y || A->n_rows < 0 || ldxc < d || ldy < d || (ldxc & 3) || (ldy & 3) || yc_row0 < 0)
     return KGAT_ERR_INVALID;
@@ -301,14 +242,14 @@ extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src
   if (row_hit != nullptr &&
       hipMemsetAsync(row_hit, 0, static_cast<size_t>(A->n_rows) * sizeof(int32_t), st) != hipSuccess)
     return KGAT_ERR_INVALID;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0};
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0, src_bits};
   return dispatch<kMasked>(*A, io, d, st);
 }
 
 extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
                                         const float* Yc_init, int64_t ldyc, float* Y, int64_t ldy, int32_t d,
                                         float* workspace, int64_t workspace_floats, void* stream) {
-  return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, workspace,
+  return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, nullptr, workspace,
                                      workspace_floats, stream);
 }
 
@@ -332,6 +273,16 @@ extern "C" int kgat_hop_compact(const int32_t* hit, int64_t n, int32_t* node_map
   const hipError_t e = hipcub::DeviceScan::ExclusiveSum(work, bytes, hit, node_map, static_cast<int>(n), st);
   if (e != hipSuccess) return static_cast<int>(e);
   hipLaunchKernelGGL(kgat::hop_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, hit, n, node_map, rows, count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_map_bits(const int32_t* node_map, int64_t n, uint32_t* bits, void* stream) {
+  if (!node_map || !bits || n < 0) return KGAT_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(bits) & 7) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::map_bits_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     node_map, n, reinterpret_cast<uint64_t*>(bits));
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -1,0 +1,130 @@
+// Shared pieces of the CSR gather (a1, src/model/KGAT/aggregator.py:54): the
+// row-per-group edge walk used by spmm.hip and by the fused propagation +
+// bi-interaction forward in biinter.hip.
+#pragma once
+
+#include "common.hpp"
+
+namespace kgat {
+
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2 };
+
+struct SpmmIo {
+  const float* X;         // source rows (dense) or compact source rows (masked)
+  int64_t ldx;
+  float* Y;
+  int64_t ldy;
+  float* part;            // [n_seg][D] long-row segment partials
+  const int32_t* src_map; // masked: node -> compact row or -1
+  const float* Yc;        // masked: compact init rows (nullable)
+  int64_t ldyc;
+  int32_t* row_hit;       // masked: set to 1 for every output row that gathered an edge or has a Yc row (nullable)
+  int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
+  const uint32_t* src_bits;  // masked: bit c set <=> src_map[c] >= 0 (nullable: test src_map directly)
+};
+
+template <int D>
+struct SpmmShape {
+  static constexpr int kLanes = D / 4;            // float4 lanes per row
+  static constexpr int kGroups = kWave / kLanes;  // rows in flight per wave
+  static constexpr int kRowsPerGroup = 4;
+  static constexpr int kRowsPerWave = kGroups * kRowsPerGroup;
+  static constexpr int kRowsPerBlock = kRowsPerWave * 4;  // 256-thread blocks
+};
+
+__device__ __forceinline__ void fma4(float v, const float4& x, float4& acc) {
+  acc.x = fmaf(v, x.x, acc.x);
+  acc.y = fmaf(v, x.y, acc.y);
+  acc.z = fmaf(v, x.z, acc.z);
+  acc.w = fmaf(v, x.w, acc.w);
+}
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+
+// Accumulate edges [beg, end) of one row into acc.  All lanes of the group
+// (base .. base+kLanes-1) run this with identical bounds (group-uniform).
+template <int D, bool MASKED>
+__device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
+                                             int gl, float4& acc, bool& any) {
+  constexpr int L = SpmmShape<D>::kLanes;
+  const float4* X4 = reinterpret_cast<const float4*>(io.X);
+  const int64_t ldx4 = io.ldx / 4;
+  for (int64_t cb = beg; cb < end; cb += L) {
+    const int n = static_cast<int>(end - cb < L ? end - cb : L);
+    int mc = 0;
+    float mv = 0.f;
+    if (MASKED) {
+      // membership first (a bit of the frontier bitmap: 1/32 of the map's bytes, cache
+      // resident), the compact row and the value only for the edges that gather;
+      // skipped edges add an exact 0, so the gathered ones keep the dense order
+      bool in = false;
+      if (gl < n) {
+        mc = A.col[cb + gl];
+        in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
+      }
+      uint64_t hit = (__ballot(in) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
+      if (hit == 0) continue;
+      any = true;
+      if (in) {
+        mc = io.src_map[mc];
+        mv = A.val[cb + gl];
+      }
+      // up to four gathers in flight, summed in edge order
+      while (hit) {
+        int jj[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          jj[k] = hit ? __ffsll(static_cast<long long>(hit)) - 1 : -1;
+          hit &= hit ? hit - 1 : 0ull;
+        }
+        float4 xs[4];
+        float vs[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int src = base + (jj[k] >= 0 ? jj[k] : 0);
+          const int c = __shfl(mc, src);
+          vs[k] = __shfl(mv, src);
+          xs[k] = jj[k] >= 0 ? X4[static_cast<int64_t>(c) * ldx4 + gl] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (jj[k] >= 0) fma4(vs[k], xs[k], acc);
+      }
+      continue;
+    }
+    if (gl < n) {
+      mc = A.col[cb + gl];
+      mv = A.val[cb + gl];
+    }
+    int j = 0;
+    for (; j + 4 <= n; j += 4) {
+      const int c0 = __shfl(mc, base + j), c1 = __shfl(mc, base + j + 1);
+      const int c2 = __shfl(mc, base + j + 2), c3 = __shfl(mc, base + j + 3);
+      const float v0 = __shfl(mv, base + j), v1 = __shfl(mv, base + j + 1);
+      const float v2 = __shfl(mv, base + j + 2), v3 = __shfl(mv, base + j + 3);
+      const float4 x0 = X4[static_cast<int64_t>(c0) * ldx4 + gl];
+      const float4 x1 = X4[static_cast<int64_t>(c1) * ldx4 + gl];
+      const float4 x2 = X4[static_cast<int64_t>(c2) * ldx4 + gl];
+      const float4 x3 = X4[static_cast<int64_t>(c3) * ldx4 + gl];
+      fma4(v0, x0, acc);
+      fma4(v1, x1, acc);
+      fma4(v2, x2, acc);
+      fma4(v3, x3, acc);
+    }
+    for (; j < n; ++j) {
+      const int c = __shfl(mc, base + j);
+      const float v = __shfl(mv, base + j);
+      fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
+    }
+  }
+}
+
+// Long rows only (segments + fix-up) of Y = A . X, kOverwrite; defined in spmm.hip.
+int spmm_long_rows(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st);
+
+}  // namespace kgat

@@ -87,7 +87,8 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
 
 
 def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor,
-                      Yc_init: torch.Tensor | None = None, row0: int = 0) -> torch.Tensor:
+                      Yc_init: torch.Tensor | None = None, row0: int = 0,
+                      src_bits: torch.Tensor | None = None) -> torch.Tensor:
     """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row); with Yc_init,
     local row r also gets Yc_init[src_map[row0 + r]] (B = rows [row0, ...) of a square matrix)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
@@ -106,7 +107,8 @@ def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.T
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
-              int(row0), out.data_ptr(), _ld(out), d, None, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+              int(row0), out.data_ptr(), _ld(out), d, None, _bits_ptr(src_bits, src_map), ws.data_ptr(), ws.numel(),
+              stream_ptr(Xc.device))
     return out
 
 
@@ -144,8 +146,26 @@ def add_(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def _bits_ptr(src_bits: torch.Tensor | None, src_map: torch.Tensor):
+    if src_bits is None:
+        return None
+    _req(src_bits, "src_bits", dtype=torch.int32, dim=1)
+    if src_bits.numel() < 2 * ((src_map.numel() + 63) // 64) or src_bits.data_ptr() % 8:
+        raise ValueError("src_bits must be map_bits(src_map)")
+    return src_bits.data_ptr()
+
+
+def map_bits(node_map: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out (int32 [2*ceil(N/64)], 8-byte aligned): bit i set <=> node_map[i] >= 0 (kgat_map_bits)."""
+    _req(node_map, "node_map", dtype=torch.int32, dim=1)
+    _bits_ptr(out, node_map)
+    _lib.call("kgat_map_bits", node_map.data_ptr(), node_map.numel(), out.data_ptr(), stream_ptr(node_map.device))
+    return out
+
+
 def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None = None,
-                transpose: bool = False, row_hit: torch.Tensor | None = None) -> torch.Tensor:
+                transpose: bool = False, row_hit: torch.Tensor | None = None,
+                src_bits: torch.Tensor | None = None) -> torch.Tensor:
     """Dense Y = A . X where X is zero outside a frontier: X[node] = Xc[src_map[node]] (src_map -1 => 0),
     plus Yc_init[src_map[r]] on frontier rows.  Returns a new dense [N, d] tensor.  With ``row_hit``
     (int32 [N]) the rows of Y that can be nonzero are flagged 1 (the next hop set, see hop_compact)."""
@@ -172,8 +192,8 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
         e0.record()
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0, 0,
-              out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None, ws.data_ptr(),
-              ws.numel(), stream_ptr(Xc.device))
+              out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None,
+              _bits_ptr(src_bits, src_map), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, transpose, "masked"))
@@ -184,13 +204,15 @@ def hop_compact(graph: DeviceGraph, sync: bool = False):
     """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked.
 
     Returns (rows int32 [N] -- the first n entries are the hop set, ascending --, node_map
-    int32 [N] node -> position or -1, count int32 [1] on the device, n).  With ``sync`` the
+    int32 [N] node -> position or -1, count int32 [1] on the device, n); the hop set's
+    membership bitmap is left in graph.hop_buffers()[6] (kgat_map_bits).  With ``sync`` the
     count is read back (one stream sync) and rows is cut to n; otherwise n is None and
     consumers read the count on the device (biinter_bwd_hop)."""
-    hit, node_map, rows, count, work, host = graph.hop_buffers()
+    hit, node_map, rows, count, work, host, bits = graph.hop_buffers()
     dev = hit.device
     _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
               count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
+    map_bits(node_map, bits)
     if not sync:
         return rows, node_map, count, None
     host.copy_(count, non_blocking=True)
@@ -332,6 +354,46 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
               ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.norm.data_ptr() if state is not None else None,
               state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
     return out
+
+
+# (d_in, d_out) pairs of the fused propagation + bi-interaction forward (kgat_spmm_biinter_fwd_f32)
+SPMM_FUSED_SHAPES = {(64, 64), (64, 32), (64, 16), (32, 32), (32, 16), (16, 16)}
+
+
+def spmm_biinter_fwd(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
+                     state: BiState | None = None):
+    """S = A . X and H = biinter(X, S) in one pass; returns (S, H).  Same bits as spmm + biinter_fwd."""
+    for t, nm in ((X, "X"), (W1, "W1"), (W2, "W2")):
+        _req(t, nm, dim=2)
+    n, din = X.shape
+    dout = W1.shape[0]
+    if n != graph.n_nodes or W1.shape != (dout, din) or W2.shape != (dout, din) or b1.numel() != dout:
+        raise ValueError("fused forward shape mismatch")
+    if (din, dout) not in SPMM_FUSED_SHAPES:
+        raise ValueError(f"no fused propagation forward for {din}->{dout}")
+    if not (W1.is_contiguous() and W2.is_contiguous()):
+        raise ValueError("W must be contiguous")
+    if state is not None and (state.kind != "fused" or state.norm.numel() < n
+                              or state.mask.numel() < (n + 15) // 16 * 64):
+        raise ValueError("bi-interaction state does not match the layer")
+    S = torch.empty(n, din, dtype=torch.float32, device=X.device)
+    H = torch.empty(n, dout, dtype=torch.float32, device=X.device)
+    csr = graph.A
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * din), dtype=torch.float32, device=X.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_biinter_fwd_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), S.data_ptr(), _ld(S),
+              W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), H.data_ptr(), _ld(H), din, dout,
+              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              state.norm.data_ptr() if state is not None else None,
+              state.mask.data_ptr() if state is not None else None, ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, din, False, "fused"))
+    return S, H
 
 
 def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,

@@ -171,7 +171,10 @@ class _CFLoss(torch.autograd.Function):
         l = L - 1
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
-        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True, row_hit=hit)
+        bits = graph.hop_buffers()[6]
+        kernels.map_bits(graph.node_map, bits)
+        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True, row_hit=hit,
+                                 src_bits=bits)
         kernels.frontier_reset(rows, graph.node_map)
         kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
         wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
@@ -208,11 +211,11 @@ class _CFLoss(torch.autograd.Function):
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
                     for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
                         kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
-                                                  Yc_init=dXdc, row0=view.r0)
+                                                  Yc_init=dXdc, row0=view.r0, src_bits=bits)
                         hook.block_ready(k, dX)
                 else:
                     dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True,
-                                             row_hit=hit if l > 0 else None)
+                                             row_hit=hit if l > 0 else None, src_bits=bits)
                 wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
                 continue
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],

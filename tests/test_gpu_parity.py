@@ -422,6 +422,14 @@ def test_spmm_masked_row_hit_hop_compact_and_row_blocks(pkg):
     assert np.all(m[~want] == -1)
     # rows outside the hop set are exactly zero
     assert float(out[torch.from_numpy(~want).to(DEV)].abs().max()) == 0.0
+    # the bitmap membership test gives the same bits (and flags)
+    bits = kernels.map_bits(nm, torch.empty(2 * ((n + 63) // 64), dtype=torch.int32, device=DEV))
+    bw = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    np.testing.assert_array_equal(bw, inF)
+    hit2 = torch.zeros_like(hit)
+    out2 = kernels.spmm_masked(g, nm, Xc, Yc_init=Yc, transpose=True, row_hit=hit2, src_bits=bits)
+    assert torch.equal(out2, out)
+    np.testing.assert_array_equal(hit2.cpu().numpy().astype(bool), want)
     # row-block views (yc_row0) give the same bits
     bounds = [(0, 1700), (1700, 3333), (3333, n)]
     blk = torch.empty_like(out)
@@ -463,6 +471,32 @@ def test_cf_hop_chain_matches_dense_backward(pkg, layers):
     assert torch.equal(sp["_user_entity_embedding.weight"], de["_user_entity_embedding.weight"])
     for k in sp:
         np.testing.assert_allclose(sp[k].cpu().numpy(), de[k].cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+@pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (32, 16), (16, 16)])
+def test_spmm_biinter_fused_forward_bit_identical(pkg, din, dout):
+    """kgat_spmm_biinter_fwd_f32 (propagation + bi-interaction in one pass, long hub rows via the
+    segment pass) against kgat_spmm_csr_f32 + kgat_biinter_fwd_f32: S, H, norms and state words
+    bit for bit, with and without dropout; ragged last sub-tile (n % 16 != 0)."""
+    graph_mod, kernels = _mods(pkg)
+    lay, _ = random_graph(graph_mod, 3001, 12, hubs=6, hub_deg=2000, seed=din + dout)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    assert g.A.n_long > 0
+    torch.manual_seed(din * dout)
+    X = torch.randn(lay.n_nodes, din, device=DEV)
+    W1, W2 = torch.randn(dout, din, device=DEV) * 0.2, torch.randn(dout, din, device=DEV) * 0.2
+    b1, b2 = torch.randn(dout, device=DEV) * 0.1, torch.randn(dout, device=DEV) * 0.1
+    for p in (0.0, 0.1):
+        st_a = kernels.make_state(lay.n_nodes, din, dout, DEV)
+        st_b = kernels.make_state(lay.n_nodes, din, dout, DEV)
+        S_ref = kernels.spmm(g, X)
+        H_ref = kernels.biinter_fwd(X, S_ref, W1, b1, W2, b2, p, 99, state=st_a)
+        S, H = kernels.spmm_biinter_fwd(g, X, W1, b1, W2, b2, p, 99, state=st_b)
+        assert torch.equal(S, S_ref)
+        assert torch.equal(H, H_ref)
+        n = lay.n_nodes
+        assert torch.equal(st_a.norm[:n], st_b.norm[:n])
+        assert torch.equal(st_a.mask[:(n + 15) // 16 * 64], st_b.mask[:(n + 15) // 16 * 64])
 
 
 def test_biinter_bwd_rows_matches_dense(pkg):

@@ -72,6 +72,10 @@ def main():
             byt + 4 * n * d)
     if want("graph"):
         graph_section(args, K, g, U, E, n, dev, rec)
+    if want("fused"):
+        fused_section(args, K, g, n, dev, rec)
+    if want("masked"):
+        masked_section(args, K, g, U, E, n, dev, rec)
     if want("nfm"):
         nfm_section(args, dev, rec)
 
@@ -116,6 +120,53 @@ def graph_section(args, K, g, U, E, n, dev, rec):
     rec("adam_table", timeit(lambda: K.adam(p, gg, m, v, 1e-3, 0.9, 0.999, 0.03, 1e-8), args.reps), 28 * p.numel())
     tables = [torch.randn(n, 64, device=dev), torch.randn(n, 64, device=dev), torch.randn(n, 32, device=dev)]
     rec("bpr_fwd", timeit(lambda: K.bpr_fwd(tables, users, pos, neg, 1e-5), args.reps))
+
+
+def fused_section(args, K, g, n, dev, rec):
+    """Propagation + bi-interaction forward: two launches (spmm, biinter_fwd) vs the fused pass."""
+    for din, dout in ((64, 64), (64, 32)):
+        X = torch.randn(n, din, device=dev)
+        W1 = torch.randn(dout, din, device=dev) * 0.1
+        W2 = torch.randn(dout, din, device=dev) * 0.1
+        b1 = torch.zeros(dout, device=dev)
+        b2 = torch.zeros(dout, device=dev)
+        st = K.BiState(n, dev, din, dout)
+        S = torch.empty(n, din, device=dev)
+        H = torch.empty(n, dout, device=dev)
+
+        def two():
+            K.spmm(g, X, out=S)
+            K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st)
+
+        rec(f"spmm+biinter_fwd_{din}x{dout}", timeit(two, args.reps))
+        rec(f"spmm_biinter_fused_{din}x{dout}",
+            timeit(lambda: K.spmm_biinter_fwd(g, X, W1, b1, W2, b2, 0.1, 5, state=st), args.reps))
+
+
+def masked_section(args, K, g, U, E, n, dev, rec):
+    """The backward hop chain's masked A^T products at C2: over the batch frontier F0 (flags
+    the hop set) and over the layer-0 hop set (35 % of the edges gather), map vs bitmap test."""
+    B = 256
+    rng = np.random.default_rng(0)
+    users = torch.from_numpy(rng.integers(0, U, B)).to(dev)
+    pos = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+    neg = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+    rows, _ = K.frontier_build(users, pos, neg, g.node_map)
+    hit, hmap, hrows, count, work, host, bits = g.hop_buffers()
+    Sc = torch.randn(3 * B, 64, device=dev)
+    K.map_bits(g.node_map, bits)
+    for nm, b in (("map", None), ("bits", bits)):
+        rec(f"masked_F0_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True, row_hit=hit,
+                                                                  src_bits=b), args.reps))
+    K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True, row_hit=hit)
+    K.frontier_reset(rows, g.node_map)
+    rec("map_bits", timeit(lambda: K.map_bits(g.node_map, bits), args.reps))
+    hr, hm, hc, nh = K.hop_compact(g, sync=True)
+    rec("hop_compact", timeit(lambda: K.hop_compact(g), args.reps), n_hop=nh)
+    Hc = torch.randn(n, 64, device=dev)
+    for nm, b in (("map", None), ("bits", bits)):
+        rec(f"masked_hop1_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, hm, Hc, Hc, transpose=True, src_bits=b),
+                                              args.reps), n_hop=nh)
 
 
 def nfm_section(args, dev, rec):
