@@ -138,6 +138,16 @@ int kgat_spmm_biinter_fwd_f32(const kgat_csr *A, const float *X, int64_t ldx, fl
                               float *norm_out, uint64_t *mask_out, float *workspace, int64_t workspace_floats,
                               void *stream);
 
+/* kgat_biinter_fwd_f32 on rows [node0, node0 + n_rows) of a larger table: X, S,
+ * H, norm_out, mask_out point at that block's first row (mask_out at word
+ * (node0 / 16) * 64), the dropout draws use the global node ids.  node0 a
+ * multiple of 16.  Lets the forward run the bi-interaction of row block b
+ * (one stream) while the propagation of block b + 1 runs (another stream). */
+int kgat_biinter_fwd_rows_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *W1,
+                              const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
+                              int64_t n_rows, int64_t node0, int32_t d_in, int32_t d_out, float dropout_p,
+                              uint64_t seed, float *norm_out, uint64_t *mask_out, void *stream);
+
 /* Workspace (floats) kgat_biinter_bwd_f32 needs for its weight-gradient slabs. */
 int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int32_t d_out);
 

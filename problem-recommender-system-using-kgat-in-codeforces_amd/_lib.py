@@ -66,6 +66,8 @@ _SIGNATURES = {
                                          c_vp]),
     "kgat_biinter_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                             c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
+    "kgat_biinter_fwd_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                                 c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_spmm_biinter_fwd_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                                  c_vp, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp, c_i64,
                                                  c_vp]),

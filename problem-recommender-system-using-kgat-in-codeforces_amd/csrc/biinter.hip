@@ -116,7 +116,8 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
                                                const float (&bias1)[DOUT / 16], const float (&bias2)[DOUT / 16],
                                                float p, float scale, uint32_t thr, uint64_t seed,
                                                float* __restrict__ H, int64_t ldh, int64_t n,
-                                               float* __restrict__ norm_out, uint64_t* __restrict__ mask_out) {
+                                               float* __restrict__ norm_out, uint64_t* __restrict__ mask_out,
+                                               int64_t node0 = 0) {
   using B = BiShape<DIN, DOUT>;
   const int q = lane >> 4, c = lane & 15;
   const int64_t r0 = st * 16;
@@ -129,7 +130,7 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, r0 + q * 4 + i, gi, c);
+      for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, node0 + r0 + q * 4 + i, gi, c);
   }
 #pragma unroll
   for (int cb = 0; cb < B::NCB; ++cb) {
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
                                                           float* __restrict__ H, int64_t ldh, int64_t n, float p,
                                                           uint64_t seed, float* __restrict__ norm_out,
-                                                          uint64_t* __restrict__ mask_out) {
+                                                          uint64_t* __restrict__ mask_out, int64_t node0) {
   using B = BiShape<DIN, DOUT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
   float* w1s = smem;
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
       load_rows<DIN>(S, lds, (st + stride) * 16 + c, n, q, ns);
     }
     bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
-                              mask_out);
+                              mask_out, node0);
   }
 }
 
@@ -230,7 +231,7 @@ struct FusedFwdShape {
 };
 
 template <int DIN, int DOUT>
-__global__ __launch_bounds__(512) void spmm_bi_fwd_kernel(kgat_csr A, const float* __restrict__ X, int64_t ldx,
+__global__ __launch_bounds__(512, 4) void spmm_bi_fwd_kernel(kgat_csr A, const float* __restrict__ X, int64_t ldx,
                                                           float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(512) void spmm_bi_fwd_kernel(kgat_csr A, const floa
           acc = *srow;  // long row: the fix-up pass wrote it
         } else {
           bool any = false;
-          gather_edges<DIN, false>(A, io, beg, end, base, gl, acc, any);
+          gather_edges<DIN, false, 8>(A, io, beg, end, base, gl, acc, any);
           *srow = acc;
         }
       }
@@ -1003,10 +1004,10 @@ static int launch_spmm_fwd(const kgat_csr& A, const float* X, int64_t ldx, float
 template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
-                      float* norm, uint64_t* mask, hipStream_t st) {
+                      float* norm, uint64_t* mask, int64_t node0, hipStream_t st) {
   const int grid = blocks_for(n, 64, kCUs * 8);
   hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, W2, b2,
-                     H, ldh, n, p, seed, norm, mask);
+                     H, ldh, n, p, seed, norm, mask, node0);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -1143,11 +1144,11 @@ static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
-                                    const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
-                                    int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
-                                    float* norm_out, uint64_t* mask_out, void* stream) {
-  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || n_rows < 0) return KGAT_ERR_INVALID;
+extern "C" int kgat_biinter_fwd_rows_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                                         const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
+                                         int64_t n_rows, int64_t node0, int32_t d_in, int32_t d_out, float dropout_p,
+                                         uint64_t seed, float* norm_out, uint64_t* mask_out, void* stream) {
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || n_rows < 0 || node0 < 0 || (node0 & 15)) return KGAT_ERR_INVALID;
   if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
@@ -1155,9 +1156,17 @@ extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S,
   if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_FWD_CALL(a, b) kgat::launch_fwd<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, seed, \
-                                                  norm_out, mask_out, st)
+                                                  norm_out, mask_out, node0, st)
   KGAT_BI_DISPATCH(KGAT_FWD_CALL)
 #undef KGAT_FWD_CALL
+}
+
+extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                                    const float* b1, const float* W2, const float* b2, float* H, int64_t ldh,
+                                    int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                                    float* norm_out, uint64_t* mask_out, void* stream) {
+  return kgat_biinter_fwd_rows_f32(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, 0, d_in, d_out, dropout_p, seed,
+                                   norm_out, mask_out, stream);
 }
 
 extern "C" int64_t kgat_biinter_bwd_workspace(int64_t n_rows, int32_t d_in, int32_t d_out) {

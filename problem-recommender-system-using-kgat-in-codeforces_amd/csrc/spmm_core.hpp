@@ -48,7 +48,7 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 
 // Accumulate edges [beg, end) of one row into acc.  All lanes of the group
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
-template <int D, bool MASKED>
+template <int D, bool MASKED, int U = 4>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
                                              int gl, float4& acc, bool& any) {
   constexpr int L = SpmmShape<D>::kLanes;
@@ -102,19 +102,31 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       mv = A.val[cb + gl];
     }
     int j = 0;
-    for (; j + 4 <= n; j += 4) {
-      const int c0 = __shfl(mc, base + j), c1 = __shfl(mc, base + j + 1);
-      const int c2 = __shfl(mc, base + j + 2), c3 = __shfl(mc, base + j + 3);
-      const float v0 = __shfl(mv, base + j), v1 = __shfl(mv, base + j + 1);
-      const float v2 = __shfl(mv, base + j + 2), v3 = __shfl(mv, base + j + 3);
-      const float4 x0 = X4[static_cast<int64_t>(c0) * ldx4 + gl];
-      const float4 x1 = X4[static_cast<int64_t>(c1) * ldx4 + gl];
-      const float4 x2 = X4[static_cast<int64_t>(c2) * ldx4 + gl];
-      const float4 x3 = X4[static_cast<int64_t>(c3) * ldx4 + gl];
-      fma4(v0, x0, acc);
-      fma4(v1, x1, acc);
-      fma4(v2, x2, acc);
-      fma4(v3, x3, acc);
+    for (; j + U <= n; j += U) {
+      // U source rows in flight, added in edge order
+      float4 xs[U];
+      float vs[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int ck = __shfl(mc, base + j + k);
+        vs[k] = __shfl(mv, base + j + k);
+        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) fma4(vs[k], xs[k], acc);
+    }
+    if (U > 4 && j + 4 <= n) {
+      float4 xs[4];
+      float vs[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ck = __shfl(mc, base + j + k);
+        vs[k] = __shfl(mv, base + j + k);
+        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fma4(vs[k], xs[k], acc);
+      j += 4;
     }
     for (; j < n; ++j) {
       const int c = __shfl(mc, base + j);

@@ -186,6 +186,7 @@ class _CSRRowView:
 
     def __init__(self, base: _DeviceCSR, r0: int, r1: int, device):
         self.base, self.r0, self.n_rows = base, int(r0), int(r1) - int(r0)
+        self.nnz = int(base.rowptr_host[r1] - base.rowptr_host[r0])
         lr, off, sr, sb = long_row_plan(base.rowptr_host[r0:r1 + 1])
         self.long_rows = torch.from_numpy(lr).to(device)
         self.long_seg_off = torch.from_numpy(off).to(device)
@@ -254,6 +255,28 @@ class DeviceGraph:
                   torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device))
             self._hop = hb
         return hb
+
+    def row_blocks(self, k: int) -> list[_CSRRowView]:
+        """k row-block views of A with (about) equal edge counts, boundaries on multiples of 16
+        rows (the bi-interaction's sub-tiles), cached per k."""
+        cache = self.__dict__.setdefault("_a_blocks", {})
+        if k not in cache:
+            rp = self.A.rowptr_host
+            n = self.n_nodes
+            cuts = [0]
+            for b in range(1, k):
+                r = int(np.searchsorted(rp, rp[-1] * b // k)) // 16 * 16
+                cuts.append(min(max(r, cuts[-1]), n))
+            cuts.append(n)
+            cache[k] = [_CSRRowView(self.A, a, b, self.device) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+        return cache[k]
+
+    def side_stream(self):
+        """The second stream of the pipelined layer forward (kernels.propagate_layer)."""
+        s = self.__dict__.get("_side")
+        if s is None:
+            s = self._side = torch.cuda.Stream(device=self.device)
+        return s
 
     def transpose_row_blocks(self, bounds) -> list[_CSRRowView]:
         """Row-block views of A^T for ``bounds`` [(r0, r1), ...] (cached per bounds)."""

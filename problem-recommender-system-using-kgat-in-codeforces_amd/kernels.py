@@ -8,6 +8,7 @@ anything is launched, HIP/launch errors raise ``RuntimeError``.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -354,6 +355,68 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
               ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.norm.data_ptr() if state is not None else None,
               state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
     return out
+
+
+# Row blocks of the pipelined layer forward (0 = one spmm launch, then one biinter_fwd launch).
+FWD_PIPELINE_BLOCKS = int(os.environ.get("KGAT_FWD_BLOCKS", "0"))
+FWD_PIPELINE_MIN_ROWS = 1 << 16
+
+
+def propagate_layer(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
+                    state: BiState | None = None):
+    """One KGAT layer forward (aggregator.py:54-65): S = A . X, H = biinter(X, S); returns (S, H).
+
+    For fused shapes on large graphs the rows are cut into FWD_PIPELINE_BLOCKS blocks of equal
+    edge count: block b's propagation (kgat_spmm_csr_f32 on a row view of A, current stream)
+    overlaps block b-1's bi-interaction (kgat_biinter_fwd_rows_f32, a second stream) -- the
+    gather is fabric-bound, the bi-interaction MFMA-bound.  Same bits as the two whole launches."""
+    n, din = X.shape
+    dout = W1.shape[0]
+    k = FWD_PIPELINE_BLOCKS
+    fused = fused_supported(din, dout) and (state is None or state.kind == "fused")
+    if k <= 1 or not fused or n < FWD_PIPELINE_MIN_ROWS or not X.is_cuda:
+        S = spmm(graph, X)
+        return S, biinter_fwd(X, S, W1, b1, W2, b2, dropout_p, seed, state=state)
+    for t, nm in ((X, "X"), (W1, "W1"), (W2, "W2")):
+        _req(t, nm, dim=2)
+    if n != graph.n_nodes or W1.shape != (dout, din) or W2.shape != (dout, din) or b1.numel() != dout:
+        raise ValueError("layer shape mismatch")
+    if not (W1.is_contiguous() and W2.is_contiguous()):
+        raise ValueError("W must be contiguous")
+    if state is not None and (state.norm.numel() < n or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
+        raise ValueError("bi-interaction state too small or d_out > 64")
+    dev = X.device
+    S = torch.empty(n, din, dtype=torch.float32, device=dev)
+    H = torch.empty(n, dout, dtype=torch.float32, device=dev)
+    main = torch.cuda.current_stream(dev)
+    side = graph.side_stream()
+    ldx, lds, ldh = _ld(X), _ld(S), _ld(H)
+    seed64 = ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF)
+    ev = SPMM_EVENTS
+    for view in graph.row_blocks(k):
+        r0, nb = view.r0, view.n_rows
+        desc = view.descriptor()
+        ws = torch.empty(max(1, view.n_seg * din), dtype=torch.float32, device=dev)
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main)
+        _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), ldx, S.data_ptr() + 4 * r0 * lds, lds, din, 0,
+                  ws.data_ptr(), ws.numel(), main.cuda_stream)
+        if ev is not None:
+            e1.record(main)
+            ev.append((e0, e1, din, False, ("block", nb, int(view.nnz))))
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side.wait_event(ready)
+        _lib.call("kgat_biinter_fwd_rows_f32", X.data_ptr() + 4 * r0 * ldx, ldx, S.data_ptr() + 4 * r0 * lds, lds,
+                  W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), H.data_ptr() + 4 * r0 * ldh, ldh, nb, r0,
+                  din, dout, float(dropout_p), seed64,
+                  state.norm.data_ptr() + 4 * r0 if state is not None else None,
+                  state.mask.data_ptr() + 8 * (r0 // 16) * 64 if state is not None else None, side.cuda_stream)
+    done = torch.cuda.Event()
+    done.record(side)
+    main.wait_event(done)
+    return S, H
 
 
 # (d_in, d_out) pairs of the fused propagation + bi-interaction forward (kgat_spmm_biinter_fwd_f32)

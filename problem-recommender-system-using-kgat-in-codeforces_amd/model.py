@@ -141,9 +141,8 @@ class _CFLoss(torch.autograd.Function):
         x = X0
         for l in range(len(drops)):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
-            s = kernels.spmm(graph, x)
             st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
-            x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
+            s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             sides.append(s)
             states.append(st)
             tables.append(x)
@@ -359,8 +358,7 @@ class KGAT(nn.Module):
             x = self._user_entity_embedding.weight.detach()
             tables = [x]
             for l, agg in enumerate(self._aggregator_layers):
-                s = kernels.spmm(g, x)
-                x = kernels.biinter_fwd(x, s, *[w.detach() for w in agg.weights()], drops[l], seeds[l])
+                _, x = kernels.propagate_layer(g, x, *[w.detach() for w in agg.weights()], drops[l], seeds[l])
                 tables.append(x)
         return tables
 

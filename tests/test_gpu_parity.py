@@ -499,6 +499,35 @@ def test_spmm_biinter_fused_forward_bit_identical(pkg, din, dout):
         assert torch.equal(st_a.mask[:(n + 15) // 16 * 64], st_b.mask[:(n + 15) // 16 * 64])
 
 
+@pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (32, 16)])
+def test_propagate_layer_pipelined_bit_identical(pkg, din, dout):
+    """The row-block pipelined layer forward (propagation of block b on the current stream while
+    block b-1's bi-interaction runs on a second stream, dropout drawn by global node id) gives the
+    same S, H and saved state as one spmm launch followed by one biinter_fwd launch."""
+    graph_mod, kernels = _mods(pkg)
+    lay, _ = random_graph(graph_mod, 5003, 10, hubs=5, hub_deg=1500, seed=din)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    torch.manual_seed(din + dout)
+    n = lay.n_nodes
+    X = torch.randn(n, din, device=DEV)
+    W1, W2 = torch.randn(dout, din, device=DEV) * 0.2, torch.randn(dout, din, device=DEV) * 0.2
+    b1, b2 = torch.randn(dout, device=DEV) * 0.1, torch.randn(dout, device=DEV) * 0.1
+    old = (kernels.FWD_PIPELINE_BLOCKS, kernels.FWD_PIPELINE_MIN_ROWS)
+    try:
+        kernels.FWD_PIPELINE_MIN_ROWS = 0
+        outs = {}
+        for k in (1, 7):
+            kernels.FWD_PIPELINE_BLOCKS = k
+            st = kernels.make_state(n, din, dout, DEV)
+            S, H = kernels.propagate_layer(g, X, W1, b1, W2, b2, 0.1, 1234, state=st)
+            outs[k] = (S, H, st.norm[:n].clone(), st.mask[:(n + 15) // 16 * 64].clone())
+        assert len(g.row_blocks(7)) > 1
+    finally:
+        kernels.FWD_PIPELINE_BLOCKS, kernels.FWD_PIPELINE_MIN_ROWS = old
+    for a, b in zip(outs[1], outs[7]):
+        assert torch.equal(a, b)
+
+
 def test_biinter_bwd_rows_matches_dense(pkg):
     _, kernels = _mods(pkg)
     torch.manual_seed(9)
