@@ -110,6 +110,30 @@ int64_t kgat_hop_compact_work_bytes(int64_t n);
 int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *rows, int32_t *count, void *work,
                      int64_t work_bytes, void *stream);
 
+/* The first hop of the backward chain without scanning the graph: for the
+ * last layer's A^T product over the batch frontier F (rows0[0..n0), -1
+ * padded, kgat_frontier_build), bits0 (uint32 [ceil(n/32)]) marks F and
+ * bits1 marks F plus every column of A's rows F -- the rows that product can
+ * reach; node_map / hop_rows / *hop_count list bits1's set in ascending node
+ * order (node_map fully written, -1 outside).  work:
+ * kgat_frontier_hop_work_bytes(n) bytes. */
+int64_t kgat_frontier_hop_work_bytes(int64_t n);
+int kgat_frontier_hop(const kgat_csr *A, const int32_t *rows0, int32_t n0, uint32_t *bits0, uint32_t *bits1,
+                      int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, void *work, int64_t work_bytes,
+                      void *stream);
+
+/* kgat_spmm_csr_masked_f32 restricted to an output row set (A = A^T of the
+ * graph; out_bits / out_map / out_rows / out_count from kgat_frontier_hop):
+ * Y[k] = row out_rows[k] of the masked product, for k < *out_count (compact,
+ * Y holds n_rows rows of capacity); rows outside the set are not visited.
+ * src_bits (nullable) = the source set's bitmap.  Per row the same edges in
+ * the same order as the dense masked product (same bits). */
+int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, const uint32_t *src_bits,
+                                  const float *Xc, int64_t ldxc, const float *Yc_init, int64_t ldyc,
+                                  const uint32_t *out_bits, const int32_t *out_map, const int32_t *out_rows,
+                                  const int32_t *out_count, float *Y, int64_t ldy, int32_t d, float *workspace,
+                                  int64_t workspace_floats, void *stream);
+
 /* a2 -- bi-interaction aggregator forward, fused:
  *   H = normalize(dropout(LReLU(W1 (X+S) + b1) + LReLU(W2 (X*S) + b2)))
  * Replaces src/model/KGAT/aggregator.py:57-65.  W1/W2 are nn.Linear weights
@@ -167,18 +191,21 @@ int kgat_biinter_bwd_f32(const float *X, int64_t ldx, const float *S, int64_t ld
                          float dropout_p, uint64_t seed, const int32_t *rows, int64_t src_rows,
                          float *workspace, int64_t workspace_floats, void *stream);
 
-/* a2 backward on a hop set of the backward chain (see kgat_hop_compact): rows /
- * count are that call's outputs (count stays on the device; n_max bounds it),
- * dH is indexed by node like X (the dense output of the previous masked
- * product), dXd / dS are compact (row i <-> node rows[i], n_max rows
- * allocated).  Saved forward state only (H, norm, mask; d_out <= 64 and
- * d_in * d_out <= 4096).  Per row the arithmetic is kgat_biinter_bwd_f32's. */
+/* a2 backward on a hop set of the backward chain (see kgat_hop_compact /
+ * kgat_frontier_hop): rows / count are that call's outputs (count stays on the
+ * device; n_max bounds it); dH is indexed by node like X (the dense output of
+ * the previous masked product) or, with dh_compact, by hop position (row i of
+ * dH <-> node rows[i], kgat_spmm_csr_masked_rows_f32's output); dXd / dS are
+ * compact (n_max rows allocated).  Saved forward state only (H, norm, mask;
+ * d_out <= 64 and d_in * d_out <= 4096).  Per row the arithmetic is
+ * kgat_biinter_bwd_f32's. */
 int kgat_biinter_bwd_hop_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H, int64_t ldh,
                              const float *norm, const uint64_t *mask, const float *dH, int64_t lddh,
                              const float *W1, const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds,
                              float *dW1, float *db1, float *dW2, float *db2, const int32_t *rows,
-                             const int32_t *count, int64_t n_max, int64_t src_rows, int32_t d_in, int32_t d_out,
-                             float dropout_p, float *workspace, int64_t workspace_floats, void *stream);
+                             const int32_t *count, int64_t n_max, int64_t src_rows, int32_t dh_compact,
+                             int32_t d_in, int32_t d_out, float dropout_p, float *workspace,
+                             int64_t workspace_floats, void *stream);
 
 /* a2 for the wide layers of C4/C5 (any d_in, d_out multiple of 16 up to 1024; used
  * where the fused kernels above do not dispatch, e.g. 256): two rocBLAS sgemm per

@@ -1069,14 +1069,14 @@ static int launch_hop(const float* X, int64_t ldx, const float* S, int64_t lds, 
                       const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
                       const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
                       float* dW2, float* db2, int64_t n_max, float p, const int32_t* rows, const int32_t* n_dev,
-                      int64_t src_rows, float* ws, int64_t ws_floats, hipStream_t st) {
+                      int64_t src_rows, int dh_by_node, float* ws, int64_t ws_floats, hipStream_t st) {
   if constexpr (!SavedBwd<DIN, DOUT>::kOk) {
     return KGAT_ERR_UNSUPPORTED_DIM;
   } else {
     const int width = 2 * DOUT * DIN + 2 * DOUT;
     int nslab = 0;
     if (int e = launch_saved<DIN, DOUT>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds,
-                                        n_max, p, rows, src_rows, ws, ws_floats, &nslab, st, n_dev, 1))
+                                        n_max, p, rows, src_rows, ws, ws_floats, &nslab, st, n_dev, dh_by_node))
       return e;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, nslab, width, dW1, dW2,
                        db1, db2, DIN, DOUT);
@@ -1218,8 +1218,8 @@ extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float
                                         int64_t lddh, const float* W1, const float* W2, float* dXd, int64_t lddxd,
                                         float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2,
                                         const int32_t* rows, const int32_t* count, int64_t n_max, int64_t src_rows,
-                                        int32_t d_in, int32_t d_out, float dropout_p, float* workspace,
-                                        int64_t workspace_floats, void* stream) {
+                                        int32_t dh_compact, int32_t d_in, int32_t d_out, float dropout_p,
+                                        float* workspace, int64_t workspace_floats, void* stream) {
   if (!X || !S || !H || !norm || !mask || !dH || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 ||
       !rows || !count || n_max < 0 || src_rows < 0)
     return KGAT_ERR_INVALID;
@@ -1230,7 +1230,7 @@ extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_HOP_CALL(a, b)                                                                                       \
   kgat::launch_hop<a, b>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, dW1, db1, dW2, \
-                         db2, n_max, dropout_p, rows, count, src_rows, workspace, workspace_floats, st)
+                         db2, n_max, dropout_p, rows, count, src_rows, dh_compact ? 0 : 1, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_HOP_CALL)
 #undef KGAT_HOP_CALL
 }

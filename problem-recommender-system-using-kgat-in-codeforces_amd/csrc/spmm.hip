@@ -31,14 +31,17 @@
 
 namespace kgat {
 
-// Final write of one output row segment (lane gl) in the three modes.
+// Final write of one output row segment (lane gl) in the four modes: row is
+// the (global-id) row of A, out the row of Y it lands in (row, or its position
+// in the output set for kMaskedRows).
 template <int MODE>
-__device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int gl, float4 acc, bool any = false) {
-  float4* y = reinterpret_cast<float4*>(io.Y + row * io.ldy) + gl;
+__device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t out, int gl, float4 acc,
+                                          bool any = false) {
+  float4* y = reinterpret_cast<float4*>(io.Y + out * io.ldy) + gl;
   if (MODE == kAccumulate) {
     const float4 o = *y;
     acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
-  } else if (MODE == kMasked) {
+  } else if (MODE == kMasked || MODE == kMaskedRows) {
     if (io.Yc != nullptr) {
       const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
@@ -47,7 +50,7 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int gl,
         any = true;
       }
     }
-    if (io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
+    if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
   *y = acc;
 }
@@ -56,7 +59,7 @@ template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
-  constexpr bool MASKED = MODE == kMasked;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
@@ -66,6 +69,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     const int s = blockIdx.x * 4 + wave;
     if (s >= A.n_seg) return;
     const int row = A.seg_row[s];
+    if (MODE == kMaskedRows && !bit_of(io.out_bits, row)) return;  // not an output row
     const int64_t beg = A.seg_beg[s];
     const int64_t row_end = A.rowptr[row + 1];
     const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
@@ -77,7 +81,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
       gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any);
     }
     // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
-    if (MASKED && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
+    if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
 #pragma unroll
     for (int o = L; o < kWave; o <<= 1) {
       acc.x += __shfl_xor(acc.x, o);
@@ -86,6 +90,26 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
       acc.w += __shfl_xor(acc.w, o);
     }
     if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
+    return;
+  }
+
+  if (MODE == kMaskedRows) {
+    // ---- short rows of the output set: one group per row, waves stride over the list
+    const int64_t cnt = *io.out_count;
+    const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * S::kRowsPerWave;
+    for (int64_t k0 = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kRowsPerWave; k0 < cnt;
+         k0 += stride) {
+      const int64_t k_end = k0 + S::kRowsPerWave < cnt ? k0 + S::kRowsPerWave : cnt;
+      for (int64_t k = k0 + g; k < k_end; k += S::kGroups) {
+        const int64_t r = io.out_rows[k];
+        const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+        if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool any = false;
+        gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
+        store_row<MODE>(io, r, k, gl, acc, any);
+      }
+    }
     return;
   }
 
@@ -100,7 +124,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     bool any = false;
     gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any);
-    store_row<MODE>(io, r, gl, acc, any);
+    store_row<MODE>(io, r, r, gl, acc, any);
   }
 }
 
@@ -116,6 +140,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   const int lr = blockIdx.x;
   const int g = threadIdx.x / L, gl = threadIdx.x % L;
   const int row = A.long_rows[lr];
+  if (MODE == kMaskedRows && !bit_of(io.out_bits, row)) return;  // block-uniform: not an output row
   const float4* P = reinterpret_cast<const float4*>(io.part);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int s_end = A.long_seg_off[lr + 1];
@@ -125,7 +150,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if (threadIdx.x < L) {
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
-    store_row<MODE>(io, row, gl, t);
+    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
   }
 }
 
@@ -133,7 +158,8 @@ template <int D, int MODE>
 static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
-  const int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
+  int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
+  if (MODE == kMaskedRows && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
@@ -183,6 +209,46 @@ static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) 
 
 static bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
 
+// The first hop of the backward chain, structurally: bits0 marks the frontier
+// rows F (rows[0..n) of kgat_frontier_build, -1 padded), bits1 marks F and
+// every column of A's rows F -- exactly the rows the A^T product over F can
+// reach (A^T[j, i] != 0 <=> A[i, j] != 0).  One block per frontier slot.
+__global__ __launch_bounds__(256) void frontier_mark_kernel(kgat_csr A, const int32_t* __restrict__ rows,
+                                                            uint32_t* __restrict__ bits0,
+                                                            uint32_t* __restrict__ bits1) {
+  const int32_t i = rows[blockIdx.x];
+  if (i < 0) return;
+  if (threadIdx.x == 0) {
+    atomicOr(&bits0[i >> 5], 1u << (i & 31));
+    atomicOr(&bits1[i >> 5], 1u << (i & 31));
+  }
+  for (int64_t e = A.rowptr[i] + threadIdx.x; e < A.rowptr[i + 1]; e += blockDim.x) {
+    const int32_t j = A.col[e];
+    atomicOr(&bits1[j >> 5], 1u << (j & 31));
+  }
+}
+
+struct Popc {
+  __device__ int32_t operator()(uint32_t w) const { return __popc(w); }
+};
+
+// node_map / rows / count of the set in bits from the exclusive scan of the
+// word popcounts (woff): thread i alone writes node_map[i].
+__global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __restrict__ bits,
+                                                          const int32_t* __restrict__ woff, int64_t n,
+                                                          int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
+                                                          int32_t* __restrict__ count) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t w = bits[i >> 5];
+  const uint32_t b = static_cast<uint32_t>(i & 31);
+  const int32_t pos = woff[i >> 5] + __popc(w & ((1u << b) - 1u));
+  const bool in = ((w >> b) & 1u) != 0;
+  node_map[i] = in ? pos : -1;
+  if (in) rows[pos] = static_cast<int32_t>(i);
+  if (i == n - 1) *count = pos + (in ? 1 : 0);
+}
+
 // Frontier bitmap from a node map: bit i of the (64-bit) word i/64 = map[i] >= 0.
 __global__ __launch_bounds__(256) void map_bits_kernel(const int32_t* __restrict__ node_map, int64_t n,
                                                        uint64_t* __restrict__ bits) {
@@ -221,7 +287,7 @@ extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx,
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr};
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return accumulate ? dispatch<kAccumulate>(*A, io, d, st) : dispatch<kOverwrite>(*A, io, d, st);
 }
@@ -242,7 +308,7 @@ extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src
   if (row_hit != nullptr &&
       hipMemsetAsync(row_hit, 0, static_cast<size_t>(A->n_rows) * sizeof(int32_t), st) != hipSuccess)
     return KGAT_ERR_INVALID;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0, src_bits};
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0, src_bits, nullptr, nullptr, nullptr, nullptr};
   return dispatch<kMasked>(*A, io, d, st);
 }
 
@@ -285,4 +351,64 @@ extern "C" int kgat_map_bits(const int32_t* node_map, int64_t n, uint32_t* bits,
                      node_map, n, reinterpret_cast<uint64_t*>(bits));
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
+}
+
+// Scratch of kgat_frontier_hop: word offsets + the scan's temporary storage.
+extern "C" int64_t kgat_frontier_hop_work_bytes(int64_t n) {
+  if (n < 0 || n > INT32_MAX) return -1;
+  const int64_t words = (n + 31) / 32;
+  size_t bytes = 0;
+  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(nullptr, kgat::Popc{});
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, static_cast<int32_t*>(nullptr),
+                                       static_cast<int>(words)) != hipSuccess)
+    return -1;
+  return 4 * (words + 64) + static_cast<int64_t>(bytes);
+}
+
+extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_t n0, uint32_t* bits0,
+                                 uint32_t* bits1, int32_t* node_map, int32_t* hop_rows, int32_t* hop_count,
+                                 void* work, int64_t work_bytes, void* stream) {
+  if (!A || !rows0 || !bits0 || !bits1 || !node_map || !hop_rows || !hop_count || n0 < 0 || A->n_rows < 0)
+    return KGAT_ERR_INVALID;
+  const int64_t n = A->n_rows;
+  const int64_t need = kgat_frontier_hop_work_bytes(n);
+  if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t words = (n + 31) / 32;
+  if (hipMemsetAsync(bits0, 0, 4 * words, st) != hipSuccess || hipMemsetAsync(bits1, 0, 4 * words, st) != hipSuccess)
+    return KGAT_ERR_INVALID;
+  if (n == 0) return hipMemsetAsync(hop_count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  if (n0 > 0) {
+    hipLaunchKernelGGL(kgat::frontier_mark_kernel, dim3(n0), dim3(256), 0, st, *A, rows0, bits0, bits1);
+    KGAT_LAUNCH_CHECK();
+  }
+  int32_t* woff = static_cast<int32_t*>(work);
+  void* temp = static_cast<char*>(work) + 4 * (words + 64);
+  size_t bytes = static_cast<size_t>(need - 4 * (words + 64));
+  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(bits1, kgat::Popc{});
+  const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits1, woff, n, node_map,
+                     hop_rows, hop_count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* src_map, const uint32_t* src_bits,
+                                             const float* Xc, int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                             const uint32_t* out_bits, const int32_t* out_map, const int32_t* out_rows,
+                                             const int32_t* out_count, float* Y, int64_t ldy, int32_t d,
+                                             float* workspace, int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !Y || !out_bits || !out_map || !out_rows || !out_count || A->n_rows < 0 || ldxc < d ||
+      ldy < d || (ldxc & 3) || (ldy & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(Y) || (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits,
+                  out_bits, out_map, out_rows, out_count};
+  return dispatch<kMaskedRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }

@@ -7,7 +7,7 @@
 
 namespace kgat {
 
-enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2 };
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3 };
 
 struct SpmmIo {
   const float* X;         // source rows (dense) or compact source rows (masked)
@@ -21,7 +21,16 @@ struct SpmmIo {
   int32_t* row_hit;       // masked: set to 1 for every output row that gathered an edge or has a Yc row (nullable)
   int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
   const uint32_t* src_bits;  // masked: bit c set <=> src_map[c] >= 0 (nullable: test src_map directly)
+  // kMaskedRows: only the rows of an output set are produced, compactly (row out_rows[k] -> Y row k)
+  const uint32_t* out_bits;  // bit r set <=> r in the set
+  const int32_t* out_map;    // r -> k or -1
+  const int32_t* out_rows;   // k -> r, ascending
+  const int32_t* out_count;  // device: the set's size
 };
+
+__device__ __forceinline__ bool bit_of(const uint32_t* bits, int64_t i) {
+  return ((bits[i >> 5] >> (i & 31)) & 1u) != 0;
+}
 
 template <int D>
 struct SpmmShape {

@@ -238,8 +238,8 @@ class DeviceGraph:
 
     def hop_buffers(self):
         """Scratch of the backward's hop chain (kernels.hop_compact): row flags, node -> hop
-        position map, hop rows, device count, scan work, pinned count, membership bitmap
-        (allocated once)."""
+        position map, hop rows, device count, scan work, pinned count, membership bitmap of the
+        hop set, bitmap of the batch frontier, kgat_frontier_hop scratch (allocated once)."""
         hb = getattr(self, "_hop", None)
         if hb is None:
             n = self.n_nodes
@@ -252,7 +252,10 @@ class DeviceGraph:
                   torch.zeros(1, dtype=torch.int32, device=self.device),
                   torch.empty(work, dtype=torch.uint8, device=self.device),
                   torch.zeros(1, dtype=torch.int32, pin_memory=True),
-                  torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device))
+                  torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
+                  torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
+                  torch.empty(max(int(_lib.lib().kgat_frontier_hop_work_bytes(n)), 1), dtype=torch.uint8,
+                              device=self.device))
             self._hop = hb
         return hb
 

@@ -209,7 +209,7 @@ def hop_compact(graph: DeviceGraph, sync: bool = False):
     membership bitmap is left in graph.hop_buffers()[6] (kgat_map_bits).  With ``sync`` the
     count is read back (one stream sync) and rows is cut to n; otherwise n is None and
     consumers read the count on the device (biinter_bwd_hop)."""
-    hit, node_map, rows, count, work, host, bits = graph.hop_buffers()
+    hit, node_map, rows, count, work, host, bits = graph.hop_buffers()[:7]
     dev = hit.device
     _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
               count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
@@ -222,16 +222,71 @@ def hop_compact(graph: DeviceGraph, sync: bool = False):
     return rows[:n], node_map, count, n
 
 
-def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int):
+def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
+    """The first hop set of the backward chain from the batch frontier rows0 (frontier_build's
+    rows, -1 padded): (hop rows int32 [N] ascending -- first count valid --, node_map, count int32 [1]
+    on the device, hop-set bitmap, frontier bitmap).  No graph scan: the frontier rows' A edges are
+    marked (kgat_frontier_hop)."""
+    _req(rows0, "rows0", dtype=torch.int32, dim=1)
+    hb = graph.hop_buffers()
+    _, node_map, rows, count, _, _, bits1, bits0, work = hb
+    desc = graph.A.descriptor()
+    _lib.call("kgat_frontier_hop", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
+              bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), work.data_ptr(), work.numel(),
+              stream_ptr(rows0.device))
+    return rows, node_map, count, bits1, bits0
+
+
+def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_rows, out_map, out_count, out_bits,
+                     transpose: bool = True) -> torch.Tensor:
+    """The masked product (see spmm_masked) on the output rows of a hop set only, written compactly:
+    Y[k] = row out_rows[k] for k < out_count (kgat_spmm_csr_masked_rows_f32); returns Y [N, d]
+    (capacity; the first count rows are valid)."""
+    _req(src_map, "src_map", dtype=torch.int32, dim=1)
+    _req(Xc, "Xc", dim=2)
+    d = Xc.shape[1]
+    if Yc_init is not None:
+        _req(Yc_init, "Yc_init", dim=2)
+        if Yc_init.shape[1] != d:
+            raise ValueError("Yc_init width mismatch")
+    for t, nm in ((out_rows, "out_rows"), (out_map, "out_map"), (out_count, "out_count")):
+        _req(t, nm, dtype=torch.int32, dim=1)
+    _bits_ptr(out_bits, out_map)
+    n = graph.n_nodes
+    if src_map.numel() != n or out_map.numel() != n or out_rows.numel() < n:
+        raise ValueError("maps must cover every node")
+    out = torch.empty(n, d, dtype=torch.float32, device=Xc.device)
+    csr = graph.AT if transpose else graph.A
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_masked_rows_f32", ctypes.byref(desc), src_map.data_ptr(), _bits_ptr(src_bits, src_map),
+              Xc.data_ptr(), _ld(Xc), Yc_init.data_ptr() if Yc_init is not None else None,
+              _ld(Yc_init) if Yc_init is not None else 0, out_bits.data_ptr(), out_map.data_ptr(),
+              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(),
+              stream_ptr(Xc.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, transpose, "masked"))
+    return out
+
+
+def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int,
+                    dh_compact: bool = False):
     """Saved-state bi-interaction backward on a hop set whose size is only known on the device:
-    rows / count from hop_compact, dH indexed by node ([N, d_out], the previous masked product's
-    output).  Returns compact (dXd, dS) with ``out_rows`` rows allocated (the first count are
-    valid) and (dW1, db1, dW2, db2)."""
+    rows / count from hop_compact or frontier_hop, dH indexed by node ([N, d_out], the previous
+    masked product's output) or, with ``dh_compact``, by hop position (spmm_masked_rows' output).
+    Returns compact (dXd, dS) with ``out_rows`` rows allocated (the first count are valid) and
+    (dW1, db1, dW2, db2)."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     for t, nm in ((X, "X"), (S, "S"), (dH, "dH"), (H, "H")):
         _req(t, nm, dim=2)
-    if dH.shape != (src_rows, dout) or H.shape != (src_rows, dout) or S.shape != X.shape:
+    if dH.shape[1] != dout or (not dh_compact and dH.shape[0] != src_rows) or (dh_compact and dH.shape[0] < out_rows) \
+            or H.shape != (src_rows, dout) or S.shape != X.shape:
         raise ValueError("hop backward shape mismatch")
     if state is None or state.kind != "fused" or not saved_state_supported(din, dout):
         raise ValueError("hop backward needs the fused saved state")
@@ -248,8 +303,8 @@ def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: B
     _lib.call("kgat_biinter_bwd_hop_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
               state.norm.data_ptr(), state.mask.data_ptr(), dH.data_ptr(), _ld(dH), W1.data_ptr(), W2.data_ptr(),
               dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(),
-              db2.data_ptr(), rows.data_ptr(), count.data_ptr(), out_rows, src_rows, din, dout, float(dropout_p),
-              ws.data_ptr(), ws.numel(), stream_ptr(dev))
+              db2.data_ptr(), rows.data_ptr(), count.data_ptr(), out_rows, src_rows, int(dh_compact), din, dout,
+              float(dropout_p), ws.data_ptr(), ws.numel(), stream_ptr(dev))
     return dXd, dS, dW1, db1, dW2, db2
 
 

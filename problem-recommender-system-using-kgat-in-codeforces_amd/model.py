@@ -94,6 +94,13 @@ def _hop_estimate(graph, l: int):
     return int(ent[0].item())
 
 
+def _hop_small(graph, l: int, n_nodes: int) -> bool:
+    """Run layer l on its hop set: its size at the previous step (unknown: yes) is at most
+    HOP_DENSE_FRACTION of the nodes."""
+    est = _hop_estimate(graph, l)
+    return est is None or est <= HOP_DENSE_FRACTION * n_nodes
+
+
 def _hop_record(graph, l: int, count: torch.Tensor) -> None:
     """Copy layer l's device-side hop count to pinned memory for the next step's choice."""
     est = graph.__dict__.setdefault("_hop_est", {})
@@ -171,22 +178,37 @@ class _CFLoss(torch.autograd.Function):
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
         bits = graph.hop_buffers()[6]
-        kernels.map_bits(graph.node_map, bits)
-        dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True, row_hit=hit,
-                                 src_bits=bits)
-        kernels.frontier_reset(rows, graph.node_map)
-        kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
+        sparse = hit is not None and HOP_DENSE_FRACTION > 0
+        pending = None
+        nxt = L - 2
+        if sparse and states[nxt] is not None and states[nxt].kind == "fused" and _hop_small(graph, nxt, n_nodes):
+            # first hop marked from the frontier rows' A edges (no graph scan); the A^T product is
+            # computed on those rows only, compactly (kgat_spmm_csr_masked_rows_f32)
+            hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows)
+            _hop_record(graph, nxt, hcount)
+            dX = kernels.spmm_masked_rows(graph, graph.node_map, fbits, dSc, dXdc, hrows, hmap, hcount, bits)
+            kernels.frontier_reset(rows, graph.node_map)
+            kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX, row_map=hmap)
+            pending = (hrows, hmap, hcount)
+        else:
+            kernels.map_bits(graph.node_map, bits)
+            dX = kernels.spmm_masked(graph, graph.node_map, dSc, Yc_init=dXdc, transpose=True, row_hit=hit,
+                                     src_bits=bits)
+            kernels.frontier_reset(rows, graph.node_map)
+            kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX)
         wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
         # ---- remaining layers: on the hop set while it stays small, then densely
-        sparse = hit is not None and HOP_DENSE_FRACTION > 0
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             fused = states[l] is not None and states[l].kind == "fused"
-            if sparse and fused:
+            compact_dh = pending is not None
+            if compact_dh:  # dX is compact over the first hop set
+                hrows, hmap, hcount = pending
+                pending = None
+            elif sparse and fused:
                 # hop size stays on the device (no host sync); the sparse/dense choice uses the
                 # size this layer's hop set had at the previous step
-                est = _hop_estimate(graph, l)
-                sparse = est is None or est <= HOP_DENSE_FRACTION * n_nodes
+                sparse = _hop_small(graph, l, n_nodes)
                 if sparse:
                     hrows, hmap, hcount, _ = kernels.hop_compact(graph)
                     _hop_record(graph, l, hcount)
@@ -199,7 +221,8 @@ class _CFLoss(torch.autograd.Function):
                 # per row and per output element the arithmetic and order are the dense path's
                 if fused:
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd_hop(
-                        tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], n_nodes)
+                        tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], n_nodes,
+                        dh_compact=compact_dh)
                 else:
                     dHc = kernels.gather_rows(dX, hrows)
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,

@@ -438,6 +438,48 @@ def test_spmm_masked_row_hit_hop_compact_and_row_blocks(pkg):
     assert torch.equal(blk, out)
 
 
+def test_frontier_hop_and_masked_rows_product(pkg):
+    """kgat_frontier_hop marks the batch frontier and its A-neighbours (= the rows the masked A^T
+    product over the frontier flags), and kgat_spmm_csr_masked_rows_f32 produces exactly those rows
+    of that product, compactly and with the same bits (hub rows included)."""
+    graph_mod, kernels = _mods(pkg)
+    rng = np.random.default_rng(8)
+    n, d = 6000, 64
+    h = np.concatenate([rng.integers(0, n, 24000), np.repeat(rng.integers(0, n, 5), 1500)])
+    t = rng.integers(0, n, h.size)
+    rowptr, col, val = graph_mod.csr_from_coo(n, np.concatenate([h, t]), np.concatenate([t, h]),
+                                              rng.random(2 * h.size).astype(np.float32))
+    lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
+                                tails=np.zeros(0, np.int64), edge_vals=np.zeros(0, np.float32), rowptr=rowptr,
+                                col=col, val=val, slot=np.zeros(0, np.int64))
+    g = graph_mod.DeviceGraph(lay, DEV)
+    B = 64
+    users = torch.from_numpy(rng.integers(0, n, B)).to(DEV)
+    pos = torch.from_numpy(np.concatenate([rng.integers(0, n, B - 1), [int(np.argmax(np.diff(rowptr)))]])).to(DEV)
+    neg = torch.from_numpy(rng.integers(0, n, B)).to(DEV)
+    rows0, cnt0 = kernels.frontier_build(users, pos, neg, g.node_map)
+    n0 = int(cnt0.item())
+    Xc = torch.randn(3 * B, d, device=DEV)
+    Yc = torch.randn(3 * B, d, device=DEV)
+    hit = g.hop_buffers()[0]
+    fb = torch.zeros_like(g.hop_buffers()[6])
+    kernels.map_bits(g.node_map, fb)
+    dense = kernels.spmm_masked(g, g.node_map, Xc, Yc_init=Yc, transpose=True, row_hit=hit, src_bits=fb)
+    want = hit.cpu().numpy().astype(bool)
+    hrows, hmap, hcount, hbits, fbits = kernels.frontier_hop(g, rows0)
+    cnt = int(hcount.item())
+    assert cnt == int(want.sum())
+    np.testing.assert_array_equal(hrows[:cnt].cpu().numpy(), np.nonzero(want)[0])
+    m = hmap.cpu().numpy()
+    np.testing.assert_array_equal(m[want], np.arange(cnt))
+    assert np.all(m[~want] == -1)
+    assert torch.equal(fbits[:fb.numel()], fb)
+    comp = kernels.spmm_masked_rows(g, g.node_map, fbits, Xc, Yc, hrows, hmap, hcount, hbits)
+    assert torch.equal(comp[:cnt], dense[hrows[:cnt].long()])
+    kernels.frontier_reset(rows0, g.node_map)
+    assert n0 > 0
+
+
 @pytest.mark.parametrize("layers", [[64, 32], [64, 32, 16]])
 def test_cf_hop_chain_matches_dense_backward(pkg, layers):
     """The hop-chain backward (lower layers on their hop sets) against the dense backward of the

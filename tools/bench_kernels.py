@@ -152,12 +152,17 @@ def masked_section(args, K, g, U, E, n, dev, rec):
     pos = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
     neg = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
     rows, _ = K.frontier_build(users, pos, neg, g.node_map)
-    hit, hmap, hrows, count, work, host, bits = g.hop_buffers()
+    hit, bits = g.hop_buffers()[0], g.hop_buffers()[6]
     Sc = torch.randn(3 * B, 64, device=dev)
     K.map_bits(g.node_map, bits)
     for nm, b in (("map", None), ("bits", bits)):
         rec(f"masked_F0_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True, row_hit=hit,
                                                                   src_bits=b), args.reps))
+    K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True, row_hit=hit)
+    rec("frontier_hop", timeit(lambda: K.frontier_hop(g, rows), args.reps))
+    hr1, hm1, hc1, hb1, fb1 = K.frontier_hop(g, rows)
+    rec("masked_rows_F0_T_d64", timeit(lambda: K.spmm_masked_rows(g, g.node_map, fb1, Sc, Sc, hr1, hm1, hc1, hb1),
+                                       args.reps), n_hop=int(hc1.item()))
     K.spmm_masked(g, g.node_map, Sc, Sc, transpose=True, row_hit=hit)
     K.frontier_reset(rows, g.node_map)
     rec("map_bits", timeit(lambda: K.map_bits(g.node_map, bits), args.reps))
