@@ -104,7 +104,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=1)
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -123,7 +123,9 @@ def main() -> None:
     replicas = importlib.import_module(PKG + ".replicas")
 
     t0 = time.perf_counter()
+    log(f"generating the synthetic CKG ({cfg['workload']}) ...")
     U, E, inter, trip = graph_mod.synthetic_ckg(cfg["nodes"], cfg["triples"], seed=2024)
+    log(f"  {time.perf_counter() - t0:.1f}s; building the layout ...")
     layout = graph_mod.build_layout(U, E, inter, trip)
     log(f"graph: N={layout.n_nodes} interactions={len(inter)} kg={len(trip)} nnz={layout.nnz} "
         f"({time.perf_counter() - t0:.1f}s host build)")
@@ -131,7 +133,9 @@ def main() -> None:
     model = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(layout.rel_order),
                                   cf_embedding_dim=cfg["dim"], kg_embedding_dim=cfg["dim"], layer_size=cfg["layers"],
                                   message_dropout=[0.1] * len(cfg["layers"])))
+    log("attaching the graph (device CSR, transpose, refresh plan) ...")
     model.attach_graph(layout, dev)
+    log(f"  attached ({time.perf_counter() - t0:.1f}s)")
     replicas.broadcast_parameters(model)  # identical replicas (no-op at N=1)
     model.train()
     model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
