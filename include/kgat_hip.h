@@ -93,14 +93,22 @@ int kgat_spmm_csr_masked_f32(const kgat_csr *A, const int32_t *src_map, const fl
  *            that gathered at least one frontier edge or has a Yc_init row,
  *            i.e. a superset of the rows of Y that can be nonzero;
  *   src_bits (nullable): kgat_map_bits(src_map) -- the membership test reads
- *            one bit per edge instead of a map entry. */
+ *            one bit per edge instead of a map entry;
+ *   src_rank (nullable; for a src_map that numbers its set in ascending node
+ *            order, e.g. kgat_hop_compact's): kgat_map_rank(src_map) -- one
+ *            8-byte load per edge gives membership and compact row. */
 int kgat_spmm_csr_masked_ex_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
                                 const float *Yc_init, int64_t ldyc, int64_t yc_row0, float *Y, int64_t ldy,
-                                int32_t d, int32_t *row_hit, const uint32_t *src_bits, float *workspace,
-                                int64_t workspace_floats, void *stream);
+                                int32_t d, int32_t *row_hit, const uint32_t *src_bits, const uint64_t *src_rank,
+                                float *workspace, int64_t workspace_floats, void *stream);
 
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
+
+/* rank (uint64 [ceil(n / 32)]): word w = (node_map of its first member) << 32 |
+ * membership bits of nodes 32w .. 32w+31.  For maps numbering their set in
+ * ascending node order the compact row of member c is hi + popcount(lower bits). */
+int kgat_map_rank(const int32_t *node_map, int64_t n, uint64_t *rank, void *stream);
 
 /* The next hop set from row_hit (int32 [n], 0/1): node_map[i] = position of i
  * among the flagged nodes (ascending node order) or -1, rows[0..count) = the

@@ -257,6 +257,25 @@ __global__ __launch_bounds__(256) void map_bits_kernel(const int32_t* __restrict
   if ((threadIdx.x & 63) == 0 && i < n) bits[i >> 6] = b;
 }
 
+// Rank words of a set given by an ascending-order node map (position = rank):
+// word w = (position of its first member) << 32 | membership bits of nodes
+// 32w .. 32w+31, so one 8-byte load answers both "in the set?" and "which
+// compact row?" (position = hi + popcount of the lower member bits).
+__global__ __launch_bounds__(256) void map_rank_kernel(const int32_t* __restrict__ node_map, int64_t n,
+                                                       uint64_t* __restrict__ rank) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int32_t m = i < n ? node_map[i] : -1;
+  const uint64_t b = __ballot(m >= 0);
+  const int lane = threadIdx.x & 63;
+  const uint32_t lo = static_cast<uint32_t>(b), hi = static_cast<uint32_t>(b >> 32);
+  const int32_t p_lo = __shfl(m, lo ? __ffs(lo) - 1 : 0);
+  const int32_t p_hi = __shfl(m, hi ? 32 + __ffs(hi) - 1 : 32);
+  if (lane == 0 && i < n) {
+    rank[i >> 5] = (static_cast<uint64_t>(lo ? static_cast<uint32_t>(p_lo) : 0u) << 32) | lo;
+    if (i + 32 < n) rank[(i >> 5) + 1] = (static_cast<uint64_t>(hi ? static_cast<uint32_t>(p_hi) : 0u) << 32) | hi;
+  }
+}
+
 // Hop set from the masked product's row flags: pos = exclusive scan of hit
 // (already in node_map); a flagged node keeps its position and is listed in
 // rows[pos], an unflagged one gets -1.  Thread i alone rewrites node_map[i],
@@ -287,15 +306,16 @@ extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx,
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return accumulate ? dispatch<kAccumulate>(*A, io, d, st) : dispatch<kOverwrite>(*A, io, d, st);
 }
 
 extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
                                            const float* Yc_init, int64_t ldyc, int64_t yc_row0, float* Y, int64_t ldy,
-                                           int32_t d, int32_t* row_hit, const uint32_t* src_bits, float* workspace,
-                                           int64_t workspace_floats, void* stream) {
+                                           int32_t d, int32_t* row_hit, const uint32_t* src_bits,
+                                           const uint64_t* src_rank, float* workspace, int64_t workspace_floats,
+                                           void* stream) {
   using namespace kgat;
   if (!A || !src_map || !Xc || !Y || A->n_rows < 0 || ldxc < d || ldy < d || (ldxc & 3) || (ldy & 3) || yc_row0 < 0)
     return KGAT_ERR_INVALID;
@@ -308,15 +328,15 @@ extern "C" int kgat_spmm_csr_masked_ex_f32(const kgat_csr* A, const int32_t* src
   if (row_hit != nullptr &&
       hipMemsetAsync(row_hit, 0, static_cast<size_t>(A->n_rows) * sizeof(int32_t), st) != hipSuccess)
     return KGAT_ERR_INVALID;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0, src_bits, nullptr, nullptr, nullptr, nullptr};
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, row_hit, yc_row0, src_bits, src_rank, nullptr, nullptr, nullptr, nullptr};
   return dispatch<kMasked>(*A, io, d, st);
 }
 
 extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc, int64_t ldxc,
                                         const float* Yc_init, int64_t ldyc, float* Y, int64_t ldy, int32_t d,
                                         float* workspace, int64_t workspace_floats, void* stream) {
-  return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, nullptr, workspace,
-                                     workspace_floats, stream);
+  return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, nullptr, nullptr,
+                                     workspace, workspace_floats, stream);
 }
 
 extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {
@@ -408,7 +428,17 @@ extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* s
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits,
+  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits, nullptr,
                   out_bits, out_map, out_rows, out_count};
   return dispatch<kMaskedRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int kgat_map_rank(const int32_t* node_map, int64_t n, uint64_t* rank, void* stream) {
+  if (!node_map || !rank || n < 0) return KGAT_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(rank) & 7) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::map_rank_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     node_map, n, rank);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }

@@ -21,6 +21,7 @@ struct SpmmIo {
   int32_t* row_hit;       // masked: set to 1 for every output row that gathered an edge or has a Yc row (nullable)
   int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
   const uint32_t* src_bits;  // masked: bit c set <=> src_map[c] >= 0 (nullable: test src_map directly)
+  const uint64_t* src_rank;  // masked, ascending compact order: word c/32 = (#members before it) << 32 | its bits
   // kMaskedRows: only the rows of an output set are produced, compactly (row out_rows[k] -> Y row k)
   const uint32_t* out_bits;  // bit r set <=> r in the set
   const int32_t* out_map;    // r -> k or -1
@@ -68,21 +69,26 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
     int mc = 0;
     float mv = 0.f;
     if (MASKED) {
-      // membership first (a bit of the frontier bitmap: 1/32 of the map's bytes, cache
-      // resident), the compact row and the value only for the edges that gather;
-      // skipped edges add an exact 0, so the gathered ones keep the dense order
+      // membership first: a bit of the source set (its rank word gives the compact row
+      // too, with one 8-byte load), then the gathers of the edges that hit; skipped
+      // edges add an exact 0, so the gathered ones keep the dense order
       bool in = false;
       if (gl < n) {
         mc = A.col[cb + gl];
-        in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
+        mv = A.val[cb + gl];
+        if (io.src_rank != nullptr) {
+          const uint64_t w = io.src_rank[mc >> 5];
+          const uint32_t b = static_cast<uint32_t>(mc & 31);
+          in = ((w >> b) & 1u) != 0;
+          mc = static_cast<int>(w >> 32) + __popc(static_cast<uint32_t>(w) & ((1u << b) - 1u));
+        } else {
+          in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
+        }
       }
       uint64_t hit = (__ballot(in) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
       if (hit == 0) continue;
       any = true;
-      if (in) {
-        mc = io.src_map[mc];
-        mv = A.val[cb + gl];
-      }
+      if (in && io.src_rank == nullptr) mc = io.src_map[mc];
       // up to four gathers in flight, summed in edge order
       while (hit) {
         int jj[4];

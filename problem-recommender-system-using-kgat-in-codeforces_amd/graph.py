@@ -239,7 +239,8 @@ class DeviceGraph:
     def hop_buffers(self):
         """Scratch of the backward's hop chain (kernels.hop_compact): row flags, node -> hop
         position map, hop rows, device count, scan work, pinned count, membership bitmap of the
-        hop set, bitmap of the batch frontier, kgat_frontier_hop scratch (allocated once)."""
+        hop set, bitmap of the batch frontier, kgat_frontier_hop scratch, rank words of the hop
+        set (allocated once)."""
         hb = getattr(self, "_hop", None)
         if hb is None:
             n = self.n_nodes
@@ -255,7 +256,8 @@ class DeviceGraph:
                   torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
                   torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
                   torch.empty(max(int(_lib.lib().kgat_frontier_hop_work_bytes(n)), 1), dtype=torch.uint8,
-                              device=self.device))
+                              device=self.device),
+                  torch.zeros((n + 31) // 32 + 1, dtype=torch.int64, device=self.device))
             self._hop = hb
         return hb
 

@@ -89,7 +89,7 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
 
 def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor,
                       Yc_init: torch.Tensor | None = None, row0: int = 0,
-                      src_bits: torch.Tensor | None = None) -> torch.Tensor:
+                      src_bits: torch.Tensor | None = None, src_rank: torch.Tensor | None = None) -> torch.Tensor:
     """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row); with Yc_init,
     local row r also gets Yc_init[src_map[row0 + r]] (B = rows [row0, ...) of a square matrix)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
@@ -108,8 +108,8 @@ def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.T
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
-              int(row0), out.data_ptr(), _ld(out), d, None, _bits_ptr(src_bits, src_map), ws.data_ptr(), ws.numel(),
-              stream_ptr(Xc.device))
+              int(row0), out.data_ptr(), _ld(out), d, None, _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map),
+              ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     return out
 
 
@@ -156,6 +156,23 @@ def _bits_ptr(src_bits: torch.Tensor | None, src_map: torch.Tensor):
     return src_bits.data_ptr()
 
 
+def _rank_ptr(src_rank: torch.Tensor | None, src_map: torch.Tensor):
+    if src_rank is None:
+        return None
+    _req(src_rank, "src_rank", dtype=torch.int64, dim=1)
+    if src_rank.numel() < (src_map.numel() + 31) // 32:
+        raise ValueError("src_rank must be map_rank(src_map)")
+    return src_rank.data_ptr()
+
+
+def map_rank(node_map: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out (int64 [ceil(N/32)]): rank words of the set of an ascending-order node map (kgat_map_rank)."""
+    _req(node_map, "node_map", dtype=torch.int32, dim=1)
+    _rank_ptr(out, node_map)
+    _lib.call("kgat_map_rank", node_map.data_ptr(), node_map.numel(), out.data_ptr(), stream_ptr(node_map.device))
+    return out
+
+
 def map_bits(node_map: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """out (int32 [2*ceil(N/64)], 8-byte aligned): bit i set <=> node_map[i] >= 0 (kgat_map_bits)."""
     _req(node_map, "node_map", dtype=torch.int32, dim=1)
@@ -166,7 +183,7 @@ def map_bits(node_map: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None = None,
                 transpose: bool = False, row_hit: torch.Tensor | None = None,
-                src_bits: torch.Tensor | None = None) -> torch.Tensor:
+                src_bits: torch.Tensor | None = None, src_rank: torch.Tensor | None = None) -> torch.Tensor:
     """Dense Y = A . X where X is zero outside a frontier: X[node] = Xc[src_map[node]] (src_map -1 => 0),
     plus Yc_init[src_map[r]] on frontier rows.  Returns a new dense [N, d] tensor.  With ``row_hit``
     (int32 [N]) the rows of Y that can be nonzero are flagged 1 (the next hop set, see hop_compact)."""
@@ -194,7 +211,8 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0, 0,
               out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None,
-              _bits_ptr(src_bits, src_map), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+              _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map), ws.data_ptr(), ws.numel(),
+              stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, transpose, "masked"))
@@ -205,15 +223,16 @@ def hop_compact(graph: DeviceGraph, sync: bool = False):
     """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked.
 
     Returns (rows int32 [N] -- the first n entries are the hop set, ascending --, node_map
-    int32 [N] node -> position or -1, count int32 [1] on the device, n); the hop set's
-    membership bitmap is left in graph.hop_buffers()[6] (kgat_map_bits).  With ``sync`` the
+    int32 [N] node -> position or -1, count int32 [1] on the device, n); the hop set's rank
+    words are left in graph.hop_buffers()[9] (kgat_map_rank).  With ``sync`` the
     count is read back (one stream sync) and rows is cut to n; otherwise n is None and
     consumers read the count on the device (biinter_bwd_hop)."""
-    hit, node_map, rows, count, work, host, bits = graph.hop_buffers()[:7]
+    hb = graph.hop_buffers()
+    hit, node_map, rows, count, work, host = hb[:6]
     dev = hit.device
     _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
               count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
-    map_bits(node_map, bits)
+    map_rank(node_map, hb[9])
     if not sync:
         return rows, node_map, count, None
     host.copy_(count, non_blocking=True)
@@ -229,11 +248,12 @@ def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
     marked (kgat_frontier_hop)."""
     _req(rows0, "rows0", dtype=torch.int32, dim=1)
     hb = graph.hop_buffers()
-    _, node_map, rows, count, _, _, bits1, bits0, work = hb
+    _, node_map, rows, count, _, _, bits1, bits0, work = hb[:9]
     desc = graph.A.descriptor()
     _lib.call("kgat_frontier_hop", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
               bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), work.data_ptr(), work.numel(),
               stream_ptr(rows0.device))
+    map_rank(node_map, hb[9])
     return rows, node_map, count, bits1, bits0
 
 

@@ -178,6 +178,7 @@ class _CFLoss(torch.autograd.Function):
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
         bits = graph.hop_buffers()[6]
+        rank = graph.hop_buffers()[9]  # rank words of the current hop set (frontier_hop / hop_compact)
         sparse = hit is not None and HOP_DENSE_FRACTION > 0
         pending = None
         nxt = L - 2
@@ -233,11 +234,11 @@ class _CFLoss(torch.autograd.Function):
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
                     for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
                         kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
-                                                  Yc_init=dXdc, row0=view.r0, src_bits=bits)
+                                                  Yc_init=dXdc, row0=view.r0, src_rank=rank)
                         hook.block_ready(k, dX)
                 else:
                     dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True,
-                                             row_hit=hit if l > 0 else None, src_bits=bits)
+                                             row_hit=hit if l > 0 else None, src_rank=rank)
                 wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
                 continue
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],

@@ -430,6 +430,13 @@ def test_spmm_masked_row_hit_hop_compact_and_row_blocks(pkg):
     out2 = kernels.spmm_masked(g, nm, Xc, Yc_init=Yc, transpose=True, row_hit=hit2, src_bits=bits)
     assert torch.equal(out2, out)
     np.testing.assert_array_equal(hit2.cpu().numpy().astype(bool), want)
+    # an ascending-order source set (the hop set): rank words (membership + compact row in one
+    # load) give the same bits as the map lookup
+    Hc = torch.randn(cnt, d, device=DEV)
+    rank = kernels.map_rank(hmap, torch.empty((n + 31) // 32, dtype=torch.int64, device=DEV))
+    by_map = kernels.spmm_masked(g, hmap, Hc, transpose=True)
+    by_rank = kernels.spmm_masked(g, hmap, Hc, transpose=True, src_rank=rank)
+    assert torch.equal(by_map, by_rank)
     # row-block views (yc_row0) give the same bits
     bounds = [(0, 1700), (1700, 3333), (3333, n)]
     blk = torch.empty_like(out)

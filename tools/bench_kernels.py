@@ -169,9 +169,11 @@ def masked_section(args, K, g, U, E, n, dev, rec):
     hr, hm, hc, nh = K.hop_compact(g, sync=True)
     rec("hop_compact", timeit(lambda: K.hop_compact(g), args.reps), n_hop=nh)
     Hc = torch.randn(n, 64, device=dev)
-    for nm, b in (("map", None), ("bits", bits)):
-        rec(f"masked_hop1_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, hm, Hc, Hc, transpose=True, src_bits=b),
-                                              args.reps), n_hop=nh)
+    rank = g.hop_buffers()[9]
+    K.map_bits(hm, bits)  # the hop set's bitmap (bits held the batch frontier's)
+    for nm, b, rk in (("map", None, None), ("bits", bits, None), ("rank", None, rank)):
+        rec(f"masked_hop1_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, hm, Hc, Hc, transpose=True, src_bits=b,
+                                                                    src_rank=rk), args.reps), n_hop=nh)
 
 
 def nfm_section(args, dev, rec):
