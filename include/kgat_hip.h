@@ -339,6 +339,12 @@ int kgat_slot_sum_f32(const int64_t *slot_edge_ptr, const int32_t *edge_order, i
 /* a7 -- val = row softmax over the stored entries (torch.sparse.softmax(dim=1), model.py:364). */
 int kgat_row_softmax_f32(const int64_t *rowptr, int64_t n_rows, const float *slot_logits, float *val,
                          void *stream);
+/* kgat_row_softmax_f32 with the rows of more than 256 entries listed
+ * (long_rows[0..n_long), e.g. the CSR's long-row plan at threshold 256): those
+ * take a block each, the others a 16-lane group with the row in registers.
+ * long_rows == NULL: the long rows are found by a scan of all rows. */
+int kgat_row_softmax_ex_f32(const int64_t *rowptr, int64_t n_rows, const int32_t *long_rows, int32_t n_long,
+                            const float *slot_logits, float *val, void *stream);
 
 /* a6 for wide embeddings (d > 128, multiple of 16, <= 1024; C5's 256): the edge scorer
  * of kgat_edge_logits_f32 as rocBLAS GEMMs over chunks of the relation-sorted edge

@@ -106,6 +106,7 @@ _SIGNATURES = {
                                             c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_slot_sum_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_row_softmax_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_row_softmax_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "kgat_biinter_gemm_state_floats": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_biinter_gemm_work_floats": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_biinter_fwd_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,

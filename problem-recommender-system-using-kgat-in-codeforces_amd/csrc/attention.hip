@@ -232,21 +232,91 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(const int64_t* __restrict
 }
 
 // val[slot] = softmax over the stored entries of each row; one wave per row.
+// Row softmax over the stored entries (model.py:355-366, torch.sparse.softmax):
+// rows of <= 256 entries (all but the hubs) take a 16-lane group each, every
+// lane keeping its <= 16 logits in registers -- one read and one write of the
+// row; the lane partials reduce in a fixed butterfly order (deterministic).
+constexpr int kSoftmaxShort = 256;
+
 __global__ __launch_bounds__(256) void row_softmax_kernel(const int64_t* __restrict__ rowptr, int64_t n_rows,
                                                           const float* __restrict__ logit, float* __restrict__ val) {
+  const int64_t row = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
+  const int gl = threadIdx.x & 15;
+  if (row >= n_rows) return;  // whole 16-lane groups leave together
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  const int64_t len = end - beg;
+  if (len == 0 || len > kSoftmaxShort) return;  // long rows: row_softmax_long_kernel
+  float x[kSoftmaxShort / 16];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
+    const int64_t e = beg + gl + 16 * k;
+    x[k] = e < end ? logit[e] : -INFINITY;
+    m = fmaxf(m, x[k]);
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
+    x[k] = beg + gl + 16 * k < end ? expf(x[k] - m) : 0.f;
+    s += x[k];
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
+    const int64_t e = beg + gl + 16 * k;
+    if (e < end) val[e] = x[k] * inv;
+  }
+}
+
+// Rows longer than kSoftmaxShort found by a scan of all rows (callers without a
+// long-row list): one wave per row.
+__global__ __launch_bounds__(256) void row_softmax_scan_long_kernel(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                                                                    const float* __restrict__ logit,
+                                                                    float* __restrict__ val) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n_rows) return;
   const int64_t beg = rowptr[row], end = rowptr[row + 1];
-  if (beg == end) return;
+  if (end - beg <= kSoftmaxShort) return;
   float m = -INFINITY;
   for (int64_t e = beg + lane; e < end; e += 64) m = fmaxf(m, logit[e]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   float s = 0.f;
   for (int64_t e = beg + lane; e < end; e += 64) s += expf(logit[e] - m);
+  const float inv = 1.f / wave_sum(s);
+  for (int64_t e = beg + lane; e < end; e += 64) val[e] = expf(logit[e] - m) * inv;
+}
+
+// Rows longer than kSoftmaxShort: one 256-thread block per row, block
+// reductions in a fixed order.
+__global__ __launch_bounds__(256) void row_softmax_long_kernel(const int64_t* __restrict__ rowptr,
+                                                               const int32_t* __restrict__ long_rows,
+                                                               const float* __restrict__ logit,
+                                                               float* __restrict__ val) {
+  __shared__ float red[4];
+  const int64_t row = long_rows[blockIdx.x];
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float m = -INFINITY;
+  for (int64_t e = beg + threadIdx.x; e < end; e += 256) m = fmaxf(m, logit[e]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int64_t e = beg + threadIdx.x; e < end; e += 256) s += expf(logit[e] - m);
   s = wave_sum(s);
-  for (int64_t e = beg + lane; e < end; e += 64) val[e] = expf(logit[e] - m) / s;
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  const float inv = 1.f / (((red[0] + red[1]) + red[2]) + red[3]);
+  for (int64_t e = beg + threadIdx.x; e < end; e += 256) val[e] = expf(logit[e] - m) * inv;
 }
 
 template <int D>
@@ -259,6 +329,27 @@ static int launch_scores(const EdgeScoreArgs& a, hipStream_t st) {
 }
 
 }  // namespace kgat
+
+extern "C" int kgat_row_softmax_ex_f32(const int64_t* rowptr, int64_t n_rows, const int32_t* long_rows,
+                                       int32_t n_long, const float* slot_logits, float* val, void* stream) {
+  if (!rowptr || !slot_logits || !val || n_rows < 0 || n_long < 0 || (n_long > 0 && !long_rows))
+    return KGAT_ERR_INVALID;
+  if (n_rows == 0) return KGAT_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows * 16 + 255) / 256), dim3(256), 0, st, rowptr, n_rows,
+                     slot_logits, val);
+  KGAT_LAUNCH_CHECK();
+  if (long_rows == nullptr) {
+    hipLaunchKernelGGL(kgat::row_softmax_scan_long_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, st, rowptr, n_rows,
+                       slot_logits, val);
+    KGAT_LAUNCH_CHECK();
+  } else if (n_long > 0) {
+    hipLaunchKernelGGL(kgat::row_softmax_long_kernel, dim3(n_long), dim3(256), 0, st, rowptr, long_rows, slot_logits,
+                       val);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
 
 extern "C" int kgat_edge_logits_f32(const float* emb, int64_t ld_emb, int64_t n_nodes, const float* trans, int32_t d,
                                     const float* Wv, const float* bv, const float* Wo, const float* bo,
@@ -295,10 +386,5 @@ extern "C" int kgat_slot_sum_f32(const int64_t* slot_edge_ptr, const int32_t* ed
 
 extern "C" int kgat_row_softmax_f32(const int64_t* rowptr, int64_t n_rows, const float* slot_logits, float* val,
                                     void* stream) {
-  if (!rowptr || !slot_logits || !val || n_rows < 0) return KGAT_ERR_INVALID;
-  if (n_rows == 0) return KGAT_OK;
-  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows + 3) / 4), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), rowptr, n_rows, slot_logits, val);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
+  return kgat_row_softmax_ex_f32(rowptr, n_rows, nullptr, 0, slot_logits, val, stream);
 }

@@ -110,7 +110,7 @@ __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const floa
 // A-operand layout (lane (q, c): row c, k in [q*KQ, (q+1)*KQ)), W staged in
 // LDS.  Writes H, the row norms and the per-lane state word.  Shared by
 // biinter_fwd_kernel and spmm_bi_fwd_kernel, so both produce the same bits.
-template <int DIN, int DOUT>
+template <int DIN, int DOUT, bool SB = true>
 __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const float (&m)[DIN / 4], int64_t st,
                                                int lane, const float* w1s, const float* w2s,
                                                const float (&bias1)[DOUT / 16], const float (&bias2)[DOUT / 16],
@@ -135,7 +135,7 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
 #pragma unroll
   for (int cb = 0; cb < B::NCB; ++cb) {
     floatx4 acc1, acc2;
-    __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
+    if (SB) __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
     bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -168,8 +168,8 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
   }
 }
 
-template <int DIN, int DOUT>
-__global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
+template <int DIN, int DOUT, bool PF, int MINW>
+__global__ __launch_bounds__(256, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
@@ -195,18 +195,24 @@ __global__ __launch_bounds__(256, 2) void biinter_fwd_kernel(const float* __rest
   const int64_t nsub = (n + 15) / 16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
   int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  // next sub-tile's rows are loaded while the current one computes
+  // PF: the next sub-tile's rows are loaded while the current one computes
   float nx[B::KQ], ns[B::KQ];
-  load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
-  load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+  if (PF) {
+    load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
+    load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+  }
   for (; st < nsub; st += stride) {
+    if (!PF) {
+      load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
+      load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+    }
     float u[B::KQ], m[B::KQ];
 #pragma unroll
     for (int t = 0; t < B::KQ; ++t) {
       u[t] = nx[t] + ns[t];
       m[t] = nx[t] * ns[t];
     }
-    if (st + stride < nsub) {
+    if (PF && st + stride < nsub) {
       load_rows<DIN>(X, ldx, (st + stride) * 16 + c, n, q, nx);
       load_rows<DIN>(S, lds, (st + stride) * 16 + c, n, q, ns);
     }
@@ -1005,9 +1011,25 @@ template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
                       float* norm, uint64_t* mask, int64_t node0, hipStream_t st) {
-  const int grid = blocks_for(n, 64, kCUs * 8);
-  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, W2, b2,
-                     H, ldh, n, p, seed, norm, mask, node0);
+  // A/B switch (KGAT_FWD_VARIANT): bit 1 = one resident round, bit 2 = 4 waves/SIMD, bit 3 = no prefetch.
+  // Default 8 (measured at C2, 64->64: 795 us vs 809 us for spmm + forward with the prefetch, whose
+  // 172 VGPRs allow 2 waves/SIMD; without it 132 VGPRs, 3 waves)
+  static int variant = -1;
+  if (variant < 0) {
+    const char* e = getenv("KGAT_FWD_VARIANT");
+    variant = e ? atoi(e) : 8;
+  }
+  const int grid = blocks_for(n, 64, (variant & 2) ? kCUs * 4 : kCUs * 8);
+#define KGAT_FWD_LAUNCH(PF, W)                                                                                   \
+  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, PF, W>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, \
+                     W2, b2, H, ldh, n, p, seed, norm, mask, node0)
+  switch (variant & 12) {
+    case 4: KGAT_FWD_LAUNCH(true, 4); break;
+    case 8: KGAT_FWD_LAUNCH(false, 2); break;
+    case 12: KGAT_FWD_LAUNCH(false, 4); break;
+    default: KGAT_FWD_LAUNCH(true, 2); break;
+  }
+#undef KGAT_FWD_LAUNCH
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -736,11 +736,22 @@ def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b
     return out[:graph.nnz]
 
 
+LONG_THRESHOLD_SOFTMAX = 256  # kSoftmaxShort in csrc/attention.hip
+
+
+def graph_long_threshold() -> int:
+    from .graph import LONG_THRESHOLD
+    return LONG_THRESHOLD
+
+
 def row_softmax(graph: DeviceGraph, slot_logits: torch.Tensor) -> None:
     """A.val <- softmax over each row's stored entries; then A^T values follow."""
     _req(slot_logits, "slot_logits", dim=1)
-    _lib.call("kgat_row_softmax_f32", graph.A.rowptr.data_ptr(), graph.n_nodes, slot_logits.data_ptr(),
-              graph.A.val.data_ptr(), stream_ptr(slot_logits.device))
+    A = graph.A
+    if LONG_THRESHOLD_SOFTMAX != graph_long_threshold():
+        raise RuntimeError("row softmax long-row split must match the CSR plan")
+    _lib.call("kgat_row_softmax_ex_f32", A.rowptr.data_ptr(), graph.n_nodes, A.long_rows.data_ptr(), A.n_long,
+              slot_logits.data_ptr(), A.val.data_ptr(), stream_ptr(slot_logits.device))
     graph.refresh_transpose()
 
 

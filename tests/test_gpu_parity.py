@@ -577,6 +577,25 @@ def test_propagate_layer_pipelined_bit_identical(pkg, din, dout):
         assert torch.equal(a, b)
 
 
+def test_row_softmax_short_and_long_rows(pkg):
+    """a7: the 16-lane short-row softmax + block-per-row long rows (model.py:355-366) against
+    torch.sparse.softmax on the same CSR; the scan fallback (no long-row list) gives the same bits."""
+    graph_mod, kernels = _mods(pkg)
+    lay, A = random_graph(graph_mod, 4000, 9, hubs=4, hub_deg=3000, seed=17)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    assert g.A.n_long > 0
+    logits = torch.randn(lay.nnz) * 3
+    kernels.row_softmax(g, logits.to(DEV))
+    got = g.A.val.detach().cpu()
+    ref = torch.sparse.softmax(torch.sparse_coo_tensor(A.indices(), logits, A.shape).coalesce(), dim=1)
+    np.testing.assert_allclose(got.numpy(), ref.values().numpy(), rtol=1e-5, atol=1e-7)
+    lib = __import__(pkg.__name__ + "._lib", fromlist=["_lib"])
+    out = torch.empty(lay.nnz, device=DEV)
+    lib.call("kgat_row_softmax_f32", g.A.rowptr.data_ptr(), g.n_nodes, logits.to(DEV).data_ptr(), out.data_ptr(),
+             torch.cuda.current_stream().cuda_stream)
+    np.testing.assert_allclose(out.cpu().numpy(), got.numpy(), rtol=1e-6, atol=1e-8)
+
+
 def test_biinter_bwd_rows_matches_dense(pkg):
     _, kernels = _mods(pkg)
     torch.manual_seed(9)

@@ -47,7 +47,7 @@ def main():
     dev = torch.device("cuda")
     U, E, inter, trip = graph.synthetic_ckg(args.nodes, args.triples, seed=2024)
     lay = graph.build_layout(U, E, inter, trip)
-    g = graph.DeviceGraph(lay, dev)
+    g = graph.DeviceGraph(lay, dev) if not args.only or set(args.only.split(",")) - {"attention", "nfm"} else None
     n, nnz = lay.n_nodes, lay.nnz
     out = []
 
@@ -76,6 +76,8 @@ def main():
         fused_section(args, K, g, n, dev, rec)
     if want("masked"):
         masked_section(args, K, g, U, E, n, dev, rec)
+    if want("attention"):
+        attention_section(args, K, lay, U, E, dev, rec)
     if want("nfm"):
         nfm_section(args, dev, rec)
 
@@ -141,6 +143,33 @@ def fused_section(args, K, g, n, dev, rec):
         rec(f"spmm+biinter_fwd_{din}x{dout}", timeit(two, args.reps))
         rec(f"spmm_biinter_fused_{din}x{dout}",
             timeit(lambda: K.spmm_biinter_fwd(g, X, W1, b1, W2, b2, 0.1, 5, state=st), args.reps))
+
+
+def attention_section(args, K, lay, U, E, dev, rec):
+    """UPDATE_ATTENTION at C2 (model.py:318-366): edge scorer over all 20M edges (MFMA: 3 d x d
+    products per edge = 6 d^2 flop) + row softmax + transpose refresh, and its kernels alone."""
+    pkg = importlib.import_module(PKG)
+    torch.manual_seed(0)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32]))
+    g = m.attach_graph(lay, dev)
+    m.eval()
+    h = torch.from_numpy(lay.heads).to(dev)
+    r = torch.from_numpy(lay.rels).to(dev)
+    t = torch.from_numpy(lay.tails).to(dev)
+    idx = torch.tensor(lay.rel_order)
+    mode = pkg.KGATMode.UPDATE_ATTENTION
+    flop = 6.0 * 64 * 64 * lay.heads.size
+    us = timeit(lambda: m(h, r, t, idx, mode=mode), max(3, args.reps // 4))
+    rec("update_attention_c2", us, tflops=round(flop / (us * 1e-6) / 1e12, 1), edges=int(lay.heads.size))
+    plan = g.refresh_plan(h, r, t)
+    mha = m._multi_head_attention
+    w = [m._user_entity_embedding.weight.detach(), m._trans_matrix.detach(), mha._value_weight.weight.detach(),
+         mha._value_weight.bias.detach(), mha._output.weight.detach(), mha._output.bias.detach(),
+         mha._layer_norm.weight.detach(), mha._layer_norm.bias.detach()]
+    us = timeit(lambda: K.edge_logits(g, plan, *w), max(3, args.reps // 4))
+    rec("edge_logits_c2", us, tflops=round(flop / (us * 1e-6) / 1e12, 1), mfma_frac=round(flop / (us * 1e-6) / 157.3e12, 3))
+    logits = K.edge_logits(g, plan, *w)
+    rec("row_softmax_c2", timeit(lambda: K.row_softmax(g, logits), args.reps), 8 * lay.nnz + 8 * lay.n_nodes)
 
 
 def masked_section(args, K, g, U, E, n, dev, rec):
