@@ -96,11 +96,13 @@ int kgat_spmm_csr_masked_f32(const kgat_csr *A, const int32_t *src_map, const fl
  *            one bit per edge instead of a map entry;
  *   src_rank (nullable; for a src_map that numbers its set in ascending node
  *            order, e.g. kgat_hop_compact's): kgat_map_rank(src_map) -- one
- *            8-byte load per edge gives membership and compact row. */
+ *            8-byte load per edge gives membership and compact row;
+ *   n_src:   the number of source nodes (columns of A, entries of src_map;
+ *            0 = unknown), reserved for a staged source set. */
 int kgat_spmm_csr_masked_ex_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
                                 const float *Yc_init, int64_t ldyc, int64_t yc_row0, float *Y, int64_t ldy,
                                 int32_t d, int32_t *row_hit, const uint32_t *src_bits, const uint64_t *src_rank,
-                                float *workspace, int64_t workspace_floats, void *stream);
+                                int64_t n_src, float *workspace, int64_t workspace_floats, void *stream);
 
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);

@@ -109,7 +109,7 @@ def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.T
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
               int(row0), out.data_ptr(), _ld(out), d, None, _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map),
-              ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+              src_map.numel(), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     return out
 
 
@@ -211,7 +211,7 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0, 0,
               out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None,
-              _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map), ws.data_ptr(), ws.numel(),
+              _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map), src_map.numel(), ws.data_ptr(), ws.numel(),
               stream_ptr(Xc.device))
     if ev is not None:
         e1.record()

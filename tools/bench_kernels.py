@@ -200,7 +200,7 @@ def masked_section(args, K, g, U, E, n, dev, rec):
     Hc = torch.randn(n, 64, device=dev)
     rank = g.hop_buffers()[9]
     K.map_bits(hm, bits)  # the hop set's bitmap (bits held the batch frontier's)
-    for nm, b, rk in (("map", None, None), ("bits", bits, None), ("rank", None, rank)):
+    for nm, b, rk in (("map", None, None), ("bits", bits, None), ("rank_lds", None, rank)):
         rec(f"masked_hop1_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, hm, Hc, Hc, transpose=True, src_bits=b,
                                                                     src_rank=rk), args.reps), n_hop=nh)
 
