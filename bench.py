@@ -241,7 +241,8 @@ def main() -> None:
                  "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / args.steps,
                  "fwd_spmm_ms_per_step": t_prop,
                  "fwd_spmm_layer_edges_per_s": nnz * L / (t_prop * 1e-3)},
-        "roofline": {"bound": "hbm", "kernel": f"spmm_main_kernel<{d0}> (+fixup), forward A.X, per row-block launch",
+        "roofline": {"bound": "hbm", "kernel": f"spmm_main_kernel<{d0}, 0> (+fixup), forward A.X"
+                     + (" (per row-block launch)" if kernels.FWD_PIPELINE_BLOCKS > 1 else ""),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo},
         "cpu_baseline": None,
