@@ -1,6 +1,8 @@
 // a9 fused Adam, small device utilities, and the host-side CSR plan builder.
 #include <cmath>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -88,6 +90,24 @@ struct AdamTable {
 
 constexpr int kAdamChunk = 256 * 4 * 4;  // floats per block-iteration: 256 threads x float4 x 4
 
+template <int V>
+__device__ __forceinline__ float4 ld4(const float* p) {
+  if constexpr (V == 2) {
+    const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  return *reinterpret_cast<const float4*>(p);
+}
+template <int V>
+__device__ __forceinline__ void st4(float* p, float4 v) {
+  if constexpr (V == 2) __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(p));
+  else *reinterpret_cast<float4*>(p) = v;
+}
+
+// V = 0: per float4 load -> update -> store; V >= 1: a chunk's 16 float4 loads issued first
+// (all four arrays, four float4 per lane), then the updates, then the stores; V = 2 with
+// non-temporal loads/stores (every byte is touched once per step).
+template <int V>
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps) {
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t total = T.chunk_off[T.count];
@@ -97,6 +117,34 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, 
     const kgat_adam_tensor& a = T.t[i];
     const int64_t base = (c - T.chunk_off[i]) * kAdamChunk;
     const float step_size = a.step_size, bc2s = a.bc2_sqrt;
+    if (V >= 1 && base + kAdamChunk <= a.n) {
+      float4 pp[4], mm[4], vv[4], gg[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
+        pp[u] = ld4<V>(a.p + e);
+        mm[u] = ld4<V>(a.m + e);
+        vv[u] = ld4<V>(a.v + e);
+        gg[u] = ld4<V>(a.g + e);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float* P = &pp[u].x;
+        float* Mv = &mm[u].x;
+        float* Vv = &vv[u].x;
+        const float* G = &gg[u].x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], Vv[k], w1, b2, w2, step_size, bc2s, eps);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
+        st4<V>(a.p + e, pp[u]);
+        st4<V>(a.m + e, mm[u]);
+        st4<V>(a.v + e, vv[u]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
@@ -106,10 +154,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, 
         const float4 gg = *reinterpret_cast<const float4*>(a.g + e);
         float* P = &pp.x;
         float* Mv = &mm.x;
-        float* V = &vv.x;
+        float* V_ = &vv.x;
         const float* G = &gg.x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], V[k], w1, b2, w2, step_size, bc2s, eps);
+        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], V_[k], w1, b2, w2, step_size, bc2s, eps);
         *reinterpret_cast<float4*>(a.p + e) = pp;
         *reinterpret_cast<float4*>(a.m + e) = mm;
         *reinterpret_cast<float4*>(a.v + e) = vv;
@@ -124,6 +172,16 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, 
       }
     }
   }
+}
+
+// Default 2 (C2 table, 64M parameters: 314 us vs 346 us for 0/1 on the same box).
+static int adam_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("KGAT_ADAM_VARIANT");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
 }
 
 }  // namespace kgat
@@ -147,8 +205,12 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
   T.chunk_off[count] = off;
   if (off == 0) return KGAT_OK;
   const int grid = static_cast<int>(off < kgat::kCUs * 8 ? off : kgat::kCUs * 8);
-  hipLaunchKernelGGL(kgat::adam_multi_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), T,
-                     beta1, beta2, eps);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (kgat::adam_variant()) {
+    case 1: hipLaunchKernelGGL(kgat::adam_multi_kernel<1>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps); break;
+    case 2: hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps); break;
+    default: hipLaunchKernelGGL(kgat::adam_multi_kernel<0>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps);
+  }
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

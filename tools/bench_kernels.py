@@ -120,6 +120,8 @@ def graph_section(args, K, g, U, E, n, dev, rec):
     m = torch.zeros_like(p)
     v = torch.zeros_like(p)
     rec("adam_table", timeit(lambda: K.adam(p, gg, m, v, 1e-3, 0.9, 0.999, 0.03, 1e-8), args.reps), 28 * p.numel())
+    rec("adam_multi_table", timeit(lambda: K.adam_multi([(p, gg, m, v, 1e-3, 0.03)], 0.9, 0.999, 1e-8), args.reps),
+        28 * p.numel(), variant=os.environ.get("KGAT_ADAM_VARIANT", "0"))
     tables = [torch.randn(n, 64, device=dev), torch.randn(n, 64, device=dev), torch.randn(n, 32, device=dev)]
     rec("bpr_fwd", timeit(lambda: K.bpr_fwd(tables, users, pos, neg, 1e-5), args.reps))
 
