@@ -125,12 +125,13 @@ int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *
  * padded, kgat_frontier_build), bits0 (uint32 [ceil(n/32)]) marks F and
  * bits1 marks F plus every column of A's rows F -- the rows that product can
  * reach; node_map / hop_rows / *hop_count list bits1's set in ascending node
- * order (node_map fully written, -1 outside).  work:
+ * order (node_map fully written, -1 outside); hop_rank (nullable, uint64
+ * [ceil(n/32)]) gets the set's rank words (kgat_map_rank's layout).  work:
  * kgat_frontier_hop_work_bytes(n) bytes. */
 int64_t kgat_frontier_hop_work_bytes(int64_t n);
 int kgat_frontier_hop(const kgat_csr *A, const int32_t *rows0, int32_t n0, uint32_t *bits0, uint32_t *bits1,
-                      int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, void *work, int64_t work_bytes,
-                      void *stream);
+                      int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, uint64_t *hop_rank, void *work,
+                      int64_t work_bytes, void *stream);
 
 /* kgat_spmm_csr_masked_f32 restricted to an output row set (A = A^T of the
  * graph; out_bits / out_map / out_rows / out_count from kgat_frontier_hop):

@@ -239,7 +239,7 @@ struct Popc {
 __global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __restrict__ bits,
                                                           const int32_t* __restrict__ woff, int64_t n,
                                                           int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
-                                                          int32_t* __restrict__ count) {
+                                                          int32_t* __restrict__ count, uint64_t* __restrict__ rank) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t w = bits[i >> 5];
@@ -249,6 +249,16 @@ __global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __rest
   node_map[i] = in ? pos : -1;
   if (in) rows[pos] = static_cast<int32_t>(i);
   if (i == n - 1) *count = pos + (in ? 1 : 0);
+  // the set's rank words (kgat_map_rank's layout): members before the word << 32 | its bits
+  if (rank != nullptr && b == 0) rank[i >> 5] = (static_cast<uint64_t>(static_cast<uint32_t>(woff[i >> 5])) << 32) | w;
+}
+
+__global__ __launch_bounds__(256) void clear2_kernel(uint32_t* __restrict__ a, uint32_t* __restrict__ b, int64_t words) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < words) {
+    a[i] = 0u;
+    b[i] = 0u;
+  }
 }
 
 // Frontier bitmap from a node map: bit i of the (64-bit) word i/64 = map[i] >= 0.
@@ -390,7 +400,7 @@ extern "C" int64_t kgat_frontier_hop_work_bytes(int64_t n) {
 
 extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_t n0, uint32_t* bits0,
                                  uint32_t* bits1, int32_t* node_map, int32_t* hop_rows, int32_t* hop_count,
-                                 void* work, int64_t work_bytes, void* stream) {
+                                 uint64_t* hop_rank, void* work, int64_t work_bytes, void* stream) {
   if (!A || !rows0 || !bits0 || !bits1 || !node_map || !hop_rows || !hop_count || n0 < 0 || A->n_rows < 0)
     return KGAT_ERR_INVALID;
   const int64_t n = A->n_rows;
@@ -398,9 +408,9 @@ extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_
   if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t words = (n + 31) / 32;
-  if (hipMemsetAsync(bits0, 0, 4 * words, st) != hipSuccess || hipMemsetAsync(bits1, 0, 4 * words, st) != hipSuccess)
-    return KGAT_ERR_INVALID;
   if (n == 0) return hipMemsetAsync(hop_count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::clear2_kernel, dim3((words + 255) / 256), dim3(256), 0, st, bits0, bits1, words);
+  KGAT_LAUNCH_CHECK();
   if (n0 > 0) {
     hipLaunchKernelGGL(kgat::frontier_mark_kernel, dim3(n0), dim3(256), 0, st, *A, rows0, bits0, bits1);
     KGAT_LAUNCH_CHECK();
@@ -411,8 +421,9 @@ extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_
   hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(bits1, kgat::Popc{});
   const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
   if (e != hipSuccess) return static_cast<int>(e);
+  if (hop_rank != nullptr && (reinterpret_cast<uintptr_t>(hop_rank) & 7)) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits1, woff, n, node_map,
-                     hop_rows, hop_count);
+                     hop_rows, hop_count, hop_rank);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -251,9 +251,8 @@ def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
     _, node_map, rows, count, _, _, bits1, bits0, work = hb[:9]
     desc = graph.A.descriptor()
     _lib.call("kgat_frontier_hop", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
-              bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), work.data_ptr(), work.numel(),
-              stream_ptr(rows0.device))
-    map_rank(node_map, hb[9])
+              bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), hb[9].data_ptr(),
+              work.data_ptr(), work.numel(), stream_ptr(rows0.device))
     return rows, node_map, count, bits1, bits0
 
 

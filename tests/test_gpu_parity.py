@@ -481,6 +481,14 @@ def test_frontier_hop_and_masked_rows_product(pkg):
     np.testing.assert_array_equal(m[want], np.arange(cnt))
     assert np.all(m[~want] == -1)
     assert torch.equal(fbits[:fb.numel()], fb)
+    # the hop set's rank words written alongside (kgat_map_rank's layout; the count half of a word
+    # without members is unused, so only member words are compared there)
+    words = (n + 31) // 32
+    got = g.hop_buffers()[9][:words].cpu().numpy().view(np.uint64)
+    ref = kernels.map_rank(hmap, torch.empty(words, dtype=torch.int64, device=DEV)).cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got & 0xFFFFFFFF, ref & 0xFFFFFFFF)
+    mem = (ref & 0xFFFFFFFF) != 0
+    np.testing.assert_array_equal(got[mem] >> 32, ref[mem] >> 32)
     comp = kernels.spmm_masked_rows(g, g.node_map, fbits, Xc, Yc, hrows, hmap, hcount, hbits)
     assert torch.equal(comp[:cnt], dense[hrows[:cnt].long()])
     kernels.frontier_reset(rows0, g.node_map)
