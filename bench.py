@@ -9,9 +9,12 @@ train mode (dropout on), inputs resident in HBM before timing starts.
 
 value = CKG layer-edges per second of the whole job = n_gpus * E * L / t_step
 (weak scaling: every rank runs full propagation for its own batch; for N > 1,
-data-parallel replicas: the table gradient is reduce-scattered by row blocks
-over RCCL, each rank runs Adam on its own rows and the rows are all-gathered
-back -- replicas.ShardedGradSync; small gradients in one flat all-reduce).
+data-parallel replicas, replicas.ShardedGradSync: by default for 2-layer
+configs the replicas all-gather their compact layer-0 hop-set gradient terms
+over RCCL and each computes the mean table gradient and the full Adam itself
+(--dp replicated); otherwise the table gradient is reduce-scattered by row
+blocks, each rank runs Adam on its own rows and the rows are all-gathered back
+(--dp sharded); small gradients in one flat all-reduce).
 Also reported: BPR pairs/s = 256 * n_gpus / t_step, forward-propagation
 edges/s, the roofline of the dominant kernel (the SpMM gather, timed live
 with HIP events on its launch stream) and the CPU baseline (the oracle's
@@ -105,6 +108,10 @@ def main() -> None:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",
+                    help="N>1 table-gradient exchange: replicated = all-gather of the compact layer-0 hop-set "
+                         "terms, every rank computes the mean gradient and full Adam; sharded = row-block "
+                         "reduce-scatter, owned-row Adam, all-gather; auto = replicated for 2-layer configs")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -157,7 +164,8 @@ def main() -> None:
         batches.append([torch.from_numpy(x.astype(np.int64)).to(dev)
                         for x in (u, su[k, 1], rng.integers(0, n_items, B))])
     params = [p for p in model.parameters() if not p.is_sparse and p.requires_grad]
-    sync = replicas.ShardedGradSync(params).attach(model)  # table-gradient exchange overlapped with its blocks
+    dp_mode = args.dp if args.dp != "auto" else ("replicated" if L <= 2 else "sharded")
+    sync = replicas.ShardedGradSync(params, replicate_table=dp_mode == "replicated").attach(model)
 
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
@@ -233,7 +241,8 @@ def main() -> None:
         "data": "synthetic (seeded CKG per SURVEY §8d; random-init weights; no dataset download)",
         "config": {"workload": cfg["workload"], "nodes": n, "nnz": nnz, "interactions": int(len(inter)),
                    "kg_triples": int(len(trip)), "embed_dim": d0, "layer_size": cfg["layers"], "global_batch": B * world,
-                   "parallelism": f"dp{world}" if world > 1 else "single", "mode": "train (dropout 0.1)"},
+                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   "dp_exchange": dp_mode if world > 1 else None, "mode": "train (dropout 0.1)"},
         "bpr_pairs_per_s": B * world / (ms * 1e-3),
         "final_loss": final_loss,
         "spmm": {"fwd_launches": len(fwd), "bwd_launches": len(bwd), "fwd_avg_ms": avg_ms,

@@ -145,6 +145,23 @@ int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, con
                                   const int32_t *out_count, float *Y, int64_t ldy, int32_t d, float *workspace,
                                   int64_t workspace_floats, void *stream);
 
+/* Data-parallel exchange of the compact table gradient (replicas.ShardedGradSync,
+ * replicate_table mode; no reference counterpart -- the reference is one
+ * process).  Every replica's layer-0 hop set is an ascending row list; after an
+ * all-gather, list g = lists[g*cap .. g*cap + counts[g]) (counts on the device).
+ * kgat_rows_union: their union, as kgat_frontier_hop's outputs (bits uint32
+ * [ceil(n/32)], node_map, rows, *count, rank words; work:
+ * kgat_frontier_hop_work_bytes(n)).  kgat_rows_merge_f32: for k < *count
+ * (<= max_rows), out[k] = scale * sum over g (in g order) of the row of vals
+ * (w floats, row g*cap + position of rows[k] in list g) of every list holding
+ * rows[k]; G <= 64, w and the leading dimensions multiples of 4. */
+int kgat_rows_union(const int32_t *lists, const int32_t *counts, int32_t G, int32_t cap, int64_t n, uint32_t *bits,
+                    int32_t *node_map, int32_t *rows, int32_t *count, uint64_t *rank, void *work, int64_t work_bytes,
+                    void *stream);
+int kgat_rows_merge_f32(const int32_t *lists, const int32_t *counts, int32_t G, int32_t cap, const float *vals,
+                        int64_t ldv, int32_t w, const int32_t *rows, const int32_t *count, int64_t max_rows,
+                        float *out, int64_t ldo, float scale, void *stream);
+
 /* a2 -- bi-interaction aggregator forward, fused:
  *   H = normalize(dropout(LReLU(W1 (X+S) + b1) + LReLU(W2 (X*S) + b2)))
  * Replaces src/model/KGAT/aggregator.py:57-65.  W1/W2 are nn.Linear weights

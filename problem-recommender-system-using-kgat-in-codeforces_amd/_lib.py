@@ -86,6 +86,10 @@ _SIGNATURES = {
     "kgat_frontier_hop_work_bytes": (c_i64, [c_i64]),
     "kgat_frontier_hop": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_i64, c_vp]),
+    "kgat_rows_union": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                       c_vp]),
+    "kgat_rows_merge_f32": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp,
+                                           c_i64, c_f32, c_vp]),
     "kgat_spmm_csr_masked_rows_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
                                                      c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
     "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,

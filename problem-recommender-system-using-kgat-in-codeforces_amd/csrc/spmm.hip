@@ -29,6 +29,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 namespace kgat {
 
 // Final write of one output row segment (lane gl) in the four modes: row is
@@ -307,6 +309,62 @@ __global__ __launch_bounds__(256) void hop_finish_kernel(const int32_t* __restri
   }
 }
 
+// Union of G row lists (list g = lists[g*cap .. g*cap + counts[g])): bit of every listed row.
+__global__ __launch_bounds__(256) void lists_mark_kernel(const int32_t* __restrict__ lists,
+                                                         const int32_t* __restrict__ counts, int32_t cap,
+                                                         int64_t total, int64_t n, uint32_t* __restrict__ bits) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t g = i / cap;
+  if (i - g * cap >= counts[g]) return;
+  const int32_t r = lists[i];
+  if (r >= 0 && r < n) atomicOr(&bits[r >> 5], 1u << (r & 31));
+}
+
+// out[k] = scale * (sum over g = 0..G-1 of vals[g*cap + pos_g(rows[k])]), pos_g = position of
+// rows[k] in list g (ascending; binary search by lane g), lists without the row skipped.
+// One wave per union row, w/4 lanes of float4; the sum runs in list order on every replica
+// alike, so every rank merging the same all-gathered lists gets the same bits.
+__global__ __launch_bounds__(256) void lists_merge_kernel(const int32_t* __restrict__ lists,
+                                                          const int32_t* __restrict__ counts, int32_t G,
+                                                          int32_t cap, const float* __restrict__ vals, int64_t ldv,
+                                                          int32_t w, const int32_t* __restrict__ rows,
+                                                          const int32_t* __restrict__ count, int64_t max_rows,
+                                                          float* __restrict__ out, int64_t ldo, float scale) {
+  __shared__ int32_t spos[4][64];  // per wave: the row's position in each list (-1: absent)
+  const int lane = threadIdx.x & 63;
+  int32_t* wpos = spos[threadIdx.x >> 6];
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
+  const int64_t nrows = min(static_cast<int64_t>(*count), max_rows);
+  for (int64_t k = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nrows;
+       k += waves) {
+    const int32_t node = rows[k];
+    int32_t pos = -1;
+    if (lane < G) {  // lane g: lower bound of node in list g
+      const int32_t* lg = lists + static_cast<int64_t>(lane) * cap;
+      int32_t lo = 0, hi = counts[lane];
+      while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (lg[mid] < node) lo = mid + 1; else hi = mid;
+      }
+      if (lo < counts[lane] && lg[lo] == node) pos = lo;
+    }
+    wpos[lane] = pos;
+    __builtin_amdgcn_wave_barrier();
+    for (int c = lane * 4; c < w; c += 256) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int g = 0; g < G; ++g) {
+        const int32_t p = wpos[g];
+        if (p < 0) continue;
+        const floatx4 v = *reinterpret_cast<const floatx4*>(vals + (static_cast<int64_t>(g) * cap + p) * ldv + c);
+        acc += v;
+      }
+      *reinterpret_cast<floatx4*>(out + k * ldo + c) = acc * scale;
+    }
+    __builtin_amdgcn_wave_barrier();  // wpos is rewritten for the wave's next row
+  }
+}
+
 }  // namespace kgat
 
 extern "C" int kgat_spmm_csr_f32(const kgat_csr* A, const float* X, int64_t ldx, float* Y, int64_t ldy,
@@ -453,6 +511,56 @@ extern "C" int kgat_map_rank(const int32_t* node_map, int64_t n, uint64_t* rank,
   if (n == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::map_rank_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      node_map, n, rank);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+// Union of the G replicas' hop sets (data-parallel exchange of the compact
+// table gradient, replicas.ShardedGradSync): the bitmap of every listed row,
+// then kgat_frontier_hop's popcount scan and finish (sorted rows, node map,
+// count, rank words).  work: kgat_frontier_hop_work_bytes(n) bytes.
+extern "C" int kgat_rows_union(const int32_t* lists, const int32_t* counts, int32_t G, int32_t cap, int64_t n,
+                               uint32_t* bits, int32_t* node_map, int32_t* rows, int32_t* count, uint64_t* rank,
+                               void* work, int64_t work_bytes, void* stream) {
+  if (!counts || !bits || !node_map || !rows || !count || G < 1 || cap < 0 || n < 0) return KGAT_ERR_INVALID;
+  if (cap > 0 && !lists) return KGAT_ERR_INVALID;
+  if (rank != nullptr && (reinterpret_cast<uintptr_t>(rank) & 7)) return KGAT_ERR_INVALID;
+  const int64_t need = kgat_frontier_hop_work_bytes(n);
+  if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return hipMemsetAsync(count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  const int64_t words = (n + 31) / 32;
+  if (hipMemsetAsync(bits, 0, 4 * words, st) != hipSuccess) return KGAT_ERR_INVALID;
+  const int64_t total = static_cast<int64_t>(G) * cap;
+  if (total > 0) {
+    hipLaunchKernelGGL(kgat::lists_mark_kernel, dim3((total + 255) / 256), dim3(256), 0, st, lists, counts, cap,
+                       total, n, bits);
+    KGAT_LAUNCH_CHECK();
+  }
+  int32_t* woff = static_cast<int32_t*>(work);
+  void* temp = static_cast<char*>(work) + 4 * (words + 64);
+  size_t bytes = static_cast<size_t>(need - 4 * (words + 64));
+  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(bits, kgat::Popc{});
+  const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits, woff, n, node_map, rows,
+                     count, rank);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_rows_merge_f32(const int32_t* lists, const int32_t* counts, int32_t G, int32_t cap,
+                                   const float* vals, int64_t ldv, int32_t w, const int32_t* rows,
+                                   const int32_t* count, int64_t max_rows, float* out, int64_t ldo, float scale,
+                                   void* stream) {
+  if (!counts || !rows || !count || !out || G < 1 || G > 64 || cap < 0 || w < 0 || max_rows < 0)
+    return KGAT_ERR_INVALID;
+  if ((w & 3) || (ldo & 3) || ldo < w || kgat::misaligned(out)) return KGAT_ERR_INVALID;
+  if (cap > 0 && (!lists || !vals || (ldv & 3) || ldv < w || kgat::misaligned(vals))) return KGAT_ERR_INVALID;
+  if (max_rows == 0 || w == 0) return KGAT_OK;
+  const int64_t blocks = std::min<int64_t>((max_rows + 3) / 4, 8192);
+  hipLaunchKernelGGL(kgat::lists_merge_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     lists, counts, G, cap, vals, ldv, w, rows, count, max_rows, out, ldo, scale);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -256,6 +256,42 @@ def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
     return rows, node_map, count, bits1, bits0
 
 
+def rows_union(graph: DeviceGraph, lists: torch.Tensor, counts: torch.Tensor, cap: int):
+    """Union of G ascending row lists (list g = lists[g*cap : g*cap + counts[g]], counts int32 [G] on
+    the device) into graph.hop_buffers(): (rows int32 [N] ascending -- first count valid --, node_map,
+    count int32 [1] on the device, rank words) (kgat_rows_union)."""
+    _req(lists, "lists", dtype=torch.int32, dim=1)
+    _req(counts, "counts", dtype=torch.int32, dim=1)
+    G = counts.numel()
+    if lists.numel() < G * cap:
+        raise ValueError("lists must hold G * cap entries")
+    hb = graph.hop_buffers()
+    _, node_map, rows, count, _, _, bits, _, work = hb[:9]
+    _lib.call("kgat_rows_union", lists.data_ptr(), counts.data_ptr(), G, cap, graph.n_nodes, bits.data_ptr(),
+              node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), hb[9].data_ptr(), work.data_ptr(), work.numel(),
+              stream_ptr(lists.device))
+    return rows, node_map, count, hb[9]
+
+
+def rows_merge(lists: torch.Tensor, counts: torch.Tensor, cap: int, vals: torch.Tensor, rows: torch.Tensor,
+               count: torch.Tensor, max_rows: int, scale: float) -> torch.Tensor:
+    """out[k] = scale * sum over the lists holding rows[k] (in list order) of their vals rows, for k <
+    count (device), out [max_rows, w] (kgat_rows_merge_f32)."""
+    _req(lists, "lists", dtype=torch.int32, dim=1)
+    _req(counts, "counts", dtype=torch.int32, dim=1)
+    _req(vals, "vals", dim=2)
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    _req(count, "count", dtype=torch.int32, dim=1)
+    G, w = counts.numel(), vals.shape[1]
+    if vals.shape[0] < G * cap or lists.numel() < G * cap:
+        raise ValueError("lists / vals must hold G * cap rows")
+    out = torch.empty(max(max_rows, 1), w, dtype=torch.float32, device=vals.device)
+    _lib.call("kgat_rows_merge_f32", lists.data_ptr(), counts.data_ptr(), G, cap, vals.data_ptr(), _ld(vals), w,
+              rows.data_ptr(), count.data_ptr(), max_rows, out.data_ptr(), _ld(out), float(scale),
+              stream_ptr(vals.device))
+    return out
+
+
 def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_rows, out_map, out_count, out_bits,
                      transpose: bool = True) -> torch.Tensor:
     """The masked product (see spmm_masked) on the output rows of a hop set only, written compactly:

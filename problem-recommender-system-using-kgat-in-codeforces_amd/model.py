@@ -230,7 +230,11 @@ class _CFLoss(torch.autograd.Function):
                                                                         drops[l], seeds[l], rows=hrows,
                                                                         **_saved(tables, states, l))
                 kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
-                if l == 0 and hook is not None:
+                if l == 0 and hook is not None and hook.replicated:
+                    # data-parallel replicas exchange the compact hop-set terms and each computes the
+                    # mean table gradient A^T . mean(dS) + mean(dXd) itself (replicas.ShardedGradSync)
+                    dX = hook.table_grad_hop(graph, hmap, hrows, hcount, dSc, dXdc, rank)
+                elif l == 0 and hook is not None:
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
                     for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
                         kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
@@ -244,7 +248,9 @@ class _CFLoss(torch.autograd.Function):
             dXd, dS, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l],
                                                               seeds[l], **_saved(tables, states, l))
             kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXd)
-            if l == 0 and hook is not None:
+            if l == 0 and hook is not None and hook.replicated:
+                dXd = hook.table_grad_dense(graph, dS, dXd)
+            elif l == 0 and hook is not None:
                 # the table gradient by row blocks: each block's exchange (replicas.ShardedGradSync)
                 # starts while the next block's A^T . dS is computed
                 for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):

@@ -16,6 +16,17 @@ all-gathered back -- the same bytes on the wire as one all-reduce, with the
 dense Adam pass cut G-fold.  Per element the arithmetic is the all-reduce
 path's (mean gradient, same Adam), so replicas stay identical.
 
+With ``replicate_table=True`` the table is not sharded at all: when the CF
+backward's layer-0 hop set is small (the hop chain, model._CFLoss), the
+replicas all-gather their compact hop-set terms (row list, dS rows, direct
+dX rows -- ~2*|hop|*d floats instead of N*d), merge them in rank order
+(kgat_rows_union / kgat_rows_merge_f32) and every rank computes the mean table
+gradient A^T . mean(dS) + mean(dXd) itself with the masked product, then runs
+the full Adam; no reduce-scatter, no all-gather of the 256 MB table.  Every
+rank computes the same bits from the same gathered data, so the replicas stay
+identical; against the all-reduce path only the summation order differs.
+(If any rank's hop set is dense, that step all-reduces the dense gradient.)
+
 Works with any torch.distributed backend: ``nccl`` (= RCCL on ROCm) on the
 GPU box, ``gloo`` for the CPU tests.
 """
@@ -83,9 +94,13 @@ class ShardedGradSync:
     ranges for ``FusedAdam.step(row_ranges=...)`` (own block + tail).  ``gather()``
     after the optimizer step all-gathers the owned blocks of the parameters."""
 
-    def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES):
+    def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES, replicate_table: bool = False):
         self.params = list(params)
         self.big_bytes = int(big_bytes)
+        self.replicate_table = bool(replicate_table)
+        self.replicated = False  # set by attach() on more than one rank with replicate_table
+        self._done = None  # the table gradient already averaged by table_grad_hop / table_grad_dense
+        self.stats: dict[str, int] = {}  # steps per table-exchange path ("hop", "dense")
         self._big: list[tuple[torch.Tensor, int, int]] = []
         self._table = None
         self.bounds: list[tuple[int, int]] = []
@@ -106,8 +121,76 @@ class ShardedGradSync:
             return self
         self._table = table
         self.bounds = [(k * s, (k + 1) * s) for k in range(n)] + ([(s * n, rows)] if s * n < rows else [])
+        self.replicated = self.replicate_table
         model._table_grad_hook = self
         return self
+
+    # ---- replicate_table mode: the mean table gradient computed on every rank from gathered hop sets
+
+    @staticmethod
+    def _all_gather(t: torch.Tensor) -> torch.Tensor:
+        """[G * t.numel()] (rank order) of a contiguous tensor, flattened."""
+        n = world()
+        flat = t.reshape(-1)
+        if _is_nccl():
+            out = torch.empty(n * flat.numel(), dtype=flat.dtype, device=flat.device)
+            dist.all_gather_into_tensor(out, flat)
+            return out
+        parts = [torch.empty_like(flat) for _ in range(n)]
+        dist.all_gather(parts, flat)
+        return torch.cat(parts)
+
+    def _agree(self, sparse: bool, count: torch.Tensor | None, dev) -> tuple[torch.Tensor, list[int], bool]:
+        """All-gather (sparse flag, hop count) of every rank: (device [G, 2], host counts, all sparse)."""
+        info = torch.zeros(2, dtype=torch.int32, device=dev)
+        if sparse:
+            info[0] = 1
+            info[1:2].copy_(count)
+        both = self._all_gather(info).view(-1, 2)
+        host = both.cpu().tolist()  # the one host sync of the step: the gather sizes
+        return both, [c for _, c in host], all(f == 1 for f, _ in host)
+
+    def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words) -> torch.Tensor:
+        """The mean table gradient from this rank's compact layer-0 hop-set terms (model._CFLoss):
+        hop rows (ascending, hcount of them), dS and direct dX rows in hop order."""
+        from . import kernels
+
+        n = world()
+        d = dSc.shape[1]
+        both, counts, all_sparse = self._agree(True, hcount, dSc.device)
+        if all_sparse:
+            cap = max(1, max(counts))
+            pack = torch.empty(cap, 2 * d, dtype=torch.float32, device=dSc.device)
+            pack[:, :d].copy_(dSc[:cap])
+            pack[:, d:].copy_(dXdc[:cap])
+            lists = self._all_gather(hrows[:cap].contiguous())
+            vals = self._all_gather(pack).view(n * cap, 2 * d)
+            cnt = both[:, 1].contiguous()
+            urows, umap, ucount, urank = kernels.rows_union(graph, lists, cnt, cap)
+            merged = kernels.rows_merge(lists, cnt, cap, vals, urows, ucount, min(graph.n_nodes, n * cap), 1.0 / n)
+            dX = kernels.spmm_masked(graph, umap, merged[:, :d], Yc_init=merged[:, d:], transpose=True,
+                                     src_rank=urank)
+        else:  # some rank's hop set is dense this step: every rank all-reduces its dense gradient
+            dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True, src_rank=rank_words)
+            dist.all_reduce(dX)
+            dX.div_(n)
+        self._done = dX
+        key = "hop" if all_sparse else "dense"
+        self.stats[key] = self.stats.get(key, 0) + 1
+        return dX
+
+    def table_grad_dense(self, graph, dS, dXd) -> torch.Tensor:
+        """The dense-backward counterpart of table_grad_hop: dXd += A^T . dS, all-reduced, mean."""
+        from . import kernels
+
+        n = world()
+        self._agree(False, None, dS.device)
+        kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
+        dist.all_reduce(dXd)
+        dXd.div_(n)
+        self._done = dXd
+        self.stats["dense"] = self.stats.get("dense", 0) + 1
+        return dXd
 
     def block_ready(self, k: int, grad: torch.Tensor) -> None:
         n = world()
@@ -129,9 +212,18 @@ class ShardedGradSync:
         ranges: dict = {}
         small = []
         early, self._early = self._early, None
+        done, self._done = self._done, None
         for p in self.params:
             g = p.grad
             if g is None:
+                continue
+            if self.replicated and p is self._table and done is not None:
+                if g.data_ptr() != done.data_ptr():  # autograd kept a copy of the averaged gradient
+                    g.copy_(done)
+                continue  # already the mean on every rank: full Adam, nothing to gather
+            if self.replicate_table and g.numel() * g.element_size() > self.big_bytes:
+                dist.all_reduce(g)  # replicated mode shards nothing
+                g.div_(n)
                 continue
             if early is not None and p is self._table and len(early[1]) == len(self.bounds):
                 for w in early[1]:

@@ -7,6 +7,13 @@ gradient exchange, Adam on the owned rows, all-gather -- and (C) the same sync a
 so the table gradient's blocks are exchanged while the backward computes the next block.  With two
 ranks every sum has two operands, so all three must agree bit for bit, and each path's replicas must
 stay identical.
+
+Two more sets use ``ShardedGradSync(replicate_table=True)`` (the replicas all-gather their compact
+layer-0 hop-set terms and each computes the mean table gradient itself): (D) as bench.py runs it, and
+(E) with rank 1's backward forced dense (HOP_DENSE_FRACTION = 0 on that rank only), so the ranks
+disagree on the hop mode and must fall back to the dense all-reduce together.  Their sums are
+associated differently (A^T . mean(dS) instead of mean(A^T . dS)), so they are compared with the
+Adam tolerance of DESIGN.md §2, and each path's replicas must stay bit-identical.
 """
 from __future__ import annotations
 
@@ -32,7 +39,8 @@ def main() -> None:
     args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
                         message_dropout=[0.1, 0.1])
     models = []
-    for _ in range(3):
+    model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
+    for _ in range(5):
         torch.manual_seed(3)
         m = pkg.KGAT(args)
         m.attach_graph(lay, "cuda")
@@ -42,7 +50,7 @@ def main() -> None:
         models.append(m)
     rng = np.random.default_rng(40 + rank)
     failures = []
-    syncs = [None, None, None]
+    syncs = [None] * 5
     for step in range(3):
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
@@ -50,11 +58,17 @@ def main() -> None:
             torch.manual_seed(1000 * step + rank)  # same dropout for every path, per rank
             if k and syncs[k] is None:
                 params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
-                syncs[k] = rep.ShardedGradSync(params)
-                if k == 2:
+                syncs[k] = rep.ShardedGradSync(params, replicate_table=k >= 3)
+                if k >= 2:
                     syncs[k].attach(m)
             loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
-            loss.backward()
+            frac = model_mod.HOP_DENSE_FRACTION
+            if k == 4 and rank == 1:
+                model_mod.HOP_DENSE_FRACTION = 0.0
+            try:
+                loss.backward()
+            finally:
+                model_mod.HOP_DENSE_FRACTION = frac
             params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
             if k == 0:
                 rep.allreduce_gradients(params)
@@ -62,17 +76,24 @@ def main() -> None:
             else:
                 m.update_cf_weights(row_ranges=syncs[k].reduce())
                 syncs[k].gather()
-    for (na, pa), (_, pb), (_, pc) in zip(models[0].named_parameters(), models[1].named_parameters(),
-                                          models[2].named_parameters()):
+    for tag, want in (("D", "hop"), ("E", "dense")):
+        got = syncs["ABCDE".index(tag)].stats
+        if got.get(want, 0) != 3:
+            failures.append(f"{tag}: table exchange paths {got}, expected 3 x {want}")
+    for named in zip(*(m.named_parameters() for m in models)):
+        na, pa = named[0]
         if pa.is_sparse:
             continue
-        for tag, other_m in (("B", pb), ("C", pc)):
-            if not torch.equal(pa.data, other_m.data):
-                failures.append(f"{tag} {na}: max |diff| {(pa.data - other_m.data).abs().max().item():.3e}")
-        other = pa.data.clone()
-        dist.broadcast(other, 0)
-        if not torch.equal(other, pa.data):
-            failures.append(f"{na}: replicas diverged")
+        for tag, (_, po) in zip("BCDE", named[1:]):
+            if tag in "BC" and not torch.equal(pa.data, po.data):
+                failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
+            if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
+                failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
+        for tag, (_, po) in zip("ABCDE", named):
+            other = po.data.clone()
+            dist.broadcast(other, 0)
+            if not torch.equal(other, po.data):
+                failures.append(f"{tag} {na}: replicas diverged")
     print(f"rank {rank}: {'OK' if not failures else failures}", flush=True)
     dist.destroy_process_group()
     sys.exit(1 if failures else 0)

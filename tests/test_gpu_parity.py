@@ -1125,3 +1125,42 @@ def test_attention_refresh_synthetic_vs_oracle(pkg, dim):
     att = m.attentive_matrix.data.coalesce()
     np.testing.assert_array_equal(att.indices().cpu().numpy(), ref.indices().numpy())
     np.testing.assert_allclose(att.values().cpu().numpy(), ref.values().numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_rows_union_and_merge(pkg):
+    """kgat_rows_union / kgat_rows_merge_f32 (the replicas' hop-set exchange): the union of G ascending
+    lists (padding after each count ignored) and, per union row, the scaled sum of the lists' rows in
+    list order -- bit-exact against numpy summing in the same order."""
+    graph_mod, kernels = _mods(pkg)
+    rng = np.random.default_rng(21)
+    n, G, cap, w = 5000, 3, 900, 128
+    h, t = rng.integers(0, n, 2000), rng.integers(0, n, 2000)
+    rowptr, col, val = graph_mod.csr_from_coo(n, h, t, rng.random(h.size).astype(np.float32))
+    lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
+                                tails=np.zeros(0, np.int64), edge_vals=np.zeros(0, np.float32), rowptr=rowptr,
+                                col=col, val=val, slot=np.zeros(0, np.int64))
+    g = graph_mod.DeviceGraph(lay, DEV)
+    counts = np.array([900, 0, 611], np.int32)
+    lists = np.full(G * cap, -7, np.int32)  # padding must be ignored
+    for k in range(G):
+        lists[k * cap:k * cap + counts[k]] = np.sort(rng.choice(n, counts[k], replace=False))
+    vals = rng.standard_normal((G * cap, w)).astype(np.float32)
+    ld, cd, vd = (torch.from_numpy(x).to(DEV) for x in (lists, counts, vals))
+    rows, node_map, count, rank = kernels.rows_union(g, ld, cd, cap)
+    want = np.unique(np.concatenate([lists[k * cap:k * cap + counts[k]] for k in range(G)]))
+    u = int(count.item())
+    assert u == want.size
+    np.testing.assert_array_equal(rows[:u].cpu().numpy(), want)
+    m = node_map.cpu().numpy()
+    np.testing.assert_array_equal(m[want], np.arange(u))
+    assert np.all(np.delete(m, want) == -1)
+    words = (n + 31) // 32
+    ref = kernels.map_rank(node_map, torch.empty(words, dtype=torch.int64, device=DEV)).cpu().numpy().view(np.uint64)
+    got = rank[:words].cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got & 0xFFFFFFFF, ref & 0xFFFFFFFF)
+    out = kernels.rows_merge(ld, cd, cap, vd, rows, count, G * cap, 0.5).cpu().numpy()
+    exp = np.zeros((u, w), np.float32)
+    for k in range(G):
+        pos = np.searchsorted(want, lists[k * cap:k * cap + counts[k]])
+        exp[pos] = exp[pos] + vals[k * cap:k * cap + counts[k]]
+    np.testing.assert_array_equal(out[:u], exp * np.float32(0.5))
