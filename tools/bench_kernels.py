@@ -76,6 +76,8 @@ def main():
         fused_section(args, K, g, n, dev, rec)
     if want("masked"):
         masked_section(args, K, g, U, E, n, dev, rec)
+    if want("dpx"):
+        dpx_section(args, K, g, U, E, n, dev, rec)
     if want("attention"):
         attention_section(args, K, lay, U, E, dev, rec)
     if want("nfm"):
@@ -205,6 +207,42 @@ def masked_section(args, K, g, U, E, n, dev, rec):
     for nm, b, rk in (("map", None, None), ("bits", bits, None), ("rank_lds", None, rank)):
         rec(f"masked_hop1_T_d64_{nm}", timeit(lambda: K.spmm_masked(g, hm, Hc, Hc, transpose=True, src_bits=b,
                                                                     src_rank=rk), args.reps), n_hop=nh)
+
+
+def dpx_section(args, K, g, U, E, n, dev, rec):
+    """The replicated-table DP exchange's compute at C2, G replicas simulated on one GPU: each
+    replica's first hop set (frontier_hop of its own 256-pair batch) is listed as after the
+    all-gather, then the union, the rank-order merge of the [cap, 2d] terms and the layer-0 masked
+    A^T product over the union (vs one replica's own product)."""
+    B, d = 256, 64
+    rng = np.random.default_rng(1)
+    for G in (1, 2, 4, 8):
+        lists, counts = [], []
+        for _ in range(G):
+            users = torch.from_numpy(rng.integers(0, U, B)).to(dev)
+            pos = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+            neg = torch.from_numpy(rng.integers(0, int(E * 0.1), B)).to(dev)
+            rows, _ = K.frontier_build(users, pos, neg, g.node_map)
+            hr, hm, hc, _, _ = K.frontier_hop(g, rows)
+            K.frontier_reset(rows, g.node_map)
+            c = int(hc.item())
+            lists.append(hr[:c].clone())
+            counts.append(c)
+        cap = max(counts)
+        L = torch.full((G * cap,), -1, dtype=torch.int32, device=dev)
+        for k, lk in enumerate(lists):
+            L[k * cap:k * cap + counts[k]] = lk
+        C = torch.tensor(counts, dtype=torch.int32, device=dev)
+        V = torch.randn(G * cap, 2 * d, device=dev)
+        rec(f"rows_union_G{G}", timeit(lambda: K.rows_union(g, L, C, cap), args.reps), cap=cap)
+        ur, um, uc, uk = K.rows_union(g, L, C, cap)
+        nu = int(uc.item())
+        rec(f"rows_merge_G{G}", timeit(lambda: K.rows_merge(L, C, cap, V, ur, uc, min(n, G * cap), 1.0 / G),
+                                       args.reps), n_union=nu, exchange_MB_per_rank=round(cap * (2 * d + 1) * 4 / 1e6, 2))
+        M = K.rows_merge(L, C, cap, V, ur, uc, min(n, G * cap), 1.0 / G)
+        rec(f"masked_union_T_d64_G{G}", timeit(lambda: K.spmm_masked(g, um, M[:, :d], Yc_init=M[:, d:],
+                                                                     transpose=True, src_rank=uk), args.reps),
+            n_union=nu, frac_rows=round(nu / n, 4))
 
 
 def nfm_section(args, dev, rec):
