@@ -188,3 +188,26 @@ def test_nfm_feature_matrix_matches_reference_construction():
     np.testing.assert_array_equal(b.feature_val.numpy(), want.data.astype(np.float32))
     with pytest.raises(IndexError):
         pkg.NFMBatcher(10, I, E, [I], [I], {0: [1]}, "cpu")
+
+
+def test_driver_dataset_split_and_early_stopping():
+    """driver.py (make train / predict / recommend): the Codeforces-shaped synthetic dataset keeps the
+    reference's KG layout and the per-user 80/20 then 90/10 split is disjoint and complete
+    (preprocess.py:55-111, 608-614); early_stopping follows main.py:173-195."""
+    import importlib
+    import math
+    drv = importlib.import_module(load_pkg().__name__ + ".driver")
+    inter, trip, E = drv.synthetic_codeforces(users=40, problems=300, contests=50, tags=10, ratings=8,
+                                              per_user=(10, 60), seed=3)
+    assert E == 300 + 50 + 6 + 10 + 8
+    assert set(np.unique(trip[:, 1]).tolist()) <= {0, 1, 2, 3}
+    assert np.all(trip[trip[:, 1] == 2, 2] >= 300) and np.all(trip[trip[:, 1] == 3, 0] >= 300)
+    assert np.unique(inter, axis=0).shape[0] == inter.shape[0]
+    tr, va, te = drv.split_interactions(inter, 40, seed=3)
+    assert tr.shape[0] + va.shape[0] + te.shape[0] == inter.shape[0]
+    for u in range(40):
+        a, b, c = (set(x[x[:, 0] == u, 1].tolist()) for x in (tr, va, te))
+        n = int((inter[:, 0] == u).sum())
+        assert not (a & b or a & c or b & c) and len(c) == math.ceil(0.2 * n)  # sklearn's sizes
+    assert drv.early_stopping([0.1, 0.2] + [0.1] * 9) == (0.2, False)
+    assert drv.early_stopping([0.1, 0.2] + [0.1] * 10) == (0.2, True)
