@@ -185,6 +185,15 @@ __global__ __launch_bounds__(256) void transr_scatter_kernel(const int64_t* __re
 // (blockIdx.y): d trans[r][i][j] = scale * sum over samples of relation r, in
 // batch order, of e_h[i] g_h'[j] + e_t+[i] g_t+'[j] + e_t-[i] g_t-'[j];
 // slice 0 also produces d rel_emb[r] = scale * sum g_er.
+// The block lists relation r's samples first (256 relation ids per pass,
+// ballot + wave counts -> batch order), then stages kWgradStage of them at a
+// time in LDS -- the three table rows and the four projected gradients, every
+// load of the stage in flight at once -- so the per-sample accumulation reads
+// LDS instead of waiting on a chain of dependent global loads per sample (the
+// former sample-serial loop was latency-bound: 1.6 ms per call at B = 512).
+// Per entry the samples are summed in batch order with the same fma chain.
+constexpr int kWgradStage = 8;
+
 __global__ __launch_bounds__(256) void transr_wgrad_kernel(const float* __restrict__ emb, int64_t lde, int d, int k,
                                                            const int64_t* __restrict__ heads,
                                                            const int64_t* __restrict__ rels,
@@ -194,32 +203,72 @@ __global__ __launch_bounds__(256) void transr_wgrad_kernel(const float* __restri
                                                            const float* __restrict__ grad_out,
                                                            float* __restrict__ d_rel, float* __restrict__ d_trans) {
   constexpr int kPer = 16;
+  extern __shared__ __attribute__((aligned(16))) float stage[];  // [kWgradStage][3d + 4k]
+  __shared__ int s_ids[256];
+  __shared__ int s_wcnt[4];
   const int r = blockIdx.x;
+  const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
   const int64_t dk = static_cast<int64_t>(d) * k;
   const int64_t e0 = static_cast<int64_t>(blockIdx.y) * 256 * kPer;
   const float scale = grad_out[0] / static_cast<float>(batch);
+  const int row_w = 3 * d + 4 * k;
   float acc[kPer];
+  int ei[kPer], ej[kPer];
 #pragma unroll
-  for (int t = 0; t < kPer; ++t) acc[t] = 0.f;
+  for (int t = 0; t < kPer; ++t) {
+    acc[t] = 0.f;
+    const int64_t e = e0 + static_cast<int64_t>(t) * 256 + tid;
+    ei[t] = e < dk ? static_cast<int>(e / k) : -1;
+    ej[t] = e < dk ? static_cast<int>(e % k) : 0;
+  }
   float racc = 0.f;
-  for (int b = 0; b < batch; ++b) {
-    if (rels[b] != r) continue;  // block-uniform
-    const float* g = gproj + static_cast<int64_t>(b) * 4 * k;
-    const float* eh = emb + heads[b] * lde;
-    const float* ep = emb + pos[b] * lde;
-    const float* en = emb + neg[b] * lde;
-#pragma unroll
-    for (int t = 0; t < kPer; ++t) {
-      const int64_t e = e0 + static_cast<int64_t>(t) * 256 + threadIdx.x;
-      if (e < dk) {
-        const int i = static_cast<int>(e / k), j = static_cast<int>(e % k);
-        float v = eh[i] * g[j];
-        v = fmaf(ep[i], g[k + j], v);
-        v = fmaf(en[i], g[2 * k + j], v);
-        acc[t] += v;
+  for (int w0 = 0; w0 < batch; w0 += 256) {
+    const int b = w0 + tid;
+    const bool hit = b < batch && rels[b] == r;
+    const uint64_t m = __ballot(hit);
+    if (lane == 0) s_wcnt[wv] = __popcll(m);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wv; ++w) base += s_wcnt[w];
+    const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    if (hit) s_ids[base + __popcll(m & ((1ull << lane) - 1ull))] = b;
+    __syncthreads();
+    for (int c0 = 0; c0 < total; c0 += kWgradStage) {
+      const int cnt = min(kWgradStage, total - c0);
+      for (int x = tid; x < cnt * row_w; x += 256) {
+        const int s = x / row_w, o = x - s * row_w;
+        const int bb = s_ids[c0 + s];
+        float v;
+        if (o < 3 * d) {
+          const int which = o / d, i = o - which * d;
+          const int64_t id = which == 0 ? heads[bb] : (which == 1 ? pos[bb] : neg[bb]);
+          v = emb[id * lde + i];
+        } else {
+          v = gproj[static_cast<int64_t>(bb) * 4 * k + (o - 3 * d)];
+        }
+        stage[x] = v;
       }
+      __syncthreads();
+      for (int s = 0; s < cnt; ++s) {
+        const float* eh = stage + s * row_w;
+        const float* ep = eh + d;
+        const float* en = ep + d;
+        const float* g = en + d;
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+          if (ei[t] >= 0) {
+            const int i = ei[t], j = ej[t];
+            float v = eh[i] * g[j];
+            v = fmaf(ep[i], g[k + j], v);
+            v = fmaf(en[i], g[2 * k + j], v);
+            acc[t] += v;
+          }
+        }
+        if (blockIdx.y == 0 && tid < k) racc += g[3 * k + tid];
+      }
+      __syncthreads();  // the stage is read before the next one overwrites it
     }
-    if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < k) racc += g[3 * k + threadIdx.x];
+    __syncthreads();  // s_ids / s_wcnt are read before the next window rewrites them
   }
 #pragma unroll
   for (int t = 0; t < kPer; ++t) {
@@ -265,7 +314,8 @@ extern "C" int kgat_transr_bwd_f32(const float* emb, int64_t ld_emb, int32_t d, 
   KGAT_LAUNCH_CHECK();
   const int64_t dk = static_cast<int64_t>(d) * k;
   const int ys = static_cast<int>((dk + 4095) / 4096);
-  hipLaunchKernelGGL(kgat::transr_wgrad_kernel, dim3(n_rel, ys), dim3(256), 0, st, emb, ld_emb, d, k, heads, rels, pos,
+  const size_t smem = sizeof(float) * kgat::kWgradStage * (3 * static_cast<size_t>(d) + 4 * static_cast<size_t>(k));
+  hipLaunchKernelGGL(kgat::transr_wgrad_kernel, dim3(n_rel, ys), dim3(256), smem, st, emb, ld_emb, d, k, heads, rels, pos,
                      neg, batch, work + off.gproj, grad_out, d_rel, d_trans);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;

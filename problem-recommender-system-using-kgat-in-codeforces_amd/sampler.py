@@ -23,10 +23,13 @@ class BatchSampler:
 
     def __init__(self, interaction_dict: Mapping[int, Sequence[int]], item_num: int, kg_heads: np.ndarray,
                  kg_rels: np.ndarray, kg_tails: np.ndarray, n_nodes: int, cf_batch_size: int = 256,
-                 kg_batch_size: int = 512, seed: int = 2024):
+                 kg_batch_size: int = 512, seed: int = 2024, pin_memory: bool = True):
         self.item_num, self.n_nodes = int(item_num), int(n_nodes)
         self._cf_batch_size, self._kg_batch_size = int(cf_batch_size), int(kg_batch_size)
         self.seed = int(seed)
+        # batches land in pinned host memory so the caller's .to(device, non_blocking=True) is a true
+        # async copy (a pageable source makes the copy wait for the device queue to drain)
+        self.pin_memory = bool(pin_memory) and torch.cuda.is_available()
         self._cf_step = self._kg_step = 0
         users = np.array(sorted(u for u, v in interaction_dict.items() if len(v)), np.int64)
         rows = [np.unique(np.asarray(interaction_dict[int(u)], np.int64)) for u in users]
@@ -58,19 +61,23 @@ class BatchSampler:
     def generate_cf_batch(self) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """(user_ids, positive_problem_ids, negative_problem_ids) -- LongTensors (preprocess.py:381-409)."""
         B = self._cf_batch_size
-        out = [np.empty(B, np.int64) for _ in range(3)]
+        out = self._buffers(3, B)
         self._cf_step += 1
         _lib.call("kgat_sample_cf_batch", self._cf_users.ctypes.data, self._cf_users.size, self._cf_rowptr.ctypes.data,
                   self._cf_items.ctypes.data, self.item_num, B, self.seed, self._cf_step,
-                  *[o.ctypes.data for o in out])
-        return tuple(torch.from_numpy(o) for o in out)
+                  *[o.data_ptr() for o in out])
+        return tuple(out)
+
+    def _buffers(self, k: int, B: int) -> list[torch.Tensor]:
+        # torch's pinned-memory cache keeps a block out of reuse until the copies reading it are done
+        return [torch.empty(B, dtype=torch.int64, pin_memory=self.pin_memory) for _ in range(k)]
 
     def generate_kg_batch(self) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
         """(heads, relations, positive_tails, negative_tails) (preprocess.py:486-525; LongTensors)."""
         B = self._kg_batch_size
-        out = [np.empty(B, np.int64) for _ in range(4)]
+        out = self._buffers(4, B)
         self._kg_step += 1
         _lib.call("kgat_sample_kg_batch", self._kg_heads.ctypes.data, self._kg_heads.size, self._kg_rowptr.ctypes.data,
                   self._kg_rel_tail.ctypes.data, self.n_nodes, B, self.seed, self._kg_step,
-                  *[o.ctypes.data for o in out])
-        return tuple(torch.from_numpy(o) for o in out)
+                  *[o.data_ptr() for o in out])
+        return tuple(out)
