@@ -334,11 +334,16 @@ int kgat_transr_fwd_f32(const float *emb, int64_t ld_emb, const float *rel_emb, 
                         const int64_t *neg, int32_t batch, float reg, float *loss, float *work, void *stream);
 /* a5 backward: d_emb[id] += (upstream * dL/de) for every gathered id (duplicates
  * summed in slot order; d_emb must be initialised, e.g. zero), d_rel [n_rel, k]
- * and d_trans [n_rel, d, k] overwritten (per-relation reduction in batch order). */
+ * and d_trans [n_rel, d, k] overwritten: each relation's samples (batch order) are
+ * cut into 32-sample chunks, one block per chunk sums its chunk in order, and the
+ * chunk partials are summed in chunk order -- deterministic, balanced when a few
+ * relations (the CKG's interaction pair) hold most samples.  workspace: float
+ * [kgat_transr_bwd_workspace_floats(batch, d, k, n_rel)]. */
+int64_t kgat_transr_bwd_workspace_floats(int32_t batch, int32_t d, int32_t k, int32_t n_rel);
 int kgat_transr_bwd_f32(const float *emb, int64_t ld_emb, int32_t d, int32_t k, const int64_t *heads,
                         const int64_t *rels, const int64_t *pos, const int64_t *neg, int32_t batch, int32_t n_rel,
                         const float *work, const float *grad_out, float *d_emb, int64_t ld_demb, float *d_rel,
-                        float *d_trans, void *stream);
+                        float *d_trans, float *workspace, int64_t workspace_floats, void *stream);
 
 /* a6 -- knowledge-aware edge scores (model.py:263-316, multi_head_attention.py:35-58):
  * logit_e = sum_j tanh(LN(W_o drop(W_v (e_t W_r) + b_v) + b_o))_j * edge_weight[e]

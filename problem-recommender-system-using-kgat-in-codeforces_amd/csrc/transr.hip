@@ -51,8 +51,21 @@ __global__ __launch_bounds__(256) void transr_fwd_kernel(const float* __restrict
   float h[kMaxCols], tp[kMaxCols], tn[kMaxCols], er[kMaxCols];
 #pragma unroll
   for (int cc = 0; cc < kMaxCols; ++cc) h[cc] = tp[cc] = tn[cc] = er[cc] = 0.f;
+  // the three gathered rows in registers (lane l holds element l + 64*ic), broadcast by
+  // shuffles in the loop below: no dependent global load per step of i
+  float rh[kMaxCols], rp[kMaxCols], rn[kMaxCols];
+#pragma unroll
+  for (int ic = 0; ic < kMaxCols; ++ic) {
+    const int i = lane + 64 * ic;
+    rh[ic] = i < d ? eh[i] : 0.f;
+    rp[ic] = i < d ? ep[i] : 0.f;
+    rn[ic] = i < d ? en[i] : 0.f;
+  }
   for (int i = 0; i < d; ++i) {
-    const float xh = eh[i], xp = ep[i], xn = en[i];
+    const int ic = i >> 6, src = i & 63;
+    const float xh = __shfl(ic == 0 ? rh[0] : ic == 1 ? rh[1] : ic == 2 ? rh[2] : rh[3], src);
+    const float xp = __shfl(ic == 0 ? rp[0] : ic == 1 ? rp[1] : ic == 2 ? rp[2] : rp[3], src);
+    const float xn = __shfl(ic == 0 ? rn[0] : ic == 1 ? rn[1] : ic == 2 ? rn[2] : rn[3], src);
 #pragma unroll
     for (int cc = 0; cc < kMaxCols; ++cc) {
       const int j = lane + 64 * cc;
@@ -181,18 +194,24 @@ __global__ __launch_bounds__(256) void transr_scatter_kernel(const int64_t* __re
   }
 }
 
-// Per relation r (blockIdx.x) and a 4096-entry slice of trans[r]
-// (blockIdx.y): d trans[r][i][j] = scale * sum over samples of relation r, in
+// Per relation r (blockIdx.x) and a slice of 16 * (256 / k) rows of trans[r]
+// (blockIdx.y; thread: column j = tid % k, 16 consecutive rows): d trans[r][i][j] = scale * sum over samples of relation r, in
 // batch order, of e_h[i] g_h'[j] + e_t+[i] g_t+'[j] + e_t-[i] g_t-'[j];
 // slice 0 also produces d rel_emb[r] = scale * sum g_er.
 // The block lists relation r's samples first (256 relation ids per pass,
-// ballot + wave counts -> batch order), then stages kWgradStage of them at a
+// ballot + wave counts -> batch order), then stages wgrad_stage(d, k) of them at a
 // time in LDS -- the three table rows and the four projected gradients, every
 // load of the stage in flight at once -- so the per-sample accumulation reads
 // LDS instead of waiting on a chain of dependent global loads per sample (the
 // former sample-serial loop was latency-bound: 1.6 ms per call at B = 512).
 // Per entry the samples are summed in batch order with the same fma chain.
-constexpr int kWgradStage = 8;
+constexpr int kWgradChunk = 32;          // samples of one relation per block (list positions)
+constexpr int kWgradStageMax = 32;       // samples staged per round (at most)
+constexpr int kWgradLdsFloats = 14336;   // 56 KB of staged rows per block
+__host__ __device__ inline int wgrad_stage(int d, int k) {
+  const int n = kWgradLdsFloats / (3 * d + 4 * k);
+  return n < 1 ? 1 : (n > kWgradStageMax ? kWgradStageMax : n);
+}
 
 __global__ __launch_bounds__(256) void transr_wgrad_kernel(const float* __restrict__ emb, int64_t lde, int d, int k,
                                                            const int64_t* __restrict__ heads,
@@ -200,53 +219,83 @@ __global__ __launch_bounds__(256) void transr_wgrad_kernel(const float* __restri
                                                            const int64_t* __restrict__ pos,
                                                            const int64_t* __restrict__ neg, int batch,
                                                            const float* __restrict__ gproj,
-                                                           const float* __restrict__ grad_out,
-                                                           float* __restrict__ d_rel, float* __restrict__ d_trans) {
+                                                           float* __restrict__ part, int* __restrict__ counts,
+                                                           int n_chunk) {
   constexpr int kPer = 16;
-  extern __shared__ __attribute__((aligned(16))) float stage[];  // [kWgradStage][3d + 4k]
-  __shared__ int s_ids[256];
+  extern __shared__ __attribute__((aligned(16))) float stage[];  // [wgrad_stage(d, k)][3d + 4k]
+  __shared__ int s_ids[kWgradChunk];
+  __shared__ int s_seen;
   __shared__ int s_wcnt[4];
+  __shared__ int64_t s_row[3 * kWgradStageMax];
   const int r = blockIdx.x;
   const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
   const int64_t dk = static_cast<int64_t>(d) * k;
-  const int64_t e0 = static_cast<int64_t>(blockIdx.y) * 256 * kPer;
-  const float scale = grad_out[0] / static_cast<float>(batch);
   const int row_w = 3 * d + 4 * k;
+  const int stage_n = wgrad_stage(d, k);
+  // this thread's entries: column j = tid % k, rows [i0, i0 + kPer) of the block's row slice
+  const int nrb = 256 / k;                       // row blocks per slice (k <= 256)
+  const bool active = tid < nrb * k;
+  const int j = active ? tid % k : 0;
+  const int i0 = blockIdx.y * nrb * kPer + (active ? tid / k : 0) * kPer;
+  const bool vec = (d % 4 == 0) && (k % 4 == 0);  // 16-byte aligned staged rows
   float acc[kPer];
-  int ei[kPer], ej[kPer];
 #pragma unroll
-  for (int t = 0; t < kPer; ++t) {
-    acc[t] = 0.f;
-    const int64_t e = e0 + static_cast<int64_t>(t) * 256 + tid;
-    ei[t] = e < dk ? static_cast<int>(e / k) : -1;
-    ej[t] = e < dk ? static_cast<int>(e % k) : 0;
-  }
+  for (int t = 0; t < kPer; ++t) acc[t] = 0.f;
   float racc = 0.f;
+  // relation r's samples in batch order; this block takes list positions [z*C, (z+1)*C)
+  const int z = blockIdx.z, lo = z * kWgradChunk;
+  if (tid == 0) s_seen = 0;
+  __syncthreads();
   for (int w0 = 0; w0 < batch; w0 += 256) {
     const int b = w0 + tid;
     const bool hit = b < batch && rels[b] == r;
     const uint64_t m = __ballot(hit);
     if (lane == 0) s_wcnt[wv] = __popcll(m);
     __syncthreads();
-    int base = 0;
+    int base = s_seen;
     for (int w = 0; w < wv; ++w) base += s_wcnt[w];
-    const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
-    if (hit) s_ids[base + __popcll(m & ((1ull << lane) - 1ull))] = b;
+    const int li = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (hit && li >= lo && li < lo + kWgradChunk) s_ids[li - lo] = b;
     __syncthreads();
-    for (int c0 = 0; c0 < total; c0 += kWgradStage) {
-      const int cnt = min(kWgradStage, total - c0);
-      for (int x = tid; x < cnt * row_w; x += 256) {
-        const int s = x / row_w, o = x - s * row_w;
+    if (tid == 0) s_seen += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    __syncthreads();
+  }
+  const int n_r = s_seen;
+  if (z == 0 && blockIdx.y == 0 && tid == 0) counts[r] = n_r;
+  const int total = min(kWgradChunk, n_r - lo);
+  if (total <= 0) return;  // block-uniform: this chunk holds no sample
+  {
+    for (int c0 = 0; c0 < total; c0 += stage_n) {
+      const int cnt = min(stage_n, total - c0);
+      if (tid < 3 * cnt) {  // the stage's table-row offsets: one dependent load, once
+        const int s = tid / 3, which = tid - 3 * s;
         const int bb = s_ids[c0 + s];
-        float v;
-        if (o < 3 * d) {
-          const int which = o / d, i = o - which * d;
-          const int64_t id = which == 0 ? heads[bb] : (which == 1 ? pos[bb] : neg[bb]);
-          v = emb[id * lde + i];
-        } else {
-          v = gproj[static_cast<int64_t>(bb) * 4 * k + (o - 3 * d)];
+        s_row[tid] = (which == 0 ? heads[bb] : (which == 1 ? pos[bb] : neg[bb])) * lde;
+      }
+      __syncthreads();
+      // kUnroll independent loads in flight per thread and pass
+      constexpr int kUnroll = 8;
+      for (int x0 = 0; x0 < cnt * row_w; x0 += 256 * kUnroll) {
+        float v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int x = x0 + u * 256 + tid;
+          v[u] = 0.f;
+          if (x < cnt * row_w) {
+            const int s = x / row_w, o = x - s * row_w;
+            if (o < 3 * d) {
+              const int which = o / d;
+              v[u] = emb[s_row[3 * s + which] + (o - which * d)];
+            } else {
+              v[u] = gproj[static_cast<int64_t>(s_ids[c0 + s]) * 4 * k + (o - 3 * d)];
+            }
+          }
         }
-        stage[x] = v;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int x = x0 + u * 256 + tid;
+          if (x < cnt * row_w) stage[x] = v[u];
+        }
       }
       __syncthreads();
       for (int s = 0; s < cnt; ++s) {
@@ -254,28 +303,68 @@ __global__ __launch_bounds__(256) void transr_wgrad_kernel(const float* __restri
         const float* ep = eh + d;
         const float* en = ep + d;
         const float* g = en + d;
+        if (blockIdx.y == 0 && tid < k) racc += g[3 * k + tid];
+        if (!active || i0 >= d) continue;  // this thread's rows lie past d
+        const float gh = g[j], gpp = g[k + j], gn = g[2 * k + j];
+        float xh[kPer], xp[kPer], xn[kPer];
+        if (vec) {
 #pragma unroll
-        for (int t = 0; t < kPer; ++t) {
-          if (ei[t] >= 0) {
-            const int i = ei[t], j = ej[t];
-            float v = eh[i] * g[j];
-            v = fmaf(ep[i], g[k + j], v);
-            v = fmaf(en[i], g[2 * k + j], v);
-            acc[t] += v;
+          for (int t = 0; t < kPer; t += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(eh + i0 + t);
+            const float4 b = *reinterpret_cast<const float4*>(ep + i0 + t);
+            const float4 c = *reinterpret_cast<const float4*>(en + i0 + t);
+            xh[t] = a.x; xh[t + 1] = a.y; xh[t + 2] = a.z; xh[t + 3] = a.w;
+            xp[t] = b.x; xp[t + 1] = b.y; xp[t + 2] = b.z; xp[t + 3] = b.w;
+            xn[t] = c.x; xn[t + 1] = c.y; xn[t + 2] = c.z; xn[t + 3] = c.w;
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < kPer; ++t) {
+            const int i = i0 + t < d ? i0 + t : 0;
+            xh[t] = eh[i];
+            xp[t] = ep[i];
+            xn[t] = en[i];
           }
         }
-        if (blockIdx.y == 0 && tid < k) racc += g[3 * k + tid];
+#pragma unroll
+        for (int t = 0; t < kPer; ++t) {
+          float v = xh[t] * gh;
+          v = fmaf(xp[t], gpp, v);
+          v = fmaf(xn[t], gn, v);
+          acc[t] += v;
+        }
       }
       __syncthreads();  // the stage is read before the next one overwrites it
     }
-    __syncthreads();  // s_ids / s_wcnt are read before the next window rewrites them
   }
+  // this chunk's partial sums: part[(r * n_chunk + z)] = [trans rows (d*k) | rel (k)]
+  float* pz = part + (static_cast<int64_t>(r) * n_chunk + z) * (dk + k);
+  if (active) {
 #pragma unroll
-  for (int t = 0; t < kPer; ++t) {
-    const int64_t e = e0 + static_cast<int64_t>(t) * 256 + threadIdx.x;
-    if (e < dk) d_trans[static_cast<int64_t>(r) * dk + e] = acc[t] * scale;
+    for (int t = 0; t < kPer; ++t)
+      if (i0 + t < d) pz[static_cast<int64_t>(i0 + t) * k + j] = acc[t];
   }
-  if (blockIdx.y == 0 && static_cast<int>(threadIdx.x) < k) d_rel[static_cast<int64_t>(r) * k + threadIdx.x] = racc * scale;
+  if (blockIdx.y == 0 && tid < k) pz[dk + tid] = racc;
+}
+
+// d trans[r] / d rel_emb[r] = scale * (sum of relation r's chunk partials in chunk order)
+__global__ __launch_bounds__(256) void transr_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                  const int* __restrict__ counts, int n_rel, int d,
+                                                                  int k, int n_chunk, int batch,
+                                                                  const float* __restrict__ grad_out,
+                                                                  float* __restrict__ d_rel,
+                                                                  float* __restrict__ d_trans) {
+  const int64_t dk = static_cast<int64_t>(d) * k, w = dk + k;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= n_rel * w) return;
+  const int r = static_cast<int>(idx / w);
+  const int64_t e = idx - r * w;
+  const int nz = (counts[r] + kWgradChunk - 1) / kWgradChunk;
+  float s = 0.f;
+  for (int z = 0; z < nz; ++z) s += part[(static_cast<int64_t>(r) * n_chunk + z) * w + e];
+  const float v = s * (grad_out[0] / static_cast<float>(batch));
+  if (e < dk) d_trans[r * dk + e] = v;
+  else d_rel[static_cast<int64_t>(r) * k + (e - dk)] = v;
 }
 
 }  // namespace kgat
@@ -299,24 +388,39 @@ extern "C" int kgat_transr_fwd_f32(const float* emb, int64_t ld_emb, const float
   return KGAT_OK;
 }
 
+extern "C" int64_t kgat_transr_bwd_workspace_floats(int32_t batch, int32_t d, int32_t k, int32_t n_rel) {
+  if (batch <= 0 || d <= 0 || k <= 0 || n_rel <= 0) return -1;
+  const int64_t n_chunk = (batch + kgat::kWgradChunk - 1) / kgat::kWgradChunk;
+  return static_cast<int64_t>(n_rel) * n_chunk * (static_cast<int64_t>(d) * k + k) + n_rel;  // partials + counts
+}
+
 extern "C" int kgat_transr_bwd_f32(const float* emb, int64_t ld_emb, int32_t d, int32_t k, const int64_t* heads,
                                    const int64_t* rels, const int64_t* pos, const int64_t* neg, int32_t batch,
                                    int32_t n_rel, const float* work, const float* grad_out, float* d_emb,
-                                   int64_t ld_demb, float* d_rel, float* d_trans, void* stream) {
+                                   int64_t ld_demb, float* d_rel, float* d_trans, float* workspace,
+                                   int64_t workspace_floats, void* stream) {
   if (!emb || !heads || !rels || !pos || !neg || !work || !grad_out || !d_emb || !d_rel || !d_trans || batch <= 0 ||
       n_rel <= 0)
     return KGAT_ERR_INVALID;
   if (d <= 0 || k <= 0 || d > 256 || k > 256 || ld_emb < d || ld_demb < d) return KGAT_ERR_INVALID;
+  if (!workspace || workspace_floats < kgat_transr_bwd_workspace_floats(batch, d, k, n_rel)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const kgat::TransrWork off = kgat::TransrWork::at(batch, d, k);
   hipLaunchKernelGGL(kgat::transr_scatter_kernel, dim3((3 * batch + 3) / 4), dim3(256), 0, st, heads, pos, neg, batch,
                      d, work + off.grow, grad_out, d_emb, ld_demb);
   KGAT_LAUNCH_CHECK();
-  const int64_t dk = static_cast<int64_t>(d) * k;
-  const int ys = static_cast<int>((dk + 4095) / 4096);
-  const size_t smem = sizeof(float) * kgat::kWgradStage * (3 * static_cast<size_t>(d) + 4 * static_cast<size_t>(k));
-  hipLaunchKernelGGL(kgat::transr_wgrad_kernel, dim3(n_rel, ys), dim3(256), smem, st, emb, ld_emb, d, k, heads, rels, pos,
-                     neg, batch, work + off.gproj, grad_out, d_rel, d_trans);
+  const int n_chunk = (batch + kgat::kWgradChunk - 1) / kgat::kWgradChunk;
+  const int64_t w = static_cast<int64_t>(d) * k + k;
+  float* part = workspace;
+  int* counts = reinterpret_cast<int*>(workspace + static_cast<int64_t>(n_rel) * n_chunk * w);
+  const int ys = (d + (256 / k) * 16 - 1) / ((256 / k) * 16);  // row slices of 16 rows per thread
+  const size_t smem = sizeof(float) * kgat::wgrad_stage(d, k) * (3 * static_cast<size_t>(d) + 4 * static_cast<size_t>(k));
+  hipLaunchKernelGGL(kgat::transr_wgrad_kernel, dim3(n_rel, ys, n_chunk), dim3(256), smem, st, emb, ld_emb, d, k, heads,
+                     rels, pos, neg, batch, work + off.gproj, part, counts, n_chunk);
+  KGAT_LAUNCH_CHECK();
+  const int64_t total = static_cast<int64_t>(n_rel) * w;
+  hipLaunchKernelGGL(kgat::transr_wgrad_reduce_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
+                     st, part, counts, n_rel, d, k, n_chunk, batch, grad_out, d_rel, d_trans);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -717,9 +717,14 @@ def transr_bwd(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out):
     d_emb = zeros(emb.shape, dev)
     d_rel = torch.empty(n_rel, k, dtype=torch.float32, device=dev)
     d_trans = torch.empty(n_rel, d, k, dtype=torch.float32, device=dev)
+    ws_n = int(_lib.lib().kgat_transr_bwd_workspace_floats(heads.numel(), d, k, n_rel))
+    if ws_n < 0:
+        raise ValueError("transr_bwd: bad shape")
+    ws = torch.empty(ws_n, dtype=torch.float32, device=dev)
     _lib.call("kgat_transr_bwd_f32", emb.data_ptr(), _ld(emb), d, k, heads.data_ptr(), rels.data_ptr(),
               pos.data_ptr(), neg.data_ptr(), heads.numel(), n_rel, work.data_ptr(), grad_out.data_ptr(),
-              d_emb.data_ptr(), _ld(d_emb), d_rel.data_ptr(), d_trans.data_ptr(), stream_ptr(dev))
+              d_emb.data_ptr(), _ld(d_emb), d_rel.data_ptr(), d_trans.data_ptr(), ws.data_ptr(), ws.numel(),
+              stream_ptr(dev))
     return d_emb, d_rel, d_trans
 
 

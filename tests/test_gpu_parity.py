@@ -668,6 +668,33 @@ def test_kg_train_steps_vs_reference(pkg, case):
             np.testing.assert_allclose(named[k[9:]].detach().cpu().numpy(), v, rtol=RTOL, atol=ADAM_ATOL, err_msg=k)
 
 
+@pytest.mark.parametrize("dim,batch,n_rel", [(64, 512, 10), (64, 700, 3), (256, 300, 10), (32, 1, 4)])
+def test_kg_step_synthetic_vs_oracle(pkg, dim, batch, n_rel):
+    """TransR loss and every gradient vs the oracle at batch sizes that cross the weight-gradient
+    kernel's 256-sample windows and LDS stages (d = 256 stages 6 samples, d = 64 16), with
+    repeated ids and relations holding no sample."""
+    n = 3000
+    torch.manual_seed(dim + batch)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=100, entity_num=n - 100, relation_num=n_rel, cf_embedding_dim=dim,
+                              kg_embedding_dim=dim, layer_size=[dim]))
+    init = {k: v.clone() for k, v in m.state_dict().items() if not v.is_sparse}
+    m.to(DEV)
+    rng = np.random.default_rng(batch)
+    rel_hi = max(1, n_rel - 1)  # the last relation gets no sample
+    ids = [torch.from_numpy(rng.integers(0, hi, batch)) for hi in (200, rel_hi, 200, n)]
+    loss = m(*[t.to(DEV) for t in ids], mode=pkg.KGATMode.TRAIN_KG)
+    loss.backward()
+    P = {k: v.clone().requires_grad_(True) for k, v in init.items()}
+    ref = K.transr_loss(P, *ids)
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5)
+    for k, prm in m.named_parameters():
+        if prm.grad is None or P[k].grad is None:
+            continue
+        np.testing.assert_allclose(prm.grad.cpu().numpy(), P[k].grad.numpy(), rtol=RTOL, atol=1e-6, err_msg=k)
+    assert float(m._trans_matrix.grad[n_rel - 1].abs().max()) == 0.0 or n_rel == 1
+
+
 def _refreshed_model(pkg, g):
     m = _model_from_golden(pkg, g)
     _load_params(m, g, ["init/", "after_cf/", "after_kg/"])
