@@ -168,11 +168,14 @@ int kgat_rows_merge_f32(const int32_t *lists, const int32_t *counts, int32_t G, 
  * [d_out, d_in].  dropout_p in [0,1); the keep mask is a counter hash of
  * (seed, row, column), regenerated by the backward.  d_in, d_out in
  * {16, 32, 64, 128}.
- * norm_out / mask_out (both or neither; d_out <= 64): the saved state the
- * backward uses instead of recomputing the forward -- norm_out float [n_rows]
- * (the row L2 norm, -eps where F.normalize's clamp was active) and mask_out
- * uint64 [ceil(n_rows/16) * 64] (per 16-row sub-tile and lane: 3 bits per
- * output element -- pre_sum > 0, pre_mul > 0, dropout keep). */
+ * norm_out / mask_out (both or neither): the saved state the backward uses
+ * instead of recomputing the forward -- norm_out float [n_rows] (the row L2
+ * norm, -eps where F.normalize's clamp was active) and mask_out uint64
+ * [ceil(n_rows/16) * NG * 64], NG = ceil(d_out/64) (per 16-row sub-tile st,
+ * word group g = 16-column block / 4 and lane: word (st*NG + g)*64 + lane
+ * holds 3 bits per output element -- pre_sum > 0, pre_mul > 0, dropout keep).
+ * d_out <= 64 (NG = 1) feeds kgat_biinter_bwd_f32 / _hop_f32; d_out = 128
+ * feeds kgat_biinter_bwd_gemm_bits_f32 (then node0 = 0). */
 int kgat_biinter_fwd_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *W1,
                          const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
                          int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
@@ -256,6 +259,18 @@ int kgat_biinter_bwd_gemm_f32(const float *X, int64_t ldx, const float *S, int64
                               float *db1, float *dW2, float *db2, int64_t n_rows, int32_t d_in, int32_t d_out,
                               float dropout_p, uint64_t seed, const int32_t *key_rows, float *work,
                               int64_t work_floats, void *stream);
+/* The same backward from the fused forward's saved state (kgat_biinter_fwd_f32's
+ * norm_out / mask_out, d_out <= 128, indexed by node = key_rows[i] or i) instead of
+ * pre-activations: C4's 128 -> 128 / 128 -> 64 layers run the fused MFMA forward
+ * (no [n, 2*d_out] pre-activation state written) and this GEMM backward.
+ * work: float [kgat_biinter_gemm_bits_work_floats]. */
+int64_t kgat_biinter_gemm_bits_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out);
+int kgat_biinter_bwd_gemm_bits_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
+                                   int64_t ldh, const float *norm, const uint64_t *mask, const float *dH,
+                                   int64_t lddh, const float *W1, const float *W2, float *dXd, int64_t lddxd,
+                                   float *dS, int64_t ldds, float *dW1, float *db1, float *dW2, float *db2,
+                                   int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p,
+                                   const int32_t *key_rows, float *work, int64_t work_floats, void *stream);
 
 /* §8(f)2 -- CF / KG batch samplers (host, src/model/KGAT/preprocess.py:328-525).
  * CF: `batch` users from users[0..n_users) (distinct when batch <= n_users, in random

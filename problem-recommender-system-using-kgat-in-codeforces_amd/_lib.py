@@ -119,6 +119,10 @@ _SIGNATURES = {
     "kgat_biinter_bwd_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp,
                                                  c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                                  c_i32, c_f32, c_u64, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_biinter_gemm_bits_work_floats": (c_i64, [c_i64, c_i32, c_i32]),
+    "kgat_biinter_bwd_gemm_bits_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                                      c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                                      c_i64, c_i32, c_i32, c_f32, c_vp, c_vp, c_i64, c_vp]),
     "kgat_sample_cf_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
     "kgat_nfm_batch_work_bytes": (c_i64, [c_i64]),
     "kgat_nfm_batch_rowptr": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),

@@ -123,8 +123,10 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
   const int64_t r0 = st * 16;
   float g[B::NCB][4];
   float sq[4] = {0.f, 0.f, 0.f, 0.f};
-  uint64_t word = 0;  // saved state: 3 bits per (cb, i) -- pre_sum > 0, pre_mul > 0, kept
   constexpr int NG = (B::NCB + 3) / 4;
+  uint64_t word[NG];  // saved state, word g: 3 bits per (cb in [4g, 4g+4), i) -- pre_sum > 0, pre_mul > 0, kept
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) word[gi] = 0;
   uint64_t dh_[4][NG];
   if (p > 0.f) {
 #pragma unroll
@@ -146,13 +148,15 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
         keep = bi_drop_keep(dh_[i][cb / 4], cb, thr);
         v = keep ? v * scale : 0.f;
       }
-      if (B::NCB * 12 <= 64)
-        word |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << ((cb * 4 + i) * 3);
+      word[cb / 4] |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << (((cb & 3) * 4 + i) * 3);
       g[cb][i] = v;
       sq[i] = fmaf(v, v, sq[i]);
     }
   }
-  if (mask_out != nullptr) mask_out[st * 64 + lane] = word;
+  if (mask_out != nullptr) {
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) mask_out[(st * NG + gi) * 64 + lane] = word[gi];
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float nrm = sqrtf(sum16(sq[i]));
@@ -168,8 +172,16 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
   }
 }
 
-template <int DIN, int DOUT, bool PF, int MINW>
-__global__ __launch_bounds__(256, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
+// Waves per block of the standalone forward: 4, or 8 where the two staged W
+// copies leave room for one block per CU only (128 -> 128: 135 KB of LDS), so
+// that one block still puts two waves on every SIMD.
+template <int DIN, int DOUT>
+struct BiFwdWaves {
+  static constexpr int k = 2 * DOUT * (DIN + 4) * 4 > 80 * 1024 ? 8 : 4;
+};
+
+template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
@@ -193,8 +205,8 @@ __global__ __launch_bounds__(256, MINW) void biinter_fwd_kernel(const float* __r
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t thr = bi_drop_threshold(p);
   const int64_t nsub = (n + 15) / 16;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
-  int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * NWV;
+  int64_t st = static_cast<int64_t>(blockIdx.x) * NWV + (threadIdx.x >> 6);
   // PF: the next sub-tile's rows are loaded while the current one computes
   float nx[B::KQ], ns[B::KQ];
   if (PF) {
@@ -1019,10 +1031,11 @@ static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
     const char* e = getenv("KGAT_FWD_VARIANT");
     variant = e ? atoi(e) : 8;
   }
-  const int grid = blocks_for(n, 64, (variant & 2) ? kCUs * 4 : kCUs * 8);
+  constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
+  const int grid = blocks_for(n, 16 * NWV, ((variant & 2) ? kCUs * 4 : kCUs * 8) * 4 / NWV);
 #define KGAT_FWD_LAUNCH(PF, W)                                                                                   \
-  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, PF, W>), dim3(grid), dim3(256), 0, st, X, ldx, S, lds, W1, b1, \
-                     W2, b2, H, ldh, n, p, seed, norm, mask, node0)
+  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, PF, W, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S,   \
+                     lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, node0)
   switch (variant & 12) {
     case 4: KGAT_FWD_LAUNCH(true, 4); break;
     case 8: KGAT_FWD_LAUNCH(false, 2); break;
@@ -1174,7 +1187,8 @@ extern "C" int kgat_biinter_fwd_rows_f32(const float* X, int64_t ldx, const floa
   if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
-  if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 64)) return KGAT_ERR_INVALID;
+  if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 128)) return KGAT_ERR_INVALID;
+  if (mask_out != nullptr && d_out > 64 && node0 != 0) return KGAT_ERR_INVALID;  // multi-word state: whole tables
   if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_FWD_CALL(a, b) kgat::launch_fwd<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, seed, \

@@ -130,6 +130,45 @@ __global__ __launch_bounds__(256) void epi_bwd_kernel(float* __restrict__ P1, fl
   }
 }
 
+// one wave per row: dA, dB from H, dH and the fused forward's saved state (row
+// norm + per-element pre_sum > 0 / pre_mul > 0 / keep bits, kgat_biinter_fwd_f32's
+// mask_out layout, indexed by node = key) instead of the pre-activations
+__global__ __launch_bounds__(256) void epi_bwd_bits_kernel(float* __restrict__ dA, float* __restrict__ dB,
+                                                           const float* __restrict__ H, int64_t ldh,
+                                                           const float* __restrict__ norm,
+                                                           const uint64_t* __restrict__ mask,
+                                                           const float* __restrict__ dH, int64_t lddh, int64_t n,
+                                                           int dout, float p, const int32_t* __restrict__ key_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int64_t key = key_rows ? static_cast<int64_t>(key_rows[r]) : r;
+  if (key < 0) {  // padding row: zero gradient
+    for (int c = lane; c < dout; c += 64) dA[r * dout + c] = dB[r * dout + c] = 0.f;
+    return;
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  float dot = 0.f;
+  for (int c = lane; c < dout; c += 64) dot = fmaf(H[r * ldh + c], dH[r * lddh + c], dot);
+  dot = wave_sum(dot);
+  const float nr = norm[key];
+  const bool clamped = nr < 0.f;
+  const float inv = clamped ? 1.f / kNormEps : 1.f / nr;
+  const float proj = clamped ? 0.f : dot;
+  const int ng = (dout / 16 + 3) / 4;
+  const int64_t st = key >> 4;
+  const int q = static_cast<int>(key & 15) >> 2, i = static_cast<int>(key & 3);
+  for (int c = lane; c < dout; c += 64) {
+    const int cb = c >> 4;
+    const uint64_t w = mask[(st * ng + (cb >> 2)) * 64 + q * 16 + (c & 15)];
+    const uint32_t bits = static_cast<uint32_t>(w >> (((cb & 3) * 4 + i) * 3)) & 7u;
+    float dg = (dH[r * lddh + c] - H[r * ldh + c] * proj) * inv;
+    dg = (bits & 4u) ? dg * scale : 0.f;
+    dA[r * dout + c] = (bits & 1u) ? dg : dg * kLeakySlope;
+    dB[r * dout + c] = (bits & 2u) ? dg : dg * kLeakySlope;
+  }
+}
+
 // in place: (du, dm) in (dXd, dS) -> dXd = du + dm*S, dS = du + dm*X
 __global__ __launch_bounds__(256) void dxs_kernel(float* __restrict__ dXd, int64_t lda, float* __restrict__ dS,
                                                   int64_t ldb, const float* __restrict__ X, int64_t ldx,
@@ -172,6 +211,64 @@ static rocblas_handle blas_handle(hipStream_t st, int* err) {
   do {                                                   \
     if ((call) != rocblas_status_success) return KGAT_ERR_INVALID; \
   } while (0)
+
+}  // namespace kgat
+
+namespace kgat {
+
+static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d_in, int32_t d_out, hipStream_t st) {
+  for (auto [ptr, count] : {std::pair<float*, size_t>{dW1, size_t(d_in) * d_out}, {dW2, size_t(d_in) * d_out},
+                            {db1, size_t(d_out)}, {db2, size_t(d_out)}})
+    if (hipError_t e = hipMemsetAsync(ptr, 0, sizeof(float) * count, st); e != hipSuccess) return static_cast<int>(e);
+  return KGAT_OK;
+}
+
+// du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, [dW | db] = dA^T [U | 1]
+// (split-K over row chunks, slabs summed in chunk order); U, M and the slabs live in work.
+static int bwd_gemm_tail(rocblas_handle h, const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                         const float* W2, const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS,
+                         int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
+                         int32_t d_out, float* work, hipStream_t st) {
+  const float one = 1.f, zero = 0.f;
+  const int ldu = d_in + 4;
+  float* U = work;
+  float* M = work + n * ldu;
+  const int64_t nb = wslab_count(n);
+  float* slab1 = work + 2 * n * ldu;
+  float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
+  // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
+                          W1, d_in, dA, d_out, &zero, dXd, static_cast<int>(lddxd)));
+  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
+                          W2, d_in, dB, d_out, &zero, dS, static_cast<int>(ldds)));
+  hipLaunchKernelGGL(um_kernel, dim3(blocks_for(n * (d_in / 4 + 1), 256, kCUs * 8)), dim3(256), 0,
+                     st, X, ldx, S, lds, U, M, n, d_in);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
+                     lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
+  KGAT_LAUNCH_CHECK();
+  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order)
+  //   column-major C_b[ldu, d_out] = U'_b-view[ldu, k] x dA_b-view^T[k, d_out]
+  const int64_t full = n / kGemmChunk, rest = n - full * kGemmChunk;
+  for (int mat = 0; mat < 2; ++mat) {
+    const float* Um = mat == 0 ? U : M;
+    const float* G = mat == 0 ? dA : dB;
+    float* sl = mat == 0 ? slab1 : slab2;
+    if (full > 0)
+      KGAT_BLAS(rocblas_sgemm_strided_batched(
+          h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(kGemmChunk), &one,
+          Um, ldu, kGemmChunk * ldu, G, d_out, kGemmChunk * d_out, &zero, sl, ldu,
+          static_cast<int64_t>(ldu) * d_out, static_cast<int>(full)));
+    if (rest > 0)
+      KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(rest),
+                              &one, Um + full * kGemmChunk * ldu, ldu, G + full * kGemmChunk * d_out, d_out,
+                              &zero, sl + full * ldu * static_cast<int64_t>(d_out), ldu));
+    hipLaunchKernelGGL(wslab_reduce_kernel, dim3((d_out * (d_in + 1) + 255) / 256), dim3(256), 0, st, sl,
+                       static_cast<int>(nb), d_in, d_out, mat == 0 ? dW1 : dW2, mat == 0 ? db1 : db2);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
 
 }  // namespace kgat
 
@@ -243,55 +340,46 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
   int err = 0;
   rocblas_handle h = kgat::blas_handle(st, &err);
   if (err) return err;
-  const float one = 1.f, zero = 0.f;
-  if (n == 0) {  // no rows: zero weight gradients
-    for (auto [ptr, count] : {std::pair<float*, size_t>{dW1, size_t(d_in) * d_out}, {dW2, size_t(d_in) * d_out},
-                              {db1, size_t(d_out)}, {db2, size_t(d_out)}})
-      if (hipError_t e = hipMemsetAsync(ptr, 0, sizeof(float) * count, st); e != hipSuccess) return static_cast<int>(e);
-    return KGAT_OK;
-  }
+  if (n == 0) return kgat::zero_wgrads(dW1, db1, dW2, db2, d_in, d_out, st);
   float* dA = state;
   float* dB = state + n * d_out;
   const float* norm = state + 2 * n * d_out;
-  const int ldu = d_in + 4;
-  float* U = work;
-  float* M = work + n * ldu;
-  const int64_t nb = kgat::wslab_count(n);
-  float* slab1 = work + 2 * n * ldu;
-  float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   hipLaunchKernelGGL(kgat::epi_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, dH, lddh, n,
                      d_out, dropout_p, seed, key_rows);
   KGAT_LAUNCH_CHECK();
-  // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
-                          W1, d_in, dA, d_out, &zero, dXd, static_cast<int>(lddxd)));
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
-                          W2, d_in, dB, d_out, &zero, dS, static_cast<int>(ldds)));
-  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
-                     st, X, ldx, S, lds, U, M, n, d_in);
+  return kgat::bwd_gemm_tail(h, X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
+                             d_out, work, st);
+}
+
+extern "C" int64_t kgat_biinter_gemm_bits_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {
+  const int64_t w = kgat_biinter_gemm_work_floats(n_rows, d_in, d_out);
+  return w < 0 ? -1 : w + 2 * n_rows * static_cast<int64_t>(d_out);  // + dA, dB
+}
+
+extern "C" int kgat_biinter_bwd_gemm_bits_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                              int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
+                                              int64_t lddh, const float* W1, const float* W2, float* dXd,
+                                              int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
+                                              float* dW2, float* db2, int64_t n, int32_t d_in, int32_t d_out,
+                                              float dropout_p, const int32_t* key_rows, float* work,
+                                              int64_t work_floats, void* stream) {
+  if (!X || !S || !H || !norm || !mask || !dH || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n < 0 ||
+      !gemm_dims_ok(d_in, d_out) || d_out > 128)
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || lddh < d_out || lddxd < d_in || ldds < d_in || (ldx & 3) ||
+      (lds & 3) || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return KGAT_ERR_INVALID;
+  if (!work || work_floats < kgat_biinter_gemm_bits_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int err = 0;
+  rocblas_handle h = kgat::blas_handle(st, &err);
+  if (err) return err;
+  if (n == 0) return kgat::zero_wgrads(dW1, db1, dW2, db2, d_in, d_out, st);
+  float* dA = work + kgat_biinter_gemm_work_floats(n, d_in, d_out);
+  float* dB = dA + n * d_out;
+  hipLaunchKernelGGL(kgat::epi_bwd_bits_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, mask, dH,
+                     lddh, n, d_out, dropout_p, key_rows);
   KGAT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kgat::dxs_kernel, dim3(kgat::blocks_for(n * d_in, 256, kgat::kCUs * 8)), dim3(256), 0, st, dXd,
-                     lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
-  KGAT_LAUNCH_CHECK();
-  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order)
-  //   column-major C_b[ldu, d_out] = U'_b-view[ldu, k] x dA_b-view^T[k, d_out]
-  const int64_t full = n / kgat::kGemmChunk, rest = n - full * kgat::kGemmChunk;
-  for (int mat = 0; mat < 2; ++mat) {
-    const float* Um = mat == 0 ? U : M;
-    const float* G = mat == 0 ? dA : dB;
-    float* sl = mat == 0 ? slab1 : slab2;
-    if (full > 0)
-      KGAT_BLAS(rocblas_sgemm_strided_batched(
-          h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(kgat::kGemmChunk), &one,
-          Um, ldu, kgat::kGemmChunk * ldu, G, d_out, kgat::kGemmChunk * d_out, &zero, sl, ldu,
-          static_cast<int64_t>(ldu) * d_out, static_cast<int>(full)));
-    if (rest > 0)
-      KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(rest),
-                              &one, Um + full * kgat::kGemmChunk * ldu, ldu, G + full * kgat::kGemmChunk * d_out, d_out,
-                              &zero, sl + full * ldu * static_cast<int64_t>(d_out), ldu));
-    hipLaunchKernelGGL(kgat::wslab_reduce_kernel, dim3((d_out * (d_in + 1) + 255) / 256), dim3(256), 0, st, sl,
-                       static_cast<int>(nb), d_in, d_out, mat == 0 ? dW1 : dW2, mat == 0 ? db1 : db2);
-    KGAT_LAUNCH_CHECK();
-  }
-  return KGAT_OK;
+  return kgat::bwd_gemm_tail(h, X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
+                             d_out, work, st);
 }

@@ -387,21 +387,37 @@ def fused_supported(d_in: int, d_out: int) -> bool:
     return (d_in, d_out) in FUSED_SHAPES
 
 
+# C4's wide fused shapes (d_out > 64 or d_in * d_out > 4096: no saved-state fused backward) run the
+# fused MFMA forward keeping its norm + sign/keep bits and the rocBLAS backward from those bits
+# (kgat_biinter_bwd_gemm_bits_f32) -- instead of the rocBLAS forward with its [n, 2*d_out]
+# pre-activation state.  KGAT_BITS_WIDE=0 restores the rocBLAS forward.
+BITS_WIDE = os.environ.get("KGAT_BITS_WIDE", "1") != "0"
+
+
+def bits_supported(d_in: int, d_out: int) -> bool:
+    return BITS_WIDE and fused_supported(d_in, d_out) and d_out <= 128 and not saved_state_supported(d_in, d_out)
+
+
 class BiState:
     """The forward's saved state for the backward, indexed by node.
     fused shapes (kgat_biinter_fwd_f32 norm_out / mask_out): row norms + per-lane sign/keep words;
-    wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
+    "bits": the same state for wide fused shapes (ceil(d_out/64) words per lane), consumed by the
+    rocBLAS backward; wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
 
     def __init__(self, n: int, device, d_in: int = 64, d_out: int = 64, kind: str | None = None):
         self.n, self.d_in, self.d_out = n, d_in, d_out
         if kind is None:
-            kind = "fused" if saved_state_supported(d_in, d_out) else "gemm"
+            kind = "fused" if saved_state_supported(d_in, d_out) else ("bits" if bits_supported(d_in, d_out)
+                                                                      else "gemm")
         if kind == "fused" and not saved_state_supported(d_in, d_out):
             raise ValueError(f"no fused saved state for {d_in}->{d_out}")
+        if kind == "bits" and not (fused_supported(d_in, d_out) and d_out <= 128):
+            raise ValueError(f"no fused forward for {d_in}->{d_out}")
         self.kind = kind
-        if self.kind == "fused":
+        if self.kind in ("fused", "bits"):
+            words = (d_out + 63) // 64
             self.norm = torch.empty(max((n + 15) // 16 * 16, 16), dtype=torch.float32, device=device)
-            self.mask = torch.empty(max((n + 15) // 16, 1) * 64, dtype=torch.int64, device=device)
+            self.mask = torch.empty(max((n + 15) // 16, 1) * 64 * words, dtype=torch.int64, device=device)
         else:
             m = int(_lib.lib().kgat_biinter_gemm_state_floats(n, d_in, d_out))
             if m < 0:
@@ -457,9 +473,10 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
                   float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), st.P.data_ptr(), work.data_ptr(),
                   work.numel(), stream_ptr(X.device))
         return out
-    if state is not None and (state.kind != "fused" or state.norm.numel() < n
-                              or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
-        raise ValueError("bi-interaction state too small or d_out > 64")
+    words = (dout + 63) // 64
+    if state is not None and (state.kind not in ("fused", "bits") or state.norm.numel() < n
+                              or state.mask.numel() < (n + 15) // 16 * 64 * words or dout > 128):
+        raise ValueError("bi-interaction state too small or d_out > 128")
     _lib.call("kgat_biinter_fwd_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
               W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout, float(dropout_p),
               ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.norm.data_ptr() if state is not None else None,
@@ -596,6 +613,9 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     dW2 = torch.empty_like(W2)
     db1 = torch.empty_like(b1)
     db2 = torch.empty_like(b2)
+    if state is not None and state.kind == "bits":
+        _biinter_bwd_bits(X, S, dH, W1, W2, dropout_p, dXd, dS, dW1, db1, dW2, db2, rows, H, state)
+        return dXd, dS, dW1, db1, dW2, db2
     if not fused_supported(din, dout) or (state is not None and state.kind == "gemm"):
         _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, dropout_p, seed, dXd, dS, dW1, db1, dW2, db2, rows, H, state)
         return dXd, dS, dW1, db1, dW2, db2
@@ -643,6 +663,29 @@ def _biinter_bwd_gemm(X, S, dH, W1, b1, W2, b2, p, seed, dXd, dS, dW1, db1, dW2,
               dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
               float(p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), key.data_ptr() if key is not None else None,
               work.data_ptr(), work.numel(), stream_ptr(dev))
+
+
+def _biinter_bwd_bits(X, S, dH, W1, W2, p, dXd, dS, dW1, db1, dW2, db2, rows, H, state) -> None:
+    """Wide-layer backward from the fused forward's norm + sign/keep bits (kgat_biinter_bwd_gemm_bits_f32);
+    frontier rows: X, S, H gathered to a compact problem, the state read by node id."""
+    src_rows, din = X.shape
+    dout = W1.shape[0]
+    dev = X.device
+    if H is None or state.n != src_rows:
+        raise ValueError("bi-interaction state does not match the layer")
+    key = None
+    if rows is not None:
+        X, S, H, key = gather_rows(X, rows), gather_rows(S, rows), gather_rows(H, rows), rows
+    n = X.shape[0]
+    m = int(_lib.lib().kgat_biinter_gemm_bits_work_floats(n, din, dout))
+    if m < 0:
+        raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
+    work = torch.empty(max(m, 1), dtype=torch.float32, device=dev)
+    _lib.call("kgat_biinter_bwd_gemm_bits_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
+              state.norm.data_ptr(), state.mask.data_ptr(), dH.data_ptr(), _ld(dH), W1.data_ptr(), W2.data_ptr(),
+              dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(),
+              db2.data_ptr(), n, din, dout, float(p), key.data_ptr() if key is not None else None, work.data_ptr(),
+              work.numel(), stream_ptr(dev))
 
 
 def make_tables(tables: list[torch.Tensor]) -> _lib.Tables:

@@ -302,7 +302,8 @@ def test_cf_step_dropout_train_mode_runs(pkg):
     m.update_cf_weights()
 
 
-@pytest.mark.parametrize("dim,layers,batch", [(64, [64, 32], 256), (64, [64, 32, 16], 512), (256, [256, 128], 256)])
+@pytest.mark.parametrize("dim,layers,batch", [(64, [64, 32], 256), (64, [64, 32, 16], 512), (256, [256, 128], 256),
+                                              (128, [128, 64, 32], 256)])
 def test_cf_step_synthetic_hubs_vs_oracle(pkg, dim, layers, batch):
     """Synthetic CKG with Zipf hub rows (long-row path in A and A^T), duplicate ids in the
     batch (users repeat, items collide with user rows): loss and every gradient vs the oracle."""
@@ -1067,6 +1068,66 @@ def test_biinter_wide_gemm_path(pkg, din, dout):
     Fd = F.to(DEV)
     np.testing.assert_allclose(comp[0][:100].cpu().numpy(), dense[0][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(comp[1][:100].cpu().numpy(), dense[1][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
+    for a, b in zip(comp[2:], dense[2:]):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("din,dout", [(128, 128), (128, 64)])
+def test_biinter_wide_bits_state(pkg, din, dout):
+    """C4's wide layers: fused MFMA forward keeping norm + sign/keep bits (ceil(d_out/64) words per
+    lane), rocBLAS backward from those bits -- vs a torch fp32 autograd reference (dropout, clamped
+    rows), frontier rows vs the dense backward, and vs the pre-activation (gemm) state path."""
+    _, kernels = _mods(pkg)
+    assert kernels.bits_supported(din, dout)
+    torch.manual_seed(din + 5 * dout)
+    n, p = 3000 + 9, 0.2
+    X, S = torch.randn(n, din), torch.randn(n, din)
+    X[10:20] = 0.0
+    S[10:20] = 0.0
+    W1, W2 = torch.randn(dout, din) * 0.1, torch.randn(dout, din) * 0.1
+    b1, b2 = torch.zeros(dout), torch.zeros(dout)
+    dv = [t.to(DEV) for t in (X, S, W1, b1, W2, b2)]
+    st = kernels.make_state(n, din, dout, DEV)
+    assert st.kind == "bits"
+    H = kernels.biinter_fwd(*dv, dropout_p=p, seed=9, state=st)
+    assert torch.equal(H, kernels.biinter_fwd(*dv, dropout_p=p, seed=9))
+    keep = (H.cpu() != 0).float()
+    keep[10:20] = 1.0
+    leaves = [t.clone().requires_grad_(True) for t in (X, S, W1, b1, W2, b2)]
+    x, s, w1, bb1, w2, bb2 = leaves
+    h = (torch.nn.functional.leaky_relu(torch.nn.functional.linear(x + s, w1, bb1), 0.01)
+         + torch.nn.functional.leaky_relu(torch.nn.functional.linear(x * s, w2, bb2), 0.01)) * keep / (1 - p)
+    ref = h / h.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    np.testing.assert_allclose(H.cpu().numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-5)
+    dH = torch.randn(n, dout)
+    dH[10:20] = 0.0
+    ref.backward(dH)
+    got = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], dropout_p=p, seed=9, H=H, state=st)
+    want = (x.grad, s.grad, w1.grad, bb1.grad, w2.grad, bb2.grad)
+    for i, (a, b) in enumerate(zip(got, want)):
+        np.testing.assert_allclose(a.cpu().numpy(), b.numpy(), rtol=1e-3, atol=1e-5 if i < 2 else 1e-4,
+                                   err_msg=f"grad {i}")
+    # the pre-activation (gemm) path agrees (its forward is rocBLAS: sums in another order)
+    sg = kernels.BiState(n, DEV, din, dout, kind="gemm")
+    Hg = kernels.biinter_fwd(*dv, dropout_p=p, seed=9, state=sg)
+    np.testing.assert_allclose(Hg.cpu().numpy(), H.cpu().numpy(), rtol=1e-4, atol=1e-6)
+    gg = kernels.biinter_bwd(dv[0], dv[1], dH.to(DEV), *dv[2:], dropout_p=p, seed=9, H=Hg, state=sg)
+    for i, (a, b) in enumerate(zip(got, gg)):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=1e-5, err_msg=f"gemm {i}")
+    # frontier rows (compact dH, -1 padding) == the dense backward restricted to those rows
+    F = torch.from_numpy(np.random.default_rng(3).choice(n, 150, replace=False))
+    F[:3] = torch.tensor([10, 11, n - 1])
+    rows = torch.cat([F, torch.full((10,), -1)]).int().to(DEV)
+    dHc = torch.zeros(160, dout)
+    dHc[:150] = torch.randn(150, dout)
+    dHd = torch.zeros(n, dout)
+    dHd[F] = dHc[:150]
+    dense = kernels.biinter_bwd(dv[0], dv[1], dHd.to(DEV), *dv[2:], dropout_p=p, seed=9, H=H, state=st)
+    comp = kernels.biinter_bwd(dv[0], dv[1], dHc.to(DEV), *dv[2:], dropout_p=p, seed=9, rows=rows, H=H, state=st)
+    Fd = F.to(DEV)
+    np.testing.assert_allclose(comp[0][:150].cpu().numpy(), dense[0][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(comp[1][:150].cpu().numpy(), dense[1][Fd].cpu().numpy(), rtol=1e-4, atol=1e-6)
+    assert float(comp[0][150:].abs().max()) == 0.0 and float(comp[1][150:].abs().max()) == 0.0
     for a, b in zip(comp[2:], dense[2:]):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-3, atol=1e-5)
 

@@ -45,9 +45,10 @@ def main():
     graph = importlib.import_module(PKG + ".graph")
     K = importlib.import_module(PKG + ".kernels")
     dev = torch.device("cuda")
-    U, E, inter, trip = graph.synthetic_ckg(args.nodes, args.triples, seed=2024)
+    small = args.only and not set(args.only.split(",")) - {"attention", "nfm", "wide"}
+    U, E, inter, trip = graph.synthetic_ckg(*((20000, 100000) if small else (args.nodes, args.triples)), seed=2024)
     lay = graph.build_layout(U, E, inter, trip)
-    g = graph.DeviceGraph(lay, dev) if not args.only or set(args.only.split(",")) - {"attention", "nfm"} else None
+    g = graph.DeviceGraph(lay, dev) if not args.only or set(args.only.split(",")) - {"attention", "nfm", "wide"} else None
     n, nnz = lay.n_nodes, lay.nnz
     out = []
 
@@ -82,6 +83,34 @@ def main():
         attention_section(args, K, lay, U, E, dev, rec)
     if want("nfm"):
         nfm_section(args, dev, rec)
+    if want("wide"):
+        wide_section(args, K, dev, rec)
+
+
+def wide_section(args, K, dev, rec):
+    """C4's wide layers (128->128, 128->64) on WIDE_ROWS rows: the fused MFMA forward keeping the sign/keep
+    bits + the rocBLAS backward from them, vs the rocBLAS forward with its pre-activation state."""
+    n = int(os.environ.get("WIDE_ROWS", "2000000"))
+    for din, dout in ((128, 128), (128, 64)):
+        X = torch.randn(n, din, device=dev)
+        S = torch.randn(n, din, device=dev)
+        W1 = torch.randn(dout, din, device=dev) * 0.1
+        W2 = torch.randn(dout, din, device=dev) * 0.1
+        b1 = torch.zeros(dout, device=dev)
+        b2 = torch.zeros(dout, device=dev)
+        H = torch.empty(n, dout, device=dev)
+        dH = torch.randn(n, dout, device=dev)
+        byt = 4 * n * (2 * din + dout)
+        for kind in ("bits", "gemm"):
+            st = K.BiState(n, dev, din, dout, kind=kind)
+            rec(f"wide_{kind}_fwd_{din}x{dout}",
+                timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st), args.reps), byt, rows=n,
+                tflops=round(4 * n * din * dout / 1e12, 4))
+            rec(f"wide_{kind}_bwd_{din}x{dout}",
+                timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5, H=H, state=st), args.reps), rows=n)
+            del st
+        del X, S, H, dH
+        torch.cuda.empty_cache()
 
 
 def graph_section(args, K, g, U, E, n, dev, rec):
