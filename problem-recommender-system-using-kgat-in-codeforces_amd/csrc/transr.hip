@@ -61,22 +61,37 @@ __global__ __launch_bounds__(256) void transr_fwd_kernel(const float* __restrict
     rp[ic] = i < d ? ep[i] : 0.f;
     rn[ic] = i < d ? en[i] : 0.f;
   }
-  for (int i = 0; i < d; ++i) {
-    const int ic = i >> 6, src = i & 63;
-    const float xh = __shfl(ic == 0 ? rh[0] : ic == 1 ? rh[1] : ic == 2 ? rh[2] : rh[3], src);
-    const float xp = __shfl(ic == 0 ? rp[0] : ic == 1 ? rp[1] : ic == 2 ? rp[2] : rp[3], src);
-    const float xn = __shfl(ic == 0 ? rn[0] : ic == 1 ? rn[1] : ic == 2 ? rn[2] : rn[3], src);
+  // rows of W_r in groups of kRowGroup: the group's loads are issued before its fmas, so a
+  // wave has kRowGroup * kMaxCols loads in flight instead of one dependent step per row
+  constexpr int kRowGroup = 8;
+  auto bcast = [&](const float (&v)[kMaxCols], int i) {
+    const int ic = i >> 6;
+    return __shfl(ic == 0 ? v[0] : ic == 1 ? v[1] : ic == 2 ? v[2] : v[3], i & 63);
+  };
+  auto rows = [&](int i0, int cnt) {
+    float w[kRowGroup][kMaxCols];
 #pragma unroll
-    for (int cc = 0; cc < kMaxCols; ++cc) {
-      const int j = lane + 64 * cc;
-      if (j < k) {
-        const float w = W[static_cast<int64_t>(i) * k + j];
-        h[cc] = fmaf(xh, w, h[cc]);
-        tp[cc] = fmaf(xp, w, tp[cc]);
-        tn[cc] = fmaf(xn, w, tn[cc]);
+    for (int u = 0; u < kRowGroup; ++u)
+#pragma unroll
+      for (int cc = 0; cc < kMaxCols; ++cc) {
+        const int j = lane + 64 * cc;
+        w[u][cc] = (u < cnt && j < k) ? W[static_cast<int64_t>(i0 + u) * k + j] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < kRowGroup; ++u) {
+      if (u >= cnt) break;  // wave-uniform
+      const float xh = bcast(rh, i0 + u), xp = bcast(rp, i0 + u), xn = bcast(rn, i0 + u);
+#pragma unroll
+      for (int cc = 0; cc < kMaxCols; ++cc) {
+        if (lane + 64 * cc < k) {
+          h[cc] = fmaf(xh, w[u][cc], h[cc]);
+          tp[cc] = fmaf(xp, w[u][cc], tp[cc]);
+          tn[cc] = fmaf(xn, w[u][cc], tn[cc]);
+        }
       }
     }
-  }
+  };
+  for (int i0 = 0; i0 < d; i0 += kRowGroup) rows(i0, min(kRowGroup, d - i0));
   float sp = 0.f, sn = 0.f, q = 0.f;
 #pragma unroll
   for (int cc = 0; cc < kMaxCols; ++cc) {
@@ -126,10 +141,17 @@ __global__ __launch_bounds__(256) void transr_fwd_kernel(const float* __restrict
 #pragma unroll
     for (int cc = 0; cc < kMaxCols; ++cc) {
       if (cc * 64 >= k) break;  // wave-uniform
-      for (int jj = 0; jj < 64 && cc * 64 + jj < k; ++jj) {
-        const float w = wr[cc * 64 + jj];
+      const int jn = min(64, k - cc * 64);
+      for (int j0 = 0; j0 < jn; j0 += kRowGroup) {  // kRowGroup loads of the row in flight
+        float w[kRowGroup];
 #pragma unroll
-        for (int v = 0; v < 3; ++v) acc[v] = fmaf(w, __shfl(g3[v][cc], jj), acc[v]);
+        for (int u = 0; u < kRowGroup; ++u) w[u] = j0 + u < jn ? wr[cc * 64 + j0 + u] : 0.f;
+#pragma unroll
+        for (int u = 0; u < kRowGroup; ++u) {
+          if (j0 + u >= jn) break;  // wave-uniform
+#pragma unroll
+          for (int v = 0; v < 3; ++v) acc[v] = fmaf(w[u], __shfl(g3[v][cc], j0 + u), acc[v]);
+        }
       }
     }
     if (i < d) {
