@@ -1,24 +1,38 @@
 """KGAT CF training-step benchmark on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5|small] [--scale F]
 
 One step = the reference's hot loop body (src/model/KGAT/main.py:299-316):
 full-graph attentive propagation over all L layers, BPR loss on a 256-pair
-batch, backward through every layer, dense Adam on the whole model -- in
-train mode (dropout on), inputs resident in HBM before timing starts.
+batch per rank, backward through every layer, dense Adam on the whole model --
+in train mode (dropout on), inputs resident in HBM before timing starts.
 
-value = CKG layer-edges per second of the whole job = n_gpus * E * L / t_step
-(weak scaling: every rank runs full propagation for its own batch; for N > 1,
-data-parallel replicas, replicas.ShardedGradSync: by default for 2-layer
-configs the replicas all-gather their compact layer-0 hop-set gradient terms
-over RCCL and each computes the mean table gradient and the full Adam itself
-(--dp replicated); otherwise the table gradient is reduce-scattered by row
-blocks, each rank runs Adam on its own rows and the rows are all-gathered back
-(--dp sharded); small gradients in one flat all-reduce).
-Also reported: BPR pairs/s = 256 * n_gpus / t_step, forward-propagation
-edges/s, the roofline of the dominant kernel (the SpMM gather, timed live
-with HIP events on its launch stream) and the CPU baseline (the oracle's
-PyTorch-CPU restatement on the same graph, rank 0 only).
+``--gpus N`` with no WORLD_SIZE in the environment relaunches this script as N
+ranks (torch.distributed.run, one process per GPU, 127.0.0.1 rendezvous) before
+anything touches the GPU; under the driver's own torchrun launch it checks that
+WORLD_SIZE == N.
+
+Configs (BASELINE.json ``configs``):
+  c2  (default, configs[1]) 1M nodes / 10M triples, d=64, [64, 32]: the single-GPU
+      headline.  N > 1: data-parallel replicas (replicas.ShardedGradSync) -- the
+      replicas all-gather their compact layer-0 hop-set gradient terms over RCCL and
+      each computes the mean table gradient and the full Adam (--dp replicated), or
+      the table gradient is reduce-scattered by row blocks, Adam on owned rows,
+      rows all-gathered (--dp sharded).  value = N * E * L / t_step (weak scaling).
+  c4  (configs[3]) 10M / 100M, d=128, [128, 64, 32]: DP replicas as c2.
+  c5  (configs[4]) 50M / 500M, d=256, [256, 128, 64]: the table row-sharded over the
+      ranks (sharded.RowShardedKGAT), each rank builds only its own rows of the graph
+      (graph.HashedCKG); needs >= 4 GPUs (memory estimate below; refused otherwise).
+      value = E * L / t_step (the whole graph once per step: strong scaling).
+  ``--scale F`` shrinks nodes and triples by F (rehearsals; recorded in the config).
+
+Also reported: BPR pairs/s, forward-propagation edges/s, the roofline of the
+dominant kernel (the forward SpMM gather: HIP events on its launch stream over the
+timed region; counter-measured bytes from profiles/pmc_<config>.json), on rank 0
+at N = 1 the CPU baseline (the oracle's PyTorch-CPU restatement of the same step
+on the same graph: thread count swept, 1 warm-up, median of --cpu-steps) and, for
+c2, a bench-scale parity check of the timed model against the oracle (eval-mode
+propagation, CF loss and table gradient on the full graph).
 """
 from __future__ import annotations
 
@@ -26,6 +40,8 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -39,14 +55,20 @@ PKG = "problem-recommender-system-using-kgat-in-codeforces_amd"
 
 # BASELINE.json configs: C2 is the single-GPU headline (configs[1]).
 CONFIGS = {
-    "c2": dict(nodes=1_000_000, triples=10_000_000, dim=64, layers=[64, 32], batch=256,
+    "c2": dict(nodes=1_000_000, triples=10_000_000, dim=64, layers=[64, 32], batch=256, mode="dp",
                workload="synthetic CKG 1M entities / 10M triples, embed_dim=64, 2 KGAT layers (BASELINE configs[1])"),
-    "c4": dict(nodes=10_000_000, triples=100_000_000, dim=128, layers=[128, 64, 32], batch=256,
+    "c4": dict(nodes=10_000_000, triples=100_000_000, dim=128, layers=[128, 64, 32], batch=256, mode="dp",
                workload="synthetic CKG 10M entities / 100M triples, embed_dim=128, 3 KGAT layers (configs[3])"),
-    "small": dict(nodes=100_000, triples=1_000_000, dim=64, layers=[64, 32], batch=256,
+    "c5": dict(nodes=50_000_000, triples=500_000_000, dim=256, layers=[256, 128, 64], batch=256, mode="sharded",
+               workload="synthetic CKG 50M entities / 500M triples, embed_dim=256, 3 KGAT layers, table row-sharded "
+                        "(configs[4])"),
+    "small": dict(nodes=100_000, triples=1_000_000, dim=64, layers=[64, 32], batch=256, mode="dp",
                   workload="synthetic CKG 100k / 1M (debug)"),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+GPU_BYTES = 288e9              # HBM3E per MI355X
+GPU_BUDGET = 0.85 * GPU_BYTES  # what a config may plan to use (allocator slack, workspaces)
+PARITY_TOL = {"emb": 1e-4, "loss_rel": 1e-4, "grad": 1e-6}  # north_star: 1e-4 fp32 (gradients as in tests/)
 
 
 def log(*a):
@@ -55,80 +77,270 @@ def log(*a):
 
 
 def spmm_bytes(n: int, nnz: int, d: int, accumulate: bool) -> int:
-    """Algorithmic bytes of one SpMM launch: rowptr (int64), col+val per edge, gathered
-    source rows, written output rows (+ read of the accumulated output)."""
+    """Algorithmic bytes of one SpMM launch: rowptr (int64), col+val per edge, one gathered
+    source row per edge, written output rows (+ read of the accumulated output)."""
     return 8 * (n + 1) + nnz * (8 + 4 * d) + 4 * n * d * (2 if accumulate else 1)
 
 
-def cpu_baseline(layout, cfg, steps: int = 2) -> dict:
-    """The oracle's PyTorch-CPU restatement of one CF step (fwd + bwd + Adam) on the same graph."""
-    from oracle import kgat_cpu as K
+def compulsory_bytes(n: int, nnz: int, d: int) -> int:
+    """Bytes one SpMM launch cannot avoid: rowptr, col+val, every source row read once, output written."""
+    return 8 * (n + 1) + 8 * nnz + 8 * n * d
 
-    torch.set_num_threads(os.cpu_count() or 1)
-    threads = torch.get_num_threads()
-    n = layout.n_nodes
-    rows, cols, vals = layout.coo()
-    A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, cols])), torch.from_numpy(vals), (n, n))
-    A = A.coalesce()
+
+def sharded_bytes_per_gpu(cfg: dict, world: int) -> float:
+    """Planned HBM per rank of the row-sharded mode (sharded.RowShardedKGAT), largest shard ~1.15x the mean.
+    Per node row (fp32): X0, its gradient and CF Adam m/v (4d), layer outputs H_l and sides S_l,
+    three backward temporaries of the widest layer; per edge: the CSR blocks and their transposes
+    (col + val each), the local values and the two position maps (28 B)."""
+    d, layers = cfg["dim"], cfg["layers"]
+    dims = [d, *layers]
+    per_row = 4 * (4 * d + sum(layers) + sum(dims[:-1]) + 3 * max(dims))
+    nnz = 2 * cfg["triples"]
+    per_rank_rows = 1.15 * cfg["nodes"] / world
+    per_rank_edges = 1.15 * nnz / world
+    return per_row * per_rank_rows + 28 * per_rank_edges + 16 * cfg["nodes"] + 8 * per_rank_rows * world
+
+
+def min_gpus(cfg: dict) -> int:
+    for g in (1, 2, 4, 8, 16, 32):
+        if sharded_bytes_per_gpu(cfg, g) <= GPU_BUDGET:
+            return g
+    return 64
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int) -> int:
+    """Relaunch this script as n ranks (one process per GPU) and return the launcher's exit code.
+    Runs before anything initialises HIP in this process (a GPU-initialised process must not exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+# --------------------------------------------------------------------------- CPU leg (oracle)
+def _oracle_params(layout, cfg, state: dict | None):
+    """Flat reference-keyed parameters on the CPU: the GPU model's (state) or seeded random ones."""
+    if state is not None:
+        return {k: v.detach().float().cpu().clone() for k, v in state.items()}
     g = torch.Generator().manual_seed(0)
     dims = [cfg["dim"], *cfg["layers"]]
-    P = {"_user_entity_embedding.weight": torch.randn(n, cfg["dim"], generator=g) * 0.01}
+    P = {"_user_entity_embedding.weight": torch.randn(layout.n_nodes, cfg["dim"], generator=g) * 0.01}
     for l in range(len(cfg["layers"])):
         for w in ("linear1", "linear2"):
             P[f"_aggregator_layers.{l}.{w}.weight"] = torch.randn(dims[l + 1], dims[l], generator=g) * 0.1
             P[f"_aggregator_layers.{l}.{w}.bias"] = torch.zeros(dims[l + 1])
+    return P
+
+
+def _sweep_threads(A, n: int, d: int) -> tuple[int, dict]:
+    """Fastest torch CPU thread count for the step's dominant op (A . X, d wide) on this host."""
+    cands = sorted({t for t in (8, 16, 32, 64, 128) if t <= (os.cpu_count() or 1)} | {min(8, os.cpu_count() or 1)})
+    X = torch.randn(n, d)
+    res = {}
+    for t in cands:
+        torch.set_num_threads(t)
+        best = float("inf")
+        for _ in range(2):
+            t0 = time.perf_counter()
+            torch.sparse.mm(A, X)
+            best = min(best, time.perf_counter() - t0)
+        res[t] = best
+    return min(res, key=res.get), res
+
+
+def cpu_leg(layout, cfg, steps: int, parity_state: dict | None = None, parity_batch=None,
+            parity_gpu: dict | None = None) -> tuple[dict, dict | None]:
+    """The oracle's PyTorch-CPU CF step (fwd + bwd + Adam) on the same graph: threads swept, then
+    one warm-up step -- the parity step when the GPU's weights are given (eval mode, compared with
+    the GPU's propagation / loss / table gradient) -- then the median of `steps` train-mode steps."""
+    from oracle import kgat_cpu as K
+
+    n = layout.n_nodes
+    rows, cols, vals = layout.coo()
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, cols])), torch.from_numpy(vals), (n, n)).coalesce()
+    threads, sweep = _sweep_threads(A, n, cfg["dim"])
+    torch.set_num_threads(threads)
+    L = len(cfg["layers"])
+    B = cfg["batch"]
     opt = K.AdamOracle(lr=1e-3)
-    times = []
-    for _ in range(steps):
-        u = torch.randint(0, n // 10, (cfg["batch"],), generator=g)
-        p = torch.randint(0, n // 10, (cfg["batch"],), generator=g)
-        q = torch.randint(0, n // 10, (cfg["batch"],), generator=g)
-        t0 = time.perf_counter()
+    parity = None
+
+    def one_step(P, u, p, q, dropout):
         leaves = {k: v.requires_grad_(True) for k, v in P.items()}
-        loss = K.cf_loss(torch.cat(K.propagate(leaves, A, dropout=[0.1] * len(cfg["layers"]), generator=g), 1),
-                         u, p, q)
+        outs = K.propagate(leaves, A, dropout=dropout, generator=g)
+        loss = K.cf_loss(torch.cat(outs, 1), u, p, q)
         loss.backward()
         grads = {k: v.grad for k, v in leaves.items()}
-        P = {k: v.detach() for k, v in leaves.items()}
-        opt.step(P, grads)
+        newP = {k: v.detach() for k, v in leaves.items()}
+        opt.step(newP, grads)
+        return newP, outs, loss, grads
+
+    g = torch.Generator().manual_seed(1)
+    P = _oracle_params(layout, cfg, parity_state)
+    t0 = time.perf_counter()
+    if parity_state is not None:  # warm-up = the parity step
+        u, p, q = (t.cpu() for t in parity_batch)
+        P, outs, loss, grads = one_step(P, u, p, q, None)
+        emb = max(float((o.detach() - gpu).abs().max()) for o, gpu in zip(outs, parity_gpu["tables"]))
+        gref = grads["_user_entity_embedding.weight"]
+        gerr = float((gref - parity_gpu["table_grad"]).abs().max())
+        lrel = abs(float(loss) - parity_gpu["loss"]) / max(abs(float(loss)), 1e-30)
+        parity = {"max_abs_emb": emb, "max_abs_grad": gerr, "max_abs_grad_ref": float(gref.abs().max()),
+                  "loss_rel": lrel, "loss": parity_gpu["loss"], "loss_oracle": float(loss),
+                  "tolerance": PARITY_TOL,
+                  "pass": bool(emb <= PARITY_TOL["emb"] and gerr <= PARITY_TOL["grad"] and lrel <= PARITY_TOL["loss_rel"]),
+                  "what": "eval-mode propagation of every layer, CF loss and table gradient of the timed model "
+                          "(after the timed steps) vs oracle/kgat_cpu.py on the full graph, one 256-pair batch"}
+        del outs, grads
+    else:
+        u = torch.randint(0, n // 10, (B,), generator=g)
+        P, *_ = one_step(P, u, u, u, [0.1] * L)
+    warm = time.perf_counter() - t0
+    times = []
+    for _ in range(steps):
+        u, p, q = (torch.randint(0, n // 10, (B,), generator=g) for _ in range(3))
+        t0 = time.perf_counter()
+        P, *_ = one_step(P, u, p, q, [0.1] * L)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    base = {"value": layout.nnz * L / t, "unit": "layer-edges/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/kgat_cpu.py CF step (fwd+bwd+Adam, dropout 0.1) on the full {cfg['workload']} graph, "
+                      f"median of {steps} after 1 warm-up ({warm:.1f} s), threads={threads} (best of sweep "
+                      + ", ".join(f"{k}:{v * 1e3:.0f}ms" for k, v in sweep.items()) + " on A.X)",
+            "ms_per_step": t * 1e3, "step_times_s": times}
+    return base, parity
+
+
+def cpu_extrapolated(layout, cfg, fracs=(0.02, 0.04)) -> dict:
+    """C4-size CPU baseline: the oracle CF step on uniformly subsampled edge sets (all N rows kept),
+    t(E) fitted as a + b * E through the points and evaluated at the full E ("extrapolated")."""
+    from oracle import kgat_cpu as K
+
+    n = layout.n_nodes
+    rows, cols, vals = layout.coo()
+    rng = np.random.default_rng(5)
+    pts = []
+    threads = None
+    for f in fracs:
+        keep = np.flatnonzero(rng.random(rows.size) < f)
+        A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows[keep], cols[keep]])),
+                                    torch.from_numpy(vals[keep]), (n, n)).coalesce()
+        if threads is None:
+            threads, _ = _sweep_threads(A, n, cfg["dim"])
+            torch.set_num_threads(threads)
+        P = _oracle_params(layout, cfg, None)
+        g = torch.Generator().manual_seed(2)
+        ts = []
+        for _ in range(2):  # warm-up + one timed step
+            u, p, q = (torch.randint(0, n // 10, (cfg["batch"],), generator=g) for _ in range(3))
+            t0 = time.perf_counter()
+            leaves = {k: v.requires_grad_(True) for k, v in P.items()}
+            loss = K.cf_loss(torch.cat(K.propagate(leaves, A, dropout=[0.1] * len(cfg["layers"]), generator=g), 1),
+                             u, p, q)
+            loss.backward()
+            grads = {k: v.grad for k, v in leaves.items()}
+            P = {k: v.detach() for k, v in leaves.items()}
+            K.AdamOracle(lr=1e-3).step(P, grads)
+            ts.append(time.perf_counter() - t0)
+        pts.append((A._nnz(), ts[-1]))
+        del A
+    (e1, t1), (e2, t2) = pts
+    b = (t2 - t1) / max(e2 - e1, 1)
+    t = t1 + b * (layout.nnz - e1)
     L = len(cfg["layers"])
     return {"value": layout.nnz * L / t, "unit": "layer-edges/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/kgat_cpu.py CF step (fwd+bwd+Adam, dropout on) on the full {cfg['workload']} graph, "
-                      f"median of {steps} steps ({t:.2f} s/step), torch CPU threads={threads}",
-            "ms_per_step": t * 1e3}
+            "extrapolated": True, "ms_per_step": t * 1e3,
+            "sample": f"oracle/kgat_cpu.py CF step on {', '.join(f'{e:,}' for e, _ in pts)}-edge uniform subsamples "
+                      f"of the {cfg['workload']} graph (all {n:,} rows; {', '.join(f'{s:.1f}' for _, s in pts)} s/step "
+                      f"after 1 warm-up each), linear in E to the full {layout.nnz:,} edges; threads={threads}"}
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",
-                    help="N>1 table-gradient exchange: replicated = all-gather of the compact layer-0 hop-set "
-                         "terms, every rank computes the mean gradient and full Adam; sharded = row-block "
-                         "reduce-scatter, owned-row Adam, all-gather; auto = replicated for 2-layer configs")
-    args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+# --------------------------------------------------------------------------- roofline
+def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kernel: str) -> tuple[dict, dict]:
+    fwd = []  # (ms, d, algorithmic bytes, compulsory bytes) per forward launch
+    for e0, e1, d, tr, acc in events:
+        if tr or acc is True or acc in ("masked",):
+            continue
+        if isinstance(acc, tuple):  # ("block", rows, nnz[, accumulate])
+            a = bool(acc[3]) if len(acc) > 3 else False
+            fwd.append((e0.elapsed_time(e1), d, spmm_bytes(acc[1], acc[2], d, a), compulsory_bytes(acc[1], acc[2], d)))
+        elif acc is False:
+            fwd.append((e0.elapsed_time(e1), d, spmm_bytes(n, nnz, d, False), compulsory_bytes(n, nnz, d)))
+    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc != "masked"]
+    masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc == "masked"]
+    fwd_d0 = [x for x in fwd if x[1] == d0]
+    avg_ms = float(np.mean([x[0] for x in fwd_d0]))
+    algo = float(np.mean([x[2] for x in fwd_d0]))
+    comp = float(np.mean([x[3] for x in fwd_d0]))
+    t_prop = sum(x[0] for x in fwd) / steps
+    traffic, pmc_src = None, None
+    pmc = ROOT / "profiles" / f"pmc_{cfg_name}.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("spmm_fwd_hbm_bytes_per_launch")
+            pmc_src = str(pmc.relative_to(ROOT))
+        except Exception:  # noqa: BLE001
+            traffic = None
+    algo_gbs = algo / (avg_ms * 1e-3) / 1e9
+    if traffic:
+        achieved, basis = traffic / (avg_ms * 1e-3) / 1e9, "counters"
+    else:
+        achieved, basis = algo_gbs, "algorithmic"
+    roof = {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "basis": basis, "pmc_source": pmc_src,
+            "avg_launch_ms": avg_ms,
+            "algorithmic_bytes_per_launch": algo, "algorithmic_GBps": algo_gbs,
+            "algorithmic_frac": algo_gbs / HBM_PEAK_GBS,
+            "compulsory_bytes_per_launch": comp, "compulsory_frac": comp / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "achieved = counter-measured bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc on "
+                    "this kernel build) / live HIP-event launch time; the SURVEY §8d algorithmic formula prices "
+                    "every gathered row as an HBM read although Zipf hub rows are served from L2 / the Infinity "
+                    "Cache, so algorithmic_frac can exceed 1; compulsory = each source row read once"}
+    spmm = {"fwd_launches": len(fwd), "bwd_launches": len(bwd), "fwd_avg_ms": avg_ms,
+            "bwd_avg_ms": float(np.mean([t for t, _ in bwd])) if bwd else None,
+            "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / steps,
+            "fwd_spmm_ms_per_step": t_prop, "fwd_spmm_layer_edges_per_s": None}
+    return roof, spmm
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+# --------------------------------------------------------------------------- timing
+def timed(step, batches, warmup: int, steps: int, world: int, dev):
+    kernels = importlib.import_module(PKG + ".kernels")
+    for i in range(warmup):
+        step(batches[i])
+    torch.cuda.synchronize()
     if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    kernels.SPMM_EVENTS = []
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(steps):
+        loss = step(batches[warmup + i])
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    events, kernels.SPMM_EVENTS = kernels.SPMM_EVENTS, None
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed, events, float(loss.item())
 
+
+def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
+    """c2 / c4: every rank holds the whole graph; data-parallel replicas for N > 1."""
     pkg = importlib.import_module(PKG)
     graph_mod = importlib.import_module(PKG + ".graph")
-    kernels = importlib.import_module(PKG + ".kernels")
     replicas = importlib.import_module(PKG + ".replicas")
-
     t0 = time.perf_counter()
     log(f"generating the synthetic CKG ({cfg['workload']}) ...")
     U, E, inter, trip = graph_mod.synthetic_ckg(cfg["nodes"], cfg["triples"], seed=2024)
@@ -137,18 +349,17 @@ def main() -> None:
     log(f"graph: N={layout.n_nodes} interactions={len(inter)} kg={len(trip)} nnz={layout.nnz} "
         f"({time.perf_counter() - t0:.1f}s host build)")
     torch.manual_seed(2024 + rank)
+    L = len(cfg["layers"])
     model = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(layout.rel_order),
                                   cf_embedding_dim=cfg["dim"], kg_embedding_dim=cfg["dim"], layer_size=cfg["layers"],
-                                  message_dropout=[0.1] * len(cfg["layers"])))
+                                  message_dropout=[0.1] * L))
     log("attaching the graph (device CSR, transpose, refresh plan) ...")
     model.attach_graph(layout, dev)
     log(f"  attached ({time.perf_counter() - t0:.1f}s)")
     replicas.broadcast_parameters(model)  # identical replicas (no-op at N=1)
     model.train()
     model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-    L = len(cfg["layers"])
     B = cfg["batch"]
-
     # batches (host sampling is outside the hot path, main.py:300-305): uniform users,
     # a positive from the user's interactions, a uniform negative item
     rng = np.random.default_rng(7 + rank)
@@ -170,100 +381,201 @@ def main() -> None:
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
-        # RCCL over xGMI (no-op at N=1): table gradient reduce-scattered by row blocks, Adam on the
-        # owned rows, updated rows all-gathered; small gradients in one flat all-reduce
+        # RCCL over xGMI (no-op at N=1): the table-gradient exchange of --dp, small gradients in
+        # one flat all-reduce
         model.update_cf_weights(row_ranges=sync.reduce())
         sync.gather()
         return loss
 
-    for i in range(args.warmup):
-        step(batches[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    kernels.SPMM_EVENTS = []
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(batches[args.warmup + i])
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    events, kernels.SPMM_EVENTS = kernels.SPMM_EVENTS, None
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    final_loss = float(loss.item())
+    elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
-
-    # dominant kernel: the forward SpMM gather A . X (d = embed dim), timed over the timed region; the
-    # pipelined forward (kernels.propagate_layer) launches it per row block: bytes and time summed
-    n, nnz = layout.n_nodes, layout.nnz
-    d0 = cfg["dim"]
-    fwd = []  # (ms, d, algorithmic bytes) per forward launch
-    for e0, e1, d, tr, acc in events:
-        if tr or acc is True or acc in ("masked",):
-            continue
-        if isinstance(acc, tuple):  # ("block", rows, nnz)
-            fwd.append((e0.elapsed_time(e1), d, spmm_bytes(acc[1], acc[2], d, False)))
-        elif acc is False:
-            fwd.append((e0.elapsed_time(e1), d, spmm_bytes(n, nnz, d, False)))
-    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc != "masked"]
-    masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc == "masked"]
-    fwd_d0 = [(t, b) for t, d, b in fwd if d == d0]
-    avg_ms = float(np.mean([t for t, _ in fwd_d0]))
-    algo = float(np.mean([b for _, b in fwd_d0]))
-    achieved = sum(b for _, b in fwd_d0) / (sum(t for t, _ in fwd_d0) * 1e-3) / 1e9
-    t_prop = sum(t for t, _, _ in fwd) / args.steps  # ms of SpMM per step, forward
-    traffic = None
-    pmc = ROOT / "profiles" / f"pmc_{args.config}.json"
-    if pmc.exists():
-        try:
-            traffic = json.loads(pmc.read_text()).get("spmm_fwd_hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
-
+    n, nnz, d0 = layout.n_nodes, layout.nnz, cfg["dim"]
+    roof, spmm = roofline(events, args.config, n, nnz, d0, args.steps, f"spmm_main_kernel<{d0}, 0> (+fixup), forward A.X")
+    spmm["fwd_spmm_layer_edges_per_s"] = nnz * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
     result = {
-        "metric": "CKG edges/sec (KGAT propagation step) + BPR pairs/sec at 1/2/4/8 MI355X",
-        "value": world * nnz * L / (ms * 1e-3),
-        "unit": "layer-edges/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (seeded CKG per SURVEY §8d; random-init weights; no dataset download)",
+        "value": world * nnz * L / (ms * 1e-3), "n_gpus": world, "ms_per_step": ms, "scaling": "weak",
         "config": {"workload": cfg["workload"], "nodes": n, "nnz": nnz, "interactions": int(len(inter)),
-                   "kg_triples": int(len(trip)), "embed_dim": d0, "layer_size": cfg["layers"], "global_batch": B * world,
-                   "parallelism": f"dp{world}" if world > 1 else "single",
+                   "kg_triples": int(len(trip)), "embed_dim": d0, "layer_size": cfg["layers"],
+                   "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
                    "dp_exchange": dp_mode if world > 1 else None, "mode": "train (dropout 0.1)"},
-        "bpr_pairs_per_s": B * world / (ms * 1e-3),
-        "final_loss": final_loss,
-        "spmm": {"fwd_launches": len(fwd), "bwd_launches": len(bwd), "fwd_avg_ms": avg_ms,
-                 "bwd_avg_ms": float(np.mean([t for t, _ in bwd])) if bwd else None,
-                 "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / args.steps,
-                 "fwd_spmm_ms_per_step": t_prop,
-                 "fwd_spmm_layer_edges_per_s": nnz * L / (t_prop * 1e-3)},
-        "roofline": {"bound": "hbm", "kernel": f"spmm_main_kernel<{d0}, 0> (+fixup), forward A.X"
-                     + (" (per row-block launch)" if kernels.FWD_PIPELINE_BLOCKS > 1 else ""),
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": algo},
+        "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
         "cpu_baseline": None,
     }
+    if world > 1:
+        result["dp_table_exchange_steps"] = dict(sync.stats)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("timing the CPU baseline (oracle restatement) ...")
-        result["cpu_baseline"] = cpu_baseline(layout, cfg, steps=args.cpu_steps)
+        if cfg["nodes"] > 2_000_000:
+            log("timing the CPU baseline (oracle restatement on subsampled edge sets, extrapolated) ...")
+            result["cpu_baseline"] = cpu_extrapolated(layout, cfg)
+        else:
+            parity_in = None
+            if not args.no_parity:
+                log("bench-scale parity: eval-mode propagation / CF loss / table gradient on the GPU ...")
+                parity_in = gpu_parity_inputs(model, pkg, batches[0])
+            log("timing the CPU baseline (oracle restatement; warm-up step = the parity check) ...")
+            base, parity = cpu_leg(layout, cfg, args.cpu_steps, *(parity_in or (None, None, None)))
+            result["cpu_baseline"] = base
+            result["parity"] = parity
+    return result
+
+
+def gpu_parity_inputs(model, pkg, batch):
+    """The timed model's weights, one eval-mode CF loss + table gradient and its propagated tables."""
+    model.eval()
+    state = {k: v.detach().clone() for k, v in model.state_dict().items() if not v.is_sparse}
+    state = {k: v for k, v in state.items() if k == "_user_entity_embedding.weight" or k.startswith("_aggregator")}
+    tables = [t.cpu() for t in model.propagate()]
+    loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
+    loss.backward()
+    grad = model._user_entity_embedding.weight.grad.detach().cpu()
+    for p in model.parameters():
+        p.grad = None
+    torch.cuda.synchronize()
+    model.train()
+    return state, [t.cpu() for t in batch], {"tables": tables, "table_grad": grad, "loss": float(loss)}
+
+
+def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
+    """c5: the table row-sharded over the ranks; each rank builds only its own rows of the graph."""
+    pkg = importlib.import_module(PKG)
+    graph_mod = importlib.import_module(PKG + ".graph")
+    sh = importlib.import_module(PKG + ".sharded")
+    t0 = time.perf_counter()
+    threads = max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
+    log(f"generating the synthetic CKG ({cfg['workload']}) row-sharded over {world} ranks, {threads} threads each ...")
+    ckg = graph_mod.HashedCKG(cfg["nodes"], cfg["triples"], seed=2024, threads=threads)
+    bounds = sh.shard_bounds(ckg.row_offsets(), world)
+    rowptr, col, val = ckg.shard(int(bounds[rank]), int(bounds[rank + 1]))
+    log(f"  rank 0 rows [{bounds[0]}, {bounds[1]}): {col.size:,} entries ({time.perf_counter() - t0:.1f}s)")
+    shard = sh.RowShard(rowptr, col, val, bounds, rank, dev, local=True)
+    del rowptr, col, val
+    comm = sh.Comm()
+    nnz_t = torch.tensor([sum(shard.nnz)], dtype=torch.int64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(nnz_t)
+    nnz = int(nnz_t.item())
+    log(f"  device shards built ({time.perf_counter() - t0:.1f}s); total nnz {nnz:,}")
+    L = len(cfg["layers"])
+    torch.manual_seed(2024)
+    model = sh.RowShardedKGAT(pkg.KGATArgs(user_num=ckg.user_num, entity_num=ckg.entity_num, relation_num=10,
+                                           cf_embedding_dim=cfg["dim"], kg_embedding_dim=cfg["dim"],
+                                           layer_size=cfg["layers"], message_dropout=[0.1] * L),
+                              None, comm, dev, shard=shard)
+    model.train()
+    model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    B = cfg["batch"]
+    rng = np.random.default_rng(7 + rank)
+    batches = []
+    for _ in range(args.warmup + args.steps):
+        u, it = ckg.sample_interactions(rng, B)  # positives: drawn interactions (raw item ids, main.py:89)
+        batches.append([torch.from_numpy(x.astype(np.int64)).to(dev)
+                        for x in (u, it, rng.integers(0, ckg.item_num, B))])
+
+    def step(b):
+        loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
+        loss.backward()
+        model.update_cf_weights()
+        return loss
+
+    elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
+    ms = elapsed / args.steps * 1e3
+    d0 = cfg["dim"]
+    roof, spmm = roofline(events, args.config, shard.n, 0, d0, args.steps,
+                          f"spmm_main_kernel<{d0}, 0> on the A[k][j] blocks (ring all-gather pipelined)")
+    spmm["fwd_spmm_layer_edges_per_s_rank0"] = sum(shard.nnz) * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
+    return {
+        "value": nnz * L / (ms * 1e-3), "n_gpus": world, "ms_per_step": ms, "scaling": "strong",
+        "config": {"workload": cfg["workload"], "nodes": ckg.n_nodes, "nnz": nnz, "interactions": ckg.n_interactions,
+                   "kg_triples": ckg.n_kg, "embed_dim": d0, "layer_size": cfg["layers"], "global_batch": B * world,
+                   "parallelism": f"row-sharded x{world}", "shard_rows": [int(x) for x in np.diff(bounds)],
+                   "mode": "train (dropout 0.1)", "graph": "graph.HashedCKG (per-rank rows, multi-edges kept)"},
+        "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
+        "cpu_baseline": None,
+        "cpu_baseline_note": "not run: the row-sharded config never runs at N = 1 and its CPU step "
+                             "(50M x 704 fp32 tables + autograd state) exceeds host RAM",
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink nodes and triples (rehearsals)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks and join the process group (gloo, no GPU), report, exit")
+    ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",
+                    help="N>1 table-gradient exchange (c2/c4): replicated = all-gather of the compact layer-0 "
+                         "hop-set terms, every rank computes the mean gradient and full Adam; sharded = row-block "
+                         "reduce-scatter, owned-row Adam, all-gather; auto = replicated for 2-layer configs")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.scale != 1.0:
+        cfg["nodes"] = max(1000, int(cfg["nodes"] * args.scale))
+        cfg["triples"] = max(5000, int(cfg["triples"] * args.scale))
+        cfg["workload"] += f" scaled x{args.scale:g} ({cfg['nodes']:,} nodes / {cfg['triples']:,} triples)"
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    if cfg["mode"] == "sharded" and world < min_gpus(cfg):
+        need = min_gpus(cfg)
+        print(f"bench.py: config {args.config} needs >= {need} GPUs (row-sharded: planned "
+              f"{sharded_bytes_per_gpu(cfg, world) / 1e9:.0f} GB per GPU at N={world}, budget "
+              f"{GPU_BUDGET / 1e9:.0f} GB); run it as --gpus {need} or more", file=sys.stderr)
+        return 2
+
+    if args.dry_run:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            joined = int(t.item())
+        else:
+            joined = 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": joined, "config": args.config,
+                              "mode": cfg["mode"], "min_gpus": min_gpus(cfg) if cfg["mode"] == "sharded" else 1}),
+                  flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
+    import torch.distributed as dist
+    if world > 1 or cfg["mode"] == "sharded":  # the row-sharded model always runs over a process group
+        torch.cuda.set_device(local)
+        kw = {} if "MASTER_ADDR" in os.environ else dict(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
+                                                           world_size=1)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), **kw)
+        if dist.get_world_size() != args.gpus:
+            raise RuntimeError(f"{dist.get_world_size()} ranks joined, --gpus {args.gpus}")
+    dev = torch.device("cuda", local)
+    run = run_sharded if cfg["mode"] == "sharded" else run_dp
+    res = run(args, cfg, world, rank, dev)
+    result = {
+        "metric": "CKG edges/sec (KGAT propagation step) + BPR pairs/sec at 1/2/4/8 MI355X",
+        "value": res.pop("value"), "unit": "layer-edges/s", "n_gpus": res.pop("n_gpus"), "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": res.pop("ms_per_step"), "higher_is_better": True,
+        "scaling": res.pop("scaling"), "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded CKG per SURVEY §8d; random-init weights; no dataset download)",
+    }
+    result.update(res)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -500,6 +500,34 @@ int kgat_scatter_rows_f32(float *dst, int64_t ldd, const int32_t *rows, int64_t 
                           int64_t lds, int32_t accumulate, void *stream);
 int kgat_add_f32(float *y, const float *x, int64_t n, void *stream);
 
+/* §8(d) synthetic CKGs at C4/C5 size, §8(f)3 graph build (host, csrc/synth.cpp).
+ * Replaces, for the row-sharded configs, the reference's input-layout producer
+ * (src/model/KGAT/preprocess.py:177-246, 628-634: per-relation blocks normalised
+ * to A^T D^-1, summed into the attentive matrix).  Each triple is a pure function
+ * of (seed, index), so every rank builds only its own rows [lo, hi):
+ *   kgat_synth_open         draws nothing, counts the degrees (all triples, n_threads)
+ *   kgat_synth_info         info[8] = {n_nodes, n_triples, users, entities, items,
+ *                           interactions, kg_triples, 0}
+ *   kgat_synth_row_offsets  [n_nodes + 1] prefix sums of each row's pre-coalesce
+ *                           entries (the balance weights of the row shards)
+ *   kgat_synth_triples      raw triples by index: rel = -1 -> (user a, item b),
+ *                           else KG (head a, rel, tail b), entity ids
+ *   kgat_synth_shard_build  coalesced CSR of rows [lo, hi) (global column ids), kept
+ *                           in the handle; *nnz = its entry count
+ *   kgat_synth_shard_copy   copies it to rowptr [hi-lo+1] (0-based), col, val [nnz]
+ *                           (host memory) and releases the handle's copy.
+ * Host-only; no HIP call.  Status codes as everywhere else. */
+typedef struct kgat_synth kgat_synth;
+int kgat_synth_open(int64_t n_nodes, int64_t n_triples, uint64_t seed, double zipf_s, int n_threads,
+                    kgat_synth **out);
+void kgat_synth_close(kgat_synth *g);
+int kgat_synth_info(const kgat_synth *g, int64_t *info);
+int kgat_synth_row_offsets(const kgat_synth *g, int64_t *offsets);
+int kgat_synth_triples(const kgat_synth *g, const int64_t *idx, int64_t count, int64_t *a, int32_t *rel,
+                       int64_t *b);
+int kgat_synth_shard_build(kgat_synth *g, int64_t lo, int64_t hi, int64_t *nnz);
+int kgat_synth_shard_copy(kgat_synth *g, int64_t *rowptr, int32_t *col, float *val);
+
 #ifdef __cplusplus
 }
 #endif

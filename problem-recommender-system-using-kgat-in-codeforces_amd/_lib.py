@@ -153,6 +153,13 @@ _SIGNATURES = {
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
+    "kgat_synth_open": (ctypes.c_int, [c_i64, c_i64, c_u64, ctypes.c_double, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "kgat_synth_close": (None, [c_vp]),
+    "kgat_synth_info": (ctypes.c_int, [c_vp, c_vp]),
+    "kgat_synth_row_offsets": (ctypes.c_int, [c_vp, c_vp]),
+    "kgat_synth_triples": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_synth_shard_build": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "kgat_synth_shard_copy": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

@@ -105,9 +105,10 @@ def metrics_at_k(cf_scores: torch.Tensor, train_interaction_dict: Mapping[int, S
 def evaluate(model, train_interaction_dict: Mapping[int, Sequence[int]],
              eval_interaction_dict: Mapping[int, Sequence[int]], item_num: int,
              k_list: Sequence[int] = METRICS_K_LIST, batch_size: int = TEST_BATCH_SIZE,
-             return_scores: bool = True):
+             return_scores: bool = True, return_per_user: bool = False):
     """main.py:70-130: returns (scores [n_eval_users, item_num] on the host or None,
-    {k: {metric: mean over users}})."""
+    {k: {metric: mean over users}}) -- plus, with return_per_user, {k: {metric: ndarray[n_eval_users]}}
+    in the eval dict's user order (what the reference averages, metrics_calculator.py:124-131)."""
     model.eval()
     tables = model.propagate()
     dev = tables[0].device
@@ -124,8 +125,10 @@ def evaluate(model, train_interaction_dict: Mapping[int, Sequence[int]],
         for k in per_k:
             for m in METRICS:
                 per_k[k][m].append(met[k][m])
-    result = {k: {m: float(np.concatenate(per_k[k][m]).mean()) for m in METRICS} for k in per_k}
-    return (torch.cat(all_scores) if return_scores else None), result
+    per_user = {k: {m: np.concatenate(per_k[k][m]) for m in METRICS} for k in per_k}
+    result = {k: {m: float(per_user[k][m].mean()) for m in METRICS} for k in per_k}
+    scores = torch.cat(all_scores) if return_scores else None
+    return (scores, result, per_user) if return_per_user else (scores, result)
 
 
 @torch.no_grad()

@@ -468,3 +468,72 @@ def synthetic_ckg(n_nodes: int, n_triples: int, seed: int = 2024, user_frac: flo
     _, first = np.unique(key, return_index=True)
     trip = trip[np.sort(first)]
     return U, E, inter, trip
+
+
+class HashedCKG:
+    """The seeded synthetic CKG of csrc/synth.cpp (C4/C5 sizes): every triple is a pure function
+    of (seed, index), so each rank builds only its own rows of the attentive matrix.
+
+    Same node layout and distributions as :func:`synthetic_ckg` (users first, items = first 10 %
+    of entities, 80 % Zipf interactions, 20 % KG triples over 4 relations); repeated triples are
+    kept and weighted by count, as the reference's coo_matrix sums them (preprocess.py:224-246).
+    """
+
+    def __init__(self, n_nodes: int, n_triples: int, seed: int = 2024, zipf_s: float = 1.1, threads: int = 0):
+        import os
+
+        threads = threads or min(16, os.cpu_count() or 1)
+        h = ctypes.c_void_p()
+        _lib.call("kgat_synth_open", int(n_nodes), int(n_triples), int(seed) & ((1 << 64) - 1), float(zipf_s),
+                  int(threads), ctypes.byref(h))
+        self._h = h
+        info = np.zeros(8, np.int64)
+        _lib.call("kgat_synth_info", self._h, info.ctypes.data)
+        self.n_nodes, self.n_triples, self.user_num, self.entity_num, self.item_num, self.n_interactions, \
+            self.n_kg = (int(x) for x in info[:7])
+
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None and h.value and _lib is not None:
+            _lib.lib().kgat_synth_close(h)
+
+    __del__ = close
+
+    def row_offsets(self) -> np.ndarray:
+        """[N+1] prefix sums of each row's pre-coalesce entry count (shard balance weights)."""
+        off = np.empty(self.n_nodes + 1, np.int64)
+        _lib.call("kgat_synth_row_offsets", self._h, off.ctypes.data)
+        return off
+
+    def triples(self, idx: np.ndarray):
+        """Raw triples by index: (a, rel, b) -- rel -1: interaction (user a, item b), else (head, rel, tail)."""
+        idx = np.ascontiguousarray(idx, np.int64)
+        a, b = np.empty(idx.size, np.int64), np.empty(idx.size, np.int64)
+        r = np.empty(idx.size, np.int32)
+        _lib.call("kgat_synth_triples", self._h, idx.ctypes.data, idx.size, a.ctypes.data, r.ctypes.data,
+                  b.ctypes.data)
+        return a, r, b
+
+    def raw(self):
+        """(user_num, entity_num, interactions [M,2], triplets [T,3]) of the whole graph (small sizes only)."""
+        a, r, b = self.triples(np.arange(self.n_triples, dtype=np.int64))
+        m = r < 0
+        inter = np.stack([a[m], b[m]], 1)
+        trip = np.stack([a[~m], r[~m].astype(np.int64), b[~m]], 1)
+        return self.user_num, self.entity_num, inter, trip
+
+    def shard(self, lo: int, hi: int):
+        """Coalesced CSR of rows [lo, hi): (rowptr [hi-lo+1] from 0, col int32 global ids, val fp32)."""
+        nnz = ctypes.c_int64()
+        _lib.call("kgat_synth_shard_build", self._h, int(lo), int(hi), ctypes.byref(nnz))
+        rowptr = np.empty(int(hi) - int(lo) + 1, np.int64)
+        col = np.empty(nnz.value, np.int32)
+        val = np.empty(nnz.value, np.float32)
+        _lib.call("kgat_synth_shard_copy", self._h, rowptr.ctypes.data, col.ctypes.data, val.ctypes.data)
+        return rowptr, col, val
+
+    def sample_interactions(self, rng: np.random.Generator, count: int):
+        """(users, items) of `count` uniformly drawn interaction triples (the bench's positives)."""
+        idx = rng.integers(0, max(self.n_interactions, 1), count)
+        a, _, b = self.triples(idx)
+        return a, b

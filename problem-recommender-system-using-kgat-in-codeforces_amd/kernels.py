@@ -71,8 +71,10 @@ def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, t
     return out
 
 
-def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
-    """Y (+)= B . X for a rectangular device CSR block B [out rows x X rows] (graph._DeviceCSR)."""
+def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+               transpose: bool = False) -> torch.Tensor:
+    """Y (+)= B . X for a rectangular device CSR block B [out rows x X rows] (graph._DeviceCSR).
+    ``transpose`` only labels the launch for SPMM_EVENTS (B is a transposed block)."""
     _req(X, "X", dim=2)
     _req(out, "out", dim=2)
     d = X.shape[1]
@@ -82,8 +84,15 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
         return out
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=X.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
     _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
               int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, transpose, ("block", int(csr.n_rows), int(csr.col.numel()), bool(accumulate))))
     return out
 
 

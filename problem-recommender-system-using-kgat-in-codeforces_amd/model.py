@@ -111,6 +111,22 @@ def _hop_record(graph, l: int, count: torch.Tensor) -> None:
     ent[1].record()
 
 
+def _check_ids(what: str, ids: list[torch.Tensor], n: int) -> None:
+    """Raise IndexError (as the reference's embedding gathers do) unless every id is in [0, n): the
+    kernels index device tables with them unchecked.  Host tensors are checked on the host; device
+    tensors by one fused min/max (one small device-to-host copy)."""
+    if not ids or all(t.numel() == 0 for t in ids):
+        return
+    if all(t.device.type == "cpu" for t in ids):
+        lo = min(int(t.min()) for t in ids if t.numel())
+        hi = max(int(t.max()) for t in ids if t.numel())
+    else:
+        flat = torch.cat([t.reshape(-1).to(ids[0].device) for t in ids])
+        lo, hi = (int(x) for x in torch.stack(torch.aminmax(flat)).tolist())
+    if lo < 0 or hi >= n:
+        raise IndexError(f"{what}: id out of range [0, {n}) (min {lo}, max {hi})")
+
+
 def _saved(tables, states, l) -> dict:
     """Layer l's forward output + saved state for the backward (none: it recomputes)."""
     return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
@@ -403,6 +419,8 @@ class KGAT(nn.Module):
     # ------------------------------------------------------------------ modes
     def _calc_cf_loss(self, user_ids, positive_item_ids, negative_item_ids) -> torch.Tensor:
         g = self.graph()
+        _check_ids("TRAIN_CF ids", [torch.as_tensor(t) for t in (user_ids, positive_item_ids, negative_item_ids)],
+                   g.n_nodes)
         drops, seeds = self._dropouts()
         cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None))
         ids = [t.to(g.device).long().contiguous() for t in (user_ids, positive_item_ids, negative_item_ids)]
@@ -412,6 +430,9 @@ class KGAT(nn.Module):
         dev = self._user_entity_embedding.weight.device
         if dev.type != "cuda":
             raise RuntimeError("KGAT runs on the MI355X HIP path only: move the model to a GPU first")
+        n = self._user_num + self._entity_num
+        _check_ids("TRAIN_KG heads/tails", [torch.as_tensor(t) for t in (heads, positive_tails, negative_tails)], n)
+        _check_ids("TRAIN_KG relations", [torch.as_tensor(relations)], self._relation_num)
         ids = [t.to(dev).long().contiguous() for t in (heads, relations, positive_tails, negative_tails)]
         return _KGLoss.apply(*ids, float(self._regularization_params[1]), self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)
@@ -444,6 +465,8 @@ class KGAT(nn.Module):
 
     def _calc_score(self, user_ids, item_ids) -> torch.Tensor:
         """Full propagation, then the fused gather + MFMA score GEMM (model.py:368-391)."""
+        _check_ids("PREDICT ids", [torch.as_tensor(user_ids), torch.as_tensor(item_ids)],
+                   self._user_num + self._entity_num)
         tables = self._propagate()
         dev = tables[0].device
         u = torch.as_tensor(user_ids).to(dev).long().contiguous()

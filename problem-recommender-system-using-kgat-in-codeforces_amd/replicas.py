@@ -94,7 +94,10 @@ class ShardedGradSync:
     ranges for ``FusedAdam.step(row_ranges=...)`` (own block + tail).  ``gather()``
     after the optimizer step all-gathers the owned blocks of the parameters."""
 
-    def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES, replicate_table: bool = False):
+    def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES, replicate_table: bool = False,
+                 force: bool = False):
+        """``force``: run the collectives even on a world of one rank (tests: RCCL at world 1)."""
+        self.force = bool(force)
         self.params = list(params)
         self.big_bytes = int(big_bytes)
         self.replicate_table = bool(replicate_table)
@@ -112,7 +115,7 @@ class ShardedGradSync:
         and calls ``block_ready`` after each, which starts block k's reduction to rank k
         (RCCL, async) while block k+1 is computed.  No-op on one rank."""
         n = world()
-        if n == 1:
+        if n == 1 and not self.force:
             return self
         table = model._user_entity_embedding.weight
         rows = table.shape[0]
@@ -159,11 +162,17 @@ class ShardedGradSync:
         d = dSc.shape[1]
         both, counts, all_sparse = self._agree(True, hcount, dSc.device)
         if all_sparse:
+            # every rank sends [cap] rows: the compact buffers hold the hop set's capacity (fused
+            # saved-state layer 0) or exactly its own count (other shapes: hop_compact(sync=True)),
+            # so pad to the largest count -- rows past a rank's count are ignored (cnt) but sized alike
             cap = max(1, max(counts))
-            pack = torch.empty(cap, 2 * d, dtype=torch.float32, device=dSc.device)
-            pack[:, :d].copy_(dSc[:cap])
-            pack[:, d:].copy_(dXdc[:cap])
-            lists = self._all_gather(hrows[:cap].contiguous())
+            k = min(cap, dSc.shape[0], hrows.numel())
+            pack = torch.zeros(cap, 2 * d, dtype=torch.float32, device=dSc.device)
+            pack[:k, :d].copy_(dSc[:k])
+            pack[:k, d:].copy_(dXdc[:k])
+            hl = torch.zeros(cap, dtype=hrows.dtype, device=hrows.device)
+            hl[:k].copy_(hrows[:k])
+            lists = self._all_gather(hl)
             vals = self._all_gather(pack).view(n * cap, 2 * d)
             cnt = both[:, 1].contiguous()
             urows, umap, ucount, urank = kernels.rows_union(graph, lists, cnt, cap)
@@ -206,7 +215,7 @@ class ShardedGradSync:
     def reduce(self) -> dict | None:
         n = world()
         self._big = []
-        if n == 1:
+        if n == 1 and not self.force:
             return None
         rank = _rank()
         ranges: dict = {}
@@ -275,7 +284,7 @@ class ShardedGradSync:
     @torch.no_grad()
     def gather(self) -> None:
         n = world()
-        if n == 1:
+        if n == 1 and not self.force:
             return
         rank = _rank()
         for p, s, main in self._big:

@@ -65,7 +65,9 @@ class _Pending:
 class Comm:
     """Ring + collectives over a torch.distributed group (rank k sends to k+1, receives from k-1)."""
 
-    def __init__(self, group=None, host_staged: bool | None = None):
+    def __init__(self, group=None, host_staged: bool | None = None, force: bool = False):
+        """``force``: collectives run even on a world of one rank (tests: RCCL at world 1)."""
+        self.force = bool(force)
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -86,7 +88,7 @@ class Comm:
         return _Pending(dist.batch_isend_irecv(ops))
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return t
         if self.host:
             c = t.detach().cpu()
@@ -98,7 +100,7 @@ class Comm:
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape], rank order."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return t.unsqueeze(0)
         if self.host:
             c = t.detach().cpu().contiguous()
@@ -123,42 +125,62 @@ def shard_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
 
 
 class RowShard:
-    """Rank k's rows of A, cut by source shard: blocks[j] = A[k][j], blocks_t[j] = A[k][j]^T."""
+    """Rank k's rows of A, cut by source shard: blocks[j] = A[k][j], blocks_t[j] = A[k][j]^T.
 
-    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, bounds: np.ndarray, rank: int, device):
+    ``local=False``: rowptr / col / val are the whole CSR (every rank holds the graph).
+    ``local=True``: they are this rank's rows only -- rowptr [hi-lo+1] from 0, global column
+    ids (graph.HashedCKG.shard: the C4/C5 sizes, where no rank holds the whole graph)."""
+
+    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, bounds: np.ndarray, rank: int, device,
+                 local: bool = False):
         self.bounds = np.asarray(bounds, np.int64)
         self.rank, self.world = rank, self.bounds.size - 1
         lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.lo, self.hi, self.n = lo, hi, hi - lo
+        self.n_nodes = int(self.bounds[-1])
         self.sizes = np.diff(self.bounds)
-        e0, e1 = int(rowptr[lo]), int(rowptr[hi])
-        lrow = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(rowptr[lo:hi + 1]))
-        lcol = col[e0:e1].astype(np.int64)
+        if local:
+            if rowptr.size != self.n + 1:
+                raise ValueError(f"local rowptr has {rowptr.size - 1} rows, shard {rank} has {self.n}")
+            lrp = np.asarray(rowptr, np.int64) - int(rowptr[0])
+            e0, e1 = int(rowptr[0]), int(rowptr[-1])
+        else:
+            lrp = np.asarray(rowptr[lo:hi + 1], np.int64) - int(rowptr[lo])
+            e0, e1 = int(rowptr[lo]), int(rowptr[hi])
+        lrow = np.repeat(np.arange(self.n, dtype=np.int32), np.diff(lrp))
+        lcol = np.asarray(col[e0:e1])
         lval = np.asarray(val[e0:e1], np.float32)
-        sid = np.searchsorted(self.bounds, lcol, side="right") - 1
+        sid = (np.searchsorted(self.bounds, lcol, side="right") - 1).astype(np.int32)
         # the local CSR (rows lo..hi, global columns): attention logits are soft-maxed here, then
         # gathered into the blocks (block_pos) and their transposes (block_t_pos)
-        self.local_rowptr = torch.from_numpy(np.ascontiguousarray(rowptr[lo:hi + 1] - rowptr[lo], np.int64)).to(device)
-        self.local_keys = lrow * int(rowptr.size - 1) + lcol  # row-major sorted (CSR order)
+        self.local_rowptr = torch.from_numpy(np.ascontiguousarray(lrp)).to(device)
+        self._lrow, self._lcol = lrow, lcol
         self.local_val = torch.from_numpy(lval.copy()).to(device)
         self.block_pos, self.block_t_pos = [], []
         self.blocks, self.blocks_t, self.nnz = [], [], []
         for j in range(self.world):
-            sel = sid == j
-            r, c, v = lrow[sel], lcol[sel] - self.bounds[j], lval[sel]
-            pos = np.flatnonzero(sel).astype(np.int32)
+            pos = np.flatnonzero(sid == j)
+            r, c, v = lrow[pos], (lcol[pos] - self.bounds[j]).astype(np.int32), lval[pos]
             nj = int(self.sizes[j])
             rp = np.zeros(self.n + 1, np.int64)
             np.cumsum(np.bincount(r, minlength=self.n), out=rp[1:])
-            self.blocks.append(_DeviceCSR(rp, c.astype(np.int32), torch.from_numpy(v.copy()).to(device), device))
+            self.blocks.append(_DeviceCSR(rp, c, torch.from_numpy(v.copy()).to(device), device))
             order = np.lexsort((r, c))
-            self.block_pos.append(torch.from_numpy(pos).to(device))
-            self.block_t_pos.append(torch.from_numpy(pos[order].copy()).to(device))
+            self.block_pos.append(torch.from_numpy(pos.astype(np.int32)).to(device))
+            self.block_t_pos.append(torch.from_numpy(pos[order].astype(np.int32)).to(device))
             rpt = np.zeros(nj + 1, np.int64)
             np.cumsum(np.bincount(c, minlength=nj), out=rpt[1:])
-            self.blocks_t.append(_DeviceCSR(rpt, r[order].astype(np.int32),
-                                            torch.from_numpy(v[order].copy()).to(device), device))
-            self.nnz.append(int(sel.sum()))
+            self.blocks_t.append(_DeviceCSR(rpt, r[order], torch.from_numpy(v[order].copy()).to(device), device))
+            self.nnz.append(int(pos.size))
+            del pos, r, c, v, order
+
+    @property
+    def local_keys(self) -> np.ndarray:
+        """row * n_nodes + col of the local CSR entries (row-major sorted; attention refresh only)."""
+        k = self.__dict__.get("_keys")
+        if k is None:
+            k = self._keys = self._lrow.astype(np.int64) * self.n_nodes + self._lcol.astype(np.int64)
+        return k
 
 
 def ring_visit(shard: RowShard, comm: Comm, X: torch.Tensor, visit) -> None:
@@ -308,7 +330,7 @@ class _ShardedCFLoss(torch.autograd.Function):
             dXd, dS, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], **saved(l))
             reduce_w(l, g)
             ring = ring_spmm_t(shard, comm, tables[l].shape[1], dev,
-                               lambda blk, out, dS=dS: kernels.spmm_block(blk, dS, out))
+                               lambda blk, out, dS=dS: kernels.spmm_block(blk, dS, out, transpose=True))
             kernels.add_(dXd, ring)
             kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dXd, row_map=rows.local)
             dX = dXd
@@ -347,17 +369,26 @@ class RowShardedKGAT(nn.Module):
     rank passes ITS OWN batch and the loss is the mean over the global batch.
     """
 
-    def __init__(self, args: KGATArgs, layout: GraphLayout, comm: Comm, device, bounds: np.ndarray | None = None):
+    def __init__(self, args: KGATArgs, layout: GraphLayout | None, comm: Comm, device,
+                 bounds: np.ndarray | None = None, shard: RowShard | None = None):
+        """``layout``: the whole graph (every rank slices its rows); or ``shard``: this rank's
+        rows already built (graph.HashedCKG at C5 size, where no rank holds the whole graph)."""
         super().__init__()
         device = torch.device(device)
         n = args.user_num + args.entity_num
-        if layout.n_nodes != n:
-            raise ValueError(f"layout has {layout.n_nodes} nodes, model has {n}")
         if device.type != "cuda":
             raise RuntimeError("RowShardedKGAT runs on the MI355X HIP path only")
         self.comm = comm
-        self.bounds = shard_bounds(layout.rowptr, comm.world) if bounds is None else np.asarray(bounds, np.int64)
-        self.shard = RowShard(layout.rowptr, layout.col, layout.val, self.bounds, comm.rank, device)
+        if shard is not None:
+            if shard.n_nodes != n or shard.world != comm.world or shard.rank != comm.rank:
+                raise ValueError(f"shard ({shard.n_nodes} nodes, rank {shard.rank}/{shard.world}) does not match "
+                                 f"the model ({n} nodes) / communicator ({comm.rank}/{comm.world})")
+            self.bounds, self.shard = shard.bounds, shard
+        else:
+            if layout.n_nodes != n:
+                raise ValueError(f"layout has {layout.n_nodes} nodes, model has {n}")
+            self.bounds = shard_bounds(layout.rowptr, comm.world) if bounds is None else np.asarray(bounds, np.int64)
+            self.shard = RowShard(layout.rowptr, layout.col, layout.val, self.bounds, comm.rank, device)
         self.lo, self.hi = self.shard.lo, self.shard.hi
         self._n_nodes = n
         self._user_num = args.user_num
@@ -403,7 +434,14 @@ class RowShardedKGAT(nn.Module):
     def _global_ids(self, *ids: torch.Tensor) -> list[np.ndarray]:
         dev = self._user_entity_embedding_shard.device
         stacked = torch.stack([t.to(dev).long().reshape(-1) for t in ids])
-        return [a.reshape(-1) for a in self.comm.all_gather(stacked).transpose(0, 1).cpu().numpy()]
+        out = [a.reshape(-1) for a in self.comm.all_gather(stacked).transpose(0, 1).cpu().numpy()]
+        return out
+
+    def _check(self, what: str, ids: list[np.ndarray], n: int) -> None:
+        """IndexError unless every id is in [0, n) (as the reference's embedding gathers)."""
+        for a in ids:
+            if a.size and (a.min() < 0 or a.max() >= n):
+                raise IndexError(f"{what}: id out of range [0, {n}) (min {a.min()}, max {a.max()})")
 
     # ------------------------------------------------------------------ modes
     def propagate(self) -> list[torch.Tensor]:
@@ -421,6 +459,7 @@ class RowShardedKGAT(nn.Module):
     def _calc_cf_loss(self, users, pos, neg) -> torch.Tensor:
         dev = self._user_entity_embedding_shard.device
         u, p, q = self._global_ids(users, pos, neg)
+        self._check("TRAIN_CF ids", [u, p, q], self._n_nodes)
         B = u.size
         rows = _BatchRows(np.concatenate([u, p, q]), self.lo, self.hi, dev)
         cu, cp, cn = (torch.from_numpy(rows.inv[i * B:(i + 1) * B]).to(dev) for i in range(3))
@@ -431,6 +470,8 @@ class RowShardedKGAT(nn.Module):
     def _calc_kg_loss(self, heads, relations, pos_tails, neg_tails) -> torch.Tensor:
         dev = self._user_entity_embedding_shard.device
         h, r, p, q = self._global_ids(heads, relations, pos_tails, neg_tails)
+        self._check("TRAIN_KG heads/tails", [h, p, q], self._n_nodes)
+        self._check("TRAIN_KG relations", [r], self._relation_embedding.weight.shape[0])
         B = h.size
         rows = _BatchRows(np.concatenate([h, p, q]), self.lo, self.hi, dev)
         ch, cp, cn = (torch.from_numpy(rows.inv[i * B:(i + 1) * B]).to(dev) for i in range(3))
@@ -512,6 +553,7 @@ class RowShardedKGAT(nn.Module):
         tables = self.propagate()
         u = torch.as_tensor(user_ids).long().reshape(-1).cpu().numpy()
         i = torch.as_tensor(item_ids).long().reshape(-1).cpu().numpy()
+        self._check("PREDICT ids", [u, i], self._n_nodes)
         rows = _BatchRows(np.concatenate([u, i]), self.lo, self.hi, dev)
         Tc = rows.gather(tables, self.comm)
         cu = torch.from_numpy(rows.inv[:u.size]).to(dev)

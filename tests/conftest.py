@@ -36,3 +36,36 @@ KGAT_CASES = ["L1_d64", "L2_d64", "L3_d64", "L3_d128"]
 @pytest.fixture(params=KGAT_CASES)
 def kgat_case(request):
     return request.param, golden("kgat_" + request.param)
+
+
+def c1_inputs(g: dict):
+    """(U, E, interactions, triplets, train dict, test dict, eval users) of the C1 (--sm shaped) fixture."""
+    U, E = int(g["user_num"]), int(g["entity_num"])
+    inter = g["interactions"].astype(np.int64)
+    trip = g["triplets"].astype(np.int64)
+    in_test = np.unpackbits(g["test_mask"])[:len(inter)].astype(bool)
+    train, test = {u: [] for u in range(U)}, {u: [] for u in range(U)}
+    for (u, i), t in zip(inter.tolist(), in_test.tolist()):
+        (test if t else train)[u].append(i)
+    train = {u: sorted(v) for u, v in train.items()}
+    test = {u: sorted(v) for u, v in test.items()}
+    return U, E, inter, trip, train, test, g["eval_users"]
+
+
+def assert_topk_with_ties(got: np.ndarray, ref: np.ndarray, ref_top_scores: np.ndarray, tol: float = 1e-5) -> int:
+    """Top-k rows equal, except rows whose reference top-(k+1) scores hold a near-tie (order of equal
+    fp32 scores is unspecified in the reference's torch.sort / topk).  Returns the excused row count."""
+    excused = 0
+    for r in np.nonzero((got != ref).any(1))[0]:
+        gaps = np.abs(np.diff(ref_top_scores[r]))
+        assert gaps.min() < tol, (r, got[r], ref[r], gaps.min())
+        excused += 1
+    return excused
+
+
+def assert_metrics_with_ties(got: dict, g: dict, k: int, ref_top_scores: np.ndarray, tol: float = 1e-5) -> None:
+    """Per-user precision / recall / nDCG@k equal the reference's, except near-tie rows (as above)."""
+    for m in ("precision", "recall", "ndcg"):
+        a, b = np.asarray(got[m]), g[f"metrics/{k}/{m}"]
+        for r in np.nonzero(~np.isclose(a, b, rtol=1e-5, atol=1e-7, equal_nan=True))[0]:
+            assert np.abs(np.diff(ref_top_scores[r])).min() < tol, (m, r, a[r], b[r])

@@ -36,8 +36,12 @@ def main() -> None:
     rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
     U, E, inter, trip = graph.synthetic_ckg(20001, 160000, seed=9)  # odd row count: a tail row
     lay = graph.build_layout(U, E, inter, trip)
-    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
-                        message_dropout=[0.1, 0.1])
+    # DP_WORKER_DIMS="128:128,64": a 128-wide layer 0 (no fused saved-state backward: its hop set is
+    # listed with hop_compact(sync=True), so the compact buffers hold exactly each rank's own count)
+    dims = os.environ.get("DP_WORKER_DIMS", "64:64,32")
+    d0, layer_size = int(dims.split(":")[0]), [int(x) for x in dims.split(":")[1].split(",")]
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layer_size,
+                        cf_embedding_dim=d0, kg_embedding_dim=d0, message_dropout=[0.1] * len(layer_size))
     models = []
     model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
     for _ in range(5):

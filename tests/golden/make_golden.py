@@ -220,6 +220,86 @@ def make_kgat_case(name: str, users: int, problems: int, contests: int, tags: in
           f"-> {(OUT / f'kgat_{name}.npz').stat().st_size / 1e6:.2f} MB")
 
 
+def make_c1_case(name: str = "C1_sm", users: int = 500, problems: int = 9500, contests: int = 1913, tags: int = 37,
+                 ratings: int = 28, cf_steps: int = 2) -> None:
+    """BASELINE configs[0] shape (the --sm dataset: 500 users, ~9.5k problems, 1,913 contests, 37 tags,
+    28 ratings; 1 KGAT layer, d = 64), ~1M nnz: heavy users with hundreds of solved problems.
+    Records only what a GPU run cannot recompute: the reference's CF losses (eval mode), its top-20
+    after an attention refresh, the 21 largest masked scores per user (the near-tie rule) and its own
+    precision / recall / nDCG@20 per user.  Initial weights are torch.manual_seed(2024)'s (the HIP
+    module creates its parameters in the reference's order, tested)."""
+    rng = np.random.default_rng(SEED + 1000)
+    divisions = 5
+    c0, d0 = problems, problems + contests
+    t0 = d0 + divisions
+    r0 = t0 + tags
+    entity_num = r0 + ratings
+    trip = set()
+    for p in range(problems):
+        trip.add((p, RelationType.IN_CONTEST.value, c0 + int(rng.integers(contests))))
+        for tg in rng.choice(tags, size=int(rng.integers(0, 5)), replace=False):
+            trip.add((p, RelationType.TAGGED.value, t0 + int(tg)))
+        if rng.random() < 0.85:
+            trip.add((p, RelationType.HAS_DIFFICULTY.value, r0 + int(rng.integers(ratings))))
+    for c in range(contests):
+        if rng.random() < 0.77:
+            trip.add((c0 + c, RelationType.HAS_CONTEST_DIVISION.value, d0 + int(rng.integers(divisions))))
+    pop = 1.0 / np.arange(1, problems + 1) ** 0.9
+    pop = pop[rng.permutation(problems)]
+    pop /= pop.sum()
+    inter = []
+    for u in range(users):
+        k = int(min(problems - 1, max(10, rng.lognormal(6.8, 0.6))))  # >= 10 per user (the scraper's floor)
+        inter += [(u, int(p)) for p in rng.choice(problems, size=k, replace=False, p=pop)]
+    inter = np.array(inter, np.int64)
+    trip = np.array(sorted(trip), np.int64)
+    pp, A, (heads, rels, tails, vals) = reference_graph(users, entity_num, inter, trip)
+    n = users + entity_num
+    train, test = split(rng, inter, users)
+    in_test = np.zeros(len(inter), bool)
+    test_keys = {(u, i) for u in test for i in test[u]}
+    for j, (u, i) in enumerate(inter):
+        in_test[j] = (int(u), int(i)) in test_keys
+    rec = {"user_num": np.array(users), "item_num": np.array(problems), "entity_num": np.array(entity_num),
+           "interactions": inter.astype(np.int32), "triplets": trip.astype(np.int32),
+           "test_mask": np.packbits(in_test), "nnz": np.array(A.coalesce().values().numel())}
+    torch.manual_seed(SEED)
+    model = KGAT(KGATArgs(user_num=users, entity_num=entity_num, relation_num=len(pp.adjacency_relations),
+                          cf_embedding_dim=64, kg_embedding_dim=64, attentive_matrix=A, layer_size=[64],
+                          message_dropout=[0.1]))
+    model.eval()
+    model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    for s in range(cf_steps):
+        u = torch.LongTensor(rng.choice(users, size=256, replace=False))
+        p = torch.LongTensor([int(rng.choice(train[int(x)])) for x in u])
+        q = torch.LongTensor(rng.integers(0, problems, size=256))
+        loss = model(u, p, q, mode=KGATMode.TRAIN_CF)
+        loss.backward()
+        model.update_cf_weights()
+        rec[f"cf{s}/users"], rec[f"cf{s}/pos"], rec[f"cf{s}/neg"] = u.numpy(), p.numpy(), q.numpy()
+        rec[f"cf{s}/loss"] = np.array(loss.item(), np.float32)
+    model(torch.tensor(heads), torch.tensor(rels), torch.tensor(tails), torch.tensor(pp.adjacency_relations),
+          mode=KGATMode.UPDATE_ATTENTION)
+    eval_users = np.array([u for u in range(users) if test[u]], np.int64)
+    items = torch.arange(problems)
+    with torch.no_grad():
+        sc = model(torch.LongTensor(eval_users), items, mode=KGATMode.PREDICT)
+    met = metrics_at_k(sc.clone(), train, test, eval_users, items.numpy(), [20])
+    masked = sc.clone()
+    for i, u in enumerate(eval_users):
+        masked[i, train[int(u)]] = -np.inf
+    top = torch.topk(masked, k=21, dim=1)
+    rec["eval_users"] = eval_users
+    rec["topk20"] = top.indices[:, :20].numpy().astype(np.int32)
+    rec["top21_scores"] = top.values.numpy()
+    for m, v in met[20].items():
+        rec[f"metrics/20/{m.value}"] = np.asarray(v, np.float64)
+    rec["recall20_mean"] = np.array(float(np.mean(met[20][[m for m in met[20] if m.value == "recall"][0]])))
+    np.savez_compressed(OUT / f"kgat_{name}.npz", **rec)
+    print(f"kgat_{name}: N={n} interactions={len(inter)} E={len(heads)} nnz(A)={int(rec['nnz'])} "
+          f"recall@20={float(rec['recall20_mean']):.4f} -> {(OUT / f'kgat_{name}.npz').stat().st_size / 1e6:.2f} MB")
+
+
 def make_nfm_case(name: str, users: int, problems: int, contests: int, tags: int, ratings: int,
                   dim: int, hidden: list[int]) -> None:
     rng = np.random.default_rng(SEED + 100 + len(name))
@@ -275,6 +355,9 @@ def make_nfm_case(name: str, users: int, problems: int, contests: int, tags: int
 
 if __name__ == "__main__":
     torch.set_num_threads(4)
+    if "--c1" in sys.argv:  # the C1 (--sm shaped) ranking fixture only
+        make_c1_case()
+        sys.exit(0)
     make_kgat_case("L1_d64", users=96, problems=200, contests=40, tags=16, ratings=8, dim=64, layers=[64])
     make_kgat_case("L3_d64", users=96, problems=200, contests=40, tags=16, ratings=8, dim=64,
                    layers=[64, 32, 16])

@@ -1,0 +1,41 @@
+"""bench.py's launch contract on the CPU (no GPU): --gpus N spawns N ranks that join one process
+group, and the row-sharded C5 config refuses a world it does not fit."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+from tests.conftest import ROOT
+
+
+def _run(*args, timeout=180):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], cwd=ROOT, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_gpus_2_launches_two_ranks():
+    p = _run("--gpus", "2", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout
+    rec = json.loads(line[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_joined"] == 2
+
+
+def test_c5_refuses_one_gpu_cleanly():
+    p = _run("--config", "c5", "--gpus", "1")
+    assert p.returncode == 2
+    assert "needs >= 4 GPUs" in p.stderr
+    assert not p.stdout.strip()
+
+
+def test_c5_world4_dry_run_accepted():
+    p = _run("--config", "c5", "--gpus", "4", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert rec["ranks_joined"] == 4 and rec["mode"] == "sharded"

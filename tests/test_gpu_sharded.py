@@ -117,3 +117,35 @@ def test_dp_sharded_grad_sync_world2_matches_allreduce():
     log.parent.mkdir(exist_ok=True)
     log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+
+
+def test_dp_replicated_exchange_wide_layer0_world2():
+    """a 128-wide layer 0 (128 -> 128, no fused saved-state backward) under
+    ShardedGradSync(replicate_table=True): each rank's compact hop buffers hold exactly its own
+    (different) hop count, so the hop-set all-gather must pad to the largest; paths A-E as in
+    tests/dp_worker.py, with d = 128 and layers [128, 64]."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    env["DP_WORKER_DIMS"] = "128:128,64"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / "dp_world2_wide.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+
+
+def test_rccl_world1_collectives_match_gloo():
+    """every collective of replicas.py / sharded.py through RCCL (backend "nccl",
+    world 1 on the box's GPU, forced) vs the gloo / no-exchange paths (tests/rccl_worker.py)."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "rccl_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / "rccl_world1.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert "rccl world1: OK" in p.stdout, p.stdout[-2000:]

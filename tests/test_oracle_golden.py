@@ -6,6 +6,7 @@ The golden vectors were produced by the reference classes themselves
 from __future__ import annotations
 
 import numpy as np
+import pytest
 import torch
 
 from oracle import kgat_cpu as K
@@ -179,3 +180,45 @@ def test_nfm():
     users = g["pred_users"]
     x = batch(np.repeat(users, I), np.tile(np.arange(I), len(users)))
     np.testing.assert_allclose(K.nfm_score(P, x).detach().numpy(), g["pred_scores"], rtol=RTOL, atol=1e-5)
+
+
+def test_c1_sm_shaped_pipeline():
+    """C1 scale (BASELINE configs[0] shape: 500 users, 9.5k problems, 1.18M nnz, 1 layer, d=64): two CF
+    steps + Adam, the attention refresh on all 1.18M edges, PREDICT and the top-20 / P/R/nDCG@20 of
+    every eval user -- against the reference's own run (tests/golden/make_golden.py --c1)."""
+    from tests.conftest import assert_metrics_with_ties, assert_topk_with_ties, c1_inputs, load_pkg
+
+    g = golden("kgat_C1_sm")
+    U, E, inter, trip, train, test, eval_users = c1_inputs(g)
+    n = U + E
+    blocks, rel_ids = K.adjacency_blocks(U, [0, 1, 2, 3], inter, trip)
+    lap = K.normalized_blocks(n, blocks)
+    A = K.initial_attentive(n, lap)
+    assert A._nnz() == int(g["nnz"])
+    heads, rels, tails, _ = K.kg_edge_arrays(lap, rel_ids)
+    pkg = load_pkg()  # the drop-in module creates its parameters in the reference's RNG order (CPU only)
+    torch.manual_seed(2024)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(rel_ids), layer_size=[64],
+                              message_dropout=[0.1]))
+    P = {k: v.detach().clone() for k, v in m.state_dict().items() if not v.is_sparse}
+    opt = K.AdamOracle(lr=1e-3)
+    for s in range(2):
+        cf = {k: v.clone().requires_grad_(True) for k, v in P.items()
+              if k == K.EMB or k.startswith("_aggregator")}
+        loss = K.cf_loss(torch.cat(K.propagate(cf, A), 1),
+                         *(torch.from_numpy(g[f"cf{s}/{x}"]) for x in ("users", "pos", "neg")))
+        loss.backward()
+        np.testing.assert_allclose(loss.item(), g[f"cf{s}/loss"], rtol=1e-5)
+        opt.step(P, {k: v.grad.detach() for k, v in cf.items()})
+    att = K.refresh_attention(P, torch.from_numpy(heads), torch.from_numpy(rels), torch.from_numpy(tails),
+                              rel_ids, n)
+    emb = torch.cat(K.propagate(P, att), 1)
+    sc = K.scores(emb, torch.from_numpy(eval_users), torch.arange(int(g["item_num"])))
+    masked = sc.clone()
+    for r, u in enumerate(eval_users):
+        masked[r, train[int(u)]] = -np.inf
+    top = torch.topk(masked, k=20, dim=1).indices.numpy()
+    assert_topk_with_ties(top, g["topk20"], g["top21_scores"])
+    _, met = K.ranking_metrics(sc, train, test, eval_users, [20])
+    assert_metrics_with_ties(met[20], g, 20, g["top21_scores"])
+    assert float(np.mean(met[20]["recall"])) == pytest.approx(float(g["recall20_mean"]), abs=1e-9)

@@ -1,4 +1,4 @@
-"""Parse the two rocprofv3 --pmc passes of tools/pmc_spmm.sh into profiles/pmc_c2.json.
+"""Parse the two rocprofv3 --pmc passes of tools/pmc_bench.sh / pmc_spmm.sh into profiles/pmc_<cfg>.json.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
 the bytes of a wide (16 B/lane) coalesced read -- the SpMM's row gathers are
@@ -27,11 +27,13 @@ def per_kernel(path_glob, counter):
 
 def main():
     src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+    cmd = sys.argv[3] if len(sys.argv) > 3 else "tools/bench_kernels.py --only spmm"
     fetch = per_kernel(str(src / "FETCH_SIZE" / "**" / "*counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(str(src / "WRITE_SIZE" / "**" / "*counter_collection.csv"), "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), tools/bench_kernels.py --only spmm",
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {cmd}",
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes", "kernels": {}}
     main_k = fix_k = None
+    d0 = int(sys.argv[4]) if len(sys.argv) > 4 else 64  # the forward SpMM's width (the bench's embed_dim)
     for name in set(fetch) | set(write):
         f = fetch.get(name, [])
         w = write.get(name, [])
@@ -40,9 +42,9 @@ def main():
         rec = {"launches": len(f), "fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
         rec["hbm_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
         out["kernels"][name] = rec
-        if "spmm_main_kernel<64, 0>" in name:
+        if f"spmm_main_kernel<{d0}, 0>" in name:
             main_k = rec
-        if "spmm_fixup_kernel<64, 0>" in name:
+        if f"spmm_fixup_kernel<{d0}, 0>" in name:
             fix_k = rec
     if main_k:
         out["spmm_fwd_hbm_bytes_per_launch"] = main_k["hbm_bytes"] + (fix_k["hbm_bytes"] if fix_k else 0.0)
