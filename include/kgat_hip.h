@@ -238,10 +238,24 @@ int kgat_biinter_bwd_hop_f32(const float *X, int64_t ldx, const float *S, int64_
                              int32_t d_in, int32_t d_out, float dropout_p, float *workspace,
                              int64_t workspace_floats, void *stream);
 
+/* The dense fp32 contractions of the wide layers (a2 / a6 at d = 128 / 256: W1, W2,
+ * W_r, W_v, W_o products and the split-K weight-gradient slabs), hand-written MFMA
+ * (v_mfma_f32_32x32x2_f32, 128 x 128 block tiles, deterministic k order):
+ *   C[m, n] (+)= sum_k op(A)[m, k] op(B)[k, n], row-major;
+ *   op(A) = A [m, k] (lda) or, trans_a, A^T of A stored [k, m];
+ *   op(B) = B [k, n] (ldb) or, trans_b, B^T of B stored [n, k];
+ *   batch z: A + z*stride_a, B + z*stride_b, C + z*stride_c.
+ * lda, ldb, strides and bases 16-byte aligned; each operand's contiguous dimension a
+ * multiple of 4.  Replaces the vendor sgemm a torch port would call for
+ * nn.Linear at aggregator.py:57-60 and the bmm / Linear of model.py:271-303. */
+int kgat_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t m, int64_t n, int64_t k, const float *A, int64_t lda,
+                  int64_t stride_a, const float *B, int64_t ldb, int64_t stride_b, float *C, int64_t ldc,
+                  int64_t stride_c, int64_t batch, int32_t accumulate, void *stream);
+
 /* a2 for the wide layers of C4/C5 (any d_in, d_out multiple of 16 up to 1024; used
- * where the fused kernels above do not dispatch, e.g. 256): two rocBLAS sgemm per
- * direction (atomics off: deterministic) around fused HIP epilogues, same
- * arithmetic and the same dropout draws as kgat_biinter_fwd_f32.
+ * where the fused kernels above do not dispatch, e.g. 256): two kgat_gemm_f32 products
+ * per direction around fused HIP epilogues, same arithmetic and the same dropout
+ * draws as kgat_biinter_fwd_f32.
  * state (float [kgat_biinter_gemm_state_floats]) is written by the forward
  * (pre-activations + row norms) and consumed (overwritten) by the backward;
  * work (float [kgat_biinter_gemm_work_floats]) is scratch for either call.
@@ -387,7 +401,7 @@ int kgat_row_softmax_ex_f32(const int64_t *rowptr, int64_t n_rows, const int32_t
                             const float *slot_logits, float *val, void *stream);
 
 /* a6 for wide embeddings (d > 128, multiple of 16, <= 1024; C5's 256): the edge scorer
- * of kgat_edge_logits_f32 as rocBLAS GEMMs over chunks of the relation-sorted edge
+ * of kgat_edge_logits_f32 as kgat_gemm_f32 products over chunks of the relation-sorted edge
  * order plus fused HIP epilogues -- same arithmetic, dropout keys and output placement.
  * seg_rel / seg_beg (HOST arrays): relation of each run of rel_perm and the runs'
  * start positions (n_seg + 1 entries, last = n_edges).  work: float
@@ -487,6 +501,19 @@ int kgat_adam_multi_f32(const kgat_adam_tensor *tensors, int32_t count, float be
 
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);
+
+/* Id validation without a host synchronisation (the reference's embedding gathers raise
+ * IndexError, src/model/KGAT/model.py:188-191, 219-222, 389-391): the ids of up to
+ * KGAT_IDS_MAX int64 arrays are copied, concatenated, into out; an id outside [0, bound)
+ * is written as 0 (so no later kernel indexes out of range) and sets *bad to 1 (the caller
+ * zeroes it and reads it back asynchronously). */
+#define KGAT_IDS_MAX 4
+typedef struct kgat_ids {
+  const int64_t *ptr[KGAT_IDS_MAX];
+  int64_t n[KGAT_IDS_MAX];
+  int32_t count;
+} kgat_ids;
+int kgat_ids_check(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *bad, void *stream);
 
 /* Fill n floats with a value. */
 int kgat_fill_f32(float *dst, int64_t n, float value, void *stream);

@@ -46,6 +46,15 @@ class Tables(ctypes.Structure):
                 ("width", c_i32 * KGAT_MAX_TABLES), ("count", c_i32)]
 
 
+KGAT_IDS_MAX = 4
+
+
+class Ids(ctypes.Structure):
+    """Mirror of ``kgat_ids``."""
+
+    _fields_ = [("ptr", c_vp * KGAT_IDS_MAX), ("n", c_i64 * KGAT_IDS_MAX), ("count", c_i32)]
+
+
 KGAT_NFM_MAX_LAYERS = 4
 
 
@@ -153,6 +162,9 @@ _SIGNATURES = {
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
+    "kgat_ids_check": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp]),
+    "kgat_gemm_f32": (ctypes.c_int, [c_i32, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                     c_i64, c_i64, c_i64, c_i32, c_vp]),
     "kgat_synth_open": (ctypes.c_int, [c_i64, c_i64, c_u64, ctypes.c_double, ctypes.c_int, ctypes.POINTER(c_vp)]),
     "kgat_synth_close": (None, [c_vp]),
     "kgat_synth_info": (ctypes.c_int, [c_vp, c_vp]),

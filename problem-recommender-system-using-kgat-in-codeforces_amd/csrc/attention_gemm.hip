@@ -1,20 +1,19 @@
 // a6 for the wide embeddings of C5 (d > 128, e.g. 256): the edge scorer of
 // attention.hip (src/model/KGAT/model.py:263-316, multi_head_attention.py:35-58)
-// as library GEMMs over relation-sorted edge chunks plus fused HIP epilogues.
+// as GEMMs over relation-sorted edge chunks plus fused HIP epilogues.
 // At d = 256 three d x d matrices no longer fit a CU's LDS beside a tile, so:
 //   per chunk of the relation-sorted edge order (rel_perm):
 //     T  = emb[tail]                      (gather_edge_rows_kernel)
-//     T' = T W_r   per relation segment   (rocBLAS sgemm)
-//     V  = T' W_v^T, + b_v, per-(edge, head) attention dropout  (sgemm, bias_drop_kernel)
-//     O  = V W_o^T                        (sgemm)
+//     T' = T W_r   per relation segment   (gemm_f32, gemm.hip)
+//     V  = T' W_v^T, + b_v, per-(edge, head) attention dropout  (gemm_f32, bias_drop_kernel)
+//     O  = V W_o^T                        (gemm_f32)
 //     logit = sum tanh(LayerNorm(O + b_o)) * degree weight      (ln_logit_kernel)
 // Same arithmetic, dropout keys (edge * 8 + head) and output placement
-// (out_pos or edge order) as kgat_edge_logits_f32.  rocBLAS atomics are off.
-#include <rocblas/rocblas.h>
-
+// (out_pos or edge order) as kgat_edge_logits_f32.
 #include <cmath>
 
 #include "common.hpp"
+#include "gemm.hpp"
 
 namespace kgat {
 
@@ -84,18 +83,6 @@ __global__ __launch_bounds__(256) void ln_logit_kernel(const float* __restrict__
   }
 }
 
-static rocblas_handle att_blas(hipStream_t st) {
-  static rocblas_handle h[16] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  if (h[dev] == nullptr) {
-    if (rocblas_create_handle(&h[dev]) != rocblas_status_success) return nullptr;
-    rocblas_set_atomics_mode(h[dev], rocblas_atomics_not_allowed);
-  }
-  rocblas_set_stream(h[dev], st);
-  return h[dev];
-}
-
 }  // namespace kgat
 
 extern "C" int64_t kgat_edge_logits_gemm_work_floats(int64_t chunk_edges, int32_t d) {
@@ -119,12 +106,9 @@ extern "C" int kgat_edge_logits_gemm_f32(const float* emb, int64_t ld_emb, int64
   if (!work || work_floats < 2 * 16 * static_cast<int64_t>(d)) return KGAT_ERR_WORKSPACE;
   const int64_t chunk = work_floats / (2 * static_cast<int64_t>(d));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  rocblas_handle h = kgat::att_blas(st);
-  if (!h) return KGAT_ERR_INVALID;
   float* T = work;                // gathered tails, later O
   float* P = work + chunk * d;    // T W_r, later V
   float* V = T;
-  const float one = 1.f, zero = 0.f;
   int sg = 0;
   for (int64_t c0 = 0; c0 < n_edges; c0 += chunk) {
     const int64_t c1 = c0 + chunk < n_edges ? c0 + chunk : n_edges;
@@ -139,22 +123,17 @@ extern "C" int kgat_edge_logits_gemm_f32(const float* emb, int64_t ld_emb, int64
       const int64_t b = seg_beg[s + 1] < c1 ? seg_beg[s + 1] : c1;
       if (b <= a) continue;
       const float* Wr = trans + static_cast<int64_t>(seg_rel[s]) * d * d;
-      // row-major [m, d] x [d, d]: column-major P^T = Wr^T-view(N) x T^T-view
-      if (rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d, static_cast<int>(b - a), d, &one, Wr,
-                        d, T + (a - c0) * d, d, &zero, P + (a - c0) * d, d) != rocblas_status_success)
-        return KGAT_ERR_INVALID;
+      if (int e = kgat::gemm_f32(false, false, b - a, d, d, T + (a - c0) * d, d, 0, Wr, d, 0, P + (a - c0) * d, d, 0,
+                                 1, false, st))
+        return e;
     }
     // V = T' W_v^T (+ b_v, dropout) into T's buffer
-    if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d, static_cast<int>(rows), d, &one, Wv, d,
-                      P, d, &zero, V, d) != rocblas_status_success)
-      return KGAT_ERR_INVALID;
+    if (int e = kgat::gemm_f32(false, true, rows, d, d, P, d, 0, Wv, d, 0, V, d, 0, 1, false, st)) return e;
     hipLaunchKernelGGL(kgat::bias_drop_kernel, dim3(kgat::blocks_for(rows * d, 256, kgat::kCUs * 8)), dim3(256), 0, st,
                        V, bv, rel_perm, c0, rows, d, dropout_p, seed);
     KGAT_LAUNCH_CHECK();
     // O = V W_o^T into P's buffer
-    if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d, static_cast<int>(rows), d, &one, Wo, d,
-                      V, d, &zero, P, d) != rocblas_status_success)
-      return KGAT_ERR_INVALID;
+    if (int e = kgat::gemm_f32(false, true, rows, d, d, V, d, 0, Wo, d, 0, P, d, 0, 1, false, st)) return e;
     hipLaunchKernelGGL(kgat::ln_logit_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, P, bo, ln_w, ln_b, edge_weight,
                        rel_perm, c0, rows, d, out_pos, out);
     KGAT_LAUNCH_CHECK();

@@ -1,25 +1,24 @@
 // a2 for the wide layers of C4/C5 (d_in or d_out of 256): the bi-interaction as
-// two library GEMMs plus fused HIP epilogues (src/model/KGAT/aggregator.py:57-65).
+// two GEMMs plus fused HIP epilogues (src/model/KGAT/aggregator.py:57-65).
 //
 // At these widths the layer is MFMA-bound (4*d_in*d_out flop per row against
 // 4*(2*d_in + d_out) bytes) and a whole row of both products no longer fits a
-// wave's registers, so the contractions go to rocBLAS sgemm (fp32, MFMA, atomics
-// off => deterministic) and everything around them is ours:
+// wave's registers, so the contractions run as the hand-written fp32 MFMA GEMM of
+// gemm.hip (deterministic k order) and everything around them is fused here:
 //   forward:  U = X+S, M = X*S                                   (um_kernel)
-//             P1 = U W1^T, P2 = M W2^T                           (rocBLAS)
+//             P1 = U W1^T, P2 = M W2^T                           (gemm_f32)
 //             H = normalize(dropout(LReLU(P1+b1) + LReLU(P2+b2))) (epi_fwd_kernel,
 //             keeps P+b and the row norm as the backward's state)
 //   backward: dA, dB from H, dH, the norm, the signs of P+b       (epi_bwd_kernel)
-//             du = dA W1, dm = dB W2                             (rocBLAS, into dXd / dS)
+//             du = dA W1, dm = dB W2                             (gemm_f32, into dXd / dS)
 //             dXd = du + dm*S, dS = du + dm*X                    (dxs_kernel, in place)
-//             dW1 = dA^T U, dW2 = dB^T M, db = column sums        (rocBLAS gemm / gemv)
+//             [dW | db] = dA^T [U | 1], dB^T [M | 1]              (gemm_f32 split-K slabs)
 // Dropout draws are the fused kernels' (one 64-bit hash per node, 16-column
 // group of 4 blocks), so both paths drop the same elements.
-#include <rocblas/rocblas.h>
-
 #include <utility>
 
 #include "common.hpp"
+#include "gemm.hpp"
 
 namespace kgat {
 
@@ -188,28 +187,9 @@ constexpr int64_t kGemmChunk = 65536;  // rows per split-K chunk of the weight-g
 
 inline int64_t wslab_count(int64_t n) { return (n + kGemmChunk - 1) / kGemmChunk; }
 
-static rocblas_handle blas_handle(hipStream_t st, int* err) {
-  static rocblas_handle h[16] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
-    *err = KGAT_ERR_INVALID;
-    return nullptr;
-  }
-  if (h[dev] == nullptr) {
-    if (rocblas_create_handle(&h[dev]) != rocblas_status_success) {
-      *err = KGAT_ERR_INVALID;
-      return nullptr;
-    }
-    rocblas_set_atomics_mode(h[dev], rocblas_atomics_not_allowed);  // deterministic reductions
-  }
-  rocblas_set_stream(h[dev], st);
-  *err = 0;
-  return h[dev];
-}
-
-#define KGAT_BLAS(call)                                  \
-  do {                                                   \
-    if ((call) != rocblas_status_success) return KGAT_ERR_INVALID; \
+#define KGAT_GEMM(call)                \
+  do {                                 \
+    if (int e_ = (call)) return e_;    \
   } while (0)
 
 }  // namespace kgat
@@ -225,11 +205,10 @@ static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d
 
 // du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, [dW | db] = dA^T [U | 1]
 // (split-K over row chunks, slabs summed in chunk order); U, M and the slabs live in work.
-static int bwd_gemm_tail(rocblas_handle h, const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
-                         const float* W2, const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS,
-                         int64_t ldds, float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
-                         int32_t d_out, float* work, hipStream_t st) {
-  const float one = 1.f, zero = 0.f;
+static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* W2,
+                         const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
+                         float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in, int32_t d_out,
+                         float* work, hipStream_t st) {
   const int ldu = d_in + 4;
   float* U = work;
   float* M = work + n * ldu;
@@ -237,32 +216,28 @@ static int bwd_gemm_tail(rocblas_handle h, const float* X, int64_t ldx, const fl
   float* slab1 = work + 2 * n * ldu;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
-                          W1, d_in, dA, d_out, &zero, dXd, static_cast<int>(lddxd)));
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, d_in, static_cast<int>(n), d_out, &one,
-                          W2, d_in, dB, d_out, &zero, dS, static_cast<int>(ldds)));
+  KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
+  KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
   hipLaunchKernelGGL(um_kernel, dim3(blocks_for(n * (d_in / 4 + 1), 256, kCUs * 8)), dim3(256), 0,
                      st, X, ldx, S, lds, U, M, n, d_in);
   KGAT_LAUNCH_CHECK();
   hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
                      lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
   KGAT_LAUNCH_CHECK();
-  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order)
-  //   column-major C_b[ldu, d_out] = U'_b-view[ldu, k] x dA_b-view^T[k, d_out]
+  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order):
+  //   slab_b[d_out, ldu] = dA_b[chunk, d_out]^T . U_b[chunk, ldu]
   const int64_t full = n / kGemmChunk, rest = n - full * kGemmChunk;
   for (int mat = 0; mat < 2; ++mat) {
     const float* Um = mat == 0 ? U : M;
     const float* G = mat == 0 ? dA : dB;
     float* sl = mat == 0 ? slab1 : slab2;
     if (full > 0)
-      KGAT_BLAS(rocblas_sgemm_strided_batched(
-          h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(kGemmChunk), &one,
-          Um, ldu, kGemmChunk * ldu, G, d_out, kGemmChunk * d_out, &zero, sl, ldu,
-          static_cast<int64_t>(ldu) * d_out, static_cast<int>(full)));
+      KGAT_GEMM(gemm_f32(true, false, d_out, ldu, kGemmChunk, G, d_out, kGemmChunk * d_out, Um, ldu,
+                         kGemmChunk * ldu, sl, ldu, static_cast<int64_t>(ldu) * d_out, full, false, st));
     if (rest > 0)
-      KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, ldu, d_out, static_cast<int>(rest),
-                              &one, Um + full * kGemmChunk * ldu, ldu, G + full * kGemmChunk * d_out, d_out,
-                              &zero, sl + full * ldu * static_cast<int64_t>(d_out), ldu));
+      KGAT_GEMM(gemm_f32(true, false, d_out, ldu, rest, G + full * kGemmChunk * d_out, d_out, 0,
+                         Um + full * kGemmChunk * ldu, ldu, 0, sl + full * ldu * static_cast<int64_t>(d_out), ldu, 0,
+                         1, false, st));
     hipLaunchKernelGGL(wslab_reduce_kernel, dim3((d_out * (d_in + 1) + 255) / 256), dim3(256), 0, st, sl,
                        static_cast<int>(nb), d_in, d_out, mat == 0 ? dW1 : dW2, mat == 0 ? db1 : db2);
     KGAT_LAUNCH_CHECK();
@@ -308,15 +283,9 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
                      st, X, ldx, S, lds, U, M, n, d_in);
   KGAT_LAUNCH_CHECK();
-  int err = 0;
-  rocblas_handle h = kgat::blas_handle(st, &err);
-  if (err) return err;
-  const float one = 1.f, zero = 0.f;
-  // row-major P[n, o] = U[n, k] W^T  <=>  column-major P^T[o, n] = W^T[o, k] ... (W row-major = W^T col-major)
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
-                          &one, W1, d_in, U, ldu, &zero, P1, d_out));
-  KGAT_BLAS(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, d_out, static_cast<int>(n), d_in,
-                          &one, W2, d_in, M, ldu, &zero, P2, d_out));
+  // P[n, o] = U[n, k] . W[o, k]^T
+  KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
+  KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh, norm, n, d_out,
                      dropout_p, seed);
   KGAT_LAUNCH_CHECK();
@@ -337,9 +306,6 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
     return KGAT_ERR_INVALID;
   if (!work || work_floats < kgat_biinter_gemm_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int err = 0;
-  rocblas_handle h = kgat::blas_handle(st, &err);
-  if (err) return err;
   if (n == 0) return kgat::zero_wgrads(dW1, db1, dW2, db2, d_in, d_out, st);
   float* dA = state;
   float* dB = state + n * d_out;
@@ -347,7 +313,7 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
   hipLaunchKernelGGL(kgat::epi_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, dH, lddh, n,
                      d_out, dropout_p, seed, key_rows);
   KGAT_LAUNCH_CHECK();
-  return kgat::bwd_gemm_tail(h, X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
+  return kgat::bwd_gemm_tail(X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
                              d_out, work, st);
 }
 
@@ -371,15 +337,12 @@ extern "C" int kgat_biinter_bwd_gemm_bits_f32(const float* X, int64_t ldx, const
     return KGAT_ERR_INVALID;
   if (!work || work_floats < kgat_biinter_gemm_bits_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int err = 0;
-  rocblas_handle h = kgat::blas_handle(st, &err);
-  if (err) return err;
   if (n == 0) return kgat::zero_wgrads(dW1, db1, dW2, db2, d_in, d_out, st);
   float* dA = work + kgat_biinter_gemm_work_floats(n, d_in, d_out);
   float* dB = dA + n * d_out;
   hipLaunchKernelGGL(kgat::epi_bwd_bits_kernel, dim3((n + 3) / 4), dim3(256), 0, st, dA, dB, H, ldh, norm, mask, dH,
                      lddh, n, d_out, dropout_p, key_rows);
   KGAT_LAUNCH_CHECK();
-  return kgat::bwd_gemm_tail(h, X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
+  return kgat::bwd_gemm_tail(X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
                              d_out, work, st);
 }

@@ -1,0 +1,207 @@
+// Hand-written fp32 MFMA GEMM for gfx950 -- the plain contractions of the wide layers
+// (d = 128 / 256 at C4 / C5): the bi-interaction's W1 / W2 products and their backward
+// (src/model/KGAT/aggregator.py:57-65), the weight gradients' split-K slabs, and the edge
+// scorer's T . W_r, W_v, W_o products (src/model/KGAT/model.py:263-316).  Replaces the
+// vendor sgemm: no library GEMM runs on the hot path.
+//
+//   C[m, n] (+)= sum_k op(A)[m, k] * op(B)[k, n]      (row-major, fp32 in / fp32 out)
+//   op(A) = A [M, K] (lda)  or, TA, A^T with A stored [K, M]
+//   op(B) = B [K, N] (ldb)  or, TB, B^T with B stored [N, K]
+//   batched: blockIdx.z selects A + z*sA, B + z*sB, C + z*sC.
+//
+// Tiling: a 256-thread block (4 waves, 2 x 2) owns a 128 x 128 tile of C; each wave a
+// 64 x 64 quarter as 2 x 2 tiles of v_mfma_f32_32x32x2_f32 (16 accumulators per tile,
+// 64 per lane).  K advances in 16-deep stages through two LDS buffers (register-staged:
+// the next stage's global loads are in flight while the current one is multiplied).
+// Both operands are kept k-contiguous in LDS ([row][k], row pitch 20 floats): lane l
+// of a wave reads its 8 k-values of row (l & 31), half h = l >> 5, with two
+// ds_read_b128 -- with the 80-byte pitch the 16 lanes of a b128 phase hit 16 distinct
+// 4-bank groups (conflict-free).  MFMA step s (s = 0..7) of a stage multiplies k = 8h + s
+// of half h, so a stage sums k in a fixed order: results are deterministic and exact
+// fp32 fma chains (the MFMA rounds once per product), not bit-equal to a library sgemm.
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace kgat {
+
+namespace {
+
+constexpr int kBM = 128, kBN = 128, kBK = 16, kPitch = 20;  // LDS row pitch in floats
+constexpr int kThreads = 256;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+  const float* A;
+  const float* B;
+  float* C;
+  int64_t lda, ldb, ldc;
+  int64_t sA, sB, sC;
+  int64_t M, N, K;
+  int accumulate;
+};
+
+// One operand stage: 128 rows x 16 k as 512 float4 (two per thread), and where they go in LDS.
+// KCONTIG: the operand's k index is its contiguous dimension (A not transposed / B transposed).
+template <bool KCONTIG>
+struct Stage {
+  float4 v[2];
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t rows, int64_t K, int64_t r0,
+                                       int64_t k0, int t) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = t + q * kThreads;
+      if (KCONTIG) {  // P[r][k]: 4 float4 per row
+        const int64_t r = r0 + (idx >> 2), k = k0 + (idx & 3) * 4;
+        v[q] = (r < rows && k < K) ? *reinterpret_cast<const float4*>(P + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {        // P[k][r]: 32 float4 per k-row
+        const int64_t k = k0 + (idx >> 5), r = r0 + (idx & 31) * 4;
+        v[q] = (k < K && r < rows) ? *reinterpret_cast<const float4*>(P + k * ld + r) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(float* __restrict__ lds, int t) const {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = t + q * kThreads;
+      if (KCONTIG) {
+        *reinterpret_cast<float4*>(lds + (idx >> 2) * kPitch + (idx & 3) * 4) = v[q];
+      } else {
+        const int k = idx >> 5, r = (idx & 31) * 4;
+        lds[(r + 0) * kPitch + k] = v[q].x;
+        lds[(r + 1) * kPitch + k] = v[q].y;
+        lds[(r + 2) * kPitch + k] = v[q].z;
+        lds[(r + 3) * kPitch + k] = v[q].w;
+      }
+    }
+  }
+};
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ float lds[2][2][kBM * kPitch];  // [buffer][A | B][row][k]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int tiles_n = static_cast<int>((g.N + kBN - 1) / kBN);
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x / tiles_n) * kBM;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x % tiles_n) * kBN;
+  const float* __restrict__ A = g.A + blockIdx.z * g.sA;
+  const float* __restrict__ B = g.B + blockIdx.z * g.sB;
+  float* __restrict__ C = g.C + blockIdx.z * g.sC;
+
+  Stage<!TA> sa;
+  Stage<TB> sb;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = static_cast<int>((g.K + kBK - 1) / kBK);
+  sa.load(A, g.lda, g.M, g.K, m0, 0, t);
+  sb.load(B, g.ldb, g.N, g.K, n0, 0, t);
+  sa.store(lds[0][0], t);
+  sb.store(lds[0][1], t);
+  __syncthreads();
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int r = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      sa.load(A, g.lda, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * kBK, t);
+      sb.load(B, g.ldb, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * kBK, t);
+    }
+    float4 fa[2][2], fb[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float* pa = &lds[cur][0][(wm + 32 * i + r) * kPitch + 8 * h];
+      const float* pb = &lds[cur][1][(wn + 32 * i + r) * kPitch + 8 * h];
+      fa[i][0] = *reinterpret_cast<const float4*>(pa);
+      fa[i][1] = *reinterpret_cast<const float4*>(pa + 4);
+      fb[i][0] = *reinterpret_cast<const float4*>(pb);
+      fb[i][1] = *reinterpret_cast<const float4*>(pb + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float a = s < 4 ? fa[i][0][s & 3] : fa[i][1][s & 3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float b = s < 4 ? fb[j][0][s & 3] : fb[j][1][s & 3];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 1 < nk) {
+      sa.store(lds[cur ^ 1][0], t);
+      sb.store(lds[cur ^ 1][1], t);
+    }
+    __syncthreads();
+  }
+  // C/D layout of 32x32: col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn + 32 * j + r;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (row < g.M) {
+          float* c = C + row * g.ldc + col;
+          *c = g.accumulate ? *c + acc[i][j][q] : acc[i][j][q];
+        }
+      }
+    }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int64_t sA,
+             const float* B, int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, int64_t batch,
+             bool accumulate, hipStream_t st) {
+  if (M < 0 || N < 0 || K < 0 || batch < 0 || !A || !B || !C) return KGAT_ERR_INVALID;
+  if (M == 0 || N == 0 || batch == 0) return KGAT_OK;
+  // float4 loads: leading dimensions, batch strides and bases 16-byte aligned; the contiguous
+  // dimension of each operand a multiple of 4 (k for A / B^T, m for A^T, n for B)
+  if ((lda | ldb | sA | sB) & 3 || !aligned16(A) || !aligned16(B)) return KGAT_ERR_INVALID;
+  if ((ta ? M : K) & 3 || (tb ? K : N) & 3) return KGAT_ERR_INVALID;
+  if (lda < (ta ? M : K) || ldb < (tb ? K : N) || ldc < N) return KGAT_ERR_INVALID;
+  if (K == 0) {
+    if (accumulate) return KGAT_OK;
+    for (int64_t z = 0; z < batch; ++z)
+      if (hipError_t e = hipMemset2DAsync(C + z * sC, ldc * sizeof(float), 0, N * sizeof(float), M, st);
+          e != hipSuccess)
+        return static_cast<int>(e);
+    return KGAT_OK;
+  }
+  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
+  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, accumulate ? 1 : 0};
+  const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
+  if (ta) {
+    if (tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(kThreads), 0, st, g);
+    else hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(kThreads), 0, st, g);
+  } else {
+    if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(kThreads), 0, st, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(kThreads), 0, st, g);
+  }
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+}  // namespace kgat
+
+extern "C" int kgat_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t m, int64_t n, int64_t k, const float* A,
+                             int64_t lda, int64_t stride_a, const float* B, int64_t ldb, int64_t stride_b, float* C,
+                             int64_t ldc, int64_t stride_c, int64_t batch, int32_t accumulate, void* stream) {
+  return kgat::gemm_f32(trans_a != 0, trans_b != 0, m, n, k, A, lda, stride_a, B, ldb, stride_b, C, ldc, stride_c,
+                        batch, accumulate != 0, reinterpret_cast<hipStream_t>(stream));
+}

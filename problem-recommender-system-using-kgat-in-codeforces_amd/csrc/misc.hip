@@ -58,6 +58,23 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ s
     dst[i] = src[idx[i]];
 }
 
+// ids of up to KGAT_IDS_MAX arrays, concatenated into out; out-of-range ids become 0 and raise *bad
+__global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t total, int64_t bound,
+                                                        int64_t* __restrict__ out, int32_t* __restrict__ bad) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  bool flag = false;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int k = 0;
+    int64_t off = i;
+    while (k + 1 < ids.count && off >= ids.n[k]) off -= ids.n[k++];
+    const int64_t v = ids.ptr[k][off];
+    const bool ok = v >= 0 && v < bound;
+    out[i] = ok ? v : 0;
+    flag |= !ok;
+  }
+  if (flag) atomicOr(bad, 1);
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ dst, int64_t n, float value) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = value;
@@ -312,6 +329,20 @@ extern "C" int kgat_gather_f32(const float* src, const int32_t* idx, int64_t n, 
   if (n == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::gather_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 8)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), src, idx, n, dst);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_ids_check(const kgat_ids* ids, int64_t bound, int64_t* out, int32_t* bad, void* stream) {
+  if (!ids || !out || !bad || ids->count < 1 || ids->count > KGAT_IDS_MAX || bound < 0) return KGAT_ERR_INVALID;
+  int64_t total = 0;
+  for (int k = 0; k < ids->count; ++k) {
+    if (ids->n[k] < 0 || (ids->n[k] && !ids->ptr[k])) return KGAT_ERR_INVALID;
+    total += ids->n[k];
+  }
+  if (total == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::ids_check_kernel, dim3(kgat::blocks_for(total, 256, kgat::kCUs * 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), *ids, total, bound, out, bad);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

