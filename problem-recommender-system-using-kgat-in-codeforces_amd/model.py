@@ -138,35 +138,42 @@ class _IdGuard:
             self._host.zero_()
             raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed)")
 
-    def check(self, what: str, ids, bound: int, device) -> list[torch.Tensor]:
-        """int64 device copies of ``ids`` (each as given, flattened), validated against [0, bound)."""
+    def check(self, what: str, ids, bound: int, device, more=()) -> list[torch.Tensor]:
+        """int64 device copies of ``ids`` (each as given, flattened), validated against [0, bound);
+        ``more`` = further (ids, bound) groups of the same call, checked under the same flag so a
+        call raises (for an earlier call's device ids) at most once, before it runs."""
         self.raise_pending()
-        ts = [torch.as_tensor(t) for t in ids]
-        if all(t.device.type == "cpu" for t in ts):
-            for t in ts:
-                if t.numel() and (int(t.min()) < 0 or int(t.max()) >= bound):
-                    raise IndexError(f"{what}: id out of range [0, {bound}) (min {int(t.min())}, max {int(t.max())})")
-            return [t.to(device).long().reshape(-1).contiguous() for t in ts]
+        groups = [(list(ids), int(bound))] + [(list(i), int(b)) for i, b in more]
+        flat = [torch.as_tensor(t) for g, _ in groups for t in g]
+        if all(t.device.type == "cpu" for t in flat):
+            for g, b in groups:
+                for t in map(torch.as_tensor, g):
+                    if t.numel() and (int(t.min()) < 0 or int(t.max()) >= b):
+                        raise IndexError(f"{what}: id out of range [0, {b}) (min {int(t.min())}, max {int(t.max())})")
+            return [t.to(device).long().reshape(-1).contiguous() for t in flat]
         if self._bad is None:
             self._bad = torch.zeros(1, dtype=torch.int32, device=device)
             self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._event = torch.cuda.Event()
-        src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
-        sizes = [t.numel() for t in src]
-        out = torch.empty(max(sum(sizes), 1), dtype=torch.int64, device=device)
-        for i in range(0, len(src), _lib.KGAT_IDS_MAX):
-            part = src[i:i + _lib.KGAT_IDS_MAX]
-            d = _lib.Ids()
-            for k, t in enumerate(part):
-                d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
-            d.count = len(part)
-            off = sum(sizes[:i])
-            _lib.call("kgat_ids_check", ctypes.byref(d), int(bound), out.data_ptr() + 8 * off, self._bad.data_ptr(),
-                      stream_ptr(device))
+        outs = []
+        for g, b in groups:
+            src = [torch.as_tensor(t).to(device).long().reshape(-1).contiguous() for t in g]
+            sizes = [t.numel() for t in src]
+            out = torch.empty(max(sum(sizes), 1), dtype=torch.int64, device=device)
+            for i in range(0, len(src), _lib.KGAT_IDS_MAX):
+                part = src[i:i + _lib.KGAT_IDS_MAX]
+                d = _lib.Ids()
+                for k, t in enumerate(part):
+                    d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
+                d.count = len(part)
+                off = sum(sizes[:i])
+                _lib.call("kgat_ids_check", ctypes.byref(d), b, out.data_ptr() + 8 * off, self._bad.data_ptr(),
+                          stream_ptr(device))
+            outs += list(out[:sum(sizes)].split(sizes))
         self._host.copy_(self._bad, non_blocking=True)
         self._event.record()
         self._pending = what
-        return list(out[:sum(sizes)].split(sizes))
+        return outs
 
 
 def _saved(tables, states, l) -> dict:
@@ -472,8 +479,8 @@ class KGAT(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("KGAT runs on the MI355X HIP path only: move the model to a GPU first")
         n = self._user_num + self._entity_num
-        h, p, q = self._ids.check("TRAIN_KG heads/tails", (heads, positive_tails, negative_tails), n, dev)
-        (r,) = self._ids.check("TRAIN_KG relations", (relations,), self._relation_num, dev)
+        h, p, q, r = self._ids.check("TRAIN_KG ids", (heads, positive_tails, negative_tails), n, dev,
+                                     more=[((relations,), self._relation_num)])
         ids = [h, r, p, q]
         return _KGLoss.apply(*ids, float(self._regularization_params[1]), self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)

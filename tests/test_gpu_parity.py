@@ -1357,6 +1357,7 @@ def test_out_of_range_ids_raise_index_error(pkg):
     for bad in (torch.full((8,), n, device=DEV), torch.full((8,), -7, device=DEV)):
         for mode_call in (lambda: m(ok.to(DEV), bad, ok.to(DEV), mode=pkg.KGATMode.TRAIN_CF),
                           lambda: m(ok.to(DEV), (ok % 10).to(DEV), bad, ok.to(DEV), mode=pkg.KGATMode.TRAIN_KG),
+                          lambda: m(ok.to(DEV), bad, ok.to(DEV), ok.to(DEV), mode=pkg.KGATMode.TRAIN_KG),
                           lambda: m(bad, ok.to(DEV), mode=pkg.KGATMode.PREDICT)):
             out = mode_call()  # device ids: runs on zeroed ids, no host sync
             if out is not None:
