@@ -361,6 +361,13 @@ int64_t kgat_transr_work_floats(int32_t batch, int32_t d, int32_t k);
 int kgat_transr_fwd_f32(const float *emb, int64_t ld_emb, const float *rel_emb, const float *trans, int32_t d,
                         int32_t k, const int64_t *heads, const int64_t *rels, const int64_t *pos,
                         const int64_t *neg, int32_t batch, float reg, float *loss, float *work, void *stream);
+/* a5 forward with the relation count: for d >= 128 (d, k in {128, 256} x {64, 128, 256})
+ * one block per (relation, 16-sample chunk of its samples in batch order) runs both
+ * products of the chunk on the fp32 MFMA with W_r read once per chunk; otherwise the
+ * per-sample kernel of kgat_transr_fwd_f32.  Same work layout, same loss definition. */
+int kgat_transr_fwd_ex_f32(const float *emb, int64_t ld_emb, const float *rel_emb, const float *trans, int32_t d,
+                           int32_t k, int32_t n_rel, const int64_t *heads, const int64_t *rels, const int64_t *pos,
+                           const int64_t *neg, int32_t batch, float reg, float *loss, float *work, void *stream);
 /* a5 backward: d_emb[id] += (upstream * dL/de) for every gathered id (duplicates
  * summed in slot order; d_emb must be initialised, e.g. zero), d_rel [n_rel, k]
  * and d_trans [n_rel, d, k] overwritten: each relation's samples (batch order) are

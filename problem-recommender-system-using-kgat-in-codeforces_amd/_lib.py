@@ -113,6 +113,8 @@ _SIGNATURES = {
     "kgat_transr_work_floats": (c_i64, [c_i32, c_i32, c_i32]),
     "kgat_transr_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32,
                                            c_vp, c_vp, c_vp]),
+    "kgat_transr_fwd_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                              c_i32, c_f32, c_vp, c_vp, c_vp]),
     "kgat_transr_bwd_workspace_floats": (c_i64, [c_i32, c_i32, c_i32, c_i32]),
     "kgat_transr_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                            c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),

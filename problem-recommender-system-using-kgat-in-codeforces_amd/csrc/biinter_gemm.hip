@@ -12,7 +12,7 @@
 //   backward: dA, dB from H, dH, the norm, the signs of P+b       (epi_bwd_kernel)
 //             du = dA W1, dm = dB W2                             (gemm_f32, into dXd / dS)
 //             dXd = du + dm*S, dS = du + dm*X                    (dxs_kernel, in place)
-//             [dW | db] = dA^T [U | 1], dB^T [M | 1]              (gemm_f32 split-K slabs)
+//             dW = dA^T U, dB^T M; db = column sums              (gemm_f32 split-K slabs)
 // Dropout draws are the fused kernels' (one 64-bit hash per node, 16-column
 // group of 4 blocks), so both paths drop the same elements.
 #include <utility>
@@ -34,7 +34,8 @@ __device__ __forceinline__ uint32_t gemm_threshold(float p) {
   return t >= 65536.f ? 65536u : static_cast<uint32_t>(t);
 }
 
-// U = X+S, M = X*S with row pitch d+4; column d is 1 (so dA^T [U | 1] = [dW | db]), d+1..d+3 are 0
+// U = X+S, M = X*S with row pitch d+4 (16-byte aligned rows; the 4 pad columns are written 1, 0, 0, 0
+// and never read)
 __global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
                                                  int64_t lds, float* __restrict__ U, float* __restrict__ M, int64_t n,
                                                  int d) {
@@ -58,15 +59,43 @@ __global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, in
   }
 }
 
-// [dW | db] = sum over row chunks of the slabs [nb][dout][d_in + 4], in chunk order
-__global__ __launch_bounds__(256) void wslab_reduce_kernel(const float* __restrict__ slabs, int nb, int din, int dout,
-                                                           float* __restrict__ dW, float* __restrict__ db) {
+// [dW | db] = sum over row chunks of the slabs [nb][dout][d_in + 4], in chunk order, in two
+// levels: pass 1 (blockIdx.y = group g of kSlabGroups) sums the slabs of group g's contiguous
+// range in order into part[g]; pass 2 sums the groups in order.  (One thread per output
+// element walking ~1k slabs left 65 blocks latency-bound: 140 us per call at C4.)
+constexpr int kSlabGroups = 16;
+
+__global__ __launch_bounds__(256) void wslab_part_kernel(const float* __restrict__ slabs, int nb, int din, int dout,
+                                                         float* __restrict__ part) {
   const int w = din + 4;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= dout * (din + 1)) return;
   const int o = i / (din + 1), k = i % (din + 1);
+  const int per = (nb + kSlabGroups - 1) / kSlabGroups;
+  const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
+  const float* p = slabs + o * w + k;
+  const int64_t sw = static_cast<int64_t>(dout) * w;
   float acc = 0.f;
-  for (int b = 0; b < nb; ++b) acc += slabs[static_cast<int64_t>(b) * dout * w + o * w + k];
+  int b = b0;
+  for (; b + 4 <= b1; b += 4) {  // four loads in flight, added in order
+    const float v0 = p[b * sw], v1 = p[(b + 1) * sw], v2 = p[(b + 2) * sw], v3 = p[(b + 3) * sw];
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
+  for (; b < b1; ++b) acc += p[b * sw];
+  part[static_cast<int64_t>(blockIdx.y) * dout * (din + 1) + i] = acc;
+}
+
+__global__ __launch_bounds__(256) void wslab_reduce_kernel(const float* __restrict__ part, int din, int dout,
+                                                           float* __restrict__ dW, float* __restrict__ db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tot = dout * (din + 1);
+  if (i >= tot) return;
+  float acc = 0.f;
+  for (int g = 0; g < kSlabGroups; ++g) acc += part[static_cast<int64_t>(g) * tot + i];
+  const int o = i / (din + 1), k = i % (din + 1);
   if (k < din) dW[o * din + k] = acc;
   else db[o] = acc;
 }
@@ -183,9 +212,17 @@ __global__ __launch_bounds__(256) void dxs_kernel(float* __restrict__ dXd, int64
   }
 }
 
-constexpr int64_t kGemmChunk = 65536;  // rows per split-K chunk of the weight-gradient GEMMs
-
-inline int64_t wslab_count(int64_t n) { return (n + kGemmChunk - 1) / kGemmChunk; }
+// Rows per split-K chunk of the weight-gradient GEMMs.  dW is one or two 128 x 128 output tiles,
+// so the chunks are the GEMM's only parallelism: about 1k chunks (>= 4 blocks per CU, so two
+// stay resident per CU and hide each other's barriers), 512 .. 65536 rows each, a multiple of
+// 256.  A function of n only: the same n always sums in the same order.  (Fixed 65536-row
+// chunks left ~150 blocks of 4096 k-steps each at C4: 5 ms per call.)
+inline int64_t gemm_chunk(int64_t n) {
+  int64_t c = (n + 1023) / 1024;
+  c = (c + 255) / 256 * 256;
+  return c < 512 ? 512 : (c > 65536 ? 65536 : c);
+}
+inline int64_t wslab_count(int64_t n) { return (n + gemm_chunk(n) - 1) / gemm_chunk(n); }
 
 #define KGAT_GEMM(call)                \
   do {                                 \
@@ -203,7 +240,7 @@ static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d
   return KGAT_OK;
 }
 
-// du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, [dW | db] = dA^T [U | 1]
+// du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, dW = dA^T U, db = colsum dA
 // (split-K over row chunks, slabs summed in chunk order); U, M and the slabs live in work.
 static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* W2,
                          const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
@@ -215,6 +252,7 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   const int64_t nb = wslab_count(n);
   float* slab1 = work + 2 * n * ldu;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
+  float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
   // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
   KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
   KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
@@ -224,22 +262,30 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
                      lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
   KGAT_LAUNCH_CHECK();
-  // [dW | db] = dA^T [U | 1], split over row chunks (deterministic: chunk slabs summed in order):
-  //   slab_b[d_out, ldu] = dA_b[chunk, d_out]^T . U_b[chunk, ldu]
-  const int64_t full = n / kGemmChunk, rest = n - full * kGemmChunk;
+  // [dW | db] = [dA^T U | colsum dA], split over row chunks (deterministic: chunk slabs summed in
+  // order): slab_b[d_out, 0:d_in] = dA_b[chunk, d_out]^T . U_b[chunk, d_in], slab_b[:, d_in] = the
+  // chunk's column sums of dA, produced by the same GEMM from its A tiles (a [U | 1] operand
+  // would add a whole 128-wide output tile for its one column)
+  const int64_t chunk = gemm_chunk(n);
+  const int64_t full = n / chunk, rest = n - full * chunk;
+  const int64_t sl_stride = static_cast<int64_t>(ldu) * d_out;
   for (int mat = 0; mat < 2; ++mat) {
     const float* Um = mat == 0 ? U : M;
     const float* G = mat == 0 ? dA : dB;
     float* sl = mat == 0 ? slab1 : slab2;
     if (full > 0)
-      KGAT_GEMM(gemm_f32(true, false, d_out, ldu, kGemmChunk, G, d_out, kGemmChunk * d_out, Um, ldu,
-                         kGemmChunk * ldu, sl, ldu, static_cast<int64_t>(ldu) * d_out, full, false, st));
+      KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, chunk, G, d_out, chunk * d_out, Um, ldu, chunk * ldu, sl, ldu,
+                                   sl_stride, sl + d_in, ldu, sl_stride, full, st));
     if (rest > 0)
-      KGAT_GEMM(gemm_f32(true, false, d_out, ldu, rest, G + full * kGemmChunk * d_out, d_out, 0,
-                         Um + full * kGemmChunk * ldu, ldu, 0, sl + full * ldu * static_cast<int64_t>(d_out), ldu, 0,
-                         1, false, st));
-    hipLaunchKernelGGL(wslab_reduce_kernel, dim3((d_out * (d_in + 1) + 255) / 256), dim3(256), 0, st, sl,
-                       static_cast<int>(nb), d_in, d_out, mat == 0 ? dW1 : dW2, mat == 0 ? db1 : db2);
+      KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, rest, G + full * chunk * d_out, d_out, 0, Um + full * chunk * ldu,
+                                   ldu, 0, sl + full * sl_stride, ldu, 0, sl + full * sl_stride + d_in, ldu, 0, 1,
+                                   st));
+    const int eblocks = (d_out * (d_in + 1) + 255) / 256;
+    hipLaunchKernelGGL(wslab_part_kernel, dim3(eblocks, kSlabGroups), dim3(256), 0, st, sl, static_cast<int>(nb), d_in,
+                       d_out, part);
+    KGAT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(wslab_reduce_kernel, dim3(eblocks), dim3(256), 0, st, part, d_in, d_out, mat == 0 ? dW1 : dW2,
+                       mat == 0 ? db1 : db2);
     KGAT_LAUNCH_CHECK();
   }
   return KGAT_OK;
@@ -260,7 +306,8 @@ extern "C" int64_t kgat_biinter_gemm_work_floats(int64_t n_rows, int32_t d_in, i
   if (n_rows < 0 || !gemm_dims_ok(d_in, d_out)) return -1;
   // U', M' [n, d_in + 4] + two sets of split-K slabs [chunks][d_out][d_in + 4]
   return n_rows * 2 * static_cast<int64_t>(d_in + 4) +
-         2 * kgat::wslab_count(n_rows) * d_out * static_cast<int64_t>(d_in + 4) + 4;
+         2 * kgat::wslab_count(n_rows) * d_out * static_cast<int64_t>(d_in + 4) +
+         kgat::kSlabGroups * static_cast<int64_t>(d_out) * (d_in + 1) + 4;
 }
 
 extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,

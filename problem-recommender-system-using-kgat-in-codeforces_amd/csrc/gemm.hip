@@ -39,6 +39,8 @@ struct GemmArgs {
   int64_t sA, sB, sC;
   int64_t M, N, K;
   int accumulate;
+  float* cs;  // TA only: column sums of op(A) over k (nullable)
+  int64_t ldcs, sCS;
 };
 
 // One operand stage: 128 rows x 16 k as 512 float4 (two per thread), and where they go in LDS.
@@ -79,6 +81,18 @@ struct Stage {
   }
 };
 
+// csum += the two float4 of a (k-major, !KCONTIG) stage this thread loaded
+template <bool KC>
+__device__ __forceinline__ void add_stage(float4& csum, const Stage<KC>& st) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    csum.x += st.v[q].x;
+    csum.y += st.v[q].y;
+    csum.z += st.v[q].z;
+    csum.w += st.v[q].w;
+  }
+}
+
 template <bool TA, bool TB>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
   __shared__ float lds[2][2][kBM * kPitch];  // [buffer][A | B][row][k]
@@ -101,10 +115,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
   const int nk = static_cast<int>((g.K + kBK - 1) / kBK);
+  // TA column sums: this thread's float4 of A^T rows k = (t >> 5) + 8 q (q = 0, 1) of every
+  // stage covers columns m0 + 4 (t & 31) .. + 3; summed over its k residues here, combined
+  // over the 8 residue threads in order at the end
+  const bool do_cs = TA && g.cs != nullptr && n0 == 0;
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
   sa.load(A, g.lda, g.M, g.K, m0, 0, t);
   sb.load(B, g.ldb, g.N, g.K, n0, 0, t);
   sa.store(lds[0][0], t);
   sb.store(lds[0][1], t);
+  if (do_cs) add_stage(csum, sa);
   __syncthreads();
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
   const int r = lane & 31, h = lane >> 5;
@@ -139,8 +159,28 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
     if (kt + 1 < nk) {
       sa.store(lds[cur ^ 1][0], t);
       sb.store(lds[cur ^ 1][1], t);
+      if (do_cs) add_stage(csum, sa);
     }
     __syncthreads();
+  }
+  if (do_cs) {
+    __shared__ float4 cpart[kThreads];
+    cpart[t] = csum;
+    __syncthreads();
+    if (t < 32) {
+      float4 s = cpart[t];
+      for (int j = 1; j < 8; ++j) {
+        const float4 o = cpart[t + 32 * j];
+        s.x += o.x;
+        s.y += o.y;
+        s.z += o.z;
+        s.w += o.w;
+      }
+      float* cs = g.cs + blockIdx.z * g.sCS;
+      const float v[4] = {s.x, s.y, s.z, s.w};
+      for (int i = 0; i < 4; ++i)
+        if (m0 + 4 * t + i < g.M) cs[(m0 + 4 * t + i) * g.ldcs] = v[i];
+    }
   }
   // C/D layout of 32x32: col = lane & 31, row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5)
 #pragma unroll
@@ -184,7 +224,7 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
   }
   const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
-  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, accumulate ? 1 : 0};
+  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, accumulate ? 1 : 0, nullptr, 0, 0};
   const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
   if (ta) {
     if (tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(kThreads), 0, st, g);
@@ -193,6 +233,22 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
     if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(kThreads), 0, st, g);
     else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(kThreads), 0, st, g);
   }
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+int gemm_f32_tn_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int64_t sA, const float* B,
+                       int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, float* cs, int64_t ldcs,
+                       int64_t sCS, int64_t batch, hipStream_t st) {
+  if (cs == nullptr) return gemm_f32(true, false, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, false, st);
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return KGAT_ERR_INVALID;
+  if ((lda | ldb | sA | sB) & 3 || !aligned16(A) || !aligned16(B) || (M & 3) || (N & 3)) return KGAT_ERR_INVALID;
+  if (lda < M || ldb < N || ldc < N) return KGAT_ERR_INVALID;
+  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
+  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, 0, cs, ldcs, sCS};
+  hipLaunchKernelGGL((gemm_kernel<true, false>), dim3(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch)),
+                     dim3(kThreads), 0, st, g);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

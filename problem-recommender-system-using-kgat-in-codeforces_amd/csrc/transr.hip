@@ -11,6 +11,8 @@
 // Backward: the table-row gradients are scattered with duplicate ids summed
 // in slot order (no atomics), and d trans[r] / d rel_emb[r] are reduced per
 // relation over the samples in batch order -- both deterministic.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -159,6 +161,197 @@ __global__ __launch_bounds__(256) void transr_fwd_kernel(const float* __restrict
       for (int v = 0; v < 3; ++v) gr[v * d + i] = acc[v];
     }
   }
+}
+
+// The same forward on the fp32 MFMA (v_mfma_f32_16x16x4_f32), one block per (relation r,
+// 16-sample chunk z of r's samples in batch order): the chunk's 3 x 16 gathered rows
+// (head / pos / neg) form one 48 x D operand in LDS and W_r is read ONCE per chunk
+// (the per-sample kernel re-reads all d x k of W_r for every sample: 256 KB per sample
+// at d = k = 256) for both products of the chunk:
+//   P  = X W_r          [48, K]   (h', t+', t-' rows)
+//   GR = G W_r^T        [48, D]   (d e_h, d e_t+, d e_t- from g_h', g_t+', g_t-')
+// Wave w owns the output column tiles w, w+4, ... of both products.  K order of the sums:
+// the first product walks k = 0..D-1 in steps of 4 (lane group q takes k0 + q); the
+// second takes the contiguous ranges q*K/4 + s, so its operands load as float4.
+constexpr int kTrChunk = 16;
+
+template <int D, int K>
+__global__ __launch_bounds__(256) void transr_fwd_mfma_kernel(const float* __restrict__ emb, int64_t lde,
+                                                              const float* __restrict__ rel_emb,
+                                                              const float* __restrict__ trans,
+                                                              const int64_t* __restrict__ heads,
+                                                              const int64_t* __restrict__ rels,
+                                                              const int64_t* __restrict__ pos,
+                                                              const int64_t* __restrict__ neg, int batch, float reg,
+                                                              float* __restrict__ work) {
+  constexpr int XP = D + 4, GP = K + 4;  // LDS row pitches (floats)
+  constexpr int NTP = (K / 16 + 3) / 4;  // column tiles per wave, first product
+  constexpr int NTG = (D / 16 + 3) / 4;  // column tiles per wave, second product
+  __shared__ __attribute__((aligned(16))) float xs[3 * kTrChunk * XP];
+  __shared__ __attribute__((aligned(16))) float gs[3 * kTrChunk * GP];
+  __shared__ int s_ids[kTrChunk];
+  __shared__ int s_wcnt[4];
+  __shared__ int s_seen;
+  const int r = blockIdx.x, z = blockIdx.y;
+  const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  // relation r's samples in batch order; this block takes list positions [z*16, z*16 + 16)
+  if (tid == 0) s_seen = 0;
+  __syncthreads();
+  const int lo = z * kTrChunk;
+  for (int w0 = 0; w0 < batch; w0 += 256) {
+    const int b = w0 + tid;
+    const bool hit = b < batch && rels[b] == r;
+    const uint64_t m = __ballot(hit);
+    if (lane == 0) s_wcnt[wv] = __popcll(m);
+    __syncthreads();
+    int base = s_seen;
+    for (int w = 0; w < wv; ++w) base += s_wcnt[w];
+    const int li = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (hit && li >= lo && li < lo + kTrChunk) s_ids[li - lo] = b;
+    __syncthreads();
+    if (tid == 0) s_seen += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    __syncthreads();
+  }
+  const int cnt = min(kTrChunk, s_seen - lo);
+  if (cnt <= 0) return;  // block-uniform
+  const TransrWork off = TransrWork::at(batch, D, K);
+  // stage the 48 gathered rows (row v*16 + s: v = head / pos / neg of sample s; zeros past cnt)
+  for (int i = tid; i < 3 * kTrChunk * (D / 4); i += 256) {
+    const int row = i / (D / 4), c4 = i % (D / 4), v = row / kTrChunk, s = row % kTrChunk;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s < cnt) {
+      const int b = s_ids[s];
+      const int64_t id = v == 0 ? heads[b] : (v == 1 ? pos[b] : neg[b]);
+      x = *reinterpret_cast<const float4*>(emb + id * lde + c4 * 4);
+    }
+    *reinterpret_cast<float4*>(xs + row * XP + c4 * 4) = x;
+  }
+  __syncthreads();
+  const float* W = trans + static_cast<int64_t>(r) * D * K;
+  // ---- P = X W_r  (lane (q, c): A = X[mt*16 + c][k0 + q], B = W[k0 + q][nt*16 + c])
+  floatx4 acc[3][NTP];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k0 = 0; k0 < D; k0 += 4) {
+    float bw[NTP];
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const int nt = wv + 4 * j;
+      bw[j] = nt < K / 16 ? W[static_cast<int64_t>(k0 + q) * K + nt * 16 + c] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+      const float a = xs[(mt * kTrChunk + c) * XP + k0 + q];
+#pragma unroll
+      for (int j = 0; j < NTP; ++j)
+        if (wv + 4 * j < K / 16) acc[mt][j] = mfma16x4(a, bw[j], acc[mt][j]);
+    }
+  }
+  // P rows into LDS (C layout: lane (q, c) element i = row q*4 + i, column nt*16 + c)
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const int nt = wv + 4 * j;
+      if (nt >= K / 16) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gs[(mt * kTrChunk + q * 4 + i) * GP + nt * 16 + c] = acc[mt][j][i];
+    }
+  __syncthreads();
+  // ---- per sample (wave w: samples w, w+4, ...): scores, loss term, the projected gradients
+  //      (gproj, for the weight gradient) and G = (g_h', g_t+', g_t-') rows over P in LDS
+  constexpr int KC = (K + 63) / 64;
+  for (int s = wv; s < cnt; s += 4) {
+    const int b = s_ids[s];
+    float h[KC], tp[KC], tn[KC], er[KC];
+    float sp = 0.f, sn = 0.f, qq = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < KC; ++cc) {
+      const int j = lane + 64 * cc;
+      h[cc] = tp[cc] = tn[cc] = er[cc] = 0.f;
+      if (j < K) {
+        h[cc] = gs[s * GP + j];
+        tp[cc] = gs[(kTrChunk + s) * GP + j];
+        tn[cc] = gs[(2 * kTrChunk + s) * GP + j];
+        er[cc] = rel_emb[static_cast<int64_t>(r) * K + j];
+        const float dp = h[cc] + er[cc] - tp[cc], dn = h[cc] + er[cc] - tn[cc];
+        sp = fmaf(dp, dp, sp);
+        sn = fmaf(dn, dn, sn);
+        qq += h[cc] * h[cc] + er[cc] * er[cc] + tp[cc] * tp[cc] + tn[cc] * tn[cc];
+      }
+    }
+    sp = wave_sum(sp);
+    sn = wave_sum(sn);
+    qq = wave_sum(qq);
+    const float x = sn - sp;  // loss = softplus(-x)
+    const float cf = 1.f / (1.f + expf(-x)) - 1.f;
+    if (lane == 0) work[off.term + b] = fmaxf(-x, 0.f) + log1pf(expf(-fabsf(x))) + reg * 0.5f * qq;
+    float* gp = work + off.gproj + static_cast<int64_t>(b) * 4 * K;
+#pragma unroll
+    for (int cc = 0; cc < KC; ++cc) {
+      const int j = lane + 64 * cc;
+      if (j < K) {
+        const float dp = h[cc] + er[cc] - tp[cc], dn = h[cc] + er[cc] - tn[cc];
+        const float g_common = 2.f * cf * (dn - dp);
+        const float g0 = g_common + reg * h[cc];
+        const float g1 = 2.f * cf * dp + reg * tp[cc];
+        const float g2 = -2.f * cf * dn + reg * tn[cc];
+        gp[j] = g0;
+        gp[K + j] = g1;
+        gp[2 * K + j] = g2;
+        gp[3 * K + j] = g_common + reg * er[cc];
+        gs[s * GP + j] = g0;
+        gs[(kTrChunk + s) * GP + j] = g1;
+        gs[(2 * kTrChunk + s) * GP + j] = g2;
+      }
+    }
+  }
+  // rows of absent samples stay zero: their X rows were staged as zeros, so their P rows are 0
+  __syncthreads();
+  // ---- GR = G W_r^T  (lane (q, c): A = G[mt*16 + c][q*K/4 + s], B = W[nt*16 + c][q*K/4 + s])
+  floatx4 ag[3][NTG];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int j = 0; j < NTG; ++j) ag[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  constexpr int KQ = K / 4;
+#pragma unroll 1
+  for (int s0 = 0; s0 < KQ; s0 += 4) {
+    float4 bw[NTG];
+#pragma unroll
+    for (int j = 0; j < NTG; ++j) {
+      const int nt = wv + 4 * j;
+      bw[j] = nt < D / 16 ? *reinterpret_cast<const float4*>(W + static_cast<int64_t>(nt * 16 + c) * K + q * KQ + s0)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 av[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) av[mt] = *reinterpret_cast<const float4*>(gs + (mt * kTrChunk + c) * GP + q * KQ + s0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int j = 0; j < NTG; ++j)
+          if (wv + 4 * j < D / 16) ag[mt][j] = mfma16x4(av[mt][t], bw[j][t], ag[mt][j]);
+  }
+  float* gr = work + off.grow;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int j = 0; j < NTG; ++j) {
+      const int nt = wv + 4 * j;
+      if (nt >= D / 16) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int s = q * 4 + i;
+        if (s < cnt) gr[(static_cast<int64_t>(s_ids[s]) * 3 + mt) * D + nt * 16 + c] = ag[mt][j][i];
+      }
+    }
 }
 
 __global__ __launch_bounds__(256) void transr_loss_kernel(const float* __restrict__ term, int batch,
@@ -404,6 +597,51 @@ extern "C" int kgat_transr_fwd_f32(const float* emb, int64_t ld_emb, const float
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(kgat::transr_fwd_kernel, dim3((batch + 3) / 4), dim3(256), 0, st, emb, ld_emb, rel_emb, trans, d,
                      k, heads, rels, pos, neg, batch, reg, work);
+  KGAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(kgat::transr_loss_kernel, dim3(1), dim3(256), 0, st, work, batch, loss);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+template <int D>
+static bool launch_fwd_mfma_d(int k, int n_rel, const float* emb, int64_t ld_emb, const float* rel_emb,
+                              const float* trans, const int64_t* heads, const int64_t* rels, const int64_t* pos,
+                              const int64_t* neg, int batch, float reg, float* work, hipStream_t st) {
+  const dim3 grid(n_rel, (batch + kgat::kTrChunk - 1) / kgat::kTrChunk);
+#define KGAT_TR_K(KK)                                                                                              \
+  case KK:                                                                                                         \
+    hipLaunchKernelGGL((kgat::transr_fwd_mfma_kernel<D, KK>), grid, dim3(256), 0, st, emb, ld_emb, rel_emb, trans, \
+                       heads, rels, pos, neg, batch, reg, work);                                                   \
+    return true;
+  switch (k) {
+    KGAT_TR_K(64)
+    KGAT_TR_K(128)
+    KGAT_TR_K(256)
+    default: return false;
+  }
+#undef KGAT_TR_K
+}
+
+extern "C" int kgat_transr_fwd_ex_f32(const float* emb, int64_t ld_emb, const float* rel_emb, const float* trans,
+                                      int32_t d, int32_t k, int32_t n_rel, const int64_t* heads, const int64_t* rels,
+                                      const int64_t* pos, const int64_t* neg, int32_t batch, float reg, float* loss,
+                                      float* work, void* stream) {
+  if (!emb || !rel_emb || !trans || !heads || !rels || !pos || !neg || !loss || !work || batch <= 0 || n_rel <= 0)
+    return KGAT_ERR_INVALID;
+  if (d <= 0 || k <= 0 || d > 256 || k > 256 || ld_emb < d) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the chunked MFMA form where W_r is big enough for its re-reads to dominate (d >= 128); the
+  // per-sample kernel otherwise (and for shapes without an instantiation)
+  static const bool force_valu = getenv("KGAT_TRANSR_VALU") != nullptr;  // A/B switch
+  bool done = false;
+  if (!force_valu && d >= 128 && (ld_emb & 3) == 0 && (reinterpret_cast<uintptr_t>(emb) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(trans) & 15) == 0 && static_cast<int64_t>(n_rel) * ((batch + 15) / 16) < (1ll << 31)) {
+    if (d == 128) done = launch_fwd_mfma_d<128>(k, n_rel, emb, ld_emb, rel_emb, trans, heads, rels, pos, neg, batch, reg, work, st);
+    else if (d == 256) done = launch_fwd_mfma_d<256>(k, n_rel, emb, ld_emb, rel_emb, trans, heads, rels, pos, neg, batch, reg, work, st);
+  }
+  if (!done)
+    hipLaunchKernelGGL(kgat::transr_fwd_kernel, dim3((batch + 3) / 4), dim3(256), 0, st, emb, ld_emb, rel_emb, trans, d,
+                       k, heads, rels, pos, neg, batch, reg, work);
   KGAT_LAUNCH_CHECK();
   hipLaunchKernelGGL(kgat::transr_loss_kernel, dim3(1), dim3(256), 0, st, work, batch, loss);
   KGAT_LAUNCH_CHECK();

@@ -756,8 +756,8 @@ def transr_fwd(emb, rel_emb, trans, heads, rels, pos, neg, reg: float):
     dev = emb.device
     loss = torch.empty(1, dtype=torch.float32, device=dev)
     work = torch.empty(int(_lib.lib().kgat_transr_work_floats(B, d, k)), dtype=torch.float32, device=dev)
-    _lib.call("kgat_transr_fwd_f32", emb.data_ptr(), _ld(emb), rel_emb.data_ptr(), trans.data_ptr(), d, k,
-              heads.data_ptr(), rels.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg), loss.data_ptr(),
+    _lib.call("kgat_transr_fwd_ex_f32", emb.data_ptr(), _ld(emb), rel_emb.data_ptr(), trans.data_ptr(), d, k,
+              trans.shape[0], heads.data_ptr(), rels.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg), loss.data_ptr(),
               work.data_ptr(), stream_ptr(dev))
     return loss, work
 

@@ -48,6 +48,11 @@ def main():
             fix_k = rec
     if main_k:
         out["spmm_fwd_hbm_bytes_per_launch"] = main_k["hbm_bytes"] + (fix_k["hbm_bytes"] if fix_k else 0.0)
+    if len(sys.argv) > 5:  # the bench log of the profiled run: the graph size the counters belong to
+        import re
+        m = re.search(r"graph: N=(\d+) .*nnz=(\d+)", Path(sys.argv[5]).read_text())
+        if m:
+            out["nodes"], out["nnz"] = int(m.group(1)), int(m.group(2))
     dst.write_text(json.dumps(out, indent=1))
     print(json.dumps(out.get("spmm_fwd_hbm_bytes_per_launch")))
 
