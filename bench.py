@@ -556,11 +556,21 @@ def main() -> int:
         return 0
 
     import torch.distributed as dist
+    # KGAT_BENCH_BACKEND=gloo: rehearse the N-rank path with every rank on the GPUs there are (ranks
+    # share a device round-robin; host-staged collectives) -- tests only, never a measurement
+    backend = os.environ.get("KGAT_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        print(f"bench.py: KGAT_BENCH_BACKEND={backend} (nccl or gloo)", file=sys.stderr)
+        return 2
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1 or cfg["mode"] == "sharded":  # the row-sharded model always runs over a process group
         torch.cuda.set_device(local)
         kw = {} if "MASTER_ADDR" in os.environ else dict(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
                                                            world_size=1)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), **kw)
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, **kw)
         if dist.get_world_size() != args.gpus:
             raise RuntimeError(f"{dist.get_world_size()} ranks joined, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
@@ -574,6 +584,8 @@ def main() -> int:
         "data": "synthetic (seeded CKG per SURVEY §8d; random-init weights; no dataset download)",
     }
     result.update(res)
+    if backend != "nccl":
+        result["rehearsal"] = f"{backend} backend, ranks sharing {torch.cuda.device_count()} GPU(s): not a measurement"
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist.is_initialized():

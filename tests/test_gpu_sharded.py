@@ -149,3 +149,27 @@ def test_rccl_world1_collectives_match_gloo():
     log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert "rccl world1: OK" in p.stdout, p.stdout[-2000:]
+
+
+@pytest.mark.parametrize("dp", ["replicated", "sharded"])
+def test_bench_two_ranks_gloo_rehearsal(dp):
+    """bench.py --gpus 2 end to end (launch, process group, DP replicas with the table exchange, timing,
+    max-over-ranks, one JSON line) with both ranks on this one GPU over gloo (KGAT_BENCH_BACKEND):
+    the N-rank path the driver's multi-GPU run takes, minus RCCL."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, KGAT_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "small", "--scale", "0.2",
+                        "--steps", "3", "--warmup", "1", "--dp", dp], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["dp_exchange"] == dp
+    assert rec["rehearsal"].startswith("gloo") and rec["value"] > 0 and np.isfinite(rec["final_loss"])
+    assert sum(rec["dp_table_exchange_steps"].values()) == 4 if dp == "replicated" else True
