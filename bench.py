@@ -273,14 +273,15 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(acc[1], acc[2], d, a), compulsory_bytes(acc[1], acc[2], d)))
         elif acc is False:
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(n, nnz, d, False), compulsory_bytes(n, nnz, d)))
-    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc != "masked"]
-    masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc == "masked"]
+    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc not in ("masked", "fused_adam")]
+    masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc in ("masked", "fused_adam")]
+    fused = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if acc == "fused_adam"]
     fwd_d0 = [x for x in fwd if x[1] == d0]
     avg_ms = float(np.mean([x[0] for x in fwd_d0]))
     algo = float(np.mean([x[2] for x in fwd_d0]))
     comp = float(np.mean([x[3] for x in fwd_d0]))
     t_prop = sum(x[0] for x in fwd) / steps
-    traffic, pmc_src = None, None
+    traffic, pmc_src, rec = None, None, {}
     pmc = ROOT / "profiles" / f"pmc_{cfg_name}.json"
     if pmc.exists():
         try:
@@ -311,6 +312,24 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
             "bwd_avg_ms": float(np.mean([t for t, _ in bwd])) if bwd else None,
             "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / steps,
             "fwd_spmm_ms_per_step": t_prop, "fwd_spmm_layer_edges_per_s": None}
+    if fused:
+        # the layer-0 A^T product fused with the table's Adam step: HBM-bound on the Adam stream
+        # (read + write of p, m, v: 24 B / parameter) plus the product's index scan; counter bytes
+        # from the same PMC file when it has them
+        ms = float(np.mean([t for t, _ in fused]))
+        d = fused[0][1]
+        adam_b = 24 * n * d
+        scan_b = 8 * (n + 1) + 8 * nnz
+        tu = {"kernel": f"spmm_main_kernel<{d}, 4> (+fixup): masked A^T.dS0 + table Adam", "avg_launch_ms": ms,
+              "launches_per_step": len(fused) / steps, "adam_bytes": adam_b, "scan_bytes": scan_b,
+              "min_bytes_GBps": (adam_b + scan_b) / (ms * 1e-3) / 1e9}
+        tu["min_bytes_frac"] = tu["min_bytes_GBps"] / HBM_PEAK_GBS
+        tb = rec.get("table_update_hbm_bytes_per_launch") if traffic else None
+        if tb:
+            tu["traffic"] = tb
+            tu["counter_GBps"] = tb / (ms * 1e-3) / 1e9
+            tu["counter_frac"] = tu["counter_GBps"] / HBM_PEAK_GBS
+        spmm["table_update"] = tu
     return roof, spmm
 
 
@@ -363,6 +382,9 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     replicas.broadcast_parameters(model)  # identical replicas (no-op at N=1)
     model.train()
     model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    # the table gradient's layer-0 A^T product runs fused with the table's Adam step inside
+    # update_cf_weights (same bits; --no-fused-update: product and Adam as two passes)
+    model.fuse_table_update = not args.no_fused_update
     B = cfg["batch"]
     # batches (host sampling is outside the hot path, main.py:300-305): uniform users,
     # a positive from the user's interactions, a uniform negative item
@@ -401,7 +423,8 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         "config": {"workload": cfg["workload"], "nodes": n, "nnz": nnz, "interactions": int(len(inter)),
                    "kg_triples": int(len(trip)), "embed_dim": d0, "layer_size": cfg["layers"],
                    "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "single",
-                   "dp_exchange": dp_mode if world > 1 else None, "mode": "train (dropout 0.1)"},
+                   "dp_exchange": dp_mode if world > 1 else None, "mode": "train (dropout 0.1)",
+                   "table_update": "unfused" if args.no_fused_update else "fused layer-0 A^T product + Adam"},
         "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
         "cpu_baseline": None,
     }
@@ -431,6 +454,7 @@ def gpu_parity_inputs(model, pkg, batch):
     tables = [t.cpu() for t in model.propagate()]
     loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
     loss.backward()
+    model.materialize_table_grad()  # fuse_table_update leaves it to update_cf_weights otherwise
     grad = model._user_entity_embedding.weight.grad.detach().cpu()
     for p in model.parameters():
         p.grad = None
@@ -510,6 +534,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-fused-update", action="store_true",
+                    help="c2/c4: materialise the table gradient and run Adam as its own pass")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and join the process group (gloo, no GPU), report, exit")
     ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",

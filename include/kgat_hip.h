@@ -104,6 +104,20 @@ int kgat_spmm_csr_masked_ex_f32(const kgat_csr *A, const int32_t *src_map, const
                                 int32_t d, int32_t *row_hit, const uint32_t *src_bits, const uint64_t *src_rank,
                                 int64_t n_src, float *workspace, int64_t workspace_floats, void *stream);
 
+/* The layer-0 masked product fused with the table's Adam step: the product's
+ * row r (kgat_spmm_csr_masked_ex_f32 with yc_row0 = 0, no row_hit) is the
+ * gradient of table row r, and instead of being written it is consumed by
+ * r's Adam update (kgat_adam_f32's arithmetic, same bits) of p / m / v
+ * ([n_rows x d] rows of stride ldp).  Replaces the sequence autograd
+ * backward of src/model/KGAT/aggregator.py:54 into the embedding table
+ * (model.py:188) + torch.optim.Adam.step() (model.py:404-413) for that
+ * table: the dense gradient never reaches HBM. */
+int kgat_spmm_csr_masked_adam_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                  const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p, float *m,
+                                  float *v, int64_t ldp, int32_t d, float step_size, float beta1, float beta2,
+                                  float bc2_sqrt, float eps, float *workspace, int64_t workspace_floats,
+                                  void *stream);
+
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 

@@ -85,6 +85,9 @@ _SIGNATURES = {
                                                 c_i32, c_vp, c_i64, c_vp]),
     "kgat_spmm_csr_masked_ex_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
                                                    c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "kgat_spmm_csr_masked_adam_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                                     c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp,
+                                                     c_i64, c_vp]),
     "kgat_map_rank": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_map_bits": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_hop_compact_work_bytes": (c_i64, [c_i64]),

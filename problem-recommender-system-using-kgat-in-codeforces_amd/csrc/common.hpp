@@ -65,6 +65,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// One torch.optim.Adam element update (model.py:404-419), same operation order as
+// torch's single/multi-tensor paths:
+//   m = m + (1-b1)(g - m)       (lerp, weight < 0.5 branch)
+//   v = v*b2 + ((1-b2) g) g     (mul_ then addcmul_)
+//   p = p + (-step_size) * (m / (sqrt(v)/bc2_sqrt + eps))
+// each operation rounded on its own (no FMA contraction), so every kernel that
+// calls it -- the Adam passes and the fused table update -- produces the same bits.
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float b2, float w2,
+                                          float step_size, float bc2s, float eps) {
+#pragma clang fp contract(off)
+  m = m + w1 * (g - m);
+  v = v * b2 + (w2 * g) * g;
+  p = p + (-step_size) * (m / (sqrtf(v) / bc2s + eps));
+}
+
 inline int blocks_for(int64_t work, int per_block, int cap) {
   int64_t b = (work + per_block - 1) / per_block;
   if (b < 1) b = 1;

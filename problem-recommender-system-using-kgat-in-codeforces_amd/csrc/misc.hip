@@ -7,22 +7,8 @@
 
 namespace kgat {
 
-// torch.optim.Adam step for one tensor (model.py:404-419), same operation
-// order as torch's single/multi-tensor CPU/GPU paths:
-//   m = m + (1-b1)(g - m)       (lerp, weight < 0.5 branch)
-//   v = v*b2 + ((1-b2) g) g     (mul_ then addcmul_)
-//   p = p + (-step_size) * (m / (sqrt(v)/bc2_sqrt + eps))
-// HBM-bound: 28 B per parameter (read p g m v, write p m v).
-// One element, each operation rounded on its own (no FMA contraction), so every
-// kernel below -- vector lanes and tails alike -- produces the same bits.
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float b2, float w2,
-                                          float step_size, float bc2s, float eps) {
-#pragma clang fp contract(off)
-  m = m + w1 * (g - m);
-  v = v * b2 + (w2 * g) * g;
-  p = p + (-step_size) * (m / (sqrtf(v) / bc2s + eps));
-}
-
+// torch.optim.Adam step for one tensor (model.py:404-419): adam_elem (common.hpp)
+// per element.  HBM-bound: 28 B per parameter (read p g m v, write p m v).
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    float step_size, float b1, float b2, float bc2s, float eps) {

@@ -33,17 +33,45 @@
 
 namespace kgat {
 
-// Final write of one output row segment (lane gl) in the four modes: row is
+// The p / m / v float4s of one table row segment (lane gl) for kMaskedAdam: every
+// byte is touched once per step, so non-temporal (keeps the gathered rows cached).
+struct AdamRow {
+  floatx4 p, m, v;
+};
+
+__device__ __forceinline__ AdamRow adam_row_load(const SpmmAdam& a, int64_t row, int gl) {
+  const int64_t o = row * a.ld + 4 * gl;
+  return AdamRow{__builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.p + o)),
+                 __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.m + o)),
+                 __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(a.v + o))};
+}
+
+// Adam on one row segment with gradient g (misc.hip's adam_multi arithmetic, same bits).
+__device__ __forceinline__ void adam_row_step(const SpmmAdam& a, int64_t row, int gl, float4 g, AdamRow r) {
+  const float w1 = 1.f - a.b1, w2 = 1.f - a.b2;
+  const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float pk = r.p[k], mk = r.m[k], vk = r.v[k];
+    adam_elem(pk, gg[k], mk, vk, w1, a.b2, w2, a.step_size, a.bc2s, a.eps);
+    r.p[k] = pk;
+    r.m[k] = mk;
+    r.v[k] = vk;
+  }
+  const int64_t o = row * a.ld + 4 * gl;
+  __builtin_nontemporal_store(r.p, reinterpret_cast<floatx4*>(a.p + o));
+  __builtin_nontemporal_store(r.m, reinterpret_cast<floatx4*>(a.m + o));
+  __builtin_nontemporal_store(r.v, reinterpret_cast<floatx4*>(a.v + o));
+}
+
+// Final write of one output row segment (lane gl) in the five modes: row is
 // the (global-id) row of A, out the row of Y it lands in (row, or its position
-// in the output set for kMaskedRows).
+// in the output set for kMaskedRows).  kMaskedAdam writes no Y: the row is the
+// gradient of table row `row` and goes straight into its Adam step.
 template <int MODE>
 __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t out, int gl, float4 acc,
                                           bool any = false) {
-  float4* y = reinterpret_cast<float4*>(io.Y + out * io.ldy) + gl;
-  if (MODE == kAccumulate) {
-    const float4 o = *y;
-    acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
-  } else if (MODE == kMasked || MODE == kMaskedRows) {
+  if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam) {
     if (io.Yc != nullptr) {
       const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
@@ -54,6 +82,15 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     }
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
+  if (MODE == kMaskedAdam) {
+    adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
+    return;
+  }
+  float4* y = reinterpret_cast<float4*>(io.Y + out * io.ldy) + gl;
+  if (MODE == kAccumulate) {
+    const float4 o = *y;
+    acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+  }
   *y = acc;
 }
 
@@ -61,7 +98,7 @@ template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
-  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
@@ -408,6 +445,27 @@ extern "C" int kgat_spmm_csr_masked_f32(const kgat_csr* A, const int32_t* src_ma
                                         float* workspace, int64_t workspace_floats, void* stream) {
   return kgat_spmm_csr_masked_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, Y, ldy, d, nullptr, nullptr, nullptr, 0,
                                      workspace, workspace_floats, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                             int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                             const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                             int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
+                                             float eps, float* workspace, int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
+      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
+            nullptr, nullptr, nullptr, nullptr};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps};
+  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {

@@ -228,6 +228,41 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     return out
 
 
+def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
+                     src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                     step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float) -> None:
+    """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
+    (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
+    _req(src_map, "src_map", dtype=torch.int32, dim=1)
+    _req(Xc, "Xc", dim=2)
+    n, d = graph.n_nodes, Xc.shape[1]
+    if src_map.numel() != n:
+        raise ValueError("src_map must cover every node")
+    for t, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _req(t, nm, dim=2)
+        if tuple(t.shape) != (n, d) or not t.is_contiguous():
+            raise ValueError(f"{nm}: contiguous [{n}, {d}] expected, got {tuple(t.shape)}")
+    if Yc_init is not None:
+        _req(Yc_init, "Yc_init", dim=2)
+        if Yc_init.shape[1] != d:
+            raise ValueError("Yc_init width mismatch")
+    csr = graph.AT
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_masked_adam_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
+              _rank_ptr(src_rank, src_map), p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
+              bc2_sqrt, eps, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, True, "fused_adam"))
+
+
 def hop_compact(graph: DeviceGraph, sync: bool = False):
     """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked.
 

@@ -176,6 +176,54 @@ class _IdGuard:
         return outs
 
 
+class _TableUpdate:
+    """The CF step's table gradient left unmaterialised until ``update_cf_weights`` (opt-in:
+    ``KGAT.fuse_table_update = True``).
+
+    The reference step is ``loss.backward(); model.update_cf_weights()`` (main.py:312-313):
+    backward writes the dense [N, d] table gradient, Adam reads it back (model.py:404-413).
+    With the hop chain that gradient is one masked product, A^T . dS_0 + dXd_0, of compact
+    hop-set terms; deferred, ``update_cf_weights`` runs it fused with the table's Adam step
+    (kgat_spmm_csr_masked_adam_f32): the product's latency-bound gather and Adam's streaming
+    p / m / v traffic share one pass and the 2 x 4 B/param gradient write + read disappears.
+    Same bits as the unfused step.  Meanwhile ``table.grad`` stays None; anything that needs
+    it (a second backward, a KG step, UPDATE_ATTENTION -- which rewrites A's values --, an
+    explicit ``materialize_table_grad()``) materialises it first."""
+
+    def __init__(self, param: torch.Tensor):
+        self.param = param
+        self.enabled = False
+        self.pending = None
+
+    def defer(self, graph, src_map, Xc, Yc, rank) -> bool:
+        if not self.enabled or self.param.grad is not None or self.pending is not None:
+            return False
+        self.pending = (graph, src_map, Xc, Yc, rank)
+        return True
+
+    @torch.no_grad()
+    def materialize(self) -> None:
+        if self.pending is None:
+            return
+        graph, src_map, Xc, Yc, rank = self.pending
+        self.pending = None
+        g = kernels.spmm_masked(graph, src_map, Xc, Yc_init=Yc, transpose=True, src_rank=rank)
+        if self.param.grad is None:
+            self.param.grad = g
+        else:
+            kernels.add_(self.param.grad, g)
+
+    def launch(self):
+        """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...))."""
+        graph, src_map, Xc, Yc, rank = self.pending
+        self.pending = None
+        p = self.param.data
+
+        def run(m, v, step_size, bc2s, b1, b2, eps):
+            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps)
+        return run
+
+
 def _saved(tables, states, l) -> dict:
     """Layer l's forward output + saved state for the backward (none: it recomputes)."""
     return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
@@ -208,7 +256,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, _hook = cfg
+        graph, drops, seeds, reg, _hook, _tu = cfg
         tables, sides, states = [X0], [], []
         x = X0
         for l in range(len(drops)):
@@ -227,7 +275,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg, hook = ctx.cfg
+        graph, drops, seeds, reg, hook, tu = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -298,13 +346,15 @@ class _CFLoss(torch.autograd.Function):
                 if l == 0 and hook is not None and hook.replicated:
                     # data-parallel replicas exchange the compact hop-set terms and each computes the
                     # mean table gradient A^T . mean(dS) + mean(dXd) itself (replicas.ShardedGradSync)
-                    dX = hook.table_grad_hop(graph, hmap, hrows, hcount, dSc, dXdc, rank)
+                    dX = hook.table_grad_hop(graph, hmap, hrows, hcount, dSc, dXdc, rank, deferral=tu)
                 elif l == 0 and hook is not None:
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
                     for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
                         kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
                                                   Yc_init=dXdc, row0=view.r0, src_rank=rank)
                         hook.block_ready(k, dX)
+                elif l == 0 and tu is not None and tu.defer(graph, hmap, dSc, dXdc, rank):
+                    dX = None  # computed fused with the table's Adam step by update_cf_weights
                 else:
                     dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True,
                                              row_hit=hit if l > 0 else None, src_rank=rank)
@@ -384,6 +434,23 @@ class KGAT(nn.Module):
         self._graph: DeviceGraph | None = None
         self._graph_key = None
         self._ids = _IdGuard()
+        self._table_update = _TableUpdate(self._user_entity_embedding.weight)
+
+    @property
+    def fuse_table_update(self) -> bool:
+        """Opt-in: leave the CF step's table gradient to ``update_cf_weights``, which computes it
+        fused with the table's Adam step (_TableUpdate); ``table.grad`` is None in between."""
+        return self._table_update.enabled
+
+    @fuse_table_update.setter
+    def fuse_table_update(self, on: bool) -> None:
+        if not on:
+            self._table_update.materialize()
+        self._table_update.enabled = bool(on)
+
+    def materialize_table_grad(self) -> None:
+        """Write a deferred table gradient into ``_user_entity_embedding.weight.grad``."""
+        self._table_update.materialize()
 
     # ------------------------------------------------------------------ graph
     def graph(self) -> DeviceGraph:
@@ -471,7 +538,8 @@ class KGAT(nn.Module):
         g = self.graph()
         ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes, g.device)
         drops, seeds = self._dropouts()
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None))
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None),
+               self._table_update)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
@@ -528,17 +596,30 @@ class KGAT(nn.Module):
         self._ids.raise_pending(block)
 
     def update_cf_weights(self, row_ranges: dict | None = None) -> None:
-        """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all."""
+        """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all.
+        A deferred table gradient (fuse_table_update) is stepped by the fused product + Adam."""
         self._ids.raise_pending()
-        self._cf_optimizer.step(row_ranges)
+        tu = self._table_update
+        fused = None
+        if tu.pending is not None:
+            if row_ranges and id(tu.param) in row_ranges:
+                tu.materialize()
+            else:
+                fused = {id(tu.param): tu.launch()}
+        self._cf_optimizer.step(row_ranges, fused=fused)
         self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
         self._ids.raise_pending()
+        self._table_update.materialize()
         self._kg_optimizer.step(row_ranges)
         self._kg_optimizer.zero_grad()
 
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:
+        if mode != KGATMode.PREDICT:
+            # a deferred table gradient refers to this step's hop buffers and A's values: a new
+            # backward or an attention refresh would change them
+            self._table_update.materialize()
         if mode == KGATMode.TRAIN_CF:
             return self._calc_cf_loss(*args)
         if mode == KGATMode.TRAIN_KG:

@@ -23,15 +23,36 @@ class FusedAdam:
         self.eps = float(eps)
         self.state: dict[int, dict] = {}
 
+    def _advance(self, key, like: torch.Tensor) -> tuple[dict, float, float]:
+        """Count one more step for state ``key`` (created zeroed like ``like``): (state, step_size, bc2_sqrt)."""
+        st = self.state.get(key)
+        if st is None:
+            st = {"step": 0, "exp_avg": kernels.zeros(like.shape, like.device),
+                  "exp_avg_sq": kernels.zeros(like.shape, like.device)}
+            self.state[key] = st
+        st["step"] += 1
+        t = st["step"]
+        return st, self.lr / (1.0 - self.beta1 ** t), math.sqrt(1.0 - self.beta2 ** t)
+
     @torch.no_grad()
-    def step(self, row_ranges: dict | None = None) -> None:
+    def step(self, row_ranges: dict | None = None, fused: dict | None = None) -> None:
         """Every parameter with a gradient in one kgat_adam_multi_f32 launch (per 16 tensors).
 
         ``row_ranges`` {id(param): [(r0, r1), ...]} restricts a parameter's update to those
         row ranges, each with its own optimizer state (replicas.ShardedGradSync: every rank
-        steps only the table rows it owns; the arithmetic per element is unchanged)."""
+        steps only the table rows it owns; the arithmetic per element is unchanged).
+
+        ``fused`` {id(param): launch} steps a parameter whose gradient was never materialised
+        (grad None): ``launch(exp_avg, exp_avg_sq, step_size, bc2_sqrt, beta1, beta2, eps)``
+        runs the kernel that computes the gradient and applies this step to it
+        (model._TableUpdate: the table's layer-0 A^T product fused with its Adam)."""
         items = []
         for p in self.params:
+            launch = fused.get(id(p)) if fused else None
+            if launch is not None:
+                st, step_size, bc2s = self._advance(id(p), p.data)
+                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps)
+                continue
             g = p.grad
             if g is None:
                 continue
@@ -42,16 +63,8 @@ class FusedAdam:
             views = [(id(p), p.data, g)] if ranges is None else \
                 [((id(p), r0, r1), p.data[r0:r1], g[r0:r1]) for r0, r1 in ranges if r1 > r0]
             for key, pv, gv in views:
-                st = self.state.get(key)
-                if st is None:
-                    st = {"step": 0, "exp_avg": kernels.zeros(pv.shape, p.device),
-                          "exp_avg_sq": kernels.zeros(pv.shape, p.device)}
-                    self.state[key] = st
-                st["step"] += 1
-                t = st["step"]
-                bc1 = 1.0 - self.beta1 ** t
-                bc2_sqrt = math.sqrt(1.0 - self.beta2 ** t)
-                items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], self.lr / bc1, bc2_sqrt))
+                st, step_size, bc2s = self._advance(key, pv)
+                items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
         if items:
             kernels.adam_multi(items, self.beta1, self.beta2, self.eps)
 

@@ -153,9 +153,11 @@ class ShardedGradSync:
         host = both.cpu().tolist()  # the one host sync of the step: the gather sizes
         return both, [c for _, c in host], all(f == 1 for f, _ in host)
 
-    def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words) -> torch.Tensor:
+    def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words, deferral=None):
         """The mean table gradient from this rank's compact layer-0 hop-set terms (model._CFLoss):
-        hop rows (ascending, hcount of them), dS and direct dX rows in hop order."""
+        hop rows (ascending, hcount of them), dS and direct dX rows in hop order.  With a
+        ``deferral`` (model._TableUpdate) that accepts it, the merged terms are handed over and
+        the product runs later, fused with the table's Adam step: returns None."""
         from . import kernels
 
         n = world()
@@ -177,6 +179,10 @@ class ShardedGradSync:
             cnt = both[:, 1].contiguous()
             urows, umap, ucount, urank = kernels.rows_union(graph, lists, cnt, cap)
             merged = kernels.rows_merge(lists, cnt, cap, vals, urows, ucount, min(graph.n_nodes, n * cap), 1.0 / n)
+            if deferral is not None and deferral.defer(graph, umap, merged[:, :d], merged[:, d:], urank):
+                self._done = None
+                self.stats["hop"] = self.stats.get("hop", 0) + 1
+                return None
             dX = kernels.spmm_masked(graph, umap, merged[:, :d], Yc_init=merged[:, d:], transpose=True,
                                      src_rank=urank)
         else:  # some rank's hop set is dense this step: every rank all-reduces its dense gradient

@@ -13,7 +13,9 @@ layer-0 hop-set terms and each computes the mean table gradient itself): (D) as 
 (E) with rank 1's backward forced dense (HOP_DENSE_FRACTION = 0 on that rank only), so the ranks
 disagree on the hop mode and must fall back to the dense all-reduce together.  Their sums are
 associated differently (A^T . mean(dS) instead of mean(A^T . dS)), so they are compared with the
-Adam tolerance of DESIGN.md §2, and each path's replicas must stay bit-identical.
+Adam tolerance of DESIGN.md §2, and each path's replicas must stay bit-identical.  (F) is (D) with
+``fuse_table_update``: the merged hop-set terms are handed to update_cf_weights, which runs the union
+product fused with the table's Adam step -- bit-identical to (D).
 """
 from __future__ import annotations
 
@@ -44,17 +46,18 @@ def main() -> None:
                         cf_embedding_dim=d0, kg_embedding_dim=d0, message_dropout=[0.1] * len(layer_size))
     models = []
     model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
-    for _ in range(5):
+    for k in range(6):
         torch.manual_seed(3)
         m = pkg.KGAT(args)
         m.attach_graph(lay, "cuda")
         rep.broadcast_parameters(m)
         m.train()
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = k == 5
         models.append(m)
     rng = np.random.default_rng(40 + rank)
     failures = []
-    syncs = [None] * 5
+    syncs = [None] * 6
     for step in range(3):
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
@@ -80,20 +83,22 @@ def main() -> None:
             else:
                 m.update_cf_weights(row_ranges=syncs[k].reduce())
                 syncs[k].gather()
-    for tag, want in (("D", "hop"), ("E", "dense")):
-        got = syncs["ABCDE".index(tag)].stats
+    for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop")):
+        got = syncs["ABCDEF".index(tag)].stats
         if got.get(want, 0) != 3:
             failures.append(f"{tag}: table exchange paths {got}, expected 3 x {want}")
     for named in zip(*(m.named_parameters() for m in models)):
         na, pa = named[0]
         if pa.is_sparse:
             continue
-        for tag, (_, po) in zip("BCDE", named[1:]):
+        if not torch.equal(named[3][1].data, named[5][1].data):
+            failures.append(f"F {na}: differs from D by {(named[3][1].data - named[5][1].data).abs().max().item():.3e}")
+        for tag, (_, po) in zip("BCDE", named[1:5]):
             if tag in "BC" and not torch.equal(pa.data, po.data):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
             if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
-        for tag, (_, po) in zip("ABCDE", named):
+        for tag, (_, po) in zip("ABCDEF", named):
             other = po.data.clone()
             dist.broadcast(other, 0)
             if not torch.equal(other, po.data):

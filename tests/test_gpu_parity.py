@@ -1407,3 +1407,60 @@ def test_c1_sm_shaped_pipeline_vs_reference(pkg):
     # the mean moves only by the excused (near-tie) users' differences
     moved = int((~np.isclose(per_user[20]["recall"], g["metrics/20/recall"], rtol=1e-5, atol=1e-7)).sum())
     assert abs(res[20]["recall"] - float(g["recall20_mean"])) <= 1e-6 + moved / len(eval_users)
+
+
+@pytest.mark.parametrize("layers", [[64, 32], [32, 16, 16], [64]])
+def test_fused_table_update_bit_identical(pkg, layers):
+    """KGAT.fuse_table_update (the layer-0 A^T product fused with the table's Adam step,
+    kgat_spmm_csr_masked_adam_f32) against the unfused backward + Adam: parameters and both
+    Adam moments bit for bit over three train-mode CF steps with a KG step in between (which
+    materialises nothing: the CF step already consumed its gradient); a deferred gradient
+    materialised on demand equals the unfused one."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    models = []
+    for fused in (False, True):
+        torch.manual_seed(2024)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                                  message_dropout=[0.1] * len(layers)))
+        m.attach_graph(lay, DEV)
+        assert m.graph().AT.n_long > 0  # hub rows take the segment + fix-up path
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = fused
+        models.append(m)
+    rng = np.random.default_rng(4)
+    R = len(lay.rel_order)
+    for step in range(3):
+        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+        kg = [torch.from_numpy(rng.integers(0, hi, 32)).to(DEV) for hi in (U + E, R, U + E, U + E)]
+        for m in models:
+            torch.manual_seed(100 + step)  # same dropout seeds
+            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            deferred = m._table_update.pending is not None
+            assert deferred == (m._user_entity_embedding.weight.grad is None)
+            if m.fuse_table_update and layers == [64, 32]:
+                assert deferred  # a compact layer-0 hop set: the fused kernel runs
+            m.update_cf_weights()
+            m(kg[0], kg[1], kg[2], kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
+            m.update_kg_weights()
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    ta = a._cf_optimizer.state[id(a._user_entity_embedding.weight)]
+    tb = b._cf_optimizer.state[id(b._user_entity_embedding.weight)]
+    assert ta["step"] == tb["step"] == 3
+    assert torch.equal(ta["exp_avg"], tb["exp_avg"]) and torch.equal(ta["exp_avg_sq"], tb["exp_avg_sq"])
+    # on-demand materialisation of a deferred gradient
+    ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+    grads = []
+    for m in models:
+        torch.manual_seed(7)
+        m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+        if m.fuse_table_update and layers == [64, 32]:
+            assert m._user_entity_embedding.weight.grad is None
+        m.materialize_table_grad()
+        grads.append(m._user_entity_embedding.weight.grad.detach().clone())
+    assert torch.equal(grads[0], grads[1])

@@ -32,7 +32,7 @@ def main():
     write = per_kernel(str(src / "WRITE_SIZE" / "**" / "*counter_collection.csv"), "WRITE_SIZE")
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {cmd}",
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes", "kernels": {}}
-    main_k = fix_k = None
+    main_k = fix_k = tu_k = tu_fix = None
     d0 = int(sys.argv[4]) if len(sys.argv) > 4 else 64  # the forward SpMM's width (the bench's embed_dim)
     for name in set(fetch) | set(write):
         f = fetch.get(name, [])
@@ -46,8 +46,14 @@ def main():
             main_k = rec
         if f"spmm_fixup_kernel<{d0}, 0>" in name:
             fix_k = rec
+        if f"spmm_main_kernel<{d0}, 4>" in name:  # the layer-0 A^T product fused with the table's Adam
+            tu_k = rec
+        if f"spmm_fixup_kernel<{d0}, 4>" in name:
+            tu_fix = rec
     if main_k:
         out["spmm_fwd_hbm_bytes_per_launch"] = main_k["hbm_bytes"] + (fix_k["hbm_bytes"] if fix_k else 0.0)
+    if tu_k:
+        out["table_update_hbm_bytes_per_launch"] = tu_k["hbm_bytes"] + (tu_fix["hbm_bytes"] if tu_fix else 0.0)
     if len(sys.argv) > 5:  # the bench log of the profiled run: the graph size the counters belong to
         import re
         m = re.search(r"graph: N=(\d+) .*nnz=(\d+)", Path(sys.argv[5]).read_text())
