@@ -238,7 +238,8 @@ def cpu_extrapolated(layout, cfg, fracs=(0.02, 0.04)) -> dict:
         P = _oracle_params(layout, cfg, None)
         g = torch.Generator().manual_seed(2)
         ts = []
-        for _ in range(2):  # warm-up + one timed step
+        for it in range(2):  # warm-up + one timed step
+            log(f"  CPU baseline: {f:.0%} edge subsample, {'warm-up' if it == 0 else 'timed'} step ...")
             u, p, q = (torch.randint(0, n // 10, (cfg["batch"],), generator=g) for _ in range(3))
             t0 = time.perf_counter()
             leaves = {k: v.requires_grad_(True) for k, v in P.items()}
