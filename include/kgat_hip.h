@@ -31,7 +31,9 @@ enum {
   KGAT_OK = 0,
   KGAT_ERR_INVALID = 1001,         /* bad argument (null pointer, negative size, misaligned) */
   KGAT_ERR_UNSUPPORTED_DIM = 1002, /* feature width not in the compiled set */
-  KGAT_ERR_WORKSPACE = 1003        /* caller workspace too small */
+  KGAT_ERR_WORKSPACE = 1003,       /* caller workspace too small */
+  KGAT_ERR_COMM_UNAVAILABLE = 1004, /* no loadable RCCL (kgat_comm_*) */
+  KGAT_ERR_COMM_BASE = 1100         /* + ncclResult_t: an RCCL call failed (kgat_comm_*) */
 };
 
 /* A CSR matrix plus its load-balancing plan.  Rows whose degree exceeds
@@ -575,6 +577,36 @@ int kgat_synth_triples(const kgat_synth *g, const int64_t *idx, int64_t count, i
                        int64_t *b);
 int kgat_synth_shard_build(kgat_synth *g, int64_t lo, int64_t hi, int64_t *nnz);
 int kgat_synth_shard_copy(kgat_synth *g, int64_t *rowptr, int32_t *col, float *val);
+
+/* (e) Multi-GPU transport: an RCCL communicator over xGMI behind
+ * an opaque handle, one process per GPU.  No reference counterpart -- the
+ * reference is single-device (src/model/KGAT/main.py:239); these are the
+ * collectives of the data-parallel replicas (replicas.py: table-gradient
+ * reduce-scatter / all-gather, hop-set all-gathers, the small-gradient
+ * all-reduce) and of the row-sharded propagation ring (sharded.py).  RCCL is
+ * bound at run time: kgat_comm_load(path) picks the library (NULL:
+ * "librccl.so.1"; a host that already carries an RCCL passes its path so the
+ * process holds one instance); the other calls load the default on first use.
+ * Every collective is stream-ordered on `stream`.  Errors: KGAT_ERR_COMM_BASE +
+ * ncclResult_t (kgat_comm_error_string), KGAT_ERR_COMM_UNAVAILABLE. */
+#define KGAT_COMM_ID_BYTES 128
+typedef struct kgat_comm kgat_comm;
+int kgat_comm_load(const char *rccl_path);
+const char *kgat_comm_error_string(int status);
+/* rank 0 makes the id and shares it out of band (e.g. a TCP store) */
+int kgat_comm_unique_id(uint8_t *id);
+int kgat_comm_init(int32_t rank, int32_t world, const uint8_t *id, int32_t device, kgat_comm **out);
+int kgat_comm_destroy(kgat_comm *comm);
+int kgat_comm_rank(const kgat_comm *comm, int32_t *rank, int32_t *world);
+/* recv = sum over ranks of send (count floats; send == recv in place) */
+int kgat_comm_allreduce_sum_f32(kgat_comm *comm, const float *send, float *recv, int64_t count, void *stream);
+/* recv[r * bytes_per_rank ..] = rank r's send (rank order; send may alias recv + rank * bytes_per_rank) */
+int kgat_comm_allgather_rows(kgat_comm *comm, const void *send, void *recv, int64_t bytes_per_rank, void *stream);
+/* recv (count_per_rank floats) = sum over ranks of send[rank * count_per_rank ..] (row blocks) */
+int kgat_comm_reduce_scatter_rows_f32(kgat_comm *comm, const float *send, float *recv, int64_t count_per_rank,
+                                      void *stream);
+/* the propagation ring's step: send -> rank + 1, rank - 1 -> recv (bytes each) */
+int kgat_comm_ring_exchange(kgat_comm *comm, const void *send, void *recv, int64_t bytes, void *stream);
 
 #ifdef __cplusplus
 }

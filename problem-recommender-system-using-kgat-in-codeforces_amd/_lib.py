@@ -37,6 +37,7 @@ class AdamTensor(ctypes.Structure):
 
 
 KGAT_ADAM_MAX_TENSORS = 16
+KGAT_COMM_ID_BYTES = 128
 
 
 class Tables(ctypes.Structure):
@@ -170,6 +171,16 @@ _SIGNATURES = {
     "kgat_ids_check": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp]),
     "kgat_gemm_f32": (ctypes.c_int, [c_i32, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
                                      c_i64, c_i64, c_i64, c_i32, c_vp]),
+    "kgat_comm_load": (ctypes.c_int, [ctypes.c_char_p]),
+    "kgat_comm_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "kgat_comm_unique_id": (ctypes.c_int, [c_vp]),
+    "kgat_comm_init": (ctypes.c_int, [c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp)]),
+    "kgat_comm_destroy": (ctypes.c_int, [c_vp]),
+    "kgat_comm_rank": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
+    "kgat_comm_allreduce_sum_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_comm_allgather_rows": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_comm_reduce_scatter_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_comm_ring_exchange": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_synth_open": (ctypes.c_int, [c_i64, c_i64, c_u64, ctypes.c_double, ctypes.c_int, ctypes.POINTER(c_vp)]),
     "kgat_synth_close": (None, [c_vp]),
     "kgat_synth_info": (ctypes.c_int, [c_vp, c_vp]),

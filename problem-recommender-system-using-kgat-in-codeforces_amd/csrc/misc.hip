@@ -74,7 +74,10 @@ extern "C" const char* kgat_strerror(int status) {
     case KGAT_ERR_INVALID: return "kgat: invalid argument (null pointer, bad size, or misaligned buffer)";
     case KGAT_ERR_UNSUPPORTED_DIM: return "kgat: feature width not supported by the compiled kernels";
     case KGAT_ERR_WORKSPACE: return "kgat: workspace too small";
-    default: return hipGetErrorString(static_cast<hipError_t>(status));
+    case KGAT_ERR_COMM_UNAVAILABLE: return "kgat: no loadable RCCL library (kgat_comm_load)";
+    default:
+      if (status >= KGAT_ERR_COMM_BASE && status < KGAT_ERR_COMM_BASE + 100) return kgat_comm_error_string(status);
+      return hipGetErrorString(static_cast<hipError_t>(status));
   }
 }
 

@@ -12,7 +12,9 @@ real RCCL library (forced at world 1) and its results are compared with the gloo
     all-gather) and in the replicated-table mode (hop-set all-gathers, kgat_rows_union / merge) against
     a model without any exchange -- bit-identical parameters;
 (3) RowShardedKGAT: one CF step with its collectives on RCCL against the same step on a gloo group
-    (host-staged transport) -- loss and every gradient bit-identical.
+    (host-staged transport) -- loss and every gradient bit-identical;
+(4) the library's own RCCL communicator (kgat_comm_*, comm.RcclComm): every call, and the same
+    RowShardedKGAT step with RcclComm as its transport -- bit-identical to (3).
 """
 from __future__ import annotations
 
@@ -102,19 +104,34 @@ def main() -> None:
     args3 = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32, 16],
                          message_dropout=[0.0, 0.0, 0.0])
     res = []
-    for group in (None, gloo):
+    comm_mod = __import__(pkg.__name__ + ".comm", fromlist=["comm"])
+    rc = comm_mod.RcclComm.from_process_group(dev, force=True)
+    for transport in (sh.Comm(None, force=True), sh.Comm(gloo, force=True), rc):
         torch.manual_seed(5)
-        m = sh.RowShardedKGAT(args3, lay, sh.Comm(group, force=True), dev)
+        m = sh.RowShardedKGAT(args3, lay, transport, dev)
         b = [torch.from_numpy(v).to(dev) for v in (np.arange(0, 128), np.arange(5, 133), np.arange(9, 137))]
         loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
         res.append([loss.detach().clone()] + [p.grad.detach().clone() for p in m.parameters()
                                               if p.grad is not None])
-    if len(res[0]) != len(res[1]):
-        failures.append("(3) gradient sets differ")
-    for i, (a, g) in enumerate(zip(*res)):
-        if not torch.equal(a, g):
-            failures.append(f"(3) tensor {i}: max |diff| {(a - g).abs().max().item():.3e}")
+    for tag, other in (("(3) gloo", res[1]), ("(4) kgat_comm", res[2])):
+        if len(res[0]) != len(other):
+            failures.append(f"{tag}: gradient sets differ")
+        for i, (a, g) in enumerate(zip(res[0], other)):
+            if not torch.equal(a, g):
+                failures.append(f"{tag} tensor {i}: max |diff| {(a - g).abs().max().item():.3e}")
+
+    # (4) kgat_comm_* calls at world 1: each collective returns its input (ring: a send to self)
+    x = torch.arange(4096, dtype=torch.float32, device=dev) * 0.25
+    got = {"all_reduce_": rc.all_reduce_(x.clone()), "all_gather": rc.all_gather(x)[0],
+           "all_gather_rows_": rc.all_gather_rows_(x.clone()), "reduce_scatter_rows": rc.reduce_scatter_rows(x.clone())}
+    recv = torch.empty_like(x)
+    rc.exchange(x, recv).wait()
+    got["ring_exchange"] = recv
+    for name, t in got.items():
+        if not torch.equal(t, x):
+            failures.append(f"(4) {name} changed the data")
+    rc.close()
 
     print(f"rccl world1: {'OK' if not failures else failures}", flush=True)
     dist.destroy_process_group()
