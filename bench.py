@@ -346,8 +346,11 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
     kernels.SPMM_EVENTS = []
     t0 = time.perf_counter()
     loss = None
+    host = []  # host time of each step's launches (the GPU runs behind; no synchronisation inside)
     for i in range(steps):
+        h0 = time.perf_counter()
         loss = step(batches[warmup + i])
+        host.append(time.perf_counter() - h0)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -357,6 +360,7 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
         tt = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
+    timed.host_ms_per_step = float(np.median(host)) * 1e3
     return elapsed, events, float(loss.item())
 
 
@@ -403,7 +407,8 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                         for x in (u, su[k, 1], rng.integers(0, n_items, B))])
     params = [p for p in model.parameters() if not p.is_sparse and p.requires_grad]
     dp_mode = args.dp if args.dp != "auto" else ("replicated" if L <= 2 else "sharded")
-    sync = replicas.ShardedGradSync(params, replicate_table=dp_mode == "replicated").attach(model)
+    sync = replicas.ShardedGradSync(params, replicate_table=dp_mode == "replicated",
+                                    force=args.exchange_at_1).attach(model)
 
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
@@ -427,10 +432,15 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                    "dp_exchange": dp_mode if world > 1 else None, "mode": "train (dropout 0.1)",
                    "table_update": "unfused" if args.no_fused_update else "fused layer-0 A^T product + Adam"},
         "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
+        "host_launch_ms_per_step": timed.host_ms_per_step,
         "cpu_baseline": None,
     }
-    if world > 1:
+    if world > 1 or args.exchange_at_1:
         result["dp_table_exchange_steps"] = dict(sync.stats)
+    if args.exchange_at_1:
+        result["config"]["dp_exchange"] = dp_mode
+        result["rehearsal"] = ("the N-rank table exchange forced at world 1 over RCCL (collectives move no data "
+                               "between GPUs): its GPU + host overhead per step, not a scaling measurement")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg["nodes"] > 2_000_000:
             log("timing the CPU baseline (oracle restatement on subsampled edge sets, extrapolated) ...")
@@ -535,6 +545,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--exchange-at-1", action="store_true",
+                    help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
     ap.add_argument("--no-fused-update", action="store_true",
                     help="c2/c4: materialise the table gradient and run Adam as its own pass")
     ap.add_argument("--dry-run", action="store_true",
@@ -591,7 +603,7 @@ def main() -> int:
         return 2
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1 or cfg["mode"] == "sharded":  # the row-sharded model always runs over a process group
+    if world > 1 or cfg["mode"] == "sharded" or args.exchange_at_1:  # (row-sharded: always a process group)
         torch.cuda.set_device(local)
         kw = {} if "MASTER_ADDR" in os.environ else dict(init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
                                                            world_size=1)

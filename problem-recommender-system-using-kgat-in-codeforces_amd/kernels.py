@@ -374,12 +374,13 @@ def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_row
 
 
 def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int,
-                    dh_compact: bool = False):
+                    dh_compact: bool = False, out=None):
     """Saved-state bi-interaction backward on a hop set whose size is only known on the device:
     rows / count from hop_compact or frontier_hop, dH indexed by node ([N, d_out], the previous
     masked product's output) or, with ``dh_compact``, by hop position (spmm_masked_rows' output).
     Returns compact (dXd, dS) with ``out_rows`` rows allocated (the first count are valid) and
-    (dW1, db1, dW2, db2)."""
+    (dW1, db1, dW2, db2).  ``out`` = (dXd, dS): caller-owned [>= out_rows, d_in] views to write
+    (e.g. the two halves of one [cap, 2*d_in] exchange buffer)."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     for t, nm in ((X, "X"), (S, "S"), (dH, "dH"), (H, "H")):
@@ -392,8 +393,15 @@ def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: B
     if out_rows < 1 or rows.numel() < out_rows:
         raise ValueError("hop rows buffer too small")
     dev = X.device
-    dXd = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
-    dS = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
+    if out is not None:
+        dXd, dS = out
+        for t, nm in ((dXd, "out dXd"), (dS, "out dS")):
+            _req(t, nm, dim=2)
+            if t.shape[0] < out_rows or t.shape[1] != din:
+                raise ValueError(f"{nm}: [>= {out_rows}, {din}] expected, got {tuple(t.shape)}")
+    else:
+        dXd = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
+        dS = torch.empty(out_rows, din, dtype=torch.float32, device=dev)
     dW1, dW2 = torch.empty_like(W1), torch.empty_like(W2)
     db1 = torch.empty(dout, dtype=torch.float32, device=dev)
     db2 = torch.empty(dout, dtype=torch.float32, device=dev)

@@ -224,6 +224,24 @@ class _TableUpdate:
         return run
 
 
+def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
+    """Data-parallel replicas exchanging the layer-0 hop-set terms (replicas.ShardedGradSync,
+    replicated) with 2 layers: the layer-0 hop set is the first hop F + N(F) of the batch rows F,
+    fixed by the batch and the graph alone.  It is marked here, before the propagation, and its
+    size is all-gathered at once (hook.announce) -- so the host learns the exchange's sizes while
+    the GPU runs the forward, instead of synchronising in the middle of the backward.  Returns
+    (frontier rows, frontier_hop outputs) for the backward, or None (the backward decides then)."""
+    if hook is None or not getattr(hook, "replicated", False) or L != 2 or HOP_DENSE_FRACTION <= 0:
+        return None
+    W1 = ws[0]
+    if not kernels.saved_state_supported(W1.shape[1], W1.shape[0]) or not _hop_small(graph, 0, graph.n_nodes):
+        return None
+    rows, _ = kernels.frontier_build(users, pos, neg, graph.node_map)
+    hop = kernels.frontier_hop(graph, rows)
+    hook.announce(True, hop[2])
+    return rows, hop
+
+
 def _saved(tables, states, l) -> dict:
     """Layer l's forward output + saved state for the backward (none: it recomputes)."""
     return {} if states[l] is None else {"H": tables[l + 1], "state": states[l]}
@@ -256,7 +274,8 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, _hook, _tu = cfg
+        graph, drops, seeds, reg, hook, _tu = cfg
+        ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook)
         tables, sides, states = [X0], [], []
         x = X0
         for l in range(len(drops)):
@@ -284,7 +303,8 @@ class _CFLoss(torch.autograd.Function):
         wgrads: list[torch.Tensor | None] = [None] * (4 * L)
         hit = graph.hop_buffers()[0] if L > 1 else None
         # ---- last layer on the batch frontier
-        rows, _count = kernels.frontier_build(users, pos, neg, graph.node_map)
+        early, ctx.early = ctx.early, None
+        rows = early[0] if early is not None else kernels.frontier_build(users, pos, neg, graph.node_map)[0]
         dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)
         kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dHc, row_map=graph.node_map)
         l = L - 1
@@ -292,13 +312,15 @@ class _CFLoss(torch.autograd.Function):
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
         bits = graph.hop_buffers()[6]
         rank = graph.hop_buffers()[9]  # rank words of the current hop set (frontier_hop / hop_compact)
-        sparse = hit is not None and HOP_DENSE_FRACTION > 0
+        # a rank that announced its layer-0 hop set to the replicas (forward) is committed to the hop path
+        sparse = early is not None or (hit is not None and HOP_DENSE_FRACTION > 0)
         pending = None
         nxt = L - 2
-        if sparse and states[nxt] is not None and states[nxt].kind == "fused" and _hop_small(graph, nxt, n_nodes):
+        if early is not None or (sparse and states[nxt] is not None and states[nxt].kind == "fused"
+                                 and _hop_small(graph, nxt, n_nodes)):
             # first hop marked from the frontier rows' A edges (no graph scan); the A^T product is
             # computed on those rows only, compactly (kgat_spmm_csr_masked_rows_f32)
-            hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows)
+            hrows, hmap, hcount, bits, fbits = early[1] if early is not None else kernels.frontier_hop(graph, rows)
             _hop_record(graph, nxt, hcount)
             dX = kernels.spmm_masked_rows(graph, graph.node_map, fbits, dSc, dXdc, hrows, hmap, hcount, bits)
             kernels.frontier_reset(rows, graph.node_map)
@@ -333,10 +355,18 @@ class _CFLoss(torch.autograd.Function):
                 # dX is zero outside the hop set: the bi-interaction backward runs on its rows
                 # only and the A^T product gathers from them only (kgat_spmm_csr_masked_ex_f32);
                 # per row and per output element the arithmetic and order are the dense path's
+                packed = None
                 if fused:
+                    out_rows, out = n_nodes, None
+                    cap = hook.exchange_cap() if l == 0 and hook is not None and hook.replicated else None
+                    if cap is not None:
+                        # the replicas' exchange buffer [cap, 2d] = dS | dXd, written by the backward itself
+                        din = W1.shape[1]
+                        packed = torch.empty(cap, 2 * din, dtype=torch.float32, device=dX.device)
+                        out_rows, out = cap, (packed[:, din:], packed[:, :din])
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd_hop(
-                        tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], n_nodes,
-                        dh_compact=compact_dh)
+                        tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], out_rows,
+                        dh_compact=compact_dh, out=out)
                 else:
                     dHc = kernels.gather_rows(dX, hrows)
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,
@@ -346,7 +376,7 @@ class _CFLoss(torch.autograd.Function):
                 if l == 0 and hook is not None and hook.replicated:
                     # data-parallel replicas exchange the compact hop-set terms and each computes the
                     # mean table gradient A^T . mean(dS) + mean(dXd) itself (replicas.ShardedGradSync)
-                    dX = hook.table_grad_hop(graph, hmap, hrows, hcount, dSc, dXdc, rank, deferral=tu)
+                    dX = hook.table_grad_hop(graph, hmap, hrows, hcount, dSc, dXdc, rank, deferral=tu, packed=packed)
                 elif l == 0 and hook is not None:
                     dX = torch.empty(n_nodes, dSc.shape[1], dtype=torch.float32, device=dSc.device)
                     for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):

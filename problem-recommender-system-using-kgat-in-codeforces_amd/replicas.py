@@ -108,6 +108,7 @@ class ShardedGradSync:
         self._table = None
         self.bounds: list[tuple[int, int]] = []
         self._early = None  # (gradient tensor, [work handles]) of the hooked table gradient
+        self._announced = None  # this step's early (flag, hop count) all-gather: (device, pinned host, event)
 
     def attach(self, model) -> "ShardedGradSync":
         """Overlap the table gradient's exchange with its computation: the CF backward then
@@ -143,40 +144,82 @@ class ShardedGradSync:
         dist.all_gather(parts, flat)
         return torch.cat(parts)
 
-    def _agree(self, sparse: bool, count: torch.Tensor | None, dev) -> tuple[torch.Tensor, list[int], bool]:
-        """All-gather (sparse flag, hop count) of every rank: (device [G, 2], host counts, all sparse)."""
-        info = torch.zeros(2, dtype=torch.int32, device=dev)
+    def _gather_info(self, sparse: bool, count: torch.Tensor | None, dev):
+        """[G] int32 in rank order: each rank's layer-0 hop count, -1 for a rank whose backward is dense."""
         if sparse:
-            info[0] = 1
-            info[1:2].copy_(count)
-        both = self._all_gather(info).view(-1, 2)
-        host = both.cpu().tolist()  # the one host sync of the step: the gather sizes
-        return both, [c for _, c in host], all(f == 1 for f, _ in host)
+            info = count.reshape(1).to(torch.int32)
+        else:
+            info = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        return self._all_gather(info)
 
-    def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words, deferral=None):
+    def announce(self, sparse: bool, count: torch.Tensor | None) -> None:
+        """All-gather this step's (hop flag, layer-0 hop count) early -- from the forward, when the
+        hop set is known before the propagation (model._early_first_hop) -- and start copying the
+        result to the host; _agree then reads it without stalling the GPU queue."""
+        if self._announced is not None:
+            raise RuntimeError("ShardedGradSync: a TRAIN_CF forward whose backward never ran (the replicas' "
+                               "exchange of that step is still open)")
+        both = self._gather_info(sparse, count, count.device)
+        host = torch.empty(tuple(both.shape), dtype=torch.int32, pin_memory=True)
+        host.copy_(both, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._announced = (both, host, ev)
+
+    def exchange_cap(self) -> int | None:
+        """Rows every rank sends in this step's hop-set all-gather (the largest hop count), once the
+        counts were announced and every rank's backward is sparse; else None."""
+        ann = self._announced
+        if ann is None:
+            return None
+        ann[2].synchronize()
+        counts = ann[1].tolist()
+        return max(1, max(counts)) if all(c >= 0 for c in counts) else None
+
+    def _agree(self, sparse: bool, count: torch.Tensor | None, dev) -> tuple[torch.Tensor, list[int], bool]:
+        """All-gather every rank's hop count (-1: dense): (device [G] counts, host counts, all sparse).
+        Announced early (the usual 2-layer case): the copy finished long ago, no stall; otherwise
+        the step's one host synchronisation."""
+        ann, self._announced = self._announced, None
+        if ann is not None:
+            both, host_t, ev = ann
+            ev.synchronize()
+            host = host_t.tolist()
+        else:
+            both = self._gather_info(sparse, count, dev)
+            host = both.cpu().tolist()  # the gather sizes
+        return both, host, all(c >= 0 for c in host)
+
+    def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words, deferral=None, packed=None):
         """The mean table gradient from this rank's compact layer-0 hop-set terms (model._CFLoss):
         hop rows (ascending, hcount of them), dS and direct dX rows in hop order.  With a
         ``deferral`` (model._TableUpdate) that accepts it, the merged terms are handed over and
-        the product runs later, fused with the table's Adam step: returns None."""
+        the product runs later, fused with the table's Adam step: returns None.  ``packed``: the
+        [exchange_cap(), 2d] buffer dSc | dXdc are the halves of (sent as it is, no copies)."""
         from . import kernels
 
         n = world()
         d = dSc.shape[1]
         both, counts, all_sparse = self._agree(True, hcount, dSc.device)
         if all_sparse:
-            # every rank sends [cap] rows: the compact buffers hold the hop set's capacity (fused
-            # saved-state layer 0) or exactly its own count (other shapes: hop_compact(sync=True)),
-            # so pad to the largest count -- rows past a rank's count are ignored (cnt) but sized alike
+            # every rank sends [cap] rows, cap = the largest count; rows past a rank's own count are
+            # never read (the union / merge kernels stop at each list's count)
             cap = max(1, max(counts))
-            k = min(cap, dSc.shape[0], hrows.numel())
-            pack = torch.zeros(cap, 2 * d, dtype=torch.float32, device=dSc.device)
-            pack[:k, :d].copy_(dSc[:k])
-            pack[:k, d:].copy_(dXdc[:k])
-            hl = torch.zeros(cap, dtype=hrows.dtype, device=hrows.device)
-            hl[:k].copy_(hrows[:k])
+            if packed is not None and packed.shape[0] == cap:
+                pack = packed
+            else:
+                k = min(cap, dSc.shape[0])
+                pack = torch.empty(cap, 2 * d, dtype=torch.float32, device=dSc.device)
+                pack[:k, :d].copy_(dSc[:k])
+                pack[:k, d:].copy_(dXdc[:k])
+            if hrows.numel() >= cap:
+                hl = hrows[:cap]
+            else:
+                hl = torch.empty(cap, dtype=hrows.dtype, device=hrows.device)
+                hl[:hrows.numel()].copy_(hrows)
             lists = self._all_gather(hl)
             vals = self._all_gather(pack).view(n * cap, 2 * d)
-            cnt = both[:, 1].contiguous()
+            cnt = both
             urows, umap, ucount, urank = kernels.rows_union(graph, lists, cnt, cap)
             merged = kernels.rows_merge(lists, cnt, cap, vals, urows, ucount, min(graph.n_nodes, n * cap), 1.0 / n)
             if deferral is not None and deferral.defer(graph, umap, merged[:, :d], merged[:, d:], urank):
@@ -275,15 +318,16 @@ class ShardedGradSync:
                 ranges[id(p)] = rr
                 self._big.append((p, s, main))
             else:
-                small.append(g)
+                small.append(p)
         if small:
-            flat = torch.cat([g.reshape(-1) for g in small])
+            # one flat bucket; the parameters' gradients become views of it (no copy-back kernels)
+            flat = torch.cat([p.grad.reshape(-1) for p in small])
             dist.all_reduce(flat)
             flat.div_(n)
             off = 0
-            for g in small:
-                k = g.numel()
-                g.copy_(flat[off:off + k].view_as(g))
+            for p in small:
+                k = p.grad.numel()
+                p.grad = flat[off:off + k].view_as(p.grad)
                 off += k
         return ranges
 

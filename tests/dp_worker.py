@@ -68,11 +68,11 @@ def main() -> None:
                 syncs[k] = rep.ShardedGradSync(params, replicate_table=k >= 3)
                 if k >= 2:
                     syncs[k].attach(m)
-            loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
             frac = model_mod.HOP_DENSE_FRACTION
-            if k == 4 and rank == 1:
+            if k == 4 and rank == 1:  # rank 1 chooses the dense backward (before its forward, as a rank does)
                 model_mod.HOP_DENSE_FRACTION = 0.0
             try:
+                loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
                 loss.backward()
             finally:
                 model_mod.HOP_DENSE_FRACTION = frac
