@@ -1,5 +1,5 @@
 """One rank of the data-parallel replica check (launched by tests/test_gpu_sharded.py through
-``python -m torch.distributed.run --nproc-per-node 2``; both ranks on cuda:0, gloo).
+``python -m torch.distributed.run --nproc-per-node 2`` (or 4); every rank on cuda:0, gloo).
 
 Three replica sets train side by side on the same rank-dependent batches with rank-dependent dropout:
 (A) replicas.allreduce_gradients + every rank's full Adam, (B) replicas.ShardedGradSync -- row-block
@@ -94,7 +94,10 @@ def main() -> None:
         if not torch.equal(named[3][1].data, named[5][1].data):
             failures.append(f"F {na}: differs from D by {(named[3][1].data - named[5][1].data).abs().max().item():.3e}")
         for tag, (_, po) in zip("BCDE", named[1:5]):
-            if tag in "BC" and not torch.equal(pa.data, po.data):
+            # two ranks: every sum has two operands, so B / C equal A bit for bit; more ranks
+            # associate the sums differently (the Adam tolerance, as D / E)
+            if tag in "BC" and (not torch.equal(pa.data, po.data) if dist.get_world_size() == 2
+                                else not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5)):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
             if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")

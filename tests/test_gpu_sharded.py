@@ -119,6 +119,23 @@ def test_dp_sharded_grad_sync_world2_matches_allreduce():
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
 
 
+def test_dp_exchange_paths_world4():
+    """tests/dp_worker.py on four ranks (all on this GPU, gloo): every exchange path (all-reduce,
+    row-block reduce-scatter with and without the backward overlap, replicated hop-set exchange,
+    its dense fallback with rank 1 dense, the fused table update) keeps the replicas identical, and
+    the fused replicated path equals the unfused one bit for bit -- the union / merge over G = 4
+    lists the 8-GPU run takes, minus RCCL."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / "dp_world4.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+
+
 def test_dp_replicated_exchange_wide_layer0_world2():
     """a 128-wide layer 0 (128 -> 128, no fused saved-state backward) under
     ShardedGradSync(replicate_table=True): each rank's compact hop buffers hold exactly its own
@@ -151,8 +168,8 @@ def test_rccl_world1_collectives_match_gloo():
     assert "rccl world1: OK" in p.stdout, p.stdout[-2000:]
 
 
-@pytest.mark.parametrize("dp", ["replicated", "sharded"])
-def test_bench_two_ranks_gloo_rehearsal(dp):
+@pytest.mark.parametrize("dp,gpus", [("replicated", 2), ("sharded", 2), ("replicated", 4)])
+def test_bench_two_ranks_gloo_rehearsal(dp, gpus):
     """bench.py --gpus 2 end to end (launch, process group, DP replicas with the table exchange, timing,
     max-over-ranks, one JSON line) with both ranks on this one GPU over gloo (KGAT_BENCH_BACKEND):
     the N-rank path the driver's multi-GPU run takes, minus RCCL."""
@@ -163,13 +180,13 @@ def test_bench_two_ranks_gloo_rehearsal(dp):
     env = dict(os.environ, KGAT_BENCH_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "small", "--scale", "0.2",
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--config", "small", "--scale", "0.2",
                         "--steps", "3", "--warmup", "1", "--dp", dp], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, p.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["dp_exchange"] == dp
+    assert rec["n_gpus"] == gpus and rec["config"]["parallelism"] == f"dp{gpus}" and rec["config"]["dp_exchange"] == dp
     assert rec["rehearsal"].startswith("gloo") and rec["value"] > 0 and np.isfinite(rec["final_loss"])
     assert sum(rec["dp_table_exchange_steps"].values()) == 4 if dp == "replicated" else True
