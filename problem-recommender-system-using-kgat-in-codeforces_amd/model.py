@@ -568,8 +568,10 @@ class KGAT(nn.Module):
         g = self.graph()
         ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes, g.device)
         drops, seeds = self._dropouts()
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), getattr(self, "_table_grad_hook", None),
-               self._table_update)
+        # the data-parallel hook only where a backward follows (a no_grad loss evaluation has none: it must
+        # not open the replicas' exchange of a step)
+        hook = getattr(self, "_table_grad_hook", None) if torch.is_grad_enabled() else None
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:

@@ -83,6 +83,9 @@ def main() -> None:
             else:
                 m.update_cf_weights(row_ranges=syncs[k].reduce())
                 syncs[k].gather()
+            if step == 0:
+                with torch.no_grad():  # a loss evaluation without backward opens no exchange
+                    m(*b, mode=pkg.KGATMode.TRAIN_CF)
     for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop")):
         got = syncs["ABCDEF".index(tag)].stats
         if got.get(want, 0) != 3:
