@@ -69,6 +69,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip tab
 GPU_BYTES = 288e9              # HBM3E per MI355X
 GPU_BUDGET = 0.85 * GPU_BYTES  # what a config may plan to use (allocator slack, workspaces)
 PARITY_TOL = {"emb": 1e-4, "loss_rel": 1e-4, "grad": 1e-6}  # north_star: 1e-4 fp32 (gradients as in tests/)
+EVENT_EVERY = 1  # --event-every
 
 
 def log(*a):
@@ -343,11 +344,17 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    kernels.SPMM_EVENTS = []
+    # HIP events around the SpMM launches of every EVENT_EVERY-th timed step (each record costs the
+    # stream a few us; --event-every 1 instruments every step)
+    events_all = []
+    timed.instrumented = 0
     t0 = time.perf_counter()
     loss = None
     host = []  # host time of each step's launches (the GPU runs behind; no synchronisation inside)
     for i in range(steps):
+        on = i % EVENT_EVERY == 0
+        kernels.SPMM_EVENTS = events_all if on else None
+        timed.instrumented += int(on)
         h0 = time.perf_counter()
         loss = step(batches[warmup + i])
         host.append(time.perf_counter() - h0)
@@ -355,7 +362,7 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    events, kernels.SPMM_EVENTS = kernels.SPMM_EVENTS, None
+    events, kernels.SPMM_EVENTS = events_all, None
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -422,8 +429,10 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
     n, nnz, d0 = layout.n_nodes, layout.nnz, cfg["dim"]
-    roof, spmm = roofline(events, args.config, n, nnz, d0, args.steps, f"spmm_main_kernel<{d0}, 0> (+fixup), forward A.X")
+    roof, spmm = roofline(events, args.config, n, nnz, d0, timed.instrumented,
+                          f"spmm_main_kernel<{d0}, 0> (+fixup), forward A.X")
     spmm["fwd_spmm_layer_edges_per_s"] = nnz * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
+    spmm["event_steps"] = timed.instrumented  # timed steps whose SpMM launches carry HIP events
     result = {
         "value": world * nnz * L / (ms * 1e-3), "n_gpus": world, "ms_per_step": ms, "scaling": "weak",
         "config": {"workload": cfg["workload"], "nodes": n, "nnz": nnz, "interactions": int(len(inter)),
@@ -519,7 +528,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
     d0 = cfg["dim"]
-    roof, spmm = roofline(events, args.config, shard.n, 0, d0, args.steps,
+    roof, spmm = roofline(events, args.config, shard.n, 0, d0, timed.instrumented,
                           f"spmm_main_kernel<{d0}, 0> on the A[k][j] blocks (ring all-gather pipelined)")
     spmm["fwd_spmm_layer_edges_per_s_rank0"] = sum(shard.nnz) * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
     return {
@@ -545,6 +554,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="HIP events (the roofline's live kernel times) around the SpMMs of every k-th timed step")
     ap.add_argument("--exchange-at-1", action="store_true",
                     help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
     ap.add_argument("--no-fused-update", action="store_true",
@@ -556,6 +567,8 @@ def main() -> int:
                          "hop-set terms, every rank computes the mean gradient and full Adam; sharded = row-block "
                          "reduce-scatter, owned-row Adam, all-gather; auto = replicated for 2-layer configs")
     args = ap.parse_args()
+    global EVENT_EVERY
+    EVENT_EVERY = max(1, args.event_every)
     cfg = dict(CONFIGS[args.config])
     if args.scale != 1.0:
         cfg["nodes"] = max(1000, int(cfg["nodes"] * args.scale))
