@@ -130,24 +130,26 @@ int kgat_map_rank(const int32_t *node_map, int64_t n, uint64_t *rank, void *stre
 
 /* The next hop set from row_hit (int32 [n], 0/1): node_map[i] = position of i
  * among the flagged nodes (ascending node order) or -1, rows[0..count) = the
- * flagged nodes, *count (device int32) = their number.  work: scan scratch of
- * kgat_hop_compact_work_bytes(n) bytes. */
+ * flagged nodes, *count (device int32) = their number; count_host (nullable: host-mapped
+ * pinned memory, e.g. hipHostMalloc) gets the same value from the kernel, with no copy launch.
+ * work: scan scratch of kgat_hop_compact_work_bytes(n) bytes. */
 int64_t kgat_hop_compact_work_bytes(int64_t n);
-int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *rows, int32_t *count, void *work,
-                     int64_t work_bytes, void *stream);
+int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *rows, int32_t *count,
+                     int32_t *count_host, void *work, int64_t work_bytes, void *stream);
 
 /* The first hop of the backward chain without scanning the graph: for the
  * last layer's A^T product over the batch frontier F (rows0[0..n0), -1
  * padded, kgat_frontier_build), bits0 (uint32 [ceil(n/32)]) marks F and
  * bits1 marks F plus every column of A's rows F -- the rows that product can
  * reach; node_map / hop_rows / *hop_count list bits1's set in ascending node
- * order (node_map fully written, -1 outside); hop_rank (nullable, uint64
+ * order (node_map fully written, -1 outside); hop_count_host (nullable) as kgat_hop_compact's
+ * count_host; hop_rank (nullable, uint64
  * [ceil(n/32)]) gets the set's rank words (kgat_map_rank's layout).  work:
  * kgat_frontier_hop_work_bytes(n) bytes. */
 int64_t kgat_frontier_hop_work_bytes(int64_t n);
 int kgat_frontier_hop(const kgat_csr *A, const int32_t *rows0, int32_t n0, uint32_t *bits0, uint32_t *bits1,
-                      int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, uint64_t *hop_rank, void *work,
-                      int64_t work_bytes, void *stream);
+                      int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, int32_t *hop_count_host,
+                      uint64_t *hop_rank, void *work, int64_t work_bytes, void *stream);
 
 /* kgat_spmm_csr_masked_f32 restricted to an output row set (A = A^T of the
  * graph; out_bits / out_map / out_rows / out_count from kgat_frontier_hop):
@@ -528,8 +530,9 @@ int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst,
 /* Id validation without a host synchronisation (the reference's embedding gathers raise
  * IndexError, src/model/KGAT/model.py:188-191, 219-222, 389-391): the ids of up to
  * KGAT_IDS_MAX int64 arrays are copied, concatenated, into out; an id outside [0, bound)
- * is written as 0 (so no later kernel indexes out of range) and sets *bad to 1 (the caller
- * zeroes it and reads it back asynchronously). */
+ * is written as 0 (so no later kernel indexes out of range) and sets *bad to 1 (a plain
+ * store: bad may be device memory or host-mapped pinned memory the caller reads after the
+ * stream passes this call; the caller zeroes it). */
 #define KGAT_IDS_MAX 4
 typedef struct kgat_ids {
   const int64_t *ptr[KGAT_IDS_MAX];

@@ -92,13 +92,13 @@ _SIGNATURES = {
     "kgat_map_rank": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_map_bits": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_hop_compact_work_bytes": (c_i64, [c_i64]),
-    "kgat_hop_compact": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_hop_compact": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_biinter_bwd_hop_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
                                                 c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_i64, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp]),
     "kgat_frontier_hop_work_bytes": (c_i64, [c_i64]),
     "kgat_frontier_hop": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                         c_i64, c_vp]),
+                                         c_vp, c_i64, c_vp]),
     "kgat_rows_union": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
                                        c_vp]),
     "kgat_rows_merge_f32": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp,

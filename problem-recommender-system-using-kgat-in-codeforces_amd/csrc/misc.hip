@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ s
     dst[i] = src[idx[i]];
 }
 
-// ids of up to KGAT_IDS_MAX arrays, concatenated into out; out-of-range ids become 0 and raise *bad
+// ids of up to KGAT_IDS_MAX arrays, concatenated into out; out-of-range ids become 0 and set *bad = 1
 __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t total, int64_t bound,
                                                         int64_t* __restrict__ out, int32_t* __restrict__ bad) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t to
     out[i] = ok ? v : 0;
     flag |= !ok;
   }
-  if (flag) atomicOr(bad, 1);
+  if (flag) *bad = 1;  // every writer stores 1: no atomic needed (bad may be host-mapped pinned memory)
 }
 
 __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ dst, int64_t n, float value) {

@@ -278,7 +278,8 @@ struct Popc {
 __global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __restrict__ bits,
                                                           const int32_t* __restrict__ woff, int64_t n,
                                                           int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
-                                                          int32_t* __restrict__ count, uint64_t* __restrict__ rank) {
+                                                          int32_t* __restrict__ count, uint64_t* __restrict__ rank,
+                                                          int32_t* __restrict__ count_host) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t w = bits[i >> 5];
@@ -287,7 +288,10 @@ __global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __rest
   const bool in = ((w >> b) & 1u) != 0;
   node_map[i] = in ? pos : -1;
   if (in) rows[pos] = static_cast<int32_t>(i);
-  if (i == n - 1) *count = pos + (in ? 1 : 0);
+  if (i == n - 1) {
+    *count = pos + (in ? 1 : 0);
+    if (count_host != nullptr) *count_host = pos + (in ? 1 : 0);  // pinned host mirror: no copy launch
+  }
   // the set's rank words (kgat_map_rank's layout): members before the word << 32 | its bits
   if (rank != nullptr && b == 0) rank[i >> 5] = (static_cast<uint64_t>(static_cast<uint32_t>(woff[i >> 5])) << 32) | w;
 }
@@ -333,12 +337,15 @@ __global__ __launch_bounds__(256) void map_rank_kernel(const int32_t* __restrict
 // so the last thread can read its own scan value for the count first.
 __global__ __launch_bounds__(256) void hop_finish_kernel(const int32_t* __restrict__ hit, int64_t n,
                                                          int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
-                                                         int32_t* __restrict__ count) {
+                                                         int32_t* __restrict__ count, int32_t* __restrict__ count_host) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t pos = node_map[i];
   const bool h = hit[i] != 0;
-  if (i == n - 1) *count = pos + (h ? 1 : 0);
+  if (i == n - 1) {
+    *count = pos + (h ? 1 : 0);
+    if (count_host != nullptr) *count_host = pos + (h ? 1 : 0);
+  }
   if (h) {
     rows[pos] = static_cast<int32_t>(i);
   } else {
@@ -478,16 +485,20 @@ extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {
 }
 
 extern "C" int kgat_hop_compact(const int32_t* hit, int64_t n, int32_t* node_map, int32_t* rows, int32_t* count,
-                                void* work, int64_t work_bytes, void* stream) {
+                                int32_t* count_host, void* work, int64_t work_bytes, void* stream) {
   if (!hit || !node_map || !rows || !count || n < 0 || n > INT32_MAX) return KGAT_ERR_INVALID;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (n == 0) return hipMemsetAsync(count, 0, sizeof(int32_t), st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  if (n == 0) {
+    if (count_host != nullptr) *count_host = 0;
+    return hipMemsetAsync(count, 0, sizeof(int32_t), st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  }
   const int64_t need = kgat_hop_compact_work_bytes(n);
   if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
   size_t bytes = static_cast<size_t>(need);
   const hipError_t e = hipcub::DeviceScan::ExclusiveSum(work, bytes, hit, node_map, static_cast<int>(n), st);
   if (e != hipSuccess) return static_cast<int>(e);
-  hipLaunchKernelGGL(kgat::hop_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, hit, n, node_map, rows, count);
+  hipLaunchKernelGGL(kgat::hop_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, hit, n, node_map, rows, count,
+                     count_host);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -516,7 +527,8 @@ extern "C" int64_t kgat_frontier_hop_work_bytes(int64_t n) {
 
 extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_t n0, uint32_t* bits0,
                                  uint32_t* bits1, int32_t* node_map, int32_t* hop_rows, int32_t* hop_count,
-                                 uint64_t* hop_rank, void* work, int64_t work_bytes, void* stream) {
+                                 int32_t* hop_count_host, uint64_t* hop_rank, void* work, int64_t work_bytes,
+                                 void* stream) {
   if (!A || !rows0 || !bits0 || !bits1 || !node_map || !hop_rows || !hop_count || n0 < 0 || A->n_rows < 0)
     return KGAT_ERR_INVALID;
   const int64_t n = A->n_rows;
@@ -539,7 +551,7 @@ extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_
   if (e != hipSuccess) return static_cast<int>(e);
   if (hop_rank != nullptr && (reinterpret_cast<uintptr_t>(hop_rank) & 7)) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits1, woff, n, node_map,
-                     hop_rows, hop_count, hop_rank);
+                     hop_rows, hop_count, hop_rank, hop_count_host);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -602,7 +614,7 @@ extern "C" int kgat_rows_union(const int32_t* lists, const int32_t* counts, int3
   const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
   if (e != hipSuccess) return static_cast<int>(e);
   hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits, woff, n, node_map, rows,
-                     count, rank);
+                     count, rank, nullptr);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

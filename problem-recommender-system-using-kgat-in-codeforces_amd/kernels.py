@@ -263,29 +263,40 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
         ev.append((e0, e1, d, True, "fused_adam"))
 
 
-def hop_compact(graph: DeviceGraph, sync: bool = False):
+def _host_ptr(t: torch.Tensor | None):
+    """A pinned int32 host tensor the kernels write directly (host-mapped memory), or None."""
+    if t is None:
+        return None
+    if t.device.type != "cpu" or not t.is_pinned() or t.dtype != torch.int32 or t.numel() < 1:
+        raise ValueError("count_host: a pinned int32 host tensor")
+    return t.data_ptr()
+
+
+def hop_compact(graph: DeviceGraph, sync: bool = False, count_host: torch.Tensor | None = None):
     """The hop set flagged in graph.hop_buffers()'s row_hit by the last spmm_masked.
 
     Returns (rows int32 [N] -- the first n entries are the hop set, ascending --, node_map
     int32 [N] node -> position or -1, count int32 [1] on the device, n); the hop set's rank
     words are left in graph.hop_buffers()[9] (kgat_map_rank).  With ``sync`` the
     count is read back (one stream sync) and rows is cut to n; otherwise n is None and
-    consumers read the count on the device (biinter_bwd_hop)."""
+    consumers read the count on the device (biinter_bwd_hop).  ``count_host`` (pinned int32): the
+    kernel also writes the count there (the next step's hop-size estimate, model._hop_record)."""
     hb = graph.hop_buffers()
     hit, node_map, rows, count, work, host = hb[:6]
     dev = hit.device
+    if sync and count_host is None:
+        count_host = host
     _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
-              count.data_ptr(), work.data_ptr(), work.numel(), stream_ptr(dev))
+              count.data_ptr(), _host_ptr(count_host), work.data_ptr(), work.numel(), stream_ptr(dev))
     map_rank(node_map, hb[9])
     if not sync:
         return rows, node_map, count, None
-    host.copy_(count, non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    n = int(host.item())
+    torch.cuda.current_stream(dev).synchronize()  # the kernel wrote count_host
+    n = int(count_host[0])
     return rows[:n], node_map, count, n
 
 
-def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
+def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor, count_host: torch.Tensor | None = None):
     """The first hop set of the backward chain from the batch frontier rows0 (frontier_build's
     rows, -1 padded): (hop rows int32 [N] ascending -- first count valid --, node_map, count int32 [1]
     on the device, hop-set bitmap, frontier bitmap).  No graph scan: the frontier rows' A edges are
@@ -295,8 +306,8 @@ def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor):
     _, node_map, rows, count, _, _, bits1, bits0, work = hb[:9]
     desc = graph.A.descriptor()
     _lib.call("kgat_frontier_hop", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
-              bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), hb[9].data_ptr(),
-              work.data_ptr(), work.numel(), stream_ptr(rows0.device))
+              bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), _host_ptr(count_host),
+              hb[9].data_ptr(), work.data_ptr(), work.numel(), stream_ptr(rows0.device))
     return rows, node_map, count, bits1, bits0
 
 

@@ -103,14 +103,19 @@ def _hop_small(graph, l: int, n_nodes: int) -> bool:
     return est is None or est <= HOP_DENSE_FRACTION * n_nodes
 
 
-def _hop_record(graph, l: int, count: torch.Tensor) -> None:
-    """Copy layer l's device-side hop count to pinned memory for the next step's choice."""
+def _hop_host(graph, l: int) -> torch.Tensor:
+    """Layer l's pinned hop-count mirror: the kernel that lists the hop set (kgat_frontier_hop /
+    kgat_hop_compact) writes the count there itself (host-mapped memory, no copy launch)."""
     est = graph.__dict__.setdefault("_hop_est", {})
     ent = est.get(l)
     if ent is None:
         ent = est[l] = (torch.zeros(1, dtype=torch.int32, pin_memory=True), torch.cuda.Event())
-    ent[0].copy_(count, non_blocking=True)
-    ent[1].record()
+    return ent[0]
+
+
+def _hop_record(graph, l: int) -> None:
+    """Mark the point after which layer l's host count is valid (the next step's choice)."""
+    graph._hop_est[l][1].record()
 
 
 class _IdGuard:
@@ -119,12 +124,12 @@ class _IdGuard:
 
     Host ids are checked on the host, at once.  Device ids are checked on the device without
     a host synchronisation (kgat_ids_check: one launch copies them, zeroes any id outside
-    [0, bound) so no kernel reads out of range, and raises a device flag); the flag is read
-    back asynchronously and IndexError is raised at the model's next call (or by
+    [0, bound) so no kernel reads out of range, and sets a flag in pinned host memory); the flag
+    is read after the call's event and IndexError is raised at the model's next call (or by
     ``raise_pending(block=True)``) -- the way PyTorch reports a device-side index error."""
 
     def __init__(self):
-        self._bad = self._host = self._event = None
+        self._host = self._event = None
         self._pending = None
 
     def raise_pending(self, block: bool = False) -> None:
@@ -134,7 +139,6 @@ class _IdGuard:
         what = self._pending
         self._pending = None
         if int(self._host[0]):
-            self._bad.zero_()
             self._host.zero_()
             raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed)")
 
@@ -151,8 +155,9 @@ class _IdGuard:
                     if t.numel() and (int(t.min()) < 0 or int(t.max()) >= b):
                         raise IndexError(f"{what}: id out of range [0, {b}) (min {int(t.min())}, max {int(t.max())})")
             return [t.to(device).long().reshape(-1).contiguous() for t in flat]
-        if self._bad is None:
-            self._bad = torch.zeros(1, dtype=torch.int32, device=device)
+        if self._host is None:
+            # the flag lives in pinned host memory, written by the check kernel itself (host-mapped:
+            # no copy launch per call)
             self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._event = torch.cuda.Event()
         outs = []
@@ -167,10 +172,9 @@ class _IdGuard:
                     d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
                 d.count = len(part)
                 off = sum(sizes[:i])
-                _lib.call("kgat_ids_check", ctypes.byref(d), b, out.data_ptr() + 8 * off, self._bad.data_ptr(),
+                _lib.call("kgat_ids_check", ctypes.byref(d), b, out.data_ptr() + 8 * off, self._host.data_ptr(),
                           stream_ptr(device))
             outs += list(out[:sum(sizes)].split(sizes))
-        self._host.copy_(self._bad, non_blocking=True)
         self._event.record()
         self._pending = what
         return outs
@@ -237,7 +241,8 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     if not kernels.saved_state_supported(W1.shape[1], W1.shape[0]) or not _hop_small(graph, 0, graph.n_nodes):
         return None
     rows, _ = kernels.frontier_build(users, pos, neg, graph.node_map)
-    hop = kernels.frontier_hop(graph, rows)
+    hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0))
+    _hop_record(graph, 0)
     hook.announce(True, hop[2])
     return rows, hop
 
@@ -320,8 +325,11 @@ class _CFLoss(torch.autograd.Function):
                                  and _hop_small(graph, nxt, n_nodes)):
             # first hop marked from the frontier rows' A edges (no graph scan); the A^T product is
             # computed on those rows only, compactly (kgat_spmm_csr_masked_rows_f32)
-            hrows, hmap, hcount, bits, fbits = early[1] if early is not None else kernels.frontier_hop(graph, rows)
-            _hop_record(graph, nxt, hcount)
+            if early is not None:
+                hrows, hmap, hcount, bits, fbits = early[1]
+            else:
+                hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, nxt))
+                _hop_record(graph, nxt)
             dX = kernels.spmm_masked_rows(graph, graph.node_map, fbits, dSc, dXdc, hrows, hmap, hcount, bits)
             kernels.frontier_reset(rows, graph.node_map)
             kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX, row_map=hmap)
@@ -346,8 +354,8 @@ class _CFLoss(torch.autograd.Function):
                 # size this layer's hop set had at the previous step
                 sparse = _hop_small(graph, l, n_nodes)
                 if sparse:
-                    hrows, hmap, hcount, _ = kernels.hop_compact(graph)
-                    _hop_record(graph, l, hcount)
+                    hrows, hmap, hcount, _ = kernels.hop_compact(graph, count_host=_hop_host(graph, l))
+                    _hop_record(graph, l)
             elif sparse:
                 hrows, hmap, hcount, n_hop = kernels.hop_compact(graph, sync=True)
                 sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
