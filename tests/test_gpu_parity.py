@@ -1464,3 +1464,45 @@ def test_fused_table_update_bit_identical(pkg, layers):
         m.materialize_table_grad()
         grads.append(m._user_entity_embedding.weight.grad.detach().clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_fused_table_update_materialises_on_demand(pkg):
+    """A deferred table gradient (KGAT.fuse_table_update) meets the calls that need it: a second CF
+    backward before the step (gradient accumulation) and an UPDATE_ATTENTION (which rewrites A's
+    values) between backward and step.  Parameters after each sequence equal the unfused model's
+    bit for bit."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=6)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    models = []
+    for fused in (False, True):
+        torch.manual_seed(2024)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                                  message_dropout=[0.1, 0.1]))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = fused
+        models.append(m)
+    rng = np.random.default_rng(9)
+    att = [torch.from_numpy(np.asarray(x, np.int64)).to(DEV) for x in (lay.heads, lay.rels, lay.tails, lay.rel_order)]
+    b1, b2 = ([torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+              for _ in range(2))
+    for m in models:
+        # accumulation: two backwards, one step
+        torch.manual_seed(11)
+        m(*b1, mode=pkg.KGATMode.TRAIN_CF).backward()
+        m(*b2, mode=pkg.KGATMode.TRAIN_CF).backward()
+        m.update_cf_weights()
+        # an attention refresh between backward and step
+        torch.manual_seed(12)
+        m(*b1, mode=pkg.KGATMode.TRAIN_CF).backward()
+        m.eval()
+        m(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+        m.train()
+        m.update_cf_weights()
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    assert torch.equal(a.attentive_matrix.data.coalesce().values(), b.attentive_matrix.data.coalesce().values())
