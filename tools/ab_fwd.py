@@ -1,0 +1,88 @@
+"""A/B of the bi-interaction forward variants (KGAT_FWD_VARIANT, read once per process).
+
+    KGAT_FWD_VARIANT=8  python tools/ab_fwd.py out_a.json
+    KGAT_FWD_VARIANT=24 python tools/ab_fwd.py out_b.json
+    python tools/ab_fwd.py --compare out_a.json out_b.json
+
+Each run times kgat_biinter_fwd_f32 (saved-state form, train-mode dropout) per shape on synthetic
+rows and records a digest of H, the row norms and the state words; --compare checks the digests are
+equal (the variants must produce the same bits) and prints the time ratio.
+"""
+from __future__ import annotations
+
+import hashlib
+import importlib
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+PKG = "problem-recommender-system-using-kgat-in-codeforces_amd"
+
+SHAPES = [(64, 64, 1_000_000), (64, 32, 1_000_000), (64, 64, 1_000_003), (64, 32, 37), (128, 64, 1_000_000),
+          (128, 128, 200_000), (32, 16, 5_001)]
+
+
+def digest(*ts) -> str:
+    h = hashlib.sha256()
+    for t in ts:
+        h.update(t.contiguous().cpu().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
+def run(out: str) -> None:
+    import torch
+
+    K = importlib.import_module(PKG + ".kernels")
+    dev = torch.device("cuda")
+    res = {"variant": os.environ.get("KGAT_FWD_VARIANT", "default")}
+    only = os.environ.get("AB_SHAPES")
+    shapes = [s for s in SHAPES if not only or f"{s[0]}x{s[1]}_n{s[2]}" in only.split(",")]
+    for din, dout, n in shapes:
+        g = torch.Generator(device=dev).manual_seed(din * 1000 + dout + n)
+        X = torch.randn(n, din, device=dev, generator=g)
+        S = torch.randn(n, din, device=dev, generator=g)
+        W1 = torch.randn(dout, din, device=dev, generator=g) * 0.1
+        W2 = torch.randn(dout, din, device=dev, generator=g) * 0.1
+        b1 = torch.randn(dout, device=dev, generator=g) * 0.1
+        b2 = torch.randn(dout, device=dev, generator=g) * 0.1
+        H = torch.empty(n, dout, device=dev)
+        st = K.BiState(n, dev, din, dout)
+        fn = lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st)  # noqa: E731
+        fn()
+        torch.cuda.synchronize()
+        d = digest(H, *([st.norm[:n], st.mask] if st.kind in ("fused", "bits") else []))
+        reps = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        key = f"{din}x{dout}_n{n}"
+        res[key] = {"us": round(us, 2), "digest": d}
+        print(key, res[key], flush=True)
+        del X, S, H, st
+    Path(out).write_text(json.dumps(res, indent=1))
+
+
+def compare(a: str, b: str) -> int:
+    ra, rb = json.loads(Path(a).read_text()), json.loads(Path(b).read_text())
+    bad = 0
+    for k in ra:
+        if k == "variant":
+            continue
+        same = ra[k]["digest"] == rb[k]["digest"]
+        bad += not same
+        print(f"{k:22s} {ra[k]['us']:9.1f} us -> {rb[k]['us']:9.1f} us  x{ra[k]['us'] / rb[k]['us']:.3f}  "
+              f"{'bits equal' if same else 'BITS DIFFER'}")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--compare":
+        sys.exit(compare(sys.argv[2], sys.argv[3]))
+    run(sys.argv[1])

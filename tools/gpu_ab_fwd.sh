@@ -1,14 +1,14 @@
 #!/bin/bash
-# A/B of the bi-interaction forward launch variants (KGAT_FWD_VARIANT) at C2 shapes, then the C2 step.
-set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
+# A/B of the bi-interaction forward variants (KGAT_FWD_VARIANT): the first is the baseline.
+# usage: tools/gpu_ab_fwd.sh 8 24 40 ...
+set -o pipefail
 mkdir -p gpurun_out
-for v in 8 12 0 4 10 14; do
-  KGAT_FWD_VARIANT=$v timeout -k 10 300 python -u tools/bench_kernels.py --only graph --reps 20 > gpurun_out/abfwd_$v.log 2>&1 || { tail -5 gpurun_out/abfwd_$v.log; exit 1; }
-  echo "variant $v: $(grep biinter_fwd_saved gpurun_out/abfwd_$v.log | tr '\n' ' ')"
+: > gpurun_out/ab_fwd.log
+for v in "$@"; do
+  KGAT_FWD_VARIANT=$v timeout -k 10 200 python -u tools/ab_fwd.py gpurun_out/fwd_$v.json >> gpurun_out/ab_fwd.log 2>&1 || { tail -20 gpurun_out/ab_fwd.log; exit 1; }
 done
-for v in 8 12; do
-  KGAT_FWD_VARIANT=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-parity > gpurun_out/abfwd_bench_$v.log 2>&1 || { tail -5 gpurun_out/abfwd_bench_$v.log; exit 1; }
-  echo "bench $v $(tail -1 gpurun_out/abfwd_bench_$v.log | grep -o '"ms_per_step": [0-9.]*')"
+for v in "${@:2}"; do
+  echo "== $1 vs $v" >> gpurun_out/ab_fwd.log
+  python tools/ab_fwd.py --compare gpurun_out/fwd_$1.json gpurun_out/fwd_$v.json >> gpurun_out/ab_fwd.log 2>&1
 done
+grep -A8 "==" gpurun_out/ab_fwd.log
