@@ -444,6 +444,18 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         "host_launch_ms_per_step": timed.host_ms_per_step,
         "cpu_baseline": None,
     }
+    if world == 1 and not args.no_frontier_leg and not args.exchange_at_1:
+        # the same CF step with KGAT.frontier_forward (each layer's forward on the rows the loss can
+        # reach only: same loss, gradients and updates bit for bit, tested) -- the training step as
+        # driver.py runs it; `value` above stays the full-propagation step
+        model.frontier_forward = True
+        fel, _, _ = timed(step, batches, args.warmup, args.steps, world, dev)
+        model.frontier_forward = False
+        fms = fel / args.steps * 1e3
+        result["frontier_forward"] = {
+            "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
+            "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer 0 of 2 on F + N(F), the "
+                    "last layer on the batch rows F); not counted in value (it does not visit every edge)"}
     if world > 1 or args.exchange_at_1:
         result["dp_table_exchange_steps"] = dict(sync.stats)
     if args.exchange_at_1:
@@ -558,6 +570,8 @@ def main() -> int:
                     help="HIP events (the roofline's live kernel times) around the SpMMs of every k-th timed step")
     ap.add_argument("--exchange-at-1", action="store_true",
                     help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
+    ap.add_argument("--no-frontier-leg", action="store_true",
+                    help="skip the second timed run with KGAT.frontier_forward (training-step speed)")
     ap.add_argument("--no-fused-update", action="store_true",
                     help="c2/c4: materialise the table gradient and run Adam as its own pass")
     ap.add_argument("--dry-run", action="store_true",

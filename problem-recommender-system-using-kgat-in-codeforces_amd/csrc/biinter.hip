@@ -180,14 +180,19 @@ struct BiFwdWaves {
   static constexpr int k = 2 * DOUT * (DIN + 4) * 4 > 80 * 1024 ? 8 : 4;
 };
 
-template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4>
+// TL: only the 16-row sub-tiles listed in tiles[0 .. *tile_count) (a hop set's tiles,
+// kgat_bits_tiles), the same per-tile arithmetic as the whole-table launch.
+template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4, bool TL = false>
 __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
                                                           float* __restrict__ H, int64_t ldh, int64_t n, float p,
                                                           uint64_t seed, float* __restrict__ norm_out,
-                                                          uint64_t* __restrict__ mask_out, int64_t node0) {
+                                                          uint64_t* __restrict__ mask_out, int64_t node0,
+                                                          const int32_t* __restrict__ tiles = nullptr,
+                                                          const int32_t* __restrict__ tile_count = nullptr) {
+  static_assert(!(TL && PF), "the tile-list forward has no prefetch");
   using B = BiShape<DIN, DOUT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
   float* w1s = smem;
@@ -204,16 +209,17 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
   }
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t thr = bi_drop_threshold(p);
-  const int64_t nsub = (n + 15) / 16;
+  const int64_t nsub = TL ? static_cast<int64_t>(*tile_count) : (n + 15) / 16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * NWV;
-  int64_t st = static_cast<int64_t>(blockIdx.x) * NWV + (threadIdx.x >> 6);
+  int64_t k = static_cast<int64_t>(blockIdx.x) * NWV + (threadIdx.x >> 6);
   // PF: the next sub-tile's rows are loaded while the current one computes
   float nx[B::KQ], ns[B::KQ];
   if (PF) {
-    load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
-    load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+    load_rows<DIN>(X, ldx, k * 16 + c, n, q, nx);
+    load_rows<DIN>(S, lds, k * 16 + c, n, q, ns);
   }
-  for (; st < nsub; st += stride) {
+  for (; k < nsub; k += stride) {
+    const int64_t st = TL ? static_cast<int64_t>(tiles[k]) : k;
     if (!PF) {
       load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
       load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
@@ -224,9 +230,9 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
       u[t] = nx[t] + ns[t];
       m[t] = nx[t] * ns[t];
     }
-    if (PF && st + stride < nsub) {
-      load_rows<DIN>(X, ldx, (st + stride) * 16 + c, n, q, nx);
-      load_rows<DIN>(S, lds, (st + stride) * 16 + c, n, q, ns);
+    if (PF && k + stride < nsub) {
+      load_rows<DIN>(X, ldx, (k + stride) * 16 + c, n, q, nx);
+      load_rows<DIN>(S, lds, (k + stride) * 16 + c, n, q, ns);
     }
     bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
                               mask_out, node0);
@@ -1048,6 +1054,20 @@ static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
 }
 
 template <int DIN, int DOUT>
+static int launch_fwd_tiles(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                            const float* b1, const float* W2, const float* b2, float* H, int64_t ldh, int64_t n,
+                            float p, uint64_t seed, float* norm, uint64_t* mask, const int32_t* tiles,
+                            const int32_t* tile_count, int64_t max_tiles, hipStream_t st) {
+  constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
+  // the list's size is on the device: the grid covers max_tiles (capped; waves stride over the list)
+  const int grid = blocks_for(max_tiles * 16, 16 * NWV, kCUs * 8 * 4 / NWV);
+  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, false, 2, NWV, true>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx,
+                     S, lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, int64_t{0}, tiles, tile_count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+template <int DIN, int DOUT>
 static int saved_grid(int64_t n) {
   return blocks_for(n, 64, kCUs);
 }
@@ -1195,6 +1215,27 @@ extern "C" int kgat_biinter_fwd_rows_f32(const float* X, int64_t ldx, const floa
                                                   norm_out, mask_out, node0, st)
   KGAT_BI_DISPATCH(KGAT_FWD_CALL)
 #undef KGAT_FWD_CALL
+}
+
+extern "C" int kgat_biinter_fwd_tiles_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
+                                          const float* W1, const float* b1, const float* W2, const float* b2,
+                                          float* H, int64_t ldh, int64_t n_rows, const int32_t* tiles,
+                                          const int32_t* tile_count, int64_t max_tiles, int32_t d_in, int32_t d_out,
+                                          float dropout_p, uint64_t seed, float* norm_out, uint64_t* mask_out,
+                                          void* stream) {
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || !tiles || !tile_count || n_rows < 0 || max_tiles < 0)
+    return KGAT_ERR_INVALID;
+  if (max_tiles > (n_rows + 15) / 16) return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 128)) return KGAT_ERR_INVALID;
+  if (n_rows == 0 || max_tiles == 0) return KGAT_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_FWDT_CALL(a, b) kgat::launch_fwd_tiles<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, \
+                                                         seed, norm_out, mask_out, tiles, tile_count, max_tiles, st)
+  KGAT_BI_DISPATCH(KGAT_FWDT_CALL)
+#undef KGAT_FWDT_CALL
 }
 
 extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     const int s = blockIdx.x * 4 + wave;
     if (s >= A.n_seg) return;
     const int row = A.seg_row[s];
-    if (MODE == kMaskedRows && !bit_of(io.out_bits, row)) return;  // not an output row
+    if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
     const int64_t beg = A.seg_beg[s];
     const int64_t row_end = A.rowptr[row + 1];
     const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
@@ -132,21 +132,23 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     return;
   }
 
-  if (MODE == kMaskedRows) {
-    // ---- short rows of the output set: one group per row, waves stride over the list
+  if (MODE == kMaskedRows || MODE == kRows) {
+    // ---- short rows of the output set: one group per row, groups stride over the list one row
+    // at a time (a set of ~10^4 rows keeps every group of the grid busy instead of a few waves
+    // walking kRowsPerWave rows each; each row is still summed by one group in edge order)
     const int64_t cnt = *io.out_count;
-    const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * S::kRowsPerWave;
-    for (int64_t k0 = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kRowsPerWave; k0 < cnt;
-         k0 += stride) {
-      const int64_t k_end = k0 + S::kRowsPerWave < cnt ? k0 + S::kRowsPerWave : cnt;
-      for (int64_t k = k0 + g; k < k_end; k += S::kGroups) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * S::kGroups;
+    {
+      for (int64_t k = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kGroups + g; k < cnt;
+           k += stride) {
         const int64_t r = io.out_rows[k];
+        if (MODE == kRows && r < 0) continue;  // padding of a frontier list
         const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
         if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         bool any = false;
-        gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
-        store_row<MODE>(io, r, k, gl, acc, any);
+        gather_edges<D, MODE == kMaskedRows>(A, io, beg, end, base, gl, acc, any);
+        store_row<MODE>(io, r, MODE == kRows ? r : k, gl, acc, any);
       }
     }
     return;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   const int lr = blockIdx.x;
   const int g = threadIdx.x / L, gl = threadIdx.x % L;
   const int row = A.long_rows[lr];
-  if (MODE == kMaskedRows && !bit_of(io.out_bits, row)) return;  // block-uniform: not an output row
+  if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
   const float4* P = reinterpret_cast<const float4*>(io.part);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int s_end = A.long_seg_off[lr + 1];
@@ -198,7 +200,7 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
   int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
-  if (MODE == kMaskedRows && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
+  if ((MODE == kMaskedRows || MODE == kRows) && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
@@ -573,6 +575,46 @@ extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* s
   const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits, nullptr,
                   out_bits, out_map, out_rows, out_count};
   return dispatch<kMaskedRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t ldx, const uint32_t* out_bits,
+                                      const int32_t* out_rows, const int32_t* out_count, float* Y, int64_t ldy,
+                                      int32_t d, float* workspace, int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !X || !Y || !out_bits || !out_rows || !out_count || A->n_rows < 0 || ldx < d || ldy < d || (ldx & 3) ||
+      (ldy & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(X) || misaligned(Y)) return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr,
+                  out_bits, nullptr, out_rows, out_count};
+  return dispatch<kRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace kgat {
+// 16-row tiles holding at least one member of a node set (bitmap, 32 nodes per word: two
+// tiles), listed in no particular order (each tile's bi-interaction is independent).
+__global__ __launch_bounds__(256) void bits_tiles_kernel(const uint32_t* __restrict__ bits, int64_t words,
+                                                         int32_t* __restrict__ tiles, int32_t* __restrict__ count) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (w >= words) return;
+  const uint32_t b = bits[w];
+  if (b & 0xffffu) tiles[atomicAdd(count, 1)] = static_cast<int32_t>(2 * w);
+  if (b >> 16) tiles[atomicAdd(count, 1)] = static_cast<int32_t>(2 * w + 1);
+}
+}  // namespace kgat
+
+extern "C" int kgat_bits_tiles(const uint32_t* bits, int64_t n, int32_t* tiles, int32_t* count, void* stream) {
+  if (!bits || !tiles || !count || n < 0 || n > INT32_MAX) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(count, 0, sizeof(int32_t), st) != hipSuccess) return KGAT_ERR_INVALID;
+  const int64_t words = (n + 31) / 32;
+  if (words == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::bits_tiles_kernel, dim3((words + 255) / 256), dim3(256), 0, st, bits, words, tiles, count);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 extern "C" int kgat_map_rank(const int32_t* node_map, int64_t n, uint64_t* rank, void* stream) {

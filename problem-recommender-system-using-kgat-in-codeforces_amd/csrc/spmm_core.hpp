@@ -7,7 +7,12 @@
 
 namespace kgat {
 
-enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4 };
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4, kRows = 5 };
+
+// kRows: the dense product A . X on the rows of an output set only (out_rows / out_bits /
+// out_count; -1 entries of out_rows are padding), each written at its own row of Y -- the
+// forward of a layer whose output is needed on a hop set only (kgat_spmm_csr_rows_f32).
+// Per row the same edges in the same order as kOverwrite (same bits).
 
 // kMaskedAdam: the masked product's row is the gradient of a table row and is
 // consumed on the spot by its Adam step (p, m, v rows of the same index), so
@@ -36,7 +41,8 @@ struct SpmmIo {
   int64_t row0;           // masked: global row of local row 0 (Yc lookup of a row-block view)
   const uint32_t* src_bits;  // masked: bit c set <=> src_map[c] >= 0 (nullable: test src_map directly)
   const uint64_t* src_rank;  // masked, ascending compact order: word c/32 = (#members before it) << 32 | its bits
-  // kMaskedRows: only the rows of an output set are produced, compactly (row out_rows[k] -> Y row k)
+  // kMaskedRows: only the rows of an output set are produced, compactly (row out_rows[k] -> Y row k);
+  // kRows: the same set, each row written at its own index
   const uint32_t* out_bits;  // bit r set <=> r in the set
   const int32_t* out_map;    // r -> k or -1
   const int32_t* out_rows;   // k -> r, ascending

@@ -384,6 +384,75 @@ def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_row
     return out
 
 
+def spmm_rows(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor, out_rows: torch.Tensor,
+              out_count: torch.Tensor, out_bits: torch.Tensor) -> torch.Tensor:
+    """out[r] = (A . X)[r] for the rows r = out_rows[k], k < out_count (device), only; the other
+    rows of ``out`` are left as they are (kgat_spmm_csr_rows_f32: same bits per row as spmm)."""
+    _req(X, "X", dim=2)
+    _req(out, "out", dim=2)
+    n, d = X.shape
+    if n != graph.n_nodes or tuple(out.shape) != (n, d):
+        raise ValueError("X / out must be [n_nodes, d]")
+    for t, nm in ((out_rows, "out_rows"), (out_count, "out_count")):
+        _req(t, nm, dtype=torch.int32, dim=1)
+    if out_bits.dtype != torch.int32 or out_bits.numel() * 32 < n:
+        raise ValueError("out_bits must be an int32 bitmap covering every node")
+    csr = graph.A
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=X.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_rows_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out_bits.data_ptr(),
+              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(),
+              stream_ptr(X.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, False, "rows"))
+    return out
+
+
+def bits_tiles(bits: torch.Tensor, n: int):
+    """(tiles int32 [ceil(n/16)] -- first count valid, any order --, count int32 [1] on the device): the
+    16-row tiles holding a member of the bitmap's set (kgat_bits_tiles)."""
+    if bits.dtype != torch.int32 or bits.numel() * 32 < n:
+        raise ValueError("bits must be an int32 bitmap covering n nodes")
+    tiles = torch.empty(max((n + 15) // 16, 1), dtype=torch.int32, device=bits.device)
+    count = torch.empty(1, dtype=torch.int32, device=bits.device)
+    _lib.call("kgat_bits_tiles", bits.data_ptr(), n, tiles.data_ptr(), count.data_ptr(), stream_ptr(bits.device))
+    return tiles, count
+
+
+def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: torch.Tensor, tiles: torch.Tensor,
+                      tile_count: torch.Tensor, state: BiState | None = None) -> torch.Tensor:
+    """biinter_fwd on the listed 16-row tiles only (kgat_biinter_fwd_tiles_f32): H / state rows of those
+    tiles get the whole-table call's bits, the rest of ``out`` and the state are left as they are."""
+    for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2"), (out, "out")):
+        _req(t, nm, dim=2)
+    _req(tiles, "tiles", dtype=torch.int32, dim=1)
+    _req(tile_count, "tile_count", dtype=torch.int32, dim=1)
+    n, din = X.shape
+    dout = W1.shape[0]
+    if S.shape != X.shape or W1.shape != (dout, din) or W2.shape != (dout, din) or tuple(out.shape) != (n, dout):
+        raise ValueError("bi-interaction shape mismatch")
+    if not fused_supported(din, dout) or dout > 128:
+        raise ValueError(f"no fused forward for {din}->{dout}")
+    if not (W1.is_contiguous() and W2.is_contiguous()):
+        raise ValueError("W must be contiguous")
+    words = (dout + 63) // 64
+    if state is not None and (state.kind not in ("fused", "bits") or state.norm.numel() < n
+                              or state.mask.numel() < (n + 15) // 16 * 64 * words):
+        raise ValueError("bi-interaction state too small")
+    max_tiles = min(tiles.numel(), (n + 15) // 16)
+    _lib.call("kgat_biinter_fwd_tiles_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
+              W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, tiles.data_ptr(), tile_count.data_ptr(),
+              max_tiles, din, dout, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              state.norm.data_ptr() if state is not None else None,
+              state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
+    return out
+
+
 def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int,
                     dh_compact: bool = False, out=None):
     """Saved-state bi-interaction backward on a hop set whose size is only known on the device:

@@ -240,11 +240,60 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     W1 = ws[0]
     if not kernels.saved_state_supported(W1.shape[1], W1.shape[0]) or not _hop_small(graph, 0, graph.n_nodes):
         return None
-    rows, _ = kernels.frontier_build(users, pos, neg, graph.node_map)
+    rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
     hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0))
     _hop_record(graph, 0)
     hook.announce(True, hop[2])
-    return rows, hop
+    return rows, hop, fcount
+
+
+def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
+    """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1 or 2, every layer
+    with the fused saved state).  The BPR loss reads the batch rows F of every table (model.py:189-191),
+    so the last layer's output is needed on F only, and with 2 layers layer 0's on the first hop
+    F + N(F) (layer 1 gathers its A rows from there) -- the same row sets the backward's hop chain
+    runs on.  Each layer then runs kgat_spmm_csr_rows_f32 on its set's rows and
+    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them: every row the step reads gets the
+    full forward's bits (same edges, order and dropout draws), rows outside are never read.  At C2
+    layer 0's set is 1.7 % of the rows (35 % of the edges), layer 1's the ~768 batch rows.
+    Returns (tables, sides, states, early) -- early as _early_first_hop's, for the backward -- or
+    None when the shapes do not qualify (the full forward runs)."""
+    L = len(drops)
+    if L not in (1, 2) or HOP_DENSE_FRACTION <= 0:
+        return None
+    dims = [X0.shape[1]] + [ws[4 * l].shape[0] for l in range(L)]
+    if not all(kernels.saved_state_supported(dims[l], dims[l + 1]) for l in range(L)):
+        return None
+    if L == 2 and early is None and not _hop_small(graph, 0, graph.n_nodes):
+        return None
+    n = graph.n_nodes
+    if early is None:
+        rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
+        hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0) if L == 2 else None)
+        if L == 2:
+            _hop_record(graph, 0)
+        early = (rows, hop, fcount)
+    rows, hop, fcount = early
+    hrows, _, hcount, bits1, fbits = hop
+    # layer l's output row set: the first hop for layer 0 of 2, the batch rows F for the last layer
+    sets = [(hrows, hcount, bits1)] * (L - 1) + [(rows, fcount, fbits)]
+    tables, sides, states = [X0], [], []
+    x = X0
+    for l in range(L):
+        W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
+        out_rows, out_count, out_bits = sets[l]
+        st = kernels.make_state(n, dims[l], dims[l + 1], x.device)
+        s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
+                              out_count, out_bits)
+        tiles, tcount = kernels.bits_tiles(out_bits, n)
+        x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
+                                      torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device), tiles,
+                                      tcount, state=st)
+        sides.append(s)
+        states.append(st)
+        tables.append(x)
+    # L = 1: the backward's last layer needs the batch rows only (no hop set is handed over)
+    return tables, sides, states, (early if L == 2 else (rows, None, fcount))
 
 
 def _saved(tables, states, l) -> dict:
@@ -279,17 +328,21 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, hook, _tu = cfg
+        graph, drops, seeds, reg, hook, _tu, frontier = cfg
         ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook)
-        tables, sides, states = [X0], [], []
-        x = X0
-        for l in range(len(drops)):
-            W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
-            st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
-            s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st)
-            sides.append(s)
-            states.append(st)
-            tables.append(x)
+        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early) if frontier else None
+        if fw is not None:
+            tables, sides, states, ctx.early = fw
+        else:
+            tables, sides, states = [X0], [], []
+            x = X0
+            for l in range(len(drops)):
+                W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
+                st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
+                s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st)
+                sides.append(s)
+                states.append(st)
+                tables.append(x)
         loss, coef = kernels.bpr_fwd(tables, users, pos, neg, reg)
         ctx.cfg = cfg
         ctx.tables, ctx.sides, ctx.states, ctx.ws = tables, sides, states, ws
@@ -299,7 +352,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg, hook, tu = ctx.cfg
+        graph, drops, seeds, reg, hook, tu, _frontier = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -310,6 +363,8 @@ class _CFLoss(torch.autograd.Function):
         # ---- last layer on the batch frontier
         early, ctx.early = ctx.early, None
         rows = early[0] if early is not None else kernels.frontier_build(users, pos, neg, graph.node_map)[0]
+        if early is not None and early[1] is None:
+            early = None  # 1-layer frontier forward: the batch rows only
         dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)
         kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dHc, row_map=graph.node_map)
         l = L - 1
@@ -473,6 +528,9 @@ class KGAT(nn.Module):
         self._graph_key = None
         self._ids = _IdGuard()
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
+        # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
+        # (_frontier_forward) -- same loss, gradients and updates, bit for bit
+        self.frontier_forward = False
 
     @property
     def fuse_table_update(self) -> bool:
@@ -579,7 +637,9 @@ class KGAT(nn.Module):
         # the data-parallel hook only where a backward follows (a no_grad loss evaluation has none: it must
         # not open the replicas' exchange of a step)
         hook = getattr(self, "_table_grad_hook", None) if torch.is_grad_enabled() else None
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update)
+        # the frontier forward only where a backward follows: its batch-row map is released by the backward
+        frontier = self.frontier_forward and torch.is_grad_enabled()
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:

@@ -6,6 +6,8 @@ atol 1e-5 on O(1) values, atol 1e-6 on gradients of size ~1e-3).
 """
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -1464,6 +1466,68 @@ def test_fused_table_update_bit_identical(pkg, layers):
         m.materialize_table_grad()
         grads.append(m._user_entity_embedding.weight.grad.detach().clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("layers", [[64], [64, 32], [64, 64], [64, 32, 16]])
+def test_frontier_forward_bit_identical(pkg, layers, monkeypatch):
+    """KGAT.frontier_forward (TRAIN_CF's forward on the rows the loss can reach: layer 0 of 2 on
+    the first hop F + N(F), the last layer on the batch rows F -- kgat_spmm_csr_rows_f32 +
+    kgat_biinter_fwd_tiles_f32) against the full forward: losses, parameters and both Adam
+    moments bit for bit over three train-mode CF steps (dropout on, fused table update on) with a
+    KG step in between, on a hub-row graph; 3 layers fall back to the full forward."""
+    graph_mod, _ = _mods(pkg)
+    kmod = sys.modules[pkg.__name__ + ".kernels"]
+    calls = {"rows": 0}
+    real = kmod.spmm_rows
+
+    def counted(*a, **k):
+        calls["rows"] += 1
+        return real(*a, **k)
+    monkeypatch.setattr(kmod, "spmm_rows", counted)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=9)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    models = []
+    for frontier in (False, True):
+        torch.manual_seed(77)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                                  message_dropout=[0.1] * len(layers)))
+        m.attach_graph(lay, DEV)
+        assert m.graph().A.n_long > 0  # hub rows take the segment + fix-up path
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = True
+        m.frontier_forward = frontier
+        models.append(m)
+    rng = np.random.default_rng(11)
+    R = len(lay.rel_order)
+    for step in range(3):
+        ids = [torch.from_numpy(rng.integers(0, hi, 96)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+        kg = [torch.from_numpy(rng.integers(0, hi, 32)).to(DEV) for hi in (U + E, R, U + E, U + E)]
+        losses = []
+        for m in models:
+            torch.manual_seed(300 + step)  # same dropout seeds
+            loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF)
+            loss.backward()
+            losses.append(loss.detach().clone())
+            m.update_cf_weights()
+            m(kg[0], kg[1], kg[2], kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
+            m.update_kg_weights()
+        assert torch.equal(losses[0], losses[1]), (step, losses)
+    assert calls["rows"] == (3 * len(layers) if len(layers) <= 2 else 0)
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    ta = a._cf_optimizer.state[id(a._user_entity_embedding.weight)]
+    tb = b._cf_optimizer.state[id(b._user_entity_embedding.weight)]
+    assert torch.equal(ta["exp_avg"], tb["exp_avg"]) and torch.equal(ta["exp_avg_sq"], tb["exp_avg_sq"])
+    # a no-grad loss evaluation takes the full forward (no backward releases the batch-row map)
+    with torch.no_grad():
+        torch.manual_seed(5)
+        la = a(*ids, mode=pkg.KGATMode.TRAIN_CF)
+        torch.manual_seed(5)
+        lb = b(*ids, mode=pkg.KGATMode.TRAIN_CF)
+    assert torch.equal(la, lb)
 
 
 def test_fused_table_update_materialises_on_demand(pkg):
