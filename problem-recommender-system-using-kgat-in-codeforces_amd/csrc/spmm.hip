@@ -94,6 +94,14 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
   *y = acc;
 }
 
+// Source rows in flight per lane group in the row-set forward (kRows): its ~10^4 rows leave
+// most of the chip's wave slots empty, so each group keeps more gathers outstanding (the sum
+// stays in edge order: same bits for any value).
+#ifndef KGAT_ROWS_U
+#define KGAT_ROWS_U 4
+#endif
+constexpr int kRowsUnroll = KGAT_ROWS_U;
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
@@ -147,7 +155,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
         if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         bool any = false;
-        gather_edges<D, MODE == kMaskedRows>(A, io, beg, end, base, gl, acc, any);
+        gather_edges<D, MODE == kMaskedRows, MODE == kRows ? kRowsUnroll : 4>(A, io, beg, end, base, gl, acc, any);
         store_row<MODE>(io, r, MODE == kRows ? r : k, gl, acc, any);
       }
     }

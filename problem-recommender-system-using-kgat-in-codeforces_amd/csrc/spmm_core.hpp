@@ -151,6 +151,19 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
 #pragma unroll
       for (int k = 0; k < U; ++k) fma4(vs[k], xs[k], acc);
     }
+    if (U > 8 && j + 8 <= n) {
+      float4 xs[8];
+      float vs[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ck = __shfl(mc, base + j + k);
+        vs[k] = __shfl(mv, base + j + k);
+        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) fma4(vs[k], xs[k], acc);
+      j += 8;
+    }
     if (U > 4 && j + 4 <= n) {
       float4 xs[4];
       float vs[4];
