@@ -79,10 +79,6 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 
 // Accumulate edges [beg, end) of one row into acc.  All lanes of the group
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
-#ifndef KGAT_LAZY_VAL
-#define KGAT_LAZY_VAL 0
-#endif
-
 template <int D, bool MASKED, int U = 4>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
                                              int gl, float4& acc, bool& any) {
@@ -100,9 +96,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       bool in = false;
       if (gl < n) {
         mc = A.col[cb + gl];
-#if !KGAT_LAZY_VAL
         mv = A.val[cb + gl];
-#endif
         if (io.src_rank != nullptr) {
           const uint64_t w = io.src_rank[mc >> 5];
           const uint32_t b = static_cast<uint32_t>(mc & 31);
@@ -111,9 +105,6 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
         } else {
           in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
         }
-#if KGAT_LAZY_VAL
-        if (in) mv = A.val[cb + gl];  // the value of a member edge only (~1/3 of the edges at C2)
-#endif
       }
       uint64_t hit = (__ballot(in) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
       if (hit == 0) continue;
