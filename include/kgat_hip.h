@@ -173,9 +173,6 @@ int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, con
 int kgat_spmm_csr_rows_f32(const kgat_csr *A, const float *X, int64_t ldx, const uint32_t *out_bits,
                            const int32_t *out_rows, const int32_t *out_count, float *Y, int64_t ldy, int32_t d,
                            float *workspace, int64_t workspace_floats, void *stream);
-/* The 16-row tiles holding a member of the node set bits (uint32 [ceil(n/32)]):
- * tiles[0 .. *count) in no particular order (count on the device). */
-int kgat_bits_tiles(const uint32_t *bits, int64_t n, int32_t *tiles, int32_t *count, void *stream);
 
 /* Data-parallel exchange of the compact table gradient (replicas.ShardedGradSync,
  * replicate_table mode; no reference counterpart -- the reference is one
@@ -225,15 +222,15 @@ int kgat_spmm_biinter_fwd_f32(const kgat_csr *A, const float *X, int64_t ldx, fl
                               float *norm_out, uint64_t *mask_out, float *workspace, int64_t workspace_floats,
                               void *stream);
 
-/* kgat_biinter_fwd_f32 on the 16-row tiles tiles[0 .. *tile_count) of the
- * table only (kgat_bits_tiles; count on the device, max_tiles bounds it): H,
- * norm_out and mask_out of those tiles are written exactly as the whole-table
- * call writes them, the rest is untouched.  aggregator.py:57-65 on a hop set. */
+/* kgat_biinter_fwd_f32 on the 16-row tiles of the table holding a member of
+ * the node set row_bits (uint32 bitmap [ceil(n_rows/32)], e.g. a hop set of
+ * kgat_frontier_hop) only: H, norm_out and mask_out of those tiles are written
+ * exactly as the whole-table call writes them, the rest is untouched.
+ * aggregator.py:57-65 on a hop set. */
 int kgat_biinter_fwd_tiles_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *W1,
                                const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
-                               int64_t n_rows, const int32_t *tiles, const int32_t *tile_count, int64_t max_tiles,
-                               int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed, float *norm_out,
-                               uint64_t *mask_out, void *stream);
+                               int64_t n_rows, const uint32_t *row_bits, int32_t d_in, int32_t d_out,
+                               float dropout_p, uint64_t seed, float *norm_out, uint64_t *mask_out, void *stream);
 
 /* kgat_biinter_fwd_f32 on rows [node0, node0 + n_rows) of a larger table: X, S,
  * H, norm_out, mask_out point at that block's first row (mask_out at word

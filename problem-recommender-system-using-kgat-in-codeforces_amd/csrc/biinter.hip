@@ -180,8 +180,9 @@ struct BiFwdWaves {
   static constexpr int k = 2 * DOUT * (DIN + 4) * 4 > 80 * 1024 ? 8 : 4;
 };
 
-// TL: only the 16-row sub-tiles listed in tiles[0 .. *tile_count) (a hop set's tiles,
-// kgat_bits_tiles), the same per-tile arithmetic as the whole-table launch.
+// TL: only the 16-row sub-tiles holding a member of the node set row_bits (a hop set's
+// bitmap: the tile's 16 bits are one half-word; other tiles are skipped by the wave that
+// tests them), the same per-tile arithmetic as the whole-table launch.
 template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4, bool TL = false>
 __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
@@ -190,8 +191,7 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
                                                           float* __restrict__ H, int64_t ldh, int64_t n, float p,
                                                           uint64_t seed, float* __restrict__ norm_out,
                                                           uint64_t* __restrict__ mask_out, int64_t node0,
-                                                          const int32_t* __restrict__ tiles = nullptr,
-                                                          const int32_t* __restrict__ tile_count = nullptr) {
+                                                          const uint32_t* __restrict__ row_bits = nullptr) {
   static_assert(!(TL && PF), "the tile-list forward has no prefetch");
   using B = BiShape<DIN, DOUT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
   }
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t thr = bi_drop_threshold(p);
-  const int64_t nsub = TL ? static_cast<int64_t>(*tile_count) : (n + 15) / 16;
+  const int64_t nsub = (n + 15) / 16;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * NWV;
   int64_t k = static_cast<int64_t>(blockIdx.x) * NWV + (threadIdx.x >> 6);
   // PF: the next sub-tile's rows are loaded while the current one computes
@@ -219,7 +219,8 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
     load_rows<DIN>(S, lds, k * 16 + c, n, q, ns);
   }
   for (; k < nsub; k += stride) {
-    const int64_t st = TL ? static_cast<int64_t>(tiles[k]) : k;
+    const int64_t st = k;
+    if (TL && ((row_bits[st >> 1] >> ((st & 1) * 16)) & 0xffffu) == 0) continue;  // wave-uniform
     if (!PF) {
       load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
       load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
@@ -1056,13 +1057,12 @@ static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
 template <int DIN, int DOUT>
 static int launch_fwd_tiles(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
                             const float* b1, const float* W2, const float* b2, float* H, int64_t ldh, int64_t n,
-                            float p, uint64_t seed, float* norm, uint64_t* mask, const int32_t* tiles,
-                            const int32_t* tile_count, int64_t max_tiles, hipStream_t st) {
+                            float p, uint64_t seed, float* norm, uint64_t* mask, const uint32_t* row_bits,
+                            hipStream_t st) {
   constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
-  // the list's size is on the device: the grid covers max_tiles (capped; waves stride over the list)
-  const int grid = blocks_for(max_tiles * 16, 16 * NWV, kCUs * 8 * 4 / NWV);
+  const int grid = blocks_for(n, 16 * NWV, kCUs * 8 * 4 / NWV);
   hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, false, 2, NWV, true>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx,
-                     S, lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, int64_t{0}, tiles, tile_count);
+                     S, lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, int64_t{0}, row_bits);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -1219,21 +1219,19 @@ extern "C" int kgat_biinter_fwd_rows_f32(const float* X, int64_t ldx, const floa
 
 extern "C" int kgat_biinter_fwd_tiles_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
                                           const float* W1, const float* b1, const float* W2, const float* b2,
-                                          float* H, int64_t ldh, int64_t n_rows, const int32_t* tiles,
-                                          const int32_t* tile_count, int64_t max_tiles, int32_t d_in, int32_t d_out,
+                                          float* H, int64_t ldh, int64_t n_rows, const uint32_t* row_bits,
+                                          int32_t d_in, int32_t d_out,
                                           float dropout_p, uint64_t seed, float* norm_out, uint64_t* mask_out,
                                           void* stream) {
-  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || !tiles || !tile_count || n_rows < 0 || max_tiles < 0)
-    return KGAT_ERR_INVALID;
-  if (max_tiles > (n_rows + 15) / 16) return KGAT_ERR_INVALID;
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || !row_bits || n_rows < 0) return KGAT_ERR_INVALID;
   if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
   if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 128)) return KGAT_ERR_INVALID;
-  if (n_rows == 0 || max_tiles == 0) return KGAT_OK;
+  if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_FWDT_CALL(a, b) kgat::launch_fwd_tiles<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, \
-                                                         seed, norm_out, mask_out, tiles, tile_count, max_tiles, st)
+                                                         seed, norm_out, mask_out, row_bits, st)
   KGAT_BI_DISPATCH(KGAT_FWDT_CALL)
 #undef KGAT_FWDT_CALL
 }

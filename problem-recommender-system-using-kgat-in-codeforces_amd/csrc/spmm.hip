@@ -601,30 +601,6 @@ extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t
   return dispatch<kRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
-namespace kgat {
-// 16-row tiles holding at least one member of a node set (bitmap, 32 nodes per word: two
-// tiles), listed in no particular order (each tile's bi-interaction is independent).
-__global__ __launch_bounds__(256) void bits_tiles_kernel(const uint32_t* __restrict__ bits, int64_t words,
-                                                         int32_t* __restrict__ tiles, int32_t* __restrict__ count) {
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (w >= words) return;
-  const uint32_t b = bits[w];
-  if (b & 0xffffu) tiles[atomicAdd(count, 1)] = static_cast<int32_t>(2 * w);
-  if (b >> 16) tiles[atomicAdd(count, 1)] = static_cast<int32_t>(2 * w + 1);
-}
-}  // namespace kgat
-
-extern "C" int kgat_bits_tiles(const uint32_t* bits, int64_t n, int32_t* tiles, int32_t* count, void* stream) {
-  if (!bits || !tiles || !count || n < 0 || n > INT32_MAX) return KGAT_ERR_INVALID;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(count, 0, sizeof(int32_t), st) != hipSuccess) return KGAT_ERR_INVALID;
-  const int64_t words = (n + 31) / 32;
-  if (words == 0) return KGAT_OK;
-  hipLaunchKernelGGL(kgat::bits_tiles_kernel, dim3((words + 255) / 256), dim3(256), 0, st, bits, words, tiles, count);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
 extern "C" int kgat_map_rank(const int32_t* node_map, int64_t n, uint64_t* rank, void* stream) {
   if (!node_map || !rank || n < 0) return KGAT_ERR_INVALID;
   if (reinterpret_cast<uintptr_t>(rank) & 7) return KGAT_ERR_INVALID;

@@ -413,27 +413,17 @@ def spmm_rows(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor, out_rows: 
     return out
 
 
-def bits_tiles(bits: torch.Tensor, n: int):
-    """(tiles int32 [ceil(n/16)] -- first count valid, any order --, count int32 [1] on the device): the
-    16-row tiles holding a member of the bitmap's set (kgat_bits_tiles)."""
-    if bits.dtype != torch.int32 or bits.numel() * 32 < n:
-        raise ValueError("bits must be an int32 bitmap covering n nodes")
-    tiles = torch.empty(max((n + 15) // 16, 1), dtype=torch.int32, device=bits.device)
-    count = torch.empty(1, dtype=torch.int32, device=bits.device)
-    _lib.call("kgat_bits_tiles", bits.data_ptr(), n, tiles.data_ptr(), count.data_ptr(), stream_ptr(bits.device))
-    return tiles, count
-
-
-def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: torch.Tensor, tiles: torch.Tensor,
-                      tile_count: torch.Tensor, state: BiState | None = None) -> torch.Tensor:
-    """biinter_fwd on the listed 16-row tiles only (kgat_biinter_fwd_tiles_f32): H / state rows of those
-    tiles get the whole-table call's bits, the rest of ``out`` and the state are left as they are."""
+def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: torch.Tensor,
+                      row_bits: torch.Tensor, state: BiState | None = None) -> torch.Tensor:
+    """biinter_fwd on the 16-row tiles holding a member of the node set ``row_bits`` (int32 bitmap)
+    only (kgat_biinter_fwd_tiles_f32): H / state rows of those tiles get the whole-table call's bits,
+    the rest of ``out`` and the state are left as they are."""
     for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2"), (out, "out")):
         _req(t, nm, dim=2)
-    _req(tiles, "tiles", dtype=torch.int32, dim=1)
-    _req(tile_count, "tile_count", dtype=torch.int32, dim=1)
     n, din = X.shape
     dout = W1.shape[0]
+    if row_bits.dtype != torch.int32 or row_bits.numel() * 32 < n or not row_bits.is_cuda:
+        raise ValueError("row_bits must be an int32 device bitmap covering every row")
     if S.shape != X.shape or W1.shape != (dout, din) or W2.shape != (dout, din) or tuple(out.shape) != (n, dout):
         raise ValueError("bi-interaction shape mismatch")
     if not fused_supported(din, dout) or dout > 128:
@@ -444,10 +434,9 @@ def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: to
     if state is not None and (state.kind not in ("fused", "bits") or state.norm.numel() < n
                               or state.mask.numel() < (n + 15) // 16 * 64 * words):
         raise ValueError("bi-interaction state too small")
-    max_tiles = min(tiles.numel(), (n + 15) // 16)
     _lib.call("kgat_biinter_fwd_tiles_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
-              W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, tiles.data_ptr(), tile_count.data_ptr(),
-              max_tiles, din, dout, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, row_bits.data_ptr(), din, dout,
+              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
               state.norm.data_ptr() if state is not None else None,
               state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
     return out

@@ -253,7 +253,7 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
     so the last layer's output is needed on F only, and with 2 layers layer 0's on the first hop
     F + N(F) (layer 1 gathers its A rows from there) -- the same row sets the backward's hop chain
     runs on.  Each layer then runs kgat_spmm_csr_rows_f32 on its set's rows and
-    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them: every row the step reads gets the
+    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them (the set's bitmap): every row the step reads gets the
     full forward's bits (same edges, order and dropout draws), rows outside are never read.  At C2
     layer 0's set is 1.7 % of the rows (35 % of the edges), layer 1's the ~768 batch rows.
     Returns (tables, sides, states, early) -- early as _early_first_hop's, for the backward -- or
@@ -285,10 +285,9 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
         st = kernels.make_state(n, dims[l], dims[l + 1], x.device)
         s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
                               out_count, out_bits)
-        tiles, tcount = kernels.bits_tiles(out_bits, n)
         x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
-                                      torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device), tiles,
-                                      tcount, state=st)
+                                      torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device), out_bits,
+                                      state=st)
         sides.append(s)
         states.append(st)
         tables.append(x)
