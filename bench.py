@@ -452,8 +452,10 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         fel, _, _ = timed(step, batches, args.warmup, args.steps, world, dev)
         model.frontier_forward = False
         fms = fel / args.steps * 1e3
+        est = getattr(model.graph(), "_hop_est", {}).get(0)  # pinned count of the last step's first hop
         result["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
+            "layer0_rows_last_step": int(est[0][0]) if est is not None and L == 2 else None,
             "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer 0 of 2 on F + N(F), the "
                     "last layer on the batch rows F); not counted in value (it does not visit every edge)"}
     if world > 1 or args.exchange_at_1:
