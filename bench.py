@@ -444,7 +444,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         "host_launch_ms_per_step": timed.host_ms_per_step,
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_frontier_leg and not args.exchange_at_1:
+    if world == 1 and L <= 2 and not args.no_frontier_leg and not args.exchange_at_1:
         # the same CF step with KGAT.frontier_forward (each layer's forward on the rows the loss can
         # reach only: same loss, gradients and updates bit for bit, tested) -- the training step as
         # driver.py runs it; `value` above stays the full-propagation step
