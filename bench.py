@@ -221,13 +221,18 @@ def cpu_leg(layout, cfg, steps: int, parity_state: dict | None = None, parity_ba
 
 def cpu_extrapolated(layout, cfg, fracs=(0.02, 0.04)) -> dict:
     """C4-size CPU baseline: the oracle CF step on uniformly subsampled edge sets (all N rows kept),
-    t(E) fitted as a + b * E through the points and evaluated at the full E ("extrapolated")."""
+    extrapolated linearly in E to the full graph ("extrapolated").  At 10M rows the step is dominated by
+    the dense per-row work, so two whole-step times differ by less than their noise (a fitted slope
+    came out negative once); the per-edge slope is therefore taken from the sparse product itself:
+    A . X timed at both subsamples (best of 3), times the step's 2 * sum_l d_in(l) / d0 products'
+    worth of gathered width (forward + backward of every layer)."""
     from oracle import kgat_cpu as K
 
     n = layout.n_nodes
     rows, cols, vals = layout.coo()
     rng = np.random.default_rng(5)
     pts = []
+    ax = []  # A . X seconds (d0 wide) per subsample
     threads = None
     for f in fracs:
         keep = np.flatnonzero(rng.random(rows.size) < f)
@@ -236,6 +241,14 @@ def cpu_extrapolated(layout, cfg, fracs=(0.02, 0.04)) -> dict:
         if threads is None:
             threads, _ = _sweep_threads(A, n, cfg["dim"])
             torch.set_num_threads(threads)
+        Xp = torch.randn(n, cfg["dim"])
+        best = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
+            torch.sparse.mm(A, Xp)
+            best = min(best, time.perf_counter() - t0)
+        ax.append(best)
+        del Xp
         P = _oracle_params(layout, cfg, None)
         g = torch.Generator().manual_seed(2)
         ts = []
@@ -254,14 +267,20 @@ def cpu_extrapolated(layout, cfg, fracs=(0.02, 0.04)) -> dict:
         pts.append((A._nnz(), ts[-1]))
         del A
     (e1, t1), (e2, t2) = pts
-    b = (t2 - t1) / max(e2 - e1, 1)
-    t = t1 + b * (layout.nnz - e1)
+    b_fit = (t2 - t1) / max(e2 - e1, 1)
+    dims_in = [cfg["dim"]] + list(cfg["layers"][:-1])
+    widths = 2.0 * sum(dims_in) / cfg["dim"]
+    b_ax = max(ax[1] - ax[0], 0.0) / max(e2 - e1, 1)
+    b = b_ax * widths
+    t = max(t1, t2) + b * (layout.nnz - e2)
     L = len(cfg["layers"])
     return {"value": layout.nnz * L / t, "unit": "layer-edges/s", "cores": threads, "kind": "port",
-            "extrapolated": True, "ms_per_step": t * 1e3,
+            "extrapolated": True, "ms_per_step": t * 1e3, "per_edge_s": b, "per_edge_s_step_fit": b_fit,
             "sample": f"oracle/kgat_cpu.py CF step on {', '.join(f'{e:,}' for e, _ in pts)}-edge uniform subsamples "
                       f"of the {cfg['workload']} graph (all {n:,} rows; {', '.join(f'{s:.1f}' for _, s in pts)} s/step "
-                      f"after 1 warm-up each), linear in E to the full {layout.nnz:,} edges; threads={threads}"}
+                      f"after 1 warm-up each), + the remaining {layout.nnz - e2:,} edges at the A.X per-edge cost "
+                      f"({', '.join(f'{x * 1e3:.0f}' for x in ax)} ms per d0-wide product at the two subsamples) x "
+                      f"{widths:g} products' width per step; threads={threads}"}
 
 
 # --------------------------------------------------------------------------- roofline

@@ -39,3 +39,20 @@ def test_c5_world4_dry_run_accepted():
     assert p.returncode == 0, p.stderr[-2000:]
     rec = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
     assert rec["ranks_joined"] == 4 and rec["mode"] == "sharded"
+
+
+def test_cpu_extrapolated_baseline_small():
+    """The C4 CPU-baseline extrapolation on a small graph: the oracle step at two edge subsamples, then
+    the remaining edges at the measured A . X per-edge cost (never below the larger measured step)."""
+    import importlib
+
+    sys.path.insert(0, str(ROOT))
+    bench = importlib.import_module("bench")
+    graph = importlib.import_module(bench.PKG + ".graph")
+    U, E, inter, trip = graph.synthetic_ckg(4000, 30000, seed=3)
+    lay = graph.build_layout(U, E, inter, trip)
+    cfg = dict(dim=16, layers=[16, 8], batch=32, workload="tiny")
+    rec = bench.cpu_extrapolated(lay, cfg, fracs=(0.2, 0.5))
+    assert rec["extrapolated"] and rec["kind"] == "port" and rec["value"] > 0
+    assert rec["per_edge_s"] >= 0 and rec["ms_per_step"] > 0
+    assert "A.X per-edge cost" in rec["sample"]
