@@ -228,6 +228,33 @@ class _TableUpdate:
         return run
 
 
+class _MarkedBatch:
+    """The batch rows a forward marked in ``graph.node_map`` (and, with 2 layers, the first hop it left
+    in the graph's hop buffers) for its own backward -- at most one outstanding per graph."""
+
+    def __init__(self, rows: torch.Tensor):
+        self.rows = rows
+        self.stale = False
+
+
+def _release_marks(graph) -> None:
+    """Undo an outstanding forward's marks (its loss was dropped, or a second forward came before its
+    backward): the map is reset and that forward's backward raises instead of reading reused buffers."""
+    tok = getattr(graph, "_marked", None)
+    if tok is not None:
+        tok.stale = True
+        kernels.frontier_reset(tok.rows, graph.node_map)
+        graph._marked = None
+
+
+def _mark_batch(graph, users, pos, neg):
+    """frontier_build for a forward that hands its marks to its backward: (rows, count, token)."""
+    _release_marks(graph)
+    rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
+    graph._marked = tok = _MarkedBatch(rows)
+    return rows, fcount, tok
+
+
 def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     """Data-parallel replicas exchanging the layer-0 hop-set terms (replicas.ShardedGradSync,
     replicated) with 2 layers: the layer-0 hop set is the first hop F + N(F) of the batch rows F,
@@ -240,11 +267,11 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     W1 = ws[0]
     if not kernels.saved_state_supported(W1.shape[1], W1.shape[0]) or not _hop_small(graph, 0, graph.n_nodes):
         return None
-    rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
+    rows, fcount, tok = _mark_batch(graph, users, pos, neg)
     hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0))
     _hop_record(graph, 0)
     hook.announce(True, hop[2])
-    return rows, hop, fcount
+    return rows, hop, fcount, tok
 
 
 def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
@@ -268,12 +295,12 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
         return None
     n = graph.n_nodes
     if early is None:
-        rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
+        rows, fcount, tok = _mark_batch(graph, users, pos, neg)
         hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0) if L == 2 else None)
         if L == 2:
             _hop_record(graph, 0)
-        early = (rows, hop, fcount)
-    rows, hop, fcount = early
+        early = (rows, hop, fcount, tok)
+    rows, hop, fcount, tok = early
     hrows, _, hcount, bits1, fbits = hop
     # layer l's output row set: the first hop for layer 0 of 2, the batch rows F for the last layer
     sets = [(hrows, hcount, bits1)] * (L - 1) + [(rows, fcount, fbits)]
@@ -292,7 +319,7 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
         states.append(st)
         tables.append(x)
     # L = 1: the backward's last layer needs the batch rows only (no hop set is handed over)
-    return tables, sides, states, (early if L == 2 else (rows, None, fcount))
+    return tables, sides, states, (early if L == 2 else (rows, None, fcount, tok))
 
 
 def _saved(tables, states, l) -> dict:
@@ -361,7 +388,16 @@ class _CFLoss(torch.autograd.Function):
         hit = graph.hop_buffers()[0] if L > 1 else None
         # ---- last layer on the batch frontier
         early, ctx.early = ctx.early, None
-        rows = early[0] if early is not None else kernels.frontier_build(users, pos, neg, graph.node_map)[0]
+        if early is not None:
+            if early[3].stale:
+                raise RuntimeError("TRAIN_CF backward: a later TRAIN_CF forward on this graph reused the batch-row "
+                                   "marks and hop buffers this step's forward left for it (frontier_forward / the "
+                                   "replicated DP exchange need each forward's backward before the next forward)")
+            graph._marked = None  # consumed: this backward resets the marks itself
+            rows = early[0]
+        else:
+            _release_marks(graph)  # a dropped forward's marks would collide with this batch's
+            rows = kernels.frontier_build(users, pos, neg, graph.node_map)[0]
         if early is not None and early[1] is None:
             early = None  # 1-layer frontier forward: the batch rows only
         dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)

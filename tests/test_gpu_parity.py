@@ -1530,6 +1530,54 @@ def test_frontier_forward_bit_identical(pkg, layers, monkeypatch):
     assert torch.equal(la, lb)
 
 
+def test_frontier_forward_dropped_and_overlapping_forwards(pkg):
+    """The frontier forward leaves its batch-row marks and first hop for its own backward.  A dropped
+    loss (forward without backward) is released by the next forward: the following steps equal the
+    full-forward model's bit for bit.  Two forwards before a backward: the first one's backward raises
+    instead of reading the second one's buffers."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(8000, 60000, seed=4)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    models = []
+    for frontier in (False, True):
+        torch.manual_seed(3)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                                  message_dropout=[0.1, 0.1]))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = True
+        m.frontier_forward = frontier
+        models.append(m)
+    rng = np.random.default_rng(2)
+    batches = [[torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+               for _ in range(3)]
+    for m in models:
+        torch.manual_seed(9)
+        m(*batches[0], mode=pkg.KGATMode.TRAIN_CF)  # dropped: no backward
+        for b in batches[1:]:
+            m(*b, mode=pkg.KGATMode.TRAIN_CF).backward()
+            m.update_cf_weights()
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    m = models[1]
+    l1 = m(*batches[0], mode=pkg.KGATMode.TRAIN_CF)
+    l2 = m(*batches[1], mode=pkg.KGATMode.TRAIN_CF)
+    with pytest.raises(RuntimeError, match="reused the batch-row marks"):
+        (l1 + l2).backward()
+    # the model recovers: the next forward matches the full-forward model's and its backward runs
+    m.zero_grad(set_to_none=True)
+    m._table_update.pending = None  # whatever the failed backward left
+    torch.manual_seed(1)
+    la = models[0](*batches[2], mode=pkg.KGATMode.TRAIN_CF)
+    torch.manual_seed(1)
+    lb = models[1](*batches[2], mode=pkg.KGATMode.TRAIN_CF)
+    assert torch.equal(la, lb)
+    lb.backward()
+
+
 def test_fused_table_update_materialises_on_demand(pkg):
     """A deferred table gradient (KGAT.fuse_table_update) meets the calls that need it: a second CF
     backward before the step (gradient accumulation) and an UPDATE_ATTENTION (which rewrites A's
