@@ -166,7 +166,7 @@ int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, con
 /* The forward restricted to a hop set (KGAT.frontier_forward; the row set a
  * training step's loss can reach, see model._CFLoss): the dense product
  * Y[r] = (A . X)[r] for the rows r of an output set only -- out_rows[k] for
- * k < *out_count (device; -1 entries are skipped), out_bits its bitmap --,
+ * k < *out_count (device; each in [0, n_rows) or -1, which is skipped), out_bits its bitmap --,
  * each written at its own row of Y (other rows untouched).  Per row the same
  * edges in the same order as kgat_spmm_csr_f32 (same bits).  Replaces
  * aggregator.py:54's product on the rows model.py:189-191 gathers from. */
