@@ -471,10 +471,12 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         fel, _, _ = timed(step, batches, args.warmup, args.steps, world, dev)
         model.frontier_forward = False
         fms = fel / args.steps * 1e3
+        same = frontier_matches_full(model, pkg, batches[0])
         est = getattr(model.graph(), "_hop_est", {}).get(0)  # pinned count of the last step's first hop
         result["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
             "layer0_rows_last_step": int(est[0][0]) if est is not None and L == 2 else None,
+            "bit_identical_to_full": same,
             "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer 0 of 2 on F + N(F), the "
                     "last layer on the batch rows F); not counted in value (it does not visit every edge)"}
     if world > 1 or args.exchange_at_1:
@@ -497,6 +499,29 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
             result["cpu_baseline"] = base
             result["parity"] = parity
     return result
+
+
+def frontier_matches_full(model, pkg, batch) -> dict:
+    """One train-mode CF loss + backward of the timed model on the full graph, with and without
+    KGAT.frontier_forward (same dropout seeds, no optimizer step): loss, table gradient and every
+    aggregator weight gradient compared bit for bit."""
+    fused = model.fuse_table_update
+    model.fuse_table_update = False
+    outs = []
+    for frontier in (False, True):
+        model.zero_grad(set_to_none=True)
+        model.frontier_forward = frontier
+        torch.manual_seed(11)
+        loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
+        loss.backward()
+        outs.append([loss.detach().clone()] + [p.grad.detach().clone() for p in model.parameters()
+                                               if not p.is_sparse and p.grad is not None])
+    model.frontier_forward = False
+    model.zero_grad(set_to_none=True)
+    model.fuse_table_update = fused
+    a, b = outs
+    return {"pass": len(a) == len(b) and all(torch.equal(x, y) for x, y in zip(a, b)), "tensors": len(a),
+            "what": "loss + table and aggregator gradients of one train-mode CF step on the full graph"}
 
 
 def gpu_parity_inputs(model, pkg, batch):
