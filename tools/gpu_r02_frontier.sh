@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 200 --timeout-method thread \
-  -k "frontier_forward or fused_table_update or driver or test_cf" > gpurun_out/frontier_tests.log 2>&1; rc=$?
+  -k "frontier_forward or fused_table_update or driver or test_cf or hop_chain" > gpurun_out/frontier_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/frontier_tests.log
 [ $rc -ne 0 ] && { grep -E "^E |FAILED|Error" gpurun_out/frontier_tests.log | head -40; exit $rc; }
 timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-parity > gpurun_out/frontier_bench.log 2>&1 || { tail -30 gpurun_out/frontier_bench.log; exit 1; }
