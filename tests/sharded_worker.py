@@ -40,8 +40,12 @@ def main() -> None:
     sh = __import__(pkg.__name__ + ".sharded", fromlist=["sharded"])
     U, E, inter, trip = graph.synthetic_ckg(30000, 240000, seed=5)
     lay = graph.build_layout(U, E, inter, trip)
-    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
-                        message_dropout=[0.0, 0.0])
+    # SHARDED_WORKER_DIMS "d:l1,l2,...": embedding dim and layer sizes (default the C2 shape; the C5
+    # shape is "256:256,128,64", configs[4])
+    dim_s, layers_s = os.environ.get("SHARDED_WORKER_DIMS", "64:64,32").split(":")
+    dim, layers = int(dim_s), [int(x) for x in layers_s.split(",")]
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                        cf_embedding_dim=dim, kg_embedding_dim=dim, message_dropout=[0.0] * len(layers))
     torch.manual_seed(11)
     ref = pkg.KGAT(args)
     ref.attach_graph(lay, "cuda")
@@ -118,7 +122,7 @@ def main() -> None:
     if FAILURES:
         print(f"rank {rank}: " + "; ".join(FAILURES), flush=True)
     else:
-        print(f"sharded parity ok: rank {rank}/{world} rows [{lo}, {hi})", flush=True)
+        print(f"sharded parity ok: rank {rank}/{world} rows [{lo}, {hi}) d={dim} layers={layers}", flush=True)
     dist.destroy_process_group()
     sys.exit(1 if FAILURES else 0)
 

@@ -305,7 +305,7 @@ def test_cf_step_dropout_train_mode_runs(pkg):
 
 
 @pytest.mark.parametrize("dim,layers,batch", [(64, [64, 32], 256), (64, [64, 32, 16], 512), (256, [256, 128], 256),
-                                              (128, [128, 64, 32], 256)])
+                                              (128, [128, 64, 32], 256), (256, [256, 128, 64], 256)])
 def test_cf_step_synthetic_hubs_vs_oracle(pkg, dim, layers, batch):
     """Synthetic CKG with Zipf hub rows (long-row path in A and A^T), duplicate ids in the
     batch (users repeat, items collide with user rows): loss and every gradient vs the oracle."""
@@ -337,7 +337,7 @@ def test_cf_step_synthetic_hubs_vs_oracle(pkg, dim, layers, batch):
         np.testing.assert_allclose(prm.grad.cpu().numpy(), P[k].grad.numpy(), rtol=RTOL, atol=1e-6, err_msg=k)
 
 
-@pytest.mark.parametrize("dim,layers", [(64, [64, 32]), (128, [128, 64, 32])])
+@pytest.mark.parametrize("dim,layers", [(64, [64, 32]), (128, [128, 64, 32]), (256, [256, 128, 64])])
 def test_cf_step_large_hub_graph_vs_oracle(pkg, dim, layers):
     """bench-like scale -- 2M nodes, 3M edges, a hub row of ~114k edges (hundreds of
     long-row segments + the ordered fix-up, in A and A^T) -- eval-mode propagation of every layer,
@@ -1466,6 +1466,67 @@ def test_fused_table_update_bit_identical(pkg, layers):
         m.materialize_table_grad()
         grads.append(m._user_entity_embedding.weight.grad.detach().clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_fused_table_update_keeps_extra_table_gradient(pkg):
+    """with fuse_table_update the CF backward defers the table's gradient, but
+    another term of the loss (here an L2 penalty on the whole table) still writes .grad through
+    autograd.  update_cf_weights must sum the two (it materialises the deferred product into .grad)
+    instead of launching the fused kernel, which never reads .grad: same parameters and moments as
+    the unfused step, bit for bit; FusedAdam refuses a fused launch for a parameter with a .grad."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    models = []
+    for fused in (False, True):
+        torch.manual_seed(2024)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                                  message_dropout=[0.1, 0.1]))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = fused
+        models.append(m)
+    rng = np.random.default_rng(9)
+    for step in range(2):
+        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+        for m in models:
+            torch.manual_seed(200 + step)
+            loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF) + 1e-3 * m._user_entity_embedding.weight.pow(2).sum()
+            loss.backward()
+            assert m._user_entity_embedding.weight.grad is not None
+            m.update_cf_weights()
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    ta = a._cf_optimizer.state[id(a._user_entity_embedding.weight)]
+    tb = b._cf_optimizer.state[id(b._user_entity_embedding.weight)]
+    assert torch.equal(ta["exp_avg"], tb["exp_avg"]) and torch.equal(ta["exp_avg_sq"], tb["exp_avg_sq"])
+    # the optimiser's own guard
+    p = b._user_entity_embedding.weight
+    p.grad = torch.zeros_like(p)
+    with pytest.raises(RuntimeError, match="fused launch"):
+        b._cf_optimizer.step(fused={id(p): lambda *a: None})
+    p.grad = None
+
+
+def test_device_id_error_raised_before_update(pkg):
+    """a device-side id out of range raises at update_cf_weights, before the
+    optimiser moves any parameter (the check's flag is waited for there)."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(6000, 60000, seed=11)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32]))
+    m.attach_graph(lay, DEV)
+    m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    before = m._user_entity_embedding.weight.detach().clone()
+    bad = torch.full((16,), U + E + 5, dtype=torch.int64, device=DEV)
+    ok = torch.zeros(16, dtype=torch.int64, device=DEV)
+    m(ok, bad, ok, mode=pkg.KGATMode.TRAIN_CF).backward()
+    with pytest.raises(IndexError):
+        m.update_cf_weights()
+    assert torch.equal(m._user_entity_embedding.weight.detach(), before)
 
 
 @pytest.mark.parametrize("layers", [[64], [64, 32], [64, 64], [64, 32, 16]])

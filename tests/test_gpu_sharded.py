@@ -92,17 +92,21 @@ def test_sharded_world1_matches_kgat(pkg):
                                    ref(users, items, mode=pkg.KGATMode.PREDICT).cpu().numpy(), atol=1e-5, rtol=1e-4)
 
 
-def test_sharded_world2_two_ranks_one_gpu():
-    env = dict(os.environ)
+@pytest.mark.parametrize("world,dims", [(2, "64:64,32"), (2, "256:256,128,64"), (4, "256:256,128,64")])
+def test_sharded_ranks_one_gpu(world, dims):
+    """tests/sharded_worker.py on `world` ranks sharing this GPU (gloo, host-staged): the row-sharded
+    model vs single-GPU KGAT on the global batch -- at the C2 shape and at C5's (d = 256, layers
+    [256, 128, 64], configs[4]) -- CF and KG loss, gradient shards, Adam, attention refresh, PREDICT."""
+    env = dict(os.environ, SHARDED_WORKER_DIMS=dims)
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "sharded_worker.py")]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / "sharded_world2.log"
+    log = ROOT / "gpurun_out" / f"sharded_world{world}_d{dims.split(':')[0]}.log"
     log.parent.mkdir(exist_ok=True)
     log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
-    assert p.stdout.count("sharded parity ok") == 2, p.stdout[-2000:]
+    assert p.stdout.count("sharded parity ok") == world, p.stdout[-2000:]
 
 
 def test_dp_sharded_grad_sync_world2_matches_allreduce():
