@@ -91,15 +91,17 @@ def compulsory_bytes(n: int, nnz: int, d: int) -> int:
 def sharded_bytes_per_gpu(cfg: dict, world: int) -> float:
     """Planned HBM per rank of the row-sharded mode (sharded.RowShardedKGAT), largest shard ~1.15x the mean.
     Per node row (fp32): X0, its gradient and CF Adam m/v (4d), layer outputs H_l and sides S_l,
-    three backward temporaries of the widest layer; per edge: the CSR blocks and their transposes
-    (col + val each), the local values and the two position maps (28 B)."""
+    three backward temporaries of the widest layer; per edge: the local rows of A and of A^T
+    (col + val each) and the refresh's two position maps (24 B); per node of the whole graph: two
+    gathered column chunks in flight (sharded.GATHER_CHUNK columns each) and the batch-row map."""
     d, layers = cfg["dim"], cfg["layers"]
     dims = [d, *layers]
     per_row = 4 * (4 * d + sum(layers) + sum(dims[:-1]) + 3 * max(dims))
     nnz = 2 * cfg["triples"]
     per_rank_rows = 1.15 * cfg["nodes"] / world
     per_rank_edges = 1.15 * nnz / world
-    return per_row * per_rank_rows + 28 * per_rank_edges + 16 * cfg["nodes"] + 8 * per_rank_rows * world
+    chunk = min(d, 64)
+    return per_row * per_rank_rows + 24 * per_rank_edges + (2 * 4 * chunk + 4) * cfg["nodes"]
 
 
 def min_gpus(cfg: dict) -> int:
@@ -297,7 +299,8 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
     bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc not in ("masked", "fused_adam")]
     masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc in ("masked", "fused_adam")]
     fused = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if acc == "fused_adam"]
-    fwd_d0 = [x for x in fwd if x[1] == d0]
+    # the layer-0 launches (d0 wide; the row-sharded mode's gathered column chunks are narrower)
+    fwd_d0 = [x for x in fwd if x[1] == d0] or [x for x in fwd if x[1] == max(y[1] for y in fwd)]
     avg_ms = float(np.mean([x[0] for x in fwd_d0]))
     algo = float(np.mean([x[2] for x in fwd_d0]))
     comp = float(np.mean([x[3] for x in fwd_d0]))
@@ -551,16 +554,19 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     log(f"generating the synthetic CKG ({cfg['workload']}) row-sharded over {world} ranks, {threads} threads each ...")
     ckg = graph_mod.HashedCKG(cfg["nodes"], cfg["triples"], seed=2024, threads=threads)
     bounds = sh.shard_bounds(ckg.row_offsets(), world)
-    rowptr, col, val = ckg.shard(int(bounds[rank]), int(bounds[rank + 1]))
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    rowptr, col, val = ckg.shard(lo, hi)
     log(f"  rank 0 rows [{bounds[0]}, {bounds[1]}): {col.size:,} entries ({time.perf_counter() - t0:.1f}s)")
-    shard = sh.RowShard(rowptr, col, val, bounds, rank, dev, local=True)
+    shard = sh.RowShard(rowptr, col, val, bounds, rank, dev, local=True, transpose=ckg.shard(lo, hi, transpose=True))
+    whole = (rowptr, col, val) if world == 1 and not args.no_parity else None  # the oracle's graph (parity leg)
     del rowptr, col, val
     comm = sh.Comm()
-    nnz_t = torch.tensor([sum(shard.nnz)], dtype=torch.int64, device=dev)
+    nnz_t = torch.tensor([shard.nnz], dtype=torch.int64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(nnz_t)
     nnz = int(nnz_t.item())
     log(f"  device shards built ({time.perf_counter() - t0:.1f}s); total nnz {nnz:,}")
+    log(f"graph: N={ckg.n_nodes} interactions={ckg.n_interactions} kg={ckg.n_kg} nnz={nnz}")
     L = len(cfg["layers"])
     torch.manual_seed(2024)
     model = sh.RowShardedKGAT(pkg.KGATArgs(user_num=ckg.user_num, entity_num=ckg.entity_num, relation_num=10,
@@ -586,20 +592,69 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
     d0 = cfg["dim"]
-    roof, spmm = roofline(events, args.config, shard.n, 0, d0, timed.instrumented,
-                          f"spmm_main_kernel<{d0}, 0> on the A[k][j] blocks (ring all-gather pipelined)")
-    spmm["fwd_spmm_layer_edges_per_s_rank0"] = sum(shard.nnz) * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
-    return {
+    chunked = comm.active and d0 > sh.GATHER_CHUNK > 0
+    roof, spmm = roofline(events, args.config, ckg.n_nodes if world == 1 else shard.n, nnz if world == 1 else 0,
+                          d0, timed.instrumented,
+                          f"spmm_main_kernel<{sh.GATHER_CHUNK if chunked else d0}, 0> on the local rows of A "
+                          f"(all-peer gathered layer input{', column chunks' if chunked else ''})")
+    spmm["fwd_spmm_layer_edges_per_s_rank0"] = shard.nnz * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)
+    res = {
         "value": nnz * L / (ms * 1e-3), "n_gpus": world, "ms_per_step": ms, "scaling": "strong",
         "config": {"workload": cfg["workload"], "nodes": ckg.n_nodes, "nnz": nnz, "interactions": ckg.n_interactions,
                    "kg_triples": ckg.n_kg, "embed_dim": d0, "layer_size": cfg["layers"], "global_batch": B * world,
                    "parallelism": f"row-sharded x{world}", "shard_rows": [int(x) for x in np.diff(bounds)],
-                   "mode": "train (dropout 0.1)", "graph": "graph.HashedCKG (per-rank rows, multi-edges kept)"},
+                   "mode": "train (dropout 0.1)",
+                   "graph": f"graph.HashedCKG (per-rank rows; {ckg.n_triples:,} distinct triples, repeats redrawn: "
+                            f"E = {nnz:,} = {nnz / max(2 * ckg.n_triples, 1):.4f} x 2T)"},
         "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
         "cpu_baseline": None,
         "cpu_baseline_note": "not run: the row-sharded config never runs at N = 1 and its CPU step "
                              "(50M x 704 fp32 tables + autograd state) exceeds host RAM",
     }
+    if whole is not None and rank == 0:
+        log("bench-scale parity: eval-mode propagation / CF loss / table gradient vs the oracle on the CPU ...")
+        res["parity"] = sharded_parity(model, pkg, batches[0], whole, ckg.n_nodes, cfg)
+    return res
+
+
+def sharded_parity(model, pkg, batch, whole, n: int, cfg: dict) -> dict:
+    """The timed row-sharded model (world 1: its shard is the whole graph) after the timed steps vs
+    oracle/kgat_cpu.py on the same graph and weights: eval-mode propagation of every layer, one CF loss
+    and its table gradient (the C5 shape, d = 256, layers [256, 128, 64], at the rehearsal's scale)."""
+    from oracle import kgat_cpu as K
+
+    model.eval()
+    tables = [t.cpu() for t in model.propagate()]
+    loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
+    loss.backward()
+    grad = model._user_entity_embedding_shard.grad.detach().cpu()
+    state = {k: v.detach().float().cpu().clone() for k, v in model.state_dict().items()
+             if k.startswith("_aggregator")}
+    state["_user_entity_embedding.weight"] = model._user_entity_embedding_shard.detach().cpu().clone()
+    for p in model.parameters():
+        p.grad = None
+    model.train()
+    rowptr, col, val = whole
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows, col.astype(np.int64)])), torch.from_numpy(val),
+                                (n, n)).coalesce()
+    del rows
+    torch.set_num_threads(min(64, os.cpu_count() or 1))
+    leaves = {k: v.requires_grad_(True) for k, v in state.items()}
+    outs = K.propagate(leaves, A)
+    u, p, q = (t.cpu() for t in batch)
+    ref = K.cf_loss(torch.cat(outs, 1), u, p, q)
+    ref.backward()
+    emb = max(float((o.detach() - g).abs().max()) for o, g in zip(outs, tables))
+    gref = leaves["_user_entity_embedding.weight"].grad
+    gerr = float((gref - grad).abs().max())
+    lrel = abs(float(ref) - float(loss)) / max(abs(float(ref)), 1e-30)
+    return {"max_abs_emb": emb, "max_abs_grad": gerr, "max_abs_grad_ref": float(gref.abs().max()), "loss_rel": lrel,
+            "loss": float(loss), "loss_oracle": float(ref), "tolerance": PARITY_TOL,
+            "pass": bool(emb <= PARITY_TOL["emb"] and gerr <= PARITY_TOL["grad"] and lrel <= PARITY_TOL["loss_rel"]),
+            "what": f"eval-mode propagation of every layer, CF loss and table gradient of the timed row-sharded "
+                    f"model (after the timed steps) vs oracle/kgat_cpu.py on the whole {n:,}-node graph, d = "
+                    f"{cfg['dim']}, layers {cfg['layers']}, one {batch[0].numel()}-pair batch"}
 
 
 def main() -> int:

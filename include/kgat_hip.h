@@ -419,6 +419,14 @@ int kgat_transr_bwd_f32(const float *emb, int64_t ld_emb, int32_t d, int32_t k, 
                         const int64_t *rels, const int64_t *pos, const int64_t *neg, int32_t batch, int32_t n_rel,
                         const float *work, const float *grad_out, float *d_emb, int64_t ld_demb, float *d_rel,
                         float *d_trans, float *workspace, int64_t workspace_floats, void *stream);
+/* As kgat_transr_bwd_f32 with the table gradient written compactly: row row_map[id] of d_emb
+ * (kgat_frontier_build's node map of the batch ids; the caller zero-fills its <= 3 * batch rows)
+ * instead of row id -- the input of kgat_adam_rows_f32 (the fused KG table update). */
+int kgat_transr_bwd_ex_f32(const float *emb, int64_t ld_emb, int32_t d, int32_t k, const int64_t *heads,
+                           const int64_t *rels, const int64_t *pos, const int64_t *neg, int32_t batch, int32_t n_rel,
+                           const float *work, const float *grad_out, float *d_emb, int64_t ld_demb,
+                           const int32_t *row_map, float *d_rel, float *d_trans, float *workspace,
+                           int64_t workspace_floats, void *stream);
 
 /* a6 -- knowledge-aware edge scores (model.py:263-316, multi_head_attention.py:35-58):
  * logit_e = sum_j tanh(LN(W_o drop(W_v (e_t W_r) + b_v) + b_o))_j * edge_weight[e]
@@ -545,6 +553,15 @@ typedef struct kgat_adam_tensor {
 int kgat_adam_multi_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
                         void *stream);
 
+/* a9 for the KG step's table (model.py:414-419 after the TransR backward, whose table gradient is
+ * nonzero on the <= 3B rows of the batch only): the dense Adam step over p / m / v [n_rows x d]
+ * where row r's gradient is Gc[row_map[r]] (ldg floats per compact row) when row_map[r] >= 0 and
+ * 0 otherwise -- the same bits as kgat_adam_f32 on the dense zero-filled gradient, which is never
+ * written.  d % 4 == 0, 16-byte aligned arrays. */
+int kgat_adam_rows_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *row_map,
+                       const float *Gc, int64_t ldg, float step_size, float beta1, float beta2, float bc2_sqrt,
+                       float eps, void *stream);
+
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);
 
@@ -562,6 +579,11 @@ typedef struct kgat_ids {
 } kgat_ids;
 int kgat_ids_check(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *bad, void *stream);
 
+/* node_map[ids[i]] = i for i < n (ids distinct; negative ids skipped): the node -> compact row
+ * map of a row list (the row-sharded backward's global batch rows, whose compact order is the
+ * host's sorted unique ids).  kgat_frontier_reset(ids, n, node_map) restores -1. */
+int kgat_map_build(const int32_t *ids, int64_t n, int32_t *node_map, void *stream);
+
 /* Fill n floats with a value. */
 int kgat_fill_f32(float *dst, int64_t n, float value, void *stream);
 
@@ -577,11 +599,16 @@ int kgat_add_f32(float *y, const float *x, int64_t n, void *stream);
 /* §8(d) synthetic CKGs at C4/C5 size, §8(f)3 graph build (host, csrc/synth.cpp).
  * Replaces, for the row-sharded configs, the reference's input-layout producer
  * (src/model/KGAT/preprocess.py:177-246, 628-634: per-relation blocks normalised
- * to A^T D^-1, summed into the attentive matrix).  Each triple is a pure function
- * of (seed, index), so every rank builds only its own rows [lo, hi):
- *   kgat_synth_open         draws nothing, counts the degrees (all triples, n_threads)
+ * to A^T D^-1, summed into the attentive matrix).  Each draw is a pure function
+ * of (seed, stream, index), so every rank builds only its own rows [lo, hi):
+ *   kgat_synth_open         finds the first n_triples distinct triples of the seeded
+ *                           draw streams (repeats dropped and redrawn),
+ *                           counts the degrees (all kept triples, n_threads); n_nodes
+ *                           < 2^30
  *   kgat_synth_info         info[8] = {n_nodes, n_triples, users, entities, items,
- *                           interactions, kg_triples, 0}
+ *                           interactions, kg_triples, draws taken} (n_triples = the
+ *                           kept count: smaller only when the type ranges cannot hold
+ *                           that many distinct triples)
  *   kgat_synth_row_offsets  [n_nodes + 1] prefix sums of each row's pre-coalesce
  *                           entries (the balance weights of the row shards)
  *   kgat_synth_triples      raw triples by index: rel = -1 -> (user a, item b),
@@ -600,6 +627,9 @@ int kgat_synth_row_offsets(const kgat_synth *g, int64_t *offsets);
 int kgat_synth_triples(const kgat_synth *g, const int64_t *idx, int64_t count, int64_t *a, int32_t *rel,
                        int64_t *b);
 int kgat_synth_shard_build(kgat_synth *g, int64_t lo, int64_t hi, int64_t *nnz);
+/* transpose != 0: rows [lo, hi) of A^T (the row-sharded backward's AT_loc, sharded.RowShard) --
+ * bit for bit the transpose of the layout's A restricted to those rows. */
+int kgat_synth_shard_build_ex(kgat_synth *g, int64_t lo, int64_t hi, int32_t transpose, int64_t *nnz);
 int kgat_synth_shard_copy(kgat_synth *g, int64_t *rowptr, int32_t *col, float *val);
 
 /* (e) Multi-GPU transport: an RCCL communicator over xGMI behind
@@ -631,6 +661,18 @@ int kgat_comm_reduce_scatter_rows_f32(kgat_comm *comm, const float *send, float 
                                       void *stream);
 /* the propagation ring's step: send -> rank + 1, rank - 1 -> recv (bytes each) */
 int kgat_comm_ring_exchange(kgat_comm *comm, const void *send, void *recv, int64_t bytes, void *stream);
+/* Uneven all-gather over every peer link at once (the row-sharded layer gather, sharded.py): rank
+ * r's block is recv[offsets[r], offsets[r+1]) (byte offsets, world + 1 of them, the same on every
+ * rank); this rank's block comes from send (which may alias recv + offsets[rank]).  One send and
+ * one receive per peer in a single RCCL group -- on a fully connected xGMI node every peer pair
+ * has its own link, so all seven links carry rows concurrently (no ring hop). */
+int kgat_comm_allgatherv(kgat_comm *comm, const void *send, void *recv, const int64_t *offsets, void *stream);
+/* All-to-all with per-peer sizes: send[send_off[p], send_off[p+1]) goes to rank p, rank p's block
+ * lands in recv[recv_off[p], recv_off[p+1]) (byte offsets, world + 1 each); the own block is
+ * copied on the stream.  The row-sharded attention refresh moves A's refreshed values to the
+ * owners of A^T's rows with it. */
+int kgat_comm_alltoallv(kgat_comm *comm, const void *send, const int64_t *send_off, void *recv,
+                        const int64_t *recv_off, void *stream);
 
 #ifdef __cplusplus
 }

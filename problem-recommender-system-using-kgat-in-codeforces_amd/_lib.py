@@ -124,6 +124,10 @@ _SIGNATURES = {
     "kgat_transr_fwd_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
                                               c_i32, c_f32, c_vp, c_vp, c_vp]),
     "kgat_transr_bwd_workspace_floats": (c_i64, [c_i32, c_i32, c_i32, c_i32]),
+    "kgat_transr_bwd_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                                              c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_adam_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32,
+                                          c_f32, c_f32, c_vp]),
     "kgat_transr_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                            c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_edge_logits_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -172,6 +176,7 @@ _SIGNATURES = {
     "kgat_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
+    "kgat_map_build": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_ids_check": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp]),
     "kgat_gemm_f32": (ctypes.c_int, [c_i32, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
                                      c_i64, c_i64, c_i64, c_i32, c_vp]),
@@ -185,12 +190,15 @@ _SIGNATURES = {
     "kgat_comm_allgather_rows": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_comm_reduce_scatter_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_comm_ring_exchange": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "kgat_comm_allgatherv": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp]),
+    "kgat_comm_alltoallv": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_vp]),
     "kgat_synth_open": (ctypes.c_int, [c_i64, c_i64, c_u64, ctypes.c_double, ctypes.c_int, ctypes.POINTER(c_vp)]),
     "kgat_synth_close": (None, [c_vp]),
     "kgat_synth_info": (ctypes.c_int, [c_vp, c_vp]),
     "kgat_synth_row_offsets": (ctypes.c_int, [c_vp, c_vp]),
     "kgat_synth_triples": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kgat_synth_shard_build": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "kgat_synth_shard_build_ex": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i32, ctypes.POINTER(c_i64)]),
     "kgat_synth_shard_copy": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
 }
 

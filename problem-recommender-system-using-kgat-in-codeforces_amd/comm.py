@@ -1,9 +1,10 @@
 """The library's own RCCL transport (kgat_comm_* in include/kgat_hip.h).
 
-``RcclComm`` is a drop-in for ``sharded.Comm`` (ring ``exchange``, ``all_reduce_``,
-``all_gather``) plus the row-block ``reduce_scatter_rows`` / ``all_gather_rows`` of the
-data-parallel exchange, with every collective issued by libkgat_hip.so on an RCCL
-communicator it owns -- the path a host without torch.distributed uses.  The reference has
+``RcclComm`` is a drop-in for ``sharded.Comm`` (the all-peer row gather ``gather_v``, the
+refresh's ``all_to_all_v``, ``all_reduce_``, ``all_gather``, the ring ``exchange``) plus the
+row-block ``reduce_scatter_rows`` / ``all_gather_rows`` of the data-parallel exchange, with
+every collective issued by libkgat_hip.so on an RCCL communicator it owns -- the path a host
+without torch.distributed uses.  The reference has
 no counterpart (single device, src/model/KGAT/main.py:239).
 
 Overlap: each collective runs on the communicator's own HIP stream, ordered after the work
@@ -118,7 +119,35 @@ class RcclComm:
         if not t.is_cuda or not t.is_contiguous():
             raise ValueError(f"{name}: a contiguous GPU tensor is required")
 
+    @property
+    def active(self) -> bool:
+        """Collectives move data (more than one rank, or forced at world 1)."""
+        return self.world > 1 or self.force
+
     # ------------------------------------------------------------ collectives
+    def gather_v(self, send: torch.Tensor, out: torch.Tensor, bounds) -> _Done:
+        """All-peer row gather (kgat_comm_allgatherv): rank r's rows land in out[bounds[r]:bounds[r+1]];
+        ``send`` = this rank's rows (may be that slice of ``out``).  wait() orders the caller after it."""
+        self._check(out, "out")
+        self._check(send, "send")
+        row = out.stride(0) * out.element_size()
+        offs = (ctypes.c_int64 * (self.world + 1))(*[int(b) * row for b in bounds])
+        st = self._begin(send, out)
+        _lib.call("kgat_comm_allgatherv", self._h, send.data_ptr(), out.data_ptr(), offs, st)
+        return self._end()
+
+    def all_to_all_v(self, send: torch.Tensor, send_off, recv: torch.Tensor, recv_off) -> None:
+        """send[send_off[p]:send_off[p+1]] -> rank p, rank p's block -> recv[recv_off[p]:...] (1-D,
+        element offsets; kgat_comm_alltoallv); the caller's stream is ordered after it."""
+        self._check(send, "send")
+        self._check(recv, "recv")
+        es = send.element_size()
+        so = (ctypes.c_int64 * (self.world + 1))(*[int(x) * es for x in send_off])
+        ro = (ctypes.c_int64 * (self.world + 1))(*[int(x) * es for x in recv_off])
+        st = self._begin(send, recv)
+        _lib.call("kgat_comm_alltoallv", self._h, send.data_ptr(), so, recv.data_ptr(), ro, st)
+        self._end().wait()
+
     def exchange(self, send: torch.Tensor, recv: torch.Tensor) -> _Done:
         """Start: send -> next rank, prev rank -> recv (kgat_comm_ring_exchange).  wait() completes both."""
         self._check(send, "send")

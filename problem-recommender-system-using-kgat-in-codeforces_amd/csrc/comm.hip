@@ -106,11 +106,22 @@ extern "C" int kgat_comm_init(int32_t rank, int32_t world, const uint8_t* id, in
   using namespace kgat;
   if (id == nullptr || out == nullptr || world < 1 || rank < 0 || rank >= world || device < 0) return KGAT_ERR_INVALID;
   if (int e = ensure_loaded()) return e;
+  // ncclCommInitRank binds the communicator to the current device: switch to `device` for the
+  // call and restore the caller's device afterwards (success or not) -- a library call must not
+  // change which GPU the calling thread launches on
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return KGAT_ERR_INVALID;
   if (hipSetDevice(device) != hipSuccess) return KGAT_ERR_INVALID;
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   ncclComm_t c = nullptr;
-  if (int e = status(g_rccl.comm_init_rank(&c, world, u, rank))) return e;
+  const int e = status(g_rccl.comm_init_rank(&c, world, u, rank));
+  const bool restored = hipSetDevice(prev) == hipSuccess;
+  if (e) return e;
+  if (!restored) {
+    g_rccl.comm_destroy(c);
+    return KGAT_ERR_INVALID;
+  }
   *out = new kgat_comm{c, rank, world, device};
   return KGAT_OK;
 }
@@ -170,4 +181,60 @@ extern "C" int kgat_comm_ring_exchange(kgat_comm* c, const void* send, void* rec
   const int e2 = status(g_rccl.recv(recv, static_cast<size_t>(bytes), ncclUint8, prev, c->comm, st));
   const int e3 = status(g_rccl.group_end());
   return e1 ? e1 : e2 ? e2 : e3;
+}
+
+extern "C" int kgat_comm_allgatherv(kgat_comm* c, const void* send, void* recv, const int64_t* offsets, void* stream) {
+  using namespace kgat;
+  if (c == nullptr || offsets == nullptr || recv == nullptr) return KGAT_ERR_INVALID;
+  for (int r = 0; r < c->world; ++r)
+    if (offsets[r + 1] < offsets[r]) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char* out = static_cast<char*>(recv);
+  const int64_t mine = offsets[c->rank + 1] - offsets[c->rank];
+  if (mine > 0 && send == nullptr) return KGAT_ERR_INVALID;
+  if (mine > 0 && send != out + offsets[c->rank] &&
+      hipMemcpyAsync(out + offsets[c->rank], send, static_cast<size_t>(mine), hipMemcpyDeviceToDevice, st) !=
+          hipSuccess)
+    return KGAT_ERR_INVALID;
+  if (c->world == 1) return KGAT_OK;
+  if (int e = status(g_rccl.group_start())) return e;
+  int err = KGAT_OK;
+  for (int p = 0; p < c->world && !err; ++p) {
+    if (p == c->rank) continue;
+    const int64_t theirs = offsets[p + 1] - offsets[p];
+    if (mine > 0) err = status(g_rccl.send(send, static_cast<size_t>(mine), ncclUint8, p, c->comm, st));
+    if (!err && theirs > 0)
+      err = status(g_rccl.recv(out + offsets[p], static_cast<size_t>(theirs), ncclUint8, p, c->comm, st));
+  }
+  const int e2 = status(g_rccl.group_end());
+  return err ? err : e2;
+}
+
+extern "C" int kgat_comm_alltoallv(kgat_comm* c, const void* send, const int64_t* send_off, void* recv,
+                                   const int64_t* recv_off, void* stream) {
+  using namespace kgat;
+  if (c == nullptr || send_off == nullptr || recv_off == nullptr) return KGAT_ERR_INVALID;
+  for (int r = 0; r < c->world; ++r)
+    if (send_off[r + 1] < send_off[r] || recv_off[r + 1] < recv_off[r]) return KGAT_ERR_INVALID;
+  if ((send_off[c->world] > send_off[0] && send == nullptr) || (recv_off[c->world] > recv_off[0] && recv == nullptr))
+    return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const char* in = static_cast<const char*>(send);
+  char* out = static_cast<char*>(recv);
+  const int64_t own = send_off[c->rank + 1] - send_off[c->rank];
+  if (own != recv_off[c->rank + 1] - recv_off[c->rank]) return KGAT_ERR_INVALID;
+  if (own > 0 && hipMemcpyAsync(out + recv_off[c->rank], in + send_off[c->rank], static_cast<size_t>(own),
+                                hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return KGAT_ERR_INVALID;
+  if (c->world == 1) return KGAT_OK;
+  if (int e = status(g_rccl.group_start())) return e;
+  int err = KGAT_OK;
+  for (int p = 0; p < c->world && !err; ++p) {
+    if (p == c->rank) continue;
+    const int64_t sb = send_off[p + 1] - send_off[p], rb = recv_off[p + 1] - recv_off[p];
+    if (sb > 0) err = status(g_rccl.send(in + send_off[p], static_cast<size_t>(sb), ncclUint8, p, c->comm, st));
+    if (!err && rb > 0) err = status(g_rccl.recv(out + recv_off[p], static_cast<size_t>(rb), ncclUint8, p, c->comm, st));
+  }
+  const int e2 = status(g_rccl.group_end());
+  return err ? err : e2;
 }

@@ -61,6 +61,14 @@ __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t to
   if (flag) *bad = 1;  // every writer stores 1: no atomic needed (bad may be host-mapped pinned memory)
 }
 
+// node_map[ids[i]] = i (distinct ids; ids[i] < 0 skipped)
+__global__ __launch_bounds__(256) void map_build_kernel(const int32_t* __restrict__ ids, int64_t n,
+                                                        int32_t* __restrict__ node_map) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (ids[i] >= 0) node_map[ids[i]] = static_cast<int32_t>(i);
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ dst, int64_t n, float value) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = value;
@@ -180,6 +188,50 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, 
   }
 }
 
+// The table's Adam step whose gradient is nonzero on a few rows only (the KG step: TransR reads
+// <= 3B rows, model.py:204-261): row r's gradient is Gc[row_map[r]] (compact, kgat_transr_bwd_ex_f32
+// with the same map) or exactly 0 -- the bits the dense step gets from its zero-filled [N, d]
+// gradient, without writing it, reading it back or zeroing it (24 B per parameter + 4 B per row
+// instead of 28 + 4 + the scatter).  adam_multi_kernel<2>'s access pattern (four float4 of each
+// array in flight per thread, non-temporal).
+__global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                        float* __restrict__ v, int64_t n4, int d4,
+                                                        const int32_t* __restrict__ row_map,
+                                                        const float* __restrict__ Gc, int64_t ldg, float step_size,
+                                                        float b1, float b2, float bc2s, float eps) {
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  const int64_t chunks = (n4 + 1023) / 1024;
+  for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+    float4 pp[4], mm[4], vv[4], gg[4];
+    int64_t e4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e4[u] = c * 1024 + u * 256 + threadIdx.x;
+      if (e4[u] < n4) {
+        pp[u] = ld4<2>(p + 4 * e4[u]);
+        mm[u] = ld4<2>(m + 4 * e4[u]);
+        vv[u] = ld4<2>(v + 4 * e4[u]);
+        const int32_t mi = row_map[e4[u] / d4];
+        gg[u] = mi >= 0 ? *reinterpret_cast<const float4*>(Gc + mi * ldg + 4 * (e4[u] % d4))
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e4[u] >= n4) continue;
+      float* P = &pp[u].x;
+      float* Mv = &mm[u].x;
+      float* Vv = &vv[u].x;
+      const float* G = &gg[u].x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], Vv[k], w1, b2, w2, step_size, bc2s, eps);
+      st4<2>(p + 4 * e4[u], pp[u]);
+      st4<2>(m + 4 * e4[u], mm[u]);
+      st4<2>(v + 4 * e4[u], vv[u]);
+    }
+  }
+}
+
 // Default 2 (C2 table, 64M parameters: 314 us vs 346 us for 0/1 on the same box).
 static int adam_variant() {
   static int v = -1;
@@ -217,6 +269,23 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
     case 2: hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps); break;
     default: hipLaunchKernelGGL(kgat::adam_multi_kernel<0>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps);
   }
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_adam_rows_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d, const int32_t* row_map,
+                                  const float* Gc, int64_t ldg, float step_size, float beta1, float beta2,
+                                  float bc2_sqrt, float eps, void* stream) {
+  if (!p || !m || !v || !row_map || !Gc || n_rows < 0 || d < 4 || (d & 3) || ldg < d || (ldg & 3)) return KGAT_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v) |
+       reinterpret_cast<uintptr_t>(Gc)) & 15)
+    return KGAT_ERR_INVALID;
+  const int64_t n4 = n_rows * (d / 4);
+  if (n4 == 0) return KGAT_OK;
+  const int64_t chunks = (n4 + 1023) / 1024;
+  const int grid = static_cast<int>(chunks < kgat::kCUs * 8 ? chunks : kgat::kCUs * 8);
+  hipLaunchKernelGGL(kgat::adam_rows_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, m, v,
+                     n4, d / 4, row_map, Gc, ldg, step_size, beta1, beta2, bc2_sqrt, eps);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -332,6 +401,15 @@ extern "C" int kgat_ids_check(const kgat_ids* ids, int64_t bound, int64_t* out, 
   if (total == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::ids_check_kernel, dim3(kgat::blocks_for(total, 256, kgat::kCUs * 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), *ids, total, bound, out, bad);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_map_build(const int32_t* ids, int64_t n, int32_t* node_map, void* stream) {
+  if (!node_map || n < 0 || (n && !ids) || n > INT32_MAX) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::map_build_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ids, n, node_map);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -13,9 +13,15 @@
 // are the first 10 % of entities; 80 % of the triples are user -> item interactions with
 // Zipf(s) item popularity (alias table over popularity ranks, ranks mapped to items by a
 // seeded permutation), 20 % are KG triples over the 4 reference relations with uniform
-// heads / tails inside the relation's type range.  Multi-edges are kept: like the
-// reference's scipy coo_matrix sums (src/model/KGAT/preprocess.py:224-246) a repeated
-// (h, t) contributes count(h, t) / outdeg(h), outdeg counting repeats.
+// heads / tails inside the relation's type range.  Repeated triples are dropped and
+// redrawn, as SURVEY §8(d) specifies ("duplicate (h, t) are dropped"; graph.synthetic_ckg
+// redraws interactions the same way): draw p of a stream is kept iff it is the first
+// draw of its triple, and the kept triples are the first M (interactions) / K (KG) kept
+// draws in draw order -- a parallel hash pass records each triple's smallest draw index,
+// so the result does not depend on the thread count.  Every kept triple is distinct, so
+// the attentive matrix holds 2T entries before (row, col) pairs of different blocks are
+// coalesced (E ~= 2T, §8(d)).  Repeats that do occur in the layout producer's input are
+// still weighted by count (preprocess.py:224-246), and the arithmetic below keeps that rule.
 //
 // Attentive matrix (preprocess.py:177-246, 628-634): adjacency blocks in the reference
 // order  0: user -> item, 1: item -> user (inverse), 2+2r: KG r, 3+2r: KG r inverse;
@@ -76,38 +82,136 @@ void parallel_for(int64_t n, int threads, F&& f) {  // f(begin, end, thread)
 
 inline void bump(uint32_t* a, int64_t i) { __atomic_fetch_add(a + i, 1u, __ATOMIC_RELAXED); }
 
+inline void atomic_min_u32(uint32_t* a, uint32_t v) {
+  uint32_t cur = __atomic_load_n(a, __ATOMIC_RELAXED);
+  while (v < cur && !__atomic_compare_exchange_n(a, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+}
+
+// The first `target` distinct keys of a draw stream, in draw order: returns the draw indices p
+// (ascending) whose key(p) occurs at no smaller index.  Open-addressing hash of key -> smallest draw
+// index (CAS insert + atomic min: the minimum does not depend on thread interleaving), over a
+// prefix of P draws, grown by 1.5x until it holds `target` distinct keys or P reaches `limit`
+// (a stream with fewer distinct keys than target: all of them are kept).  *draws = the prefix
+// length that yields the kept set (index of the last kept draw + 1).
+template <class Key>
+std::vector<uint32_t> first_distinct(int64_t target, int64_t limit, int threads, Key&& key, int64_t* draws) {
+  std::vector<uint32_t> kept;
+  *draws = 0;
+  if (target <= 0) return kept;
+  constexpr uint64_t kEmpty = ~uint64_t{0};
+  int64_t P = std::min(limit, target + target / 2 + 4096);
+  for (;;) {
+    uint64_t S = 1024;
+    while (S < static_cast<uint64_t>(P + P / 2)) S <<= 1;
+    std::vector<uint64_t> keys(S, kEmpty);
+    std::vector<uint32_t> first(S, ~uint32_t{0});
+    const uint64_t mask = S - 1;
+    auto slot_of = [&](uint64_t k, bool insert) -> uint64_t {
+      uint64_t s = mix64(k) & mask;
+      for (;;) {
+        uint64_t cur = __atomic_load_n(&keys[s], __ATOMIC_RELAXED);
+        if (cur == k) return s;
+        if (cur == kEmpty) {
+          if (!insert) return S;  // not present (cannot happen on the second pass)
+          if (__atomic_compare_exchange_n(&keys[s], &cur, k, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED) || cur == k)
+            return s;
+        }
+        s = (s + 1) & mask;
+      }
+    };
+    parallel_for(P, threads, [&](int64_t b, int64_t e, int) {
+      for (int64_t p = b; p < e; ++p) atomic_min_u32(&first[slot_of(key(p), true)], static_cast<uint32_t>(p));
+    });
+    // count, then list, the first occurrences per contiguous chunk (draw order kept)
+    const int nt = std::max(1, threads);
+    std::vector<int64_t> cnt(nt + 1, 0);
+    auto is_first = [&](int64_t p) {
+      const uint64_t sl = slot_of(key(p), false);
+      return sl < S && first[sl] == static_cast<uint32_t>(p);
+    };
+    parallel_for(nt, nt, [&](int64_t tb, int64_t te, int) {
+      for (int64_t t = tb; t < te; ++t) {
+        const int64_t b = P * t / nt, e = P * (t + 1) / nt;
+        int64_t c = 0;
+        for (int64_t p = b; p < e; ++p) c += is_first(p);
+        cnt[t + 1] = c;
+      }
+    });
+    for (int t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+    if (cnt[nt] >= target || P >= limit) {
+      const int64_t take = std::min<int64_t>(target, cnt[nt]);
+      kept.assign(static_cast<size_t>(take), 0);
+      parallel_for(nt, nt, [&](int64_t tb, int64_t te, int) {
+        for (int64_t t = tb; t < te; ++t) {
+          int64_t at = cnt[t];
+          if (at >= take) continue;
+          const int64_t b = P * t / nt, e = P * (t + 1) / nt;
+          for (int64_t p = b; p < e && at < take; ++p)
+            if (is_first(p)) kept[static_cast<size_t>(at++)] = static_cast<uint32_t>(p);
+        }
+      });
+      *draws = take ? static_cast<int64_t>(kept.back()) + 1 : 0;
+      return kept;
+    }
+    P = std::min(limit, P + P / 2);
+  }
+}
+
 }  // namespace
 
 struct kgat_synth {
   int64_t n = 0, T = 0, U = 0, E = 0, I = 0, M = 0, K = 0;
+  int64_t M_draws = 0, K_draws = 0;  // draws taken to find the M / K distinct triples
   uint64_t seed = 0;
   int threads = 1;
   Range head[4], tail[4];          // per KG relation, entity ids
   std::vector<double> prob;        // alias table over popularity ranks
   std::vector<int32_t> alias;
   std::vector<int32_t> item_perm;  // rank -> item
+  std::vector<uint32_t> kept_int, kept_kg;  // kept triple -> its draw index in its stream
   std::vector<uint32_t> deg_user, deg_item, out_r[4], in_r[4];
   // the last built shard
   std::vector<int64_t> rowptr;
   std::vector<int32_t> col;
   std::vector<float> val;
 
-  // triple i: (a, rel, b) raw ids -- rel = -1: interaction (user a, item b); else KG (head a, tail b)
+  // interaction draw p of the interaction stream: (user a, item b)
+  inline void draw_interaction(int64_t p, int64_t& a, int64_t& b) const {
+    a = static_cast<int64_t>(below(draw(seed, p, 0), U));
+    const uint64_t k = below(draw(seed, p, 1), I);
+    const int64_t rank = unit(draw(seed, p, 2)) < prob[k] ? static_cast<int64_t>(k) : alias[k];
+    b = item_perm[rank];
+  }
+  // KG draw q of the KG stream: (head a, rel, tail b)
+  inline void draw_kg(int64_t q, int64_t& a, int32_t& rel, int64_t& b) const {
+    rel = static_cast<int32_t>(below(draw(seed, q, 3), 4));
+    const Range& h = head[rel];
+    a = h.lo + static_cast<int64_t>(below(draw(seed, q, 4), h.size()));
+    const Range& t = tail[rel];
+    b = std::min<int64_t>(t.lo + static_cast<int64_t>(unit(draw(seed, q, 5)) * static_cast<double>(t.size())), E - 1);
+  }
+  // distinct keys of the two streams (< 2^63: n < 2^30 is checked at open)
+  inline uint64_t interaction_key(int64_t p) const {
+    int64_t a, b;
+    draw_interaction(p, a, b);
+    return static_cast<uint64_t>(a) * static_cast<uint64_t>(I) + static_cast<uint64_t>(b);
+  }
+  inline uint64_t kg_key(int64_t q) const {
+    int64_t a, b;
+    int32_t r;
+    draw_kg(q, a, r, b);
+    return (static_cast<uint64_t>(a) * 4 + static_cast<uint64_t>(r)) * static_cast<uint64_t>(E) + static_cast<uint64_t>(b);
+  }
+
+  // kept triple i: (a, rel, b) raw ids -- rel = -1: interaction (user a, item b); else KG (head a, tail b)
   inline void triple(int64_t i, int64_t& a, int32_t& rel, int64_t& b) const {
     if (i < M) {
-      a = static_cast<int64_t>(below(draw(seed, i, 0), U));
-      const uint64_t k = below(draw(seed, i, 1), I);
-      const int64_t rank = unit(draw(seed, i, 2)) < prob[k] ? static_cast<int64_t>(k) : alias[k];
-      b = item_perm[rank];
+      draw_interaction(kept_int[i], a, b);
       rel = -1;
       return;
     }
-    const int64_t j = i - M;
-    rel = static_cast<int32_t>(below(draw(seed, j, 3), 4));
-    const Range& h = head[rel];
-    a = h.lo + static_cast<int64_t>(below(draw(seed, j, 4), h.size()));
-    const Range& t = tail[rel];
-    b = std::min<int64_t>(t.lo + static_cast<int64_t>(unit(draw(seed, j, 5)) * static_cast<double>(t.size())), E - 1);
+    draw_kg(kept_kg[i - M], a, rel, b);
   }
 
   // node-id entries of triple i: (row, col, block) x 2
@@ -150,7 +254,7 @@ extern "C" {
 
 int kgat_synth_open(int64_t n_nodes, int64_t n_triples, uint64_t seed, double zipf_s, int n_threads,
                     kgat_synth** out) {
-  if (!out || n_nodes < 2 || n_triples < 0 || n_nodes >= (int64_t{1} << 31)) return KGAT_ERR_INVALID;
+  if (!out || n_nodes < 2 || n_triples < 0 || n_nodes >= (int64_t{1} << 30)) return KGAT_ERR_INVALID;
   *out = nullptr;
   kgat_synth* g = new (std::nothrow) kgat_synth();
   if (!g) return KGAT_ERR_INVALID;
@@ -207,7 +311,17 @@ int kgat_synth_open(int64_t n_nodes, int64_t n_triples, uint64_t seed, double zi
     for (int64_t k = 0; k < I; ++k) g->item_perm[k] = static_cast<int32_t>(k);
     for (int64_t k = I - 1; k > 0; --k)
       std::swap(g->item_perm[k], g->item_perm[below(draw(g->seed, k, 7), static_cast<uint64_t>(k + 1))]);
-    // degrees (pass 1 over every triple)
+    // distinct triples: the first M interaction draws / K KG draws of distinct keys (draw indices
+    // are uint32: at most 2^32 - 1 draws per stream)
+    const int64_t lim_m = std::min<int64_t>(int64_t{0xFFFFFFFF}, 64 * g->M + 4096);
+    const int64_t lim_k = std::min<int64_t>(int64_t{0xFFFFFFFF}, 64 * g->K + 4096);
+    g->kept_int = first_distinct(g->M, lim_m, g->threads, [g](int64_t p) { return g->interaction_key(p); },
+                                 &g->M_draws);
+    g->kept_kg = first_distinct(g->K, lim_k, g->threads, [g](int64_t q) { return g->kg_key(q); }, &g->K_draws);
+    g->M = static_cast<int64_t>(g->kept_int.size());
+    g->K = static_cast<int64_t>(g->kept_kg.size());
+    g->T = g->M + g->K;
+    // degrees (pass 1 over every kept triple)
     g->deg_user.assign(g->U, 0);
     g->deg_item.assign(I, 0);
     for (int r = 0; r < 4; ++r) {
@@ -240,7 +354,7 @@ void kgat_synth_close(kgat_synth* g) { delete g; }
 
 int kgat_synth_info(const kgat_synth* g, int64_t* info) {
   if (!g || !info) return KGAT_ERR_INVALID;
-  const int64_t v[8] = {g->n, g->T, g->U, g->E, g->I, g->M, g->K, 0};
+  const int64_t v[8] = {g->n, g->T, g->U, g->E, g->I, g->M, g->K, g->M_draws + g->K_draws};
   for (int k = 0; k < 8; ++k) info[k] = v[k];
   return KGAT_OK;
 }
@@ -263,6 +377,15 @@ int kgat_synth_triples(const kgat_synth* g, const int64_t* idx, int64_t count, i
 }
 
 int kgat_synth_shard_build(kgat_synth* g, int64_t lo, int64_t hi, int64_t* nnz) {
+  return kgat_synth_shard_build_ex(g, lo, hi, 0, nnz);
+}
+
+// transpose = 1: rows [lo, hi) of A^T instead -- the entries of A whose COLUMN lies in [lo, hi),
+// keyed by that column (the A^T row) with the A row as their column.  The value of an entry is
+// A's (count / outdeg of the head, summed over blocks in block order), so these rows are the
+// transpose of the layout's A bit for bit.  A node's A^T row has as many pre-coalesce entries as
+// its A row (every triple enters A in both directions), so row_entries sizes both.
+int kgat_synth_shard_build_ex(kgat_synth* g, int64_t lo, int64_t hi, int32_t transpose, int64_t* nnz) {
   if (!g || !nnz || lo < 0 || hi < lo || hi > g->n) return KGAT_ERR_INVALID;
   try {
     const int64_t rows = hi - lo;
@@ -277,9 +400,11 @@ int kgat_synth_shard_build(kgat_synth* g, int64_t lo, int64_t hi, int64_t* nnz) 
       for (int64_t i = b; i < e; ++i) {
         g->entries(i, row, c, blk);
         for (int s = 0; s < 2; ++s) {
-          if (row[s] < lo || row[s] >= hi) continue;
-          const int64_t at = __atomic_fetch_add(&cursor[row[s] - lo], 1, __ATOMIC_RELAXED);
-          keys[at] = (static_cast<uint64_t>(c[s]) << 4) | static_cast<uint64_t>(blk[s]);
+          // A: entry (row, col); A^T: the same entry as (col, row) -- the block's head is col
+          const int64_t r = transpose ? c[s] : row[s], cc = transpose ? row[s] : c[s];
+          if (r < lo || r >= hi) continue;
+          const int64_t at = __atomic_fetch_add(&cursor[r - lo], 1, __ATOMIC_RELAXED);
+          keys[at] = (static_cast<uint64_t>(cc) << 4) | static_cast<uint64_t>(blk[s]);
         }
       }
     });
@@ -312,7 +437,8 @@ int kgat_synth_shard_build(kgat_synth* g, int64_t lo, int64_t hi, int64_t* nnz) 
           while (p < end && *p == key) ++p, ++cnt;
           const int64_t c = static_cast<int64_t>(key >> 4);
           const int32_t blk = static_cast<int32_t>(key & 15);
-          const double v = static_cast<double>(cnt) / static_cast<double>(g->head_degree(blk, c));
+          // the block's head: A's column (A) or the A^T row itself (transpose)
+          const double v = static_cast<double>(cnt) / static_cast<double>(g->head_degree(blk, transpose ? lo + x : c));
           if (c != prev_col) {
             if (out >= g->rowptr[x]) g->val[out] = static_cast<float>(sum);
             ++out;

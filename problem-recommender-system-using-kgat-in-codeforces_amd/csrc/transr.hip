@@ -370,12 +370,15 @@ __global__ __launch_bounds__(256) void transr_loss_kernel(const float* __restric
 
 // d_emb[id] += scale * sum of the table-row gradients of every slot with that
 // id, slots = [heads | pos | neg]; first occurrence owns the row (no atomics).
+// With row_map the row is d_emb[row_map[id]] (a compact gradient, kgat_frontier_build's
+// numbering; -1 skipped).
 __global__ __launch_bounds__(256) void transr_scatter_kernel(const int64_t* __restrict__ heads,
                                                              const int64_t* __restrict__ pos,
                                                              const int64_t* __restrict__ neg, int batch, int d,
                                                              const float* __restrict__ grow,
                                                              const float* __restrict__ grad_out,
-                                                             float* __restrict__ dst, int64_t lddst) {
+                                                             float* __restrict__ dst, int64_t lddst,
+                                                             const int32_t* __restrict__ row_map) {
   const int slots = 3 * batch;
   const int s0k = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -402,10 +405,12 @@ __global__ __launch_bounds__(256) void transr_scatter_kernel(const int64_t* __re
       }
     }
   }
+  const int64_t row = row_map ? static_cast<int64_t>(row_map[id]) : id;
+  if (row < 0) return;
 #pragma unroll
   for (int cc = 0; cc < kMaxCols; ++cc) {
     const int j = lane + 64 * cc;
-    if (j < d) dst[id * lddst + j] += g[cc];
+    if (j < d) dst[row * lddst + j] += g[cc];
   }
 }
 
@@ -659,6 +664,15 @@ extern "C" int kgat_transr_bwd_f32(const float* emb, int64_t ld_emb, int32_t d, 
                                    int32_t n_rel, const float* work, const float* grad_out, float* d_emb,
                                    int64_t ld_demb, float* d_rel, float* d_trans, float* workspace,
                                    int64_t workspace_floats, void* stream) {
+  return kgat_transr_bwd_ex_f32(emb, ld_emb, d, k, heads, rels, pos, neg, batch, n_rel, work, grad_out, d_emb,
+                                ld_demb, nullptr, d_rel, d_trans, workspace, workspace_floats, stream);
+}
+
+extern "C" int kgat_transr_bwd_ex_f32(const float* emb, int64_t ld_emb, int32_t d, int32_t k, const int64_t* heads,
+                                      const int64_t* rels, const int64_t* pos, const int64_t* neg, int32_t batch,
+                                      int32_t n_rel, const float* work, const float* grad_out, float* d_emb,
+                                      int64_t ld_demb, const int32_t* row_map, float* d_rel, float* d_trans,
+                                      float* workspace, int64_t workspace_floats, void* stream) {
   if (!emb || !heads || !rels || !pos || !neg || !work || !grad_out || !d_emb || !d_rel || !d_trans || batch <= 0 ||
       n_rel <= 0)
     return KGAT_ERR_INVALID;
@@ -667,7 +681,7 @@ extern "C" int kgat_transr_bwd_f32(const float* emb, int64_t ld_emb, int32_t d, 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const kgat::TransrWork off = kgat::TransrWork::at(batch, d, k);
   hipLaunchKernelGGL(kgat::transr_scatter_kernel, dim3((3 * batch + 3) / 4), dim3(256), 0, st, heads, pos, neg, batch,
-                     d, work + off.grow, grad_out, d_emb, ld_demb);
+                     d, work + off.grow, grad_out, d_emb, ld_demb, row_map);
   KGAT_LAUNCH_CHECK();
   const int n_chunk = (batch + kgat::kWgradChunk - 1) / kgat::kWgradChunk;
   const int64_t w = static_cast<int64_t>(d) * k + k;

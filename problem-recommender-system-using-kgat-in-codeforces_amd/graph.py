@@ -485,7 +485,8 @@ class HashedCKG:
 
     Same node layout and distributions as :func:`synthetic_ckg` (users first, items = first 10 %
     of entities, 80 % Zipf interactions, 20 % KG triples over 4 relations); repeated triples are
-    kept and weighted by count, as the reference's coo_matrix sums them (preprocess.py:224-246).
+    dropped and redrawn, so the graph holds exactly ``n_triples`` distinct triples
+    and E ~= 2 * n_triples attentive-matrix entries.  ``draws`` = the draws that took.
     """
 
     def __init__(self, n_nodes: int, n_triples: int, seed: int = 2024, zipf_s: float = 1.1, threads: int = 0):
@@ -499,7 +500,7 @@ class HashedCKG:
         info = np.zeros(8, np.int64)
         _lib.call("kgat_synth_info", self._h, info.ctypes.data)
         self.n_nodes, self.n_triples, self.user_num, self.entity_num, self.item_num, self.n_interactions, \
-            self.n_kg = (int(x) for x in info[:7])
+            self.n_kg, self.draws = (int(x) for x in info[:8])
 
     def close(self) -> None:
         h, self._h = getattr(self, "_h", None), None
@@ -531,10 +532,11 @@ class HashedCKG:
         trip = np.stack([a[~m], r[~m].astype(np.int64), b[~m]], 1)
         return self.user_num, self.entity_num, inter, trip
 
-    def shard(self, lo: int, hi: int):
-        """Coalesced CSR of rows [lo, hi): (rowptr [hi-lo+1] from 0, col int32 global ids, val fp32)."""
+    def shard(self, lo: int, hi: int, transpose: bool = False):
+        """Coalesced CSR of rows [lo, hi): (rowptr [hi-lo+1] from 0, col int32 global ids, val fp32); with
+        ``transpose`` the rows of A^T (sharded.RowShard's AT_loc)."""
         nnz = ctypes.c_int64()
-        _lib.call("kgat_synth_shard_build", self._h, int(lo), int(hi), ctypes.byref(nnz))
+        _lib.call("kgat_synth_shard_build_ex", self._h, int(lo), int(hi), int(bool(transpose)), ctypes.byref(nnz))
         rowptr = np.empty(int(hi) - int(lo) + 1, np.int64)
         col = np.empty(nnz.value, np.int32)
         val = np.empty(nnz.value, np.float32)

@@ -892,6 +892,43 @@ def transr_bwd(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out):
     return d_emb, d_rel, d_trans
 
 
+def transr_bwd_compact(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out, row_map: torch.Tensor,
+                       n_rows: int):
+    """transr_bwd with the table gradient written compactly (kgat_transr_bwd_ex_f32): row row_map[id]
+    of a zero-filled [n_rows, d] buffer per batch id (kgat_frontier_build's map).  Returns (Gc, d_rel,
+    d_trans)."""
+    _req(row_map, "row_map", dtype=torch.int32, dim=1)
+    dev = emb.device
+    d = emb.shape[1]
+    Gc = zeros((max(n_rows, 1), d), dev)
+    d_rel = torch.empty(n_rel, k, dtype=torch.float32, device=dev)
+    d_trans = torch.empty(n_rel, d, k, dtype=torch.float32, device=dev)
+    ws_n = int(_lib.lib().kgat_transr_bwd_workspace_floats(heads.numel(), d, k, n_rel))
+    if ws_n < 0:
+        raise ValueError("transr_bwd: bad shape")
+    ws = torch.empty(ws_n, dtype=torch.float32, device=dev)
+    _lib.call("kgat_transr_bwd_ex_f32", emb.data_ptr(), _ld(emb), d, k, heads.data_ptr(), rels.data_ptr(),
+              pos.data_ptr(), neg.data_ptr(), heads.numel(), n_rel, work.data_ptr(), grad_out.data_ptr(),
+              Gc.data_ptr(), _ld(Gc), row_map.data_ptr(), d_rel.data_ptr(), d_trans.data_ptr(), ws.data_ptr(),
+              ws.numel(), stream_ptr(dev))
+    return Gc, d_rel, d_trans
+
+
+def adam_rows(p, m, v, row_map: torch.Tensor, Gc: torch.Tensor, step_size: float, beta1: float, beta2: float,
+              bc2_sqrt: float, eps: float) -> None:
+    """Adam over the whole [N, d] table with row r's gradient Gc[row_map[r]] or 0 (kgat_adam_rows_f32)."""
+    for t, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _req(t, nm, dim=2)
+        if not t.is_contiguous() or t.shape != p.shape:
+            raise ValueError(f"{nm}: contiguous {tuple(p.shape)} expected")
+    _req(row_map, "row_map", dtype=torch.int32, dim=1)
+    _req(Gc, "Gc", dim=2)
+    if row_map.numel() != p.shape[0] or Gc.shape[1] != p.shape[1]:
+        raise ValueError("adam_rows: row_map must cover every row, Gc must be [rows, d]")
+    _lib.call("kgat_adam_rows_f32", p.data_ptr(), m.data_ptr(), v.data_ptr(), p.shape[0], p.shape[1],
+              row_map.data_ptr(), Gc.data_ptr(), _ld(Gc), step_size, beta1, beta2, bc2_sqrt, eps, stream_ptr(p.device))
+
+
 def score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out: torch.Tensor, dropout_p: float = 0.0,
                 seed: int = 0) -> None:
     """Edge scores of a plan: out[plan.out_pos[e]] (or out[e]) = logit of edge e; the fused MFMA

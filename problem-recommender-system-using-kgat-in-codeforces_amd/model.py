@@ -126,7 +126,9 @@ class _IdGuard:
     a host synchronisation (kgat_ids_check: one launch copies them, zeroes any id outside
     [0, bound) so no kernel reads out of range, and sets a flag in pinned host memory); the flag
     is read after the call's event and IndexError is raised at the model's next call (or by
-    ``raise_pending(block=True)``) -- the way PyTorch reports a device-side index error."""
+    ``raise_pending(block=True)``) -- the way PyTorch reports a device-side index error.
+    ``update_cf_weights`` / ``update_kg_weights`` wait for the flag (block=True), so a step whose
+    ids were bad raises there, before the optimiser moves any parameter."""
 
     def __init__(self):
         self._host = self._event = None
@@ -225,6 +227,65 @@ class _TableUpdate:
 
         def run(m, v, step_size, bc2s, b1, b2, eps):
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps)
+        return run
+
+
+class _KGTableUpdate:
+    """The KG step's table gradient kept compact until ``update_kg_weights`` (opt-in:
+    ``KGAT.fuse_kg_table_update = True``).
+
+    The reference KG step is ``loss.backward(); model.update_kg_weights()`` (main.py:334-342):
+    nn.Embedding's dense backward writes a [N, d] table gradient that is zero except on the <= 3B
+    rows TransR gathered (model.py:211-221), and Adam reads it back (model.py:414-419).  Here the
+    TransR backward writes those rows compactly (kgat_transr_bwd_ex_f32, rows numbered by
+    kgat_frontier_build's map) and ``update_kg_weights`` runs the table's Adam with row r's gradient
+    looked up through the map, 0 elsewhere (kgat_adam_rows_f32): the same bits as the dense step,
+    without writing, zeroing or re-reading the [N, d] gradient.  Anything that needs the gradient
+    first materialises it (a second backward, the next forward, ``materialize_table_grad()``)."""
+
+    def __init__(self, param: torch.Tensor):
+        self.param = param
+        self.enabled = False
+        self.pending = None
+        self._map = None
+
+    def node_map(self) -> torch.Tensor:
+        """node -> compact row of the batch ids (-1 between steps), allocated once."""
+        n = self.param.shape[0]
+        if self._map is None or self._map.numel() != n or self._map.device != self.param.device:
+            self._map = torch.full((n,), -1, dtype=torch.int32, device=self.param.device)
+        return self._map
+
+    def wants(self, batch: int) -> bool:
+        # kgat_frontier_build numbers at most 4096 slots (3 per sample)
+        return self.enabled and self.pending is None and self.param.grad is None and 3 * batch <= 4096
+
+    def defer(self, rows: torch.Tensor, Gc: torch.Tensor) -> None:
+        self.pending = (rows, Gc)
+
+    @torch.no_grad()
+    def materialize(self) -> None:
+        if self.pending is None:
+            return
+        rows, Gc = self.pending
+        self.pending = None
+        g = kernels.zeros(tuple(self.param.shape), self.param.device)
+        kernels.scatter_rows(g, rows, Gc[:rows.numel()], accumulate=False)
+        kernels.frontier_reset(rows, self._map)
+        if self.param.grad is None:
+            self.param.grad = g
+        else:
+            kernels.add_(self.param.grad, g)
+
+    def launch(self):
+        """The table's Adam step on the compact gradient (FusedAdam.step(fused=...))."""
+        rows, Gc = self.pending
+        self.pending = None
+        p, row_map = self.param.data, self._map
+
+        def run(m, v, step_size, bc2s, b1, b2, eps):
+            kernels.adam_rows(p, m, v, row_map, Gc, step_size, b1, b2, bc2s, eps)
+            kernels.frontier_reset(rows, row_map)
         return run
 
 
@@ -510,13 +571,16 @@ class _CFLoss(torch.autograd.Function):
 class _KGLoss(torch.autograd.Function):
     """TransR KG loss as one autograd node (model.py:204-261): kgat_transr_fwd_f32 /
     kgat_transr_bwd_f32.  Gradients: dense table (zero except the gathered rows,
-    as nn.Embedding's dense backward), relation embeddings, trans matrices."""
+    as nn.Embedding's dense backward), relation embeddings, trans matrices.  With the
+    fused KG table update (_KGTableUpdate) the table's rows are handed over compactly
+    instead and the table gets no .grad."""
 
     @staticmethod
-    def forward(ctx, heads, rels, pos, neg, reg, emb, rel_emb, trans):
+    def forward(ctx, heads, rels, pos, neg, reg, ktu, emb, rel_emb, trans):
         loss, work = kernels.transr_fwd(emb, rel_emb, trans, heads, rels, pos, neg, reg)
         ctx.save_for_backward(heads, rels, pos, neg, work, emb)
         ctx.shape = (rel_emb.shape[0], rel_emb.shape[1])
+        ctx.ktu = ktu
         return loss.view(())
 
     @staticmethod
@@ -524,8 +588,16 @@ class _KGLoss(torch.autograd.Function):
         heads, rels, pos, neg, work, emb = ctx.saved_tensors
         n_rel, k = ctx.shape
         gout = gout.reshape(1).to(torch.float32).contiguous()
+        ktu, ctx.ktu = ctx.ktu, None
+        if ktu is not None and ktu.wants(heads.numel()):
+            row_map = ktu.node_map()
+            rows, _ = kernels.frontier_build(heads, pos, neg, row_map)
+            Gc, d_rel, d_trans = kernels.transr_bwd_compact(emb, n_rel, k, heads, rels, pos, neg, work, gout, row_map,
+                                                            rows.numel())
+            ktu.defer(rows, Gc)
+            return None, None, None, None, None, None, None, d_rel, d_trans
         d_emb, d_rel, d_trans = kernels.transr_bwd(emb, n_rel, k, heads, rels, pos, neg, work, gout)
-        return None, None, None, None, None, d_emb, d_rel, d_trans
+        return None, None, None, None, None, None, d_emb, d_rel, d_trans
 
 
 class KGAT(nn.Module):
@@ -563,6 +635,7 @@ class KGAT(nn.Module):
         self._graph_key = None
         self._ids = _IdGuard()
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
+        self._kg_table_update = _KGTableUpdate(self._user_entity_embedding.weight)
         # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
         # (_frontier_forward) -- same loss, gradients and updates, bit for bit
         self.frontier_forward = False
@@ -579,9 +652,22 @@ class KGAT(nn.Module):
             self._table_update.materialize()
         self._table_update.enabled = bool(on)
 
+    @property
+    def fuse_kg_table_update(self) -> bool:
+        """Opt-in: the KG step's table gradient stays compact and ``update_kg_weights`` steps the
+        table from it (_KGTableUpdate); ``table.grad`` is None in between."""
+        return self._kg_table_update.enabled
+
+    @fuse_kg_table_update.setter
+    def fuse_kg_table_update(self, on: bool) -> None:
+        if not on:
+            self._kg_table_update.materialize()
+        self._kg_table_update.enabled = bool(on)
+
     def materialize_table_grad(self) -> None:
-        """Write a deferred table gradient into ``_user_entity_embedding.weight.grad``."""
+        """Write a deferred table gradient (CF or KG step) into ``_user_entity_embedding.weight.grad``."""
         self._table_update.materialize()
+        self._kg_table_update.materialize()
 
     # ------------------------------------------------------------------ graph
     def graph(self) -> DeviceGraph:
@@ -685,7 +771,8 @@ class KGAT(nn.Module):
         h, p, q, r = self._ids.check("TRAIN_KG ids", (heads, positive_tails, negative_tails), n, dev,
                                      more=[((relations,), self._relation_num)])
         ids = [h, r, p, q]
-        return _KGLoss.apply(*ids, float(self._regularization_params[1]), self._user_entity_embedding.weight,
+        ktu = self._kg_table_update if torch.is_grad_enabled() else None
+        return _KGLoss.apply(*ids, float(self._regularization_params[1]), ktu, self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)
 
     def _update_attention(self, heads, relations, tails, relation_indices) -> None:
@@ -733,11 +820,16 @@ class KGAT(nn.Module):
     def update_cf_weights(self, row_ranges: dict | None = None) -> None:
         """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all.
         A deferred table gradient (fuse_table_update) is stepped by the fused product + Adam."""
-        self._ids.raise_pending()
+        # a device-side id error of this step's forward surfaces here, before any parameter moves
+        # (one wait on the id check's event: the host stays within the step the GPU runs)
+        self._ids.raise_pending(block=True)
         tu = self._table_update
         fused = None
         if tu.pending is not None:
-            if row_ranges and id(tu.param) in row_ranges:
+            # another term of the loss may have written the table's .grad after the deferral (autograd
+            # order, an extra regulariser on the table): the fused launch never reads .grad, so such a
+            # gradient is summed with the deferred product first (materialize adds into .grad)
+            if (row_ranges and id(tu.param) in row_ranges) or tu.param.grad is not None:
                 tu.materialize()
             else:
                 fused = {id(tu.param): tu.launch()}
@@ -745,16 +837,25 @@ class KGAT(nn.Module):
         self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
-        self._ids.raise_pending()
+        """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
+        self._ids.raise_pending(block=True)
         self._table_update.materialize()
-        self._kg_optimizer.step(row_ranges)
+        ktu = self._kg_table_update
+        fused = None
+        if ktu.pending is not None:
+            if (row_ranges and id(ktu.param) in row_ranges) or ktu.param.grad is not None:
+                ktu.materialize()
+            else:
+                fused = {id(ktu.param): ktu.launch()}
+        self._kg_optimizer.step(row_ranges, fused=fused)
         self._kg_optimizer.zero_grad()
 
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:
         if mode != KGATMode.PREDICT:
-            # a deferred table gradient refers to this step's hop buffers and A's values: a new
-            # backward or an attention refresh would change them
+            # a deferred table gradient refers to this step's hop buffers and A's values (CF) or
+            # holds the batch-row map (KG): a new backward or an attention refresh would change them
             self._table_update.materialize()
+            self._kg_table_update.materialize()
         if mode == KGATMode.TRAIN_CF:
             return self._calc_cf_loss(*args)
         if mode == KGATMode.TRAIN_KG:

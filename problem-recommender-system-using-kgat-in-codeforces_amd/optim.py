@@ -50,6 +50,11 @@ class FusedAdam:
         for p in self.params:
             launch = fused.get(id(p)) if fused else None
             if launch is not None:
+                if p.grad is not None:
+                    # the fused kernel computes the gradient itself and never reads .grad: a gradient
+                    # already there would be dropped without a trace
+                    raise RuntimeError("FusedAdam: a parameter stepped by a fused launch also has a .grad "
+                                       "(materialise the deferred gradient into it first)")
                 st, step_size, bc2s = self._advance(id(p), p.data)
                 launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps)
                 continue

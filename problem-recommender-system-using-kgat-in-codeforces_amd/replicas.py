@@ -156,9 +156,11 @@ class ShardedGradSync:
         """All-gather this step's (hop flag, layer-0 hop count) early -- from the forward, when the
         hop set is known before the propagation (model._early_first_hop) -- and start copying the
         result to the host; _agree then reads it without stalling the GPU queue."""
-        if self._announced is not None:
-            raise RuntimeError("ShardedGradSync: a TRAIN_CF forward whose backward never ran (the replicas' "
-                               "exchange of that step is still open)")
+        # A grad-enabled TRAIN_CF forward whose backward never ran (a loss only logged) left its
+        # announcement open.  Every rank runs the same program, so every rank dropped the same
+        # forward and made the same all-gather: the stale announcement is simply discarded.  That
+        # forward's own backward cannot run later -- model._mark_batch marked its token stale.
+        self._announced = None
         both = self._gather_info(sparse, count, count.device)
         host = torch.empty(tuple(both.shape), dtype=torch.int32, pin_memory=True)
         host.copy_(both, non_blocking=True)

@@ -2,41 +2,50 @@
 
 A table of 50M x 256 fp32 rows plus two Adam states does not fit one GPU, so
 rank k owns a contiguous row range [lo_k, hi_k) of every node table (X0, H1,
-..., HL, the side S_l) and the same rows of the attentive matrix A.  Its rows
-of A are cut by source shard into CSR blocks A[k][j] (columns rebased to shard
-j) and their transposes.
+..., HL, the side S_l).  It holds the same rows of the attentive matrix A
+(``A_loc``: its rows, global column ids) and of its transpose (``AT_loc``:
+rows [lo_k, hi_k) of A^T -- the in-edges of its nodes, global column ids).
 
-Forward, per layer (ring all-gather, pipelined):
-    S_k = sum_j A[k][j] . X_j      X_j travels the ring k -> k+1 while rank k
-                                    multiplies the block it holds
-    H_k = biinter(X_k, S_k)        row-local
-Backward, per layer (ring reduce-scatter, fused):
-    dX_j = dXd_j + sum_k A[k][j]^T . dS_k
-    the partial for owner j starts at rank j+1, gains each rank's
-    A[k][j]^T . dS_k on its way round the ring and ends at j -- one fixed
-    summation order (deterministic); the last layer uses the batch frontier
-    (masked SpMM), as the single-GPU path does.
-The BPR loss is taken over the GLOBAL batch (every rank's pairs, as data-
-parallel training would): the batch rows are assembled on every rank by one
-exact all-reduce (each row has exactly one owner, the others add zeros), every
-rank evaluates the same loss, and each scatters the row gradients into the rows
-it owns.  Aggregator weight gradients are all-reduced (each rank holds the
-contribution of its rows); relation / trans gradients of the KG step are
-already identical on every rank.  Adam runs on the local shard + replicas.
+Forward, per layer (aggregator.py:54-65):
+    Xg   = every rank's rows of X_l   all-peer gather (one P2P send + receive per peer,
+                                      all in flight together: on a fully connected xGMI
+                                      node each peer pair has its own link), in column
+                                      chunks so chunk c+1 is on the wire while chunk c's
+                                      product runs
+    S_k  = A_loc . Xg                 the single-GPU SpMM on the local rows: per row the
+                                      same edges in the same order as one GPU -- bit for bit
+    H_k  = biinter(X_k, S_k)          row-local
+Backward ("pull": the transpose of the forward, no reduce-scatter):
+    last layer: dS is nonzero on the global batch rows only.  Each rank computes the
+      bi-interaction backward of the batch rows it owns; one exact all-reduce (one owner per
+      row, zeros elsewhere) gives every rank the compact [dS | dXd] rows of the whole batch;
+      dX_k = AT_loc . dS (masked to the batch rows) + dXd -- kgat_spmm_csr_masked_ex_f32
+    lower layers: dSg = all-peer gather of dS_l; dX_k = dXd_k + AT_loc . dSg
+  Per output row the single-GPU backward's edges in its order, so the table gradient is the
+  single GPU's bit for bit; only the aggregator weight gradients (per-rank partial sums,
+  all-reduced) are summed in another order.
+The BPR loss is taken over the GLOBAL batch (every rank's pairs, as data-parallel
+training would): the batch rows are assembled on every rank by one exact all-reduce,
+every rank evaluates the same loss, and each keeps the row gradients of the rows it
+owns.  Relation / trans gradients of the KG step are already identical on every rank.
+Adam runs on the local shard + replicas.
 
-Transport: RCCL point-to-point (``dist.batch_isend_irecv``) and collectives
-on device buffers; with a non-NCCL backend (gloo, used to run several ranks on
-one test GPU) buffers are staged through host memory.  All arithmetic is the
-HIP kernels of libkgat_hip.so.
+Wire bytes per rank and layer: (G-1)/G of the layer input table forward and of the
+layer's dS backward (DESIGN.md §6 has the per-step budget at G = 8).
 
-Attention refresh (UPDATE_ATTENTION): rank k scores the edges of its rows; the
-X0 shards travel the same ring and each arriving shard scores the local edges
-whose tail it holds; logits are soft-maxed over the local CSR rows and
-gathered back into the blocks and their transposes.
+Transport: ``Comm`` (torch.distributed; RCCL point-to-point on device buffers, or gloo
+staged through host memory to run several ranks on one test GPU) or comm.RcclComm (the
+library's own kgat_comm_allgatherv / kgat_comm_alltoallv).  All arithmetic is the HIP
+kernels of libkgat_hip.so.
+
+Attention refresh (UPDATE_ATTENTION, model.py:318-366): the X0 shards are gathered, rank k
+scores the edges of its rows, soft-maxes them over its local CSR rows (A_loc's values), and
+an all-to-all moves each refreshed value to the owner of its A^T row (AT_loc's values).
 """
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -49,21 +58,25 @@ from .graph import GraphLayout, RefreshPlan, _DeviceCSR, degree_weights, stream_
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
 from .optim import FusedAdam
 
+# columns per gathered chunk: chunk c+1 travels while chunk c's SpMM runs (a 256-wide layer in four
+# 64-wide chunks; per output element the sum is the unchunked one, the chunk only splits columns)
+GATHER_CHUNK = int(os.environ.get("KGAT_SHARD_CHUNK", "64"))
+
 
 # ---------------------------------------------------------------- transport
 class _Pending:
-    def __init__(self, works, host_recv=None, recv=None):
-        self._works, self._host_recv, self._recv = works, host_recv, recv
+    def __init__(self, works, copies=()):
+        self._works, self._copies = works, copies
 
     def wait(self) -> None:
         for w in self._works:
             w.wait()
-        if self._host_recv is not None:
-            self._recv.copy_(self._host_recv)
+        for dst, src in self._copies:
+            dst.copy_(src)
 
 
 class Comm:
-    """Ring + collectives over a torch.distributed group (rank k sends to k+1, receives from k-1)."""
+    """Collectives over a torch.distributed group for the row-sharded model."""
 
     def __init__(self, group=None, host_staged: bool | None = None, force: bool = False):
         """``force``: collectives run even on a world of one rank (tests: RCCL at world 1)."""
@@ -73,22 +86,86 @@ class Comm:
         self.world = dist.get_world_size(group)
         backend = dist.get_backend(group)
         self.host = (backend != "nccl") if host_staged is None else host_staged
-        to_global = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
-        self.next = to_global((self.rank + 1) % self.world)
-        self.prev = to_global((self.rank - 1) % self.world)
+        self._glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+        self.next = self._glob((self.rank + 1) % self.world)
+        self.prev = self._glob((self.rank - 1) % self.world)
+
+    @property
+    def active(self) -> bool:
+        """Collectives move data (more than one rank, or forced at world 1)."""
+        return self.world > 1 or self.force
 
     def exchange(self, send: torch.Tensor, recv: torch.Tensor) -> _Pending:
         """Start: send -> next rank, prev rank -> recv.  wait() completes both."""
         if self.host:
             s, r = send.detach().cpu(), torch.empty(recv.shape, dtype=recv.dtype)
             ops = [dist.P2POp(dist.isend, s, self.next, self.group), dist.P2POp(dist.irecv, r, self.prev, self.group)]
-            return _Pending(dist.batch_isend_irecv(ops), r, recv)
+            return _Pending(dist.batch_isend_irecv(ops), [(recv, r)])
         ops = [dist.P2POp(dist.isend, send, self.next, self.group),
                dist.P2POp(dist.irecv, recv, self.prev, self.group)]
         return _Pending(dist.batch_isend_irecv(ops))
 
+    def gather_v(self, send: torch.Tensor, out: torch.Tensor, bounds) -> _Pending:
+        """Start the all-peer gather: rank r's rows land in out[bounds[r]:bounds[r+1]] on every rank
+        (send = this rank's rows; it may be that slice of ``out`` itself).  One send and one receive
+        per peer, all in one batch."""
+        lo, hi = int(bounds[self.rank]), int(bounds[self.rank + 1])
+        own = out[lo:hi]
+        if send.data_ptr() != own.data_ptr():
+            own.copy_(send)
+        if not self.active or self.world == 1:
+            return _Pending([])
+        peers = [r for r in range(self.world) if r != self.rank]
+        if self.host:
+            s = own.detach().cpu()
+            bufs = {r: torch.empty((int(bounds[r + 1]) - int(bounds[r]), *out.shape[1:]), dtype=out.dtype)
+                    for r in peers}
+            ops = []
+            for r in peers:
+                if s.shape[0]:
+                    ops.append(dist.P2POp(dist.isend, s, self._glob(r), self.group))
+                if bufs[r].shape[0]:
+                    ops.append(dist.P2POp(dist.irecv, bufs[r], self._glob(r), self.group))
+            works = dist.batch_isend_irecv(ops) if ops else []
+            return _Pending(works, [(out[int(bounds[r]):int(bounds[r + 1])], bufs[r]) for r in peers
+                                    if bufs[r].shape[0]])
+        ops = []
+        for r in peers:
+            if hi > lo:
+                ops.append(dist.P2POp(dist.isend, own, self._glob(r), self.group))
+            a, b = int(bounds[r]), int(bounds[r + 1])
+            if b > a:
+                ops.append(dist.P2POp(dist.irecv, out[a:b], self._glob(r), self.group))
+        return _Pending(dist.batch_isend_irecv(ops) if ops else [])
+
+    def all_to_all_v(self, send: torch.Tensor, send_off, recv: torch.Tensor, recv_off) -> None:
+        """send[send_off[p]:send_off[p+1]] -> rank p; rank p's block -> recv[recv_off[p]:recv_off[p+1]]
+        (1-D tensors, element offsets); completes before returning."""
+        k = self.rank
+        recv[int(recv_off[k]):int(recv_off[k + 1])].copy_(send[int(send_off[k]):int(send_off[k + 1])])
+        if not self.active or self.world == 1:
+            return
+        peers = [r for r in range(self.world) if r != k]
+        src = send.detach().cpu() if self.host else send
+        dst = torch.empty(recv.shape, dtype=recv.dtype) if self.host else recv
+        ops = []
+        for r in peers:
+            a, b = int(send_off[r]), int(send_off[r + 1])
+            if b > a:
+                ops.append(dist.P2POp(dist.isend, src[a:b], self._glob(r), self.group))
+            a, b = int(recv_off[r]), int(recv_off[r + 1])
+            if b > a:
+                ops.append(dist.P2POp(dist.irecv, dst[a:b], self._glob(r), self.group))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        if self.host:
+            for r in peers:
+                a, b = int(recv_off[r]), int(recv_off[r + 1])
+                if b > a:
+                    recv[a:b].copy_(dst[a:b])
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1 and not self.force:
+        if not self.active:
             return t
         if self.host:
             c = t.detach().cpu()
@@ -100,7 +177,7 @@ class Comm:
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape], rank order."""
-        if self.world == 1 and not self.force:
+        if not self.active:
             return t.unsqueeze(0)
         if self.host:
             c = t.detach().cpu().contiguous()
@@ -124,112 +201,144 @@ def shard_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
     return np.maximum.accumulate(b)
 
 
-class RowShard:
-    """Rank k's rows of A, cut by source shard: blocks[j] = A[k][j], blocks_t[j] = A[k][j]^T.
+def _transpose_rows(rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, lo: int, hi: int):
+    """Rows [lo, hi) of the transpose of a whole CSR: (rowptr from 0, col int32, val fp32) with the
+    columns of each row ascending (graph.DeviceGraph's CSR(A^T) order)."""
+    n = rowptr.size - 1
+    col = np.asarray(col)
+    sel = np.flatnonzero((col >= lo) & (col < hi))
+    rows = np.searchsorted(rowptr, sel, side="right") - 1          # source row of each kept entry
+    order = np.lexsort((rows, col[sel]))
+    tr = col[sel][order].astype(np.int64) - lo
+    rp = np.zeros(hi - lo + 1, np.int64)
+    np.cumsum(np.bincount(tr, minlength=hi - lo), out=rp[1:])
+    del n
+    return rp, rows[order].astype(np.int32), np.asarray(val, np.float32)[sel][order]
 
-    ``local=False``: rowptr / col / val are the whole CSR (every rank holds the graph).
-    ``local=True``: they are this rank's rows only -- rowptr [hi-lo+1] from 0, global column
-    ids (graph.HashedCKG.shard: the C4/C5 sizes, where no rank holds the whole graph)."""
+
+class RowShard:
+    """Rank k's rows of A (``A``: local rows, global columns) and of A^T (``AT``).
+
+    ``local=False``: rowptr / col / val are the whole CSR (every rank holds the graph; the
+    transpose rows are cut from it).  ``local=True``: they are this rank's rows only (rowptr
+    [hi-lo+1] from 0, global column ids) and ``transpose`` = (rowptr, col, val) of its rows of A^T
+    (graph.HashedCKG.shard(lo, hi, transpose=True): the C4/C5 sizes, where no rank holds the
+    whole graph)."""
 
     def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, bounds: np.ndarray, rank: int, device,
-                 local: bool = False):
+                 local: bool = False, transpose=None):
         self.bounds = np.asarray(bounds, np.int64)
         self.rank, self.world = rank, self.bounds.size - 1
         lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.lo, self.hi, self.n = lo, hi, hi - lo
         self.n_nodes = int(self.bounds[-1])
         self.sizes = np.diff(self.bounds)
+        self.device = torch.device(device)
         if local:
             if rowptr.size != self.n + 1:
                 raise ValueError(f"local rowptr has {rowptr.size - 1} rows, shard {rank} has {self.n}")
+            if transpose is None:
+                raise ValueError("local rows need their rows of A^T too (transpose=)")
             lrp = np.asarray(rowptr, np.int64) - int(rowptr[0])
             e0, e1 = int(rowptr[0]), int(rowptr[-1])
+            trp, tcol, tval = transpose
+            trp = np.asarray(trp, np.int64) - int(trp[0])
         else:
             lrp = np.asarray(rowptr[lo:hi + 1], np.int64) - int(rowptr[lo])
             e0, e1 = int(rowptr[lo]), int(rowptr[hi])
-        lrow = np.repeat(np.arange(self.n, dtype=np.int32), np.diff(lrp))
-        lcol = np.asarray(col[e0:e1])
+            trp, tcol, tval = _transpose_rows(rowptr, col, val, lo, hi)
+        lcol = np.ascontiguousarray(col[e0:e1], np.int32)
         lval = np.asarray(val[e0:e1], np.float32)
-        sid = (np.searchsorted(self.bounds, lcol, side="right") - 1).astype(np.int32)
-        # the local CSR (rows lo..hi, global columns): attention logits are soft-maxed here, then
-        # gathered into the blocks (block_pos) and their transposes (block_t_pos)
-        self.local_rowptr = torch.from_numpy(np.ascontiguousarray(lrp)).to(device)
-        self._lrow, self._lcol = lrow, lcol
-        self.local_val = torch.from_numpy(lval.copy()).to(device)
-        self.block_pos, self.block_t_pos = [], []
-        self.blocks, self.blocks_t, self.nnz = [], [], []
-        for j in range(self.world):
-            pos = np.flatnonzero(sid == j)
-            r, c, v = lrow[pos], (lcol[pos] - self.bounds[j]).astype(np.int32), lval[pos]
-            nj = int(self.sizes[j])
-            rp = np.zeros(self.n + 1, np.int64)
-            np.cumsum(np.bincount(r, minlength=self.n), out=rp[1:])
-            self.blocks.append(_DeviceCSR(rp, c, torch.from_numpy(v.copy()).to(device), device))
-            order = np.lexsort((r, c))
-            self.block_pos.append(torch.from_numpy(pos.astype(np.int32)).to(device))
-            self.block_t_pos.append(torch.from_numpy(pos[order].astype(np.int32)).to(device))
-            rpt = np.zeros(nj + 1, np.int64)
-            np.cumsum(np.bincount(c, minlength=nj), out=rpt[1:])
-            self.blocks_t.append(_DeviceCSR(rpt, r[order], torch.from_numpy(v[order].copy()).to(device), device))
-            self.nnz.append(int(pos.size))
-            del pos, r, c, v, order
+        self._lrp, self._lcol = lrp, lcol
+        self._trp, self._tcol = trp, np.ascontiguousarray(tcol, np.int32)
+        self.A = _DeviceCSR(lrp, lcol, torch.from_numpy(lval.copy()).to(self.device), self.device)
+        self.AT = _DeviceCSR(trp, self._tcol, torch.from_numpy(np.asarray(tval, np.float32).copy()).to(self.device),
+                             self.device)
+        self.nnz = int(lcol.size)
+        # the local CSR's row pointers / values under the names the attention refresh uses
+        self.local_rowptr = self.A.rowptr
+        self.local_val = self.A.val
+        # node -> compact batch row of the last layer's masked backward (-1 between steps)
+        self.node_map = torch.full((self.n_nodes,), -1, dtype=torch.int32, device=self.device)
+        self._ident = None
+
+    def ident(self, n: int) -> torch.Tensor:
+        """int32 [0, n) on the device (row list of the pack copies)."""
+        if self._ident is None or self._ident.numel() < n:
+            self._ident = torch.arange(max(n, self.n, 1), dtype=torch.int32, device=self.device)
+        return self._ident[:n]
 
     @property
     def local_keys(self) -> np.ndarray:
         """row * n_nodes + col of the local CSR entries (row-major sorted; attention refresh only)."""
         k = self.__dict__.get("_keys")
         if k is None:
-            k = self._keys = self._lrow.astype(np.int64) * self.n_nodes + self._lcol.astype(np.int64)
+            lrow = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self._lrp))
+            k = self._keys = lrow * self.n_nodes + self._lcol.astype(np.int64)
         return k
 
-
-def ring_visit(shard: RowShard, comm: Comm, X: torch.Tensor, visit) -> None:
-    """Ring all-gather of the row shards X_j (k -> k+1): visit(j, X_j) runs on each shard while the
-    next one is in flight."""
-    G, k, d = comm.world, comm.rank, X.shape[1]
-    buf = X.contiguous()
-    for s in range(G):
-        j = (k - s) % G
-        pend = None
-        if s < G - 1:
-            nxt = torch.empty(int(shard.sizes[(j - 1) % G]), d, dtype=torch.float32, device=X.device)
-            pend = comm.exchange(buf, nxt)
-        visit(j, buf)
-        if pend is not None:
-            pend.wait()
-            buf = nxt
-
-
-def ring_spmm(shard: RowShard, comm: Comm, X: torch.Tensor) -> torch.Tensor:
-    """S_k = sum_j A[k][j] . X_j with X_j arriving over the ring (all-gather pipelined with the SpMM)."""
-    S = torch.empty(shard.n, X.shape[1], dtype=torch.float32, device=X.device)
-    first = [True]
-
-    def visit(j, buf):
-        kernels.spmm_block(shard.blocks[j], buf, S, accumulate=not first[0])
-        first[0] = False
-
-    ring_visit(shard, comm, X, visit)
-    return S
+    def value_plan(self):
+        """The refresh's value exchange (built once): A_loc entries whose column lies in shard j, in
+        (column, row) order, go to rank j, where they are exactly its AT rows' entries from shard k in
+        CSR order.  Returns (send_pos int32 [nnz], send_off [G+1], recv_inv int32 [nnz], recv_off [G+1])
+        with AT.val = recv[recv_inv]."""
+        plan = self.__dict__.get("_vplan")
+        if plan is not None:
+            return plan
+        lrow = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self._lrp))
+        order = np.lexsort((lrow, self._lcol))                        # by column, then row
+        sid = np.searchsorted(self.bounds, self._lcol[order], side="right") - 1
+        send_off = np.zeros(self.world + 1, np.int64)
+        np.cumsum(np.bincount(sid, minlength=self.world), out=send_off[1:])
+        tsid = np.searchsorted(self.bounds, self._tcol, side="right") - 1
+        recv_order = np.argsort(tsid, kind="stable")                   # grouped by source shard, CSR order
+        recv_off = np.zeros(self.world + 1, np.int64)
+        np.cumsum(np.bincount(tsid, minlength=self.world), out=recv_off[1:])
+        recv_inv = np.empty(recv_order.size, np.int64)
+        recv_inv[recv_order] = np.arange(recv_order.size)
+        dev = self.device
+        plan = (torch.from_numpy(order.astype(np.int32)).to(dev), send_off,
+                torch.from_numpy(recv_inv.astype(np.int32)).to(dev), recv_off)
+        self._vplan = plan
+        return plan
 
 
-def ring_spmm_t(shard: RowShard, comm: Comm, d: int, device, block_product) -> torch.Tensor:
-    """dX_k = sum_r A[r][k]^T . dS_r: a ring reduce-scatter whose partial for owner j gains
-    block_product(A[k][j]^T, out) at every rank it passes."""
-    G, k = comm.world, comm.rank
-    pend, recv = None, None
-    for s in range(G):
-        j = (k - 1 - s) % G
-        part = torch.empty(int(shard.sizes[j]), d, dtype=torch.float32, device=device)
-        block_product(shard.blocks_t[j], part)
-        if pend is not None:
-            pend.wait()
-            kernels.add_(part, recv)
-        if s == G - 1:
-            return part
-        recv = torch.empty(int(shard.sizes[(j - 1) % G]), d, dtype=torch.float32, device=device)
-        pend = comm.exchange(part, recv)
-    raise AssertionError("unreachable")
+def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+                  transpose: bool = False) -> torch.Tensor:
+    """out (+)= csr . Xg, Xg = [N, d] every rank's rows of X (all-peer gather), csr = shard.A (forward)
+    or shard.AT (backward).  Column chunks of GATHER_CHUNK: chunk c+1 is on the wire while chunk c's
+    product runs; each product is the single-GPU kernel on the local rows."""
+    n, d = X.shape
+    if not comm.active:  # one rank: X is the whole table
+        return kernels.spmm_block(csr, X, out, accumulate=accumulate, transpose=transpose)
+    w = min(d, GATHER_CHUNK) if GATHER_CHUNK > 0 else d
+    chunks = [(c, min(c + w, d)) for c in range(0, d, w)]
+    N, lo, hi = shard.n_nodes, shard.lo, shard.hi
+
+    def start(c0, c1):
+        buf = torch.empty(N, c1 - c0, dtype=torch.float32, device=X.device)
+        own = buf[lo:hi]
+        if hi > lo:
+            kernels.gather_rows(X[:, c0:c1], shard.ident(n), out=own)  # pack this rank's columns
+        return buf, comm.gather_v(own, buf, shard.bounds)
+
+    nxt = start(*chunks[0])
+    for i, (c0, c1) in enumerate(chunks):
+        buf, pend = nxt
+        if i + 1 < len(chunks):
+            nxt = start(*chunks[i + 1])
+        pend.wait()
+        kernels.spmm_block(csr, buf, out[:, c0:c1], accumulate=accumulate, transpose=transpose)
+    return out
+
+
+def gather_table(shard: RowShard, comm, X: torch.Tensor) -> torch.Tensor:
+    """[N, d]: every rank's rows of X (the refresh's edge scorer reads whole rows)."""
+    if not comm.active:
+        return X
+    buf = torch.empty(shard.n_nodes, X.shape[1], dtype=torch.float32, device=X.device)
+    comm.gather_v(X.contiguous(), buf, shard.bounds).wait()
+    return buf
 
 
 # ---------------------------------------------------------------- batch rows
@@ -240,6 +349,7 @@ class _BatchRows:
         uniq, inv = np.unique(ids, return_inverse=True)
         self.n = uniq.size
         self.inv = inv.astype(np.int64)
+        self.uniq = torch.from_numpy(uniq.astype(np.int32)).to(device)   # compact -> global id
         owned = (uniq >= lo) & (uniq < hi)
         self.local_np = np.where(owned, uniq - lo, -1).astype(np.int32)
         self.local = torch.from_numpy(self.local_np).to(device)          # compact -> local row or -1
@@ -248,11 +358,13 @@ class _BatchRows:
         # never empty: a -1 row is padding every kernel reads as zero and writes nowhere
         fr = self.frontier_np if self.n_frontier else np.full(1, -1, np.int32)
         self.frontier = torch.from_numpy(fr.copy()).to(device)
+        oc = np.flatnonzero(owned).astype(np.int32)
+        self.owned_compact = torch.from_numpy(oc if oc.size else np.full(1, -1, np.int32)).to(device)
         pos = np.full(self.n, -1, np.int32)
         pos[owned] = np.arange(int(owned.sum()), dtype=np.int32)
         self.pos = torch.from_numpy(pos).to(device)                       # compact -> frontier position or -1
 
-    def gather(self, tables: list[torch.Tensor], comm: Comm) -> list[torch.Tensor]:
+    def gather(self, tables: list[torch.Tensor], comm) -> list[torch.Tensor]:
         """Every rank gets the compact rows of every table (exact: one owner per row)."""
         widths = [t.shape[1] for t in tables]
         R = torch.empty(self.n, sum(widths), dtype=torch.float32, device=tables[0].device)
@@ -276,7 +388,8 @@ class _ShardedCFLoss(torch.autograd.Function):
         x = X0
         for l in range(len(drops)):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
-            s = ring_spmm(shard, comm, x)
+            s = torch.empty(shard.n, x.shape[1], dtype=torch.float32, device=x.device)
+            gathered_spmm(shard, comm, shard.A, x, s)
             st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
             x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             sides.append(s)
@@ -310,29 +423,32 @@ class _ShardedCFLoss(torch.autograd.Function):
                 off += g.numel()
             wgrads[4 * l: 4 * l + 4] = out
 
-        # ---- last layer on the owned batch frontier
+        # ---- last layer: the bi-interaction backward on the batch rows this rank owns
         l = L - 1
+        din = tables[l].shape[1]
         dHc = kernels.zeros((rows.frontier.numel(), tables[L].shape[1]), dev)
         kernels.bpr_bwd(Tc, L, cu, cp, cn, reg, coef, gout, dHc, row_map=rows.pos)
         dXdc, dSc, *g = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4], drops[l], seeds[l],
                                             rows=rows.frontier, **saved(l))
         reduce_w(l, g)
-        node_map = torch.full((shard.n,), -1, dtype=torch.int32, device=dev)
+        # every rank's [dS | dXd] batch rows, compact (one exact all-reduce: one owner per row)
+        P = kernels.zeros((rows.n, 2 * din), dev)
         if rows.n_frontier:
-            node_map[rows.frontier.long()] = torch.arange(rows.n_frontier, dtype=torch.int32, device=dev)
-        dX = ring_spmm_t(shard, comm, tables[l].shape[1], dev,
-                         lambda blk, out: kernels.spmm_block_masked(blk, node_map, dSc, out))
-        kernels.scatter_rows(dX, rows.frontier, dXdc, accumulate=True)
+            kernels.scatter_rows(P[:, :din], rows.owned_compact, dSc[:rows.n_frontier], accumulate=False)
+            kernels.scatter_rows(P[:, din:], rows.owned_compact, dXdc[:rows.n_frontier], accumulate=False)
+        comm.all_reduce_(P)
+        _lib.call("kgat_map_build", rows.uniq.data_ptr(), rows.n, shard.node_map.data_ptr(), stream_ptr(dev))
+        dX = torch.empty(shard.n, din, dtype=torch.float32, device=dev)
+        kernels.spmm_block_masked(shard.AT, shard.node_map, P[:, :din], dX, Yc_init=P[:, din:], row0=shard.lo)
+        kernels.frontier_reset(rows.uniq, shard.node_map)
         kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dX, row_map=rows.local)
-        # ---- remaining layers densely
+        # ---- remaining layers densely: dX_l = dXd + AT_loc . (every rank's dS)
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             dXd, dS, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], **saved(l))
             reduce_w(l, g)
-            ring = ring_spmm_t(shard, comm, tables[l].shape[1], dev,
-                               lambda blk, out, dS=dS: kernels.spmm_block(blk, dS, out, transpose=True))
-            kernels.add_(dXd, ring)
             kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dXd, row_map=rows.local)
+            gathered_spmm(shard, comm, shard.AT, dS, dXd, accumulate=True, transpose=True)
             dX = dXd
         ctx.saved = None
         return (None, None, None, None, dX, *wgrads)
@@ -365,11 +481,11 @@ class _ShardedKGLoss(torch.autograd.Function):
 class RowShardedKGAT(nn.Module):
     """KGAT with the node tables row-sharded over the ranks of ``comm``.
 
-    Same modes as KGAT (model.py:421-431) for TRAIN_CF, TRAIN_KG and PREDICT; each
-    rank passes ITS OWN batch and the loss is the mean over the global batch.
+    Same modes as KGAT (model.py:421-431) for TRAIN_CF, TRAIN_KG, UPDATE_ATTENTION and
+    PREDICT; each rank passes ITS OWN batch and the loss is the mean over the global batch.
     """
 
-    def __init__(self, args: KGATArgs, layout: GraphLayout | None, comm: Comm, device,
+    def __init__(self, args: KGATArgs, layout: GraphLayout | None, comm, device,
                  bounds: np.ndarray | None = None, shard: RowShard | None = None):
         """``layout``: the whole graph (every rank slices its rows); or ``shard``: this rank's
         rows already built (graph.HashedCKG at C5 size, where no rank holds the whole graph)."""
@@ -451,7 +567,8 @@ class RowShardedKGAT(nn.Module):
             x = self._user_entity_embedding_shard.detach()
             tables = [x]
             for l, agg in enumerate(self._aggregator_layers):
-                s = ring_spmm(self.shard, self.comm, x)
+                s = torch.empty(self.shard.n, x.shape[1], dtype=torch.float32, device=x.device)
+                gathered_spmm(self.shard, self.comm, self.shard.A, x, s)
                 x = kernels.biinter_fwd(x, s, *[w.detach() for w in agg.weights()], drops[l], seeds[l])
                 tables.append(x)
         return tables
@@ -480,8 +597,8 @@ class RowShardedKGAT(nn.Module):
                                     self._relation_embedding.weight, self._trans_matrix)
 
     def _refresh_plan(self, h: np.ndarray, r: np.ndarray, t: np.ndarray):
-        """Per source shard j: a scoring plan over this rank's edges whose tail lies in shard j
-        (tails rebased into X_j), logits landing by local edge id; slot sums onto the local CSR."""
+        """One scoring plan over this rank's edges (tails: global rows of the gathered X0), logits
+        landing by local edge id; slot sums onto the local CSR."""
         key = (h.size, h.tobytes()[:64], r.tobytes()[:64], t.tobytes()[:64], int(h.sum()), int(t.sum()))
         cached = getattr(self, "_att_plan", None)
         if cached is not None and cached[0] == key:
@@ -499,25 +616,21 @@ class RowShardedKGAT(nn.Module):
         if not ok.all() or not covered.all():
             raise NotImplementedError("row-sharded attention refresh needs the edge list of the sharded graph")
         eid = np.arange(hl.size, dtype=np.int64)
-        sid = np.searchsorted(sh.bounds, tl, side="right") - 1
-        plans = []
-        for j in range(sh.world):
-            m = sid == j
-            plans.append(RefreshPlan.for_edges(tl[m] - sh.bounds[j], rl[m], wl[m], eid[m], dev)
-                         if m.any() else None)
+        plan = RefreshPlan.for_edges(tl, rl, wl, eid, dev) if hl.size else None
         so = np.argsort(slot, kind="stable")
         slot_order = torch.from_numpy(so.astype(np.int32)).to(dev)
         slot_ptr = torch.from_numpy(np.searchsorted(slot[so], np.arange(sh.local_keys.size + 1)).astype(np.int64)).to(dev)
-        plan = (plans, slot_ptr, slot_order, int(hl.size))
-        self._att_plan = (key, plan)
-        return plan
+        out = (plan, slot_ptr, slot_order, int(hl.size))
+        self._att_plan = (key, out)
+        return out
 
     @torch.no_grad()
     def _update_attention(self, heads, relations, tails, relation_indices) -> None:
-        """UPDATE_ATTENTION (model.py:318-366) on this rank's rows: X0 shards pass on the ring, each
-        scores the local edges whose tail it holds; softmax over the local rows; blocks refreshed."""
+        """UPDATE_ATTENTION (model.py:318-366) on this rank's rows: the X0 shards are gathered, the local
+        edges scored and soft-maxed over the local rows (A_loc's values); an all-to-all hands every
+        refreshed value to the owner of its A^T row (AT_loc's values)."""
         h, r, t = (torch.as_tensor(x).cpu().numpy().astype(np.int64) for x in (heads, relations, tails))
-        plans, slot_ptr, slot_order, n_edges = self._refresh_plan(h, r, t)
+        plan, slot_ptr, slot_order, n_edges = self._refresh_plan(h, r, t)
         sh, dev = self.shard, self._user_entity_embedding_shard.device
         mha = self._multi_head_attention
         p = mha.dropout if self.training else 0.0
@@ -527,24 +640,28 @@ class RowShardedKGAT(nn.Module):
                                                 mha._output.weight, mha._output.bias, mha._layer_norm.weight,
                                                 mha._layer_norm.bias)]
         logits = torch.empty(max(n_edges, 1), dtype=torch.float32, device=dev)
-
-        def visit(j, buf):
-            if plans[j] is not None:
-                kernels.score_edges(plans[j], buf, *W, logits, p, seed)
-
-        ring_visit(sh, self.comm, self._user_entity_embedding_shard.detach(), visit)
-        nnz = sh.local_keys.size
+        Xg = gather_table(sh, self.comm, self._user_entity_embedding_shard.detach())
+        if plan is not None:
+            kernels.score_edges(plan, Xg, *W, logits, p, seed)
+        del Xg
+        nnz = sh.nnz
         slot_logits = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
         st = stream_ptr(dev)
         _lib.call("kgat_slot_sum_f32", slot_ptr.data_ptr(), slot_order.data_ptr(), nnz, logits.data_ptr(),
                   slot_logits.data_ptr(), st)
-        _lib.call("kgat_row_softmax_f32", sh.local_rowptr.data_ptr(), sh.n, slot_logits.data_ptr(),
-                  sh.local_val.data_ptr(), st)
-        for j in range(sh.world):
-            for blk, pos in ((sh.blocks[j], sh.block_pos[j]), (sh.blocks_t[j], sh.block_t_pos[j])):
-                if pos.numel():
-                    _lib.call("kgat_gather_f32", sh.local_val.data_ptr(), pos.data_ptr(), pos.numel(),
-                              blk.val.data_ptr(), st)
+        A = sh.A
+        _lib.call("kgat_row_softmax_ex_f32", A.rowptr.data_ptr(), sh.n, A.long_rows.data_ptr(), A.n_long,
+                  slot_logits.data_ptr(), A.val.data_ptr(), st)
+        # A^T's rows live with the owners of A's columns: move the refreshed values there
+        send_pos, send_off, recv_inv, recv_off = sh.value_plan()
+        send = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+        if nnz:
+            _lib.call("kgat_gather_f32", A.val.data_ptr(), send_pos.data_ptr(), nnz, send.data_ptr(), st)
+        nt = int(recv_off[-1])
+        recv = torch.empty(max(nt, 1), dtype=torch.float32, device=dev)
+        self.comm.all_to_all_v(send, send_off, recv, recv_off)
+        if nt:
+            _lib.call("kgat_gather_f32", recv.data_ptr(), recv_inv.data_ptr(), nt, sh.AT.val.data_ptr(), st)
 
     @torch.no_grad()
     def _calc_score(self, user_ids, item_ids) -> torch.Tensor:

@@ -73,6 +73,9 @@ def main() -> None:
     close("cf loss", ls, lr, 1e-6)
     close("cf d table shard", m._user_entity_embedding_shard.grad, ref._user_entity_embedding.weight.grad[lo:hi],
           ATOL_GRAD)
+    # the pull backward sums every table-gradient row over the single GPU's edges in its order
+    exact = {"cf_table_grad": torch.equal(m._user_entity_embedding_shard.grad,
+                                          ref._user_entity_embedding.weight.grad[lo:hi])}
     for a, b in zip(m._cf_weights(), ref._cf_weights()):
         close("cf d aggregator", a.grad, b.grad, 1e-5)
     ref.update_cf_weights()
@@ -113,6 +116,21 @@ def main() -> None:
     m(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
     A = ref.graph().A
     close("refreshed A rows", m.shard.local_val, A.val[int(lay.rowptr[lo]):int(lay.rowptr[hi])], 1e-6)
+    with torch.no_grad():
+        tabs_s, tabs_r = m.propagate(), ref.propagate()
+    for l, (a, b) in enumerate(zip(tabs_s, tabs_r)):
+        close(f"propagated table {l}", a, b[lo:hi], 1e-5)
+    exact["tables"] = all(torch.equal(a, b[lo:hi]) for a, b in zip(tabs_s, tabs_r))
+    # a CF backward on the refreshed graph: A^T's local rows got their values by the all-to-all
+    m.load_full_state(ref.state_dict())
+    for mm in (ref, m):
+        mm.zero_grad(set_to_none=True)
+    ref(*allb, mode=pkg.KGATMode.TRAIN_CF).backward()
+    m(*mine, mode=pkg.KGATMode.TRAIN_CF).backward()
+    close("cf d table shard after refresh", m._user_entity_embedding_shard.grad,
+          ref._user_entity_embedding.weight.grad[lo:hi], ATOL_GRAD)
+    exact["cf_table_grad_after_refresh"] = torch.equal(m._user_entity_embedding_shard.grad,
+                                                       ref._user_entity_embedding.weight.grad[lo:hi])
     users = torch.arange(0, 50, device="cuda")
     items = torch.arange(0, 300, device="cuda")
     with torch.no_grad():
@@ -122,7 +140,8 @@ def main() -> None:
     if FAILURES:
         print(f"rank {rank}: " + "; ".join(FAILURES), flush=True)
     else:
-        print(f"sharded parity ok: rank {rank}/{world} rows [{lo}, {hi}) d={dim} layers={layers}", flush=True)
+        print(f"sharded parity ok: rank {rank}/{world} rows [{lo}, {hi}) d={dim} layers={layers} "
+              f"bit-identical {exact}", flush=True)
     dist.destroy_process_group()
     sys.exit(1 if FAILURES else 0)
 

@@ -1511,6 +1511,61 @@ def test_fused_table_update_keeps_extra_table_gradient(pkg):
     p.grad = None
 
 
+@pytest.mark.parametrize("dim,batch", [(64, 512), (256, 300), (64, 2000)])
+def test_fused_kg_table_update_bit_identical(pkg, dim, batch):
+    """KGAT.fuse_kg_table_update (TransR's table rows written compactly,
+    kgat_transr_bwd_ex_f32, and the KG Adam stepping the table from them, kgat_adam_rows_f32)
+    against the dense backward + Adam: parameters and both KG Adam moments bit for bit over
+    alternating CF / KG steps (batches with repeated ids); a deferred KG gradient materialised on
+    demand equals the dense one.  B = 2000 exceeds the compact map's 4096 slots: the dense path
+    runs, same bits."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    R = len(lay.rel_order)
+    models = []
+    for fused in (False, True):
+        torch.manual_seed(2024)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=R, layer_size=[dim, dim // 2],
+                                  cf_embedding_dim=dim, kg_embedding_dim=dim, message_dropout=[0.1, 0.1]))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_kg_table_update = fused
+        models.append(m)
+    rng = np.random.default_rng(6)
+    for step in range(3):
+        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+        kg = [torch.from_numpy(rng.integers(0, hi, batch)).to(DEV) for hi in (U + E, R, U + E, U + E)]
+        kg[2][:7] = kg[0][:7]  # repeated ids across heads / tails: summed in slot order
+        for m in models:
+            torch.manual_seed(300 + step)
+            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            m.update_cf_weights()
+            m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
+            deferred = m._kg_table_update.pending is not None
+            assert deferred == (m.fuse_kg_table_update and 3 * batch <= 4096)
+            assert deferred == (m._user_entity_embedding.weight.grad is None)
+            m.update_kg_weights()
+    a, b = models
+    for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+    ta = a._kg_optimizer.state[id(a._user_entity_embedding.weight)]
+    tb = b._kg_optimizer.state[id(b._user_entity_embedding.weight)]
+    assert ta["step"] == tb["step"] == 3
+    assert torch.equal(ta["exp_avg"], tb["exp_avg"]) and torch.equal(ta["exp_avg_sq"], tb["exp_avg_sq"])
+    kg = [torch.from_numpy(rng.integers(0, hi, batch)).to(DEV) for hi in (U + E, R, U + E, U + E)]
+    grads = []
+    for m in models:
+        m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
+        m.materialize_table_grad()
+        grads.append(m._user_entity_embedding.weight.grad.detach().clone())
+        m.zero_grad(set_to_none=True)
+    assert torch.equal(grads[0], grads[1])
+    assert int((b._kg_table_update.node_map() >= 0).sum()) == 0  # the batch-row map is reset
+
+
 def test_device_id_error_raised_before_update(pkg):
     """a device-side id out of range raises at update_cf_weights, before the
     optimiser moves any parameter (the check's flag is waited for there)."""

@@ -39,7 +39,8 @@ def test_shard_bounds_cover_and_balance(world):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_row_shard_blocks_reassemble_A(world):
+def test_row_shard_reassembles_A_and_AT(world):
+    """Every rank's A rows (global columns) and A^T rows reassemble A and A^T, columns ascending."""
     n = 700
     rowptr, col, val = _random_csr(n, 9000, 7)
     dense = np.zeros((n, n), np.float32)
@@ -48,17 +49,15 @@ def test_row_shard_blocks_reassemble_A(world):
     b = sharded.shard_bounds(rowptr, world)
     for k in range(world):
         sh = sharded.RowShard(rowptr, col, val, b, k, "cpu")
-        assert sum(sh.nnz) == rowptr[b[k + 1]] - rowptr[b[k]]
-        for j in range(world):
-            for blk, t in ((sh.blocks[j], False), (sh.blocks_t[j], True)):
-                rp, cc, vv = blk.rowptr.numpy(), blk.col.numpy(), blk.val.numpy()
-                rr = np.repeat(np.arange(blk.n_rows), np.diff(rp))
-                m = np.zeros((sh.n, b[j + 1] - b[j]) if not t else (b[j + 1] - b[j], sh.n), np.float32)
-                m[rr, cc] = vv
-                want = dense[b[k]:b[k + 1], b[j]:b[j + 1]]
-                np.testing.assert_array_equal(m.T if t else m, want)
-                # rows sorted, columns sorted within a row (the reference's coalesced order)
-                assert np.all(np.diff(rr) >= 0)
+        assert sh.nnz == rowptr[b[k + 1]] - rowptr[b[k]]
+        for csr, want in ((sh.A, dense[b[k]:b[k + 1]]), (sh.AT, dense.T[b[k]:b[k + 1]])):
+            rp, cc, vv = csr.rowptr.numpy(), csr.col.numpy(), csr.val.numpy()
+            rr = np.repeat(np.arange(csr.n_rows), np.diff(rp))
+            m = np.zeros((sh.n, n), np.float32)
+            m[rr, cc] = vv
+            np.testing.assert_array_equal(m, want)
+            assert np.all(np.diff(rr) >= 0)
+            assert all(np.all(np.diff(cc[rp[r]:rp[r + 1]]) > 0) for r in range(csr.n_rows))
 
 
 def _rendezvous() -> str:
@@ -74,25 +73,37 @@ def _comm_worker(rank: int, world: int, port: int, q) -> None:
     try:
         comm = sharded.Comm()
         assert comm.host and comm.next == (rank + 1) % world and comm.prev == (rank - 1) % world
-        # ring: after world-1 hops every rank has seen every shard once, in ring order
+        # ring exchange (kept for the library transport's tests)
         buf = torch.full((3 + rank, 2), float(rank))
-        seen = [rank]
-        for s in range(world - 1):
-            src = (rank - s - 1) % world
-            nxt = torch.empty(3 + src, 2)
-            comm.exchange(buf, nxt).wait()
-            buf = nxt
-            seen.append(int(buf[0, 0].item()))
-            assert buf.shape[0] == 3 + src
+        nxt = torch.empty(3 + (rank - 1) % world, 2)
+        comm.exchange(buf, nxt).wait()
+        ring_ok = bool((nxt == float((rank - 1) % world)).all())
+        # all-peer gather of uneven shards (one rank owns no rows when world = 3)
+        sizes = [3, 0, 5][:world] if world == 3 else [4, 2]
+        bounds = np.concatenate([[0], np.cumsum(sizes)])
+        out = torch.full((int(bounds[-1]), 3), -1.0)
+        mine = torch.arange(sizes[rank] * 3, dtype=torch.float32).reshape(-1, 3) + 100 * rank
+        comm.gather_v(mine, out, bounds).wait()
+        want = torch.cat([torch.arange(sizes[r] * 3, dtype=torch.float32).reshape(-1, 3) + 100 * r for r in range(world)])
+        gather_ok = torch.equal(out, want)
+        # all-to-all with per-peer sizes: rank r sends (r + 1) * (p + 1) values to rank p
+        send_cnt = [(rank + 1) * (p + 1) for p in range(world)]
+        send_off = np.concatenate([[0], np.cumsum(send_cnt)])
+        send = torch.cat([torch.full((c,), float(10 * rank + p)) for p, c in enumerate(send_cnt)])
+        recv_cnt = [(p + 1) * (rank + 1) for p in range(world)]
+        recv_off = np.concatenate([[0], np.cumsum(recv_cnt)])
+        recv = torch.empty(int(recv_off[-1]))
+        comm.all_to_all_v(send, send_off, recv, recv_off)
+        a2a_ok = torch.equal(recv, torch.cat([torch.full((c,), float(10 * p + rank)) for p, c in enumerate(recv_cnt)]))
         red = comm.all_reduce_(torch.full((4,), float(rank + 1)))
         gat = comm.all_gather(torch.tensor([rank, 10 * rank]))
-        q.put((rank, seen, red.tolist(), gat.tolist()))
+        q.put((rank, ring_ok, gather_ok, a2a_ok, red.tolist(), gat.tolist()))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_comm_ring_and_collectives_gloo(world):
+def test_comm_collectives_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _rendezvous()
@@ -104,8 +115,8 @@ def test_comm_ring_and_collectives_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     total = float(sum(range(1, world + 1)))
-    for rank, seen, red, gat in res:
-        assert seen == [(rank - s) % world for s in range(world)]
+    for rank, ring_ok, gather_ok, a2a_ok, red, gat in res:
+        assert ring_ok and gather_ok and a2a_ok, (rank, ring_ok, gather_ok, a2a_ok)
         assert red == [total] * 4
         assert gat == [[r, 10 * r] for r in range(world)]
 
@@ -118,10 +129,11 @@ def _csr_dense(blk, n_cols):
     return m
 
 
-def _ring_worker(rank: int, world: int, port: str, q) -> None:
-    """Ring all-gather SpMM and ring reduce-scatter of sharded.py with TEST-ONLY dense stand-ins for
-    the three block kernels (the product path calls the HIP library; here only the ring's indexing
-    and ordering are under test)."""
+def _pull_worker(rank: int, world: int, port: str, q) -> None:
+    """The gathered SpMM of sharded.py (column-chunked all-peer gather + local-row product) forward
+    with A's rows and backward with A^T's rows, and the refresh's value exchange, with TEST-ONLY dense
+    stand-ins for the HIP kernels (the product path calls the HIP library; here only the gather's
+    chunking, offsets and ordering are under test)."""
     dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         n = 500
@@ -132,26 +144,20 @@ def _ring_worker(rank: int, world: int, port: str, q) -> None:
 
         class FakeKernels:
             @staticmethod
-            def spmm_block(blk, X, out, accumulate=False):
+            def spmm_block(blk, X, out, accumulate=False, transpose=False):
                 y = _csr_dense(blk, X.shape[0]) @ X
                 out.copy_(out + y if accumulate else y)
                 return out
 
             @staticmethod
-            def spmm_block_masked(blk, src_map, Xc, out):
-                X = torch.zeros(src_map.numel(), Xc.shape[1])
-                m = src_map >= 0
-                X[m] = Xc[src_map[m].long()]
-                out.copy_(_csr_dense(blk, X.shape[0]) @ X)
+            def gather_rows(src, rows, out=None):
+                out.copy_(src[rows.long()])
                 return out
-
-            @staticmethod
-            def add_(y, x):
-                y += x
-                return y
 
         real = sharded.kernels
         sharded.kernels = FakeKernels
+        old_chunk = sharded.GATHER_CHUNK
+        sharded.GATHER_CHUNK = 3  # 8 columns in chunks of 3, 3, 2
         try:
             g = torch.Generator().manual_seed(5)
             X = torch.randn(n, 8, generator=g)
@@ -160,44 +166,45 @@ def _ring_worker(rank: int, world: int, port: str, q) -> None:
             A = torch.zeros(n, n)
             A[torch.from_numpy(rows), torch.from_numpy(col.astype(np.int64))] = torch.from_numpy(val)
             lo, hi = sh.lo, sh.hi
-            S = sharded.ring_spmm(sh, comm, X[lo:hi].contiguous())
+            S = torch.empty(hi - lo, 8)
+            sharded.gathered_spmm(sh, comm, sh.A, X[lo:hi].contiguous(), S)
             fwd_ok = torch.allclose(S, (A @ X)[lo:hi], atol=1e-4)
-            # every rank holds its rows of G (= dS); the reduce-scatter returns (A^T G)[own rows]
-            T = sharded.ring_spmm_t(sh, comm, 8, "cpu",
-                                    lambda blk, out: FakeKernels.spmm_block(blk, G[lo:hi].contiguous(), out))
-            bwd_ok = torch.allclose(T, (A.T @ G)[lo:hi], atol=1e-4)
-            # frontier variant: only some local rows of G are nonzero (compact + src_map)
-            F = torch.arange(0, hi - lo, 3)
-            src_map = torch.full((hi - lo,), -1, dtype=torch.int32)
-            src_map[F] = torch.arange(F.numel(), dtype=torch.int32)
-            Gc = G[lo:hi][F].contiguous()
-            Tm = sharded.ring_spmm_t(sh, comm, 8, "cpu",
-                                     lambda blk, out: FakeKernels.spmm_block_masked(blk, src_map, Gc, out))
-            Gm = torch.zeros_like(G)
-            Gm[lo + F] = G[lo + F]
-            gathered = comm.all_gather(Gm)  # every rank's frontier rows
-            Gfull = gathered.sum(0)
-            mask_ok = torch.allclose(Tm, (A.T @ Gfull)[lo:hi], atol=1e-4)
+            T = torch.ones(hi - lo, 8)
+            sharded.gathered_spmm(sh, comm, sh.AT, G[lo:hi].contiguous(), T, accumulate=True, transpose=True)
+            bwd_ok = torch.allclose(T, 1.0 + (A.T @ G)[lo:hi], atol=1e-4)
+            # the refresh's value exchange: new values on A's rows reach A^T's rows of the owners
+            newA = A * 2.0 + 1.0 * (A != 0)
+            sh.A.val = newA[torch.from_numpy(np.repeat(np.arange(lo, hi), np.diff(sh._lrp))),
+                            torch.from_numpy(sh._lcol.astype(np.int64))].contiguous()
+            send_pos, send_off, recv_inv, recv_off = sh.value_plan()
+            send = sh.A.val[send_pos.long()]
+            recv = torch.empty(int(recv_off[-1]))
+            comm.all_to_all_v(send, send_off, recv, recv_off)
+            at_val = recv[recv_inv.long()]
+            at_rows = torch.from_numpy(np.repeat(np.arange(lo, hi), np.diff(sh._trp)))
+            want = newA.T[at_rows, torch.from_numpy(sh._tcol.astype(np.int64))]
+            val_ok = torch.equal(at_val, want)
         finally:
             sharded.kernels = real
-        q.put((rank, bool(fwd_ok), bool(bwd_ok), bool(mask_ok)))
+            sharded.GATHER_CHUNK = old_chunk
+        q.put((rank, bool(fwd_ok), bool(bwd_ok), bool(val_ok)))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_ring_spmm_and_reduce_scatter_gloo(world):
+def test_gathered_spmm_and_value_exchange_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _rendezvous()
-    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pull_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=180) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, f, b_, m in res:
-        assert f, f"rank {rank}: ring all-gather SpMM wrong"
-        assert b_, f"rank {rank}: ring reduce-scatter wrong"
-        assert m, f"rank {rank}: masked ring reduce-scatter wrong"
+    for rank, f, b_, v in res:
+        assert f, f"rank {rank}: gathered forward SpMM wrong"
+        assert b_, f"rank {rank}: gathered transposed SpMM wrong"
+        assert v, f"rank {rank}: refresh value exchange wrong"
