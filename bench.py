@@ -449,6 +449,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         return loss
 
     elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
+    exchange_steps = dict(sync.stats)  # the full-propagation run's table exchanges (warm-up + timed)
     ms = elapsed / args.steps * 1e3
     n, nnz, d0 = layout.n_nodes, layout.nnz, cfg["dim"]
     roof, spmm = roofline(events, args.config, n, nnz, d0, timed.instrumented,
@@ -466,15 +467,20 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         "host_launch_ms_per_step": timed.host_ms_per_step,
         "cpu_baseline": None,
     }
-    if world == 1 and L <= 2 and not args.no_frontier_leg and not args.exchange_at_1:
+    if L <= 2 and not args.no_frontier_leg and not args.exchange_at_1:
         # the same CF step with KGAT.frontier_forward (each layer's forward on the rows the loss can
         # reach only: same loss, gradients and updates bit for bit, tested) -- the training step as
-        # driver.py runs it; `value` above stays the full-propagation step
+        # driver.py runs it; `value` above stays the full-propagation step.  N > 1: the replicas'
+        # replicated hop-set exchange composes with it (both mark the same first hop before the
+        # propagation); its BPR pairs/s is the data-parallel training throughput.
         model.frontier_forward = True
+        before = dict(sync.stats)
         fel, _, _ = timed(step, batches, args.warmup, args.steps, world, dev)
         model.frontier_forward = False
+        fr_exchange = {k: v - before.get(k, 0) for k, v in sync.stats.items()}
         fms = fel / args.steps * 1e3
-        same = frontier_matches_full(model, pkg, batches[0])
+        # bit identity vs the full forward: checked here at N = 1 (and, with the exchange, in tests/dp_worker.py)
+        same = frontier_matches_full(model, pkg, batches[0]) if world == 1 else None
         est = getattr(model.graph(), "_hop_est", {}).get(0)  # pinned count of the last step's first hop
         result["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
@@ -482,12 +488,21 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
             "bit_identical_to_full": same,
             "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer 0 of 2 on F + N(F), the "
                     "last layer on the batch rows F); not counted in value (it does not visit every edge)"}
+        if world > 1:
+            result["frontier_forward"]["dp_table_exchange_steps"] = fr_exchange
+    result["value_note"] = ("value = n_gpus x nnz x L / t_step: each data-parallel replica runs the reference step's "
+                            "full propagation over every edge for its own 256-pair batch (weak scaling; replicas "
+                            "repeat the same graph's work); bpr_pairs_per_s (and frontier_forward.bpr_pairs_per_s, "
+                            "the training step driver.py runs) is the job's training throughput")
     if world > 1 or args.exchange_at_1:
-        result["dp_table_exchange_steps"] = dict(sync.stats)
+        result["dp_table_exchange_steps"] = exchange_steps
     if args.exchange_at_1:
         result["config"]["dp_exchange"] = dp_mode
         result["rehearsal"] = ("the N-rank table exchange forced at world 1 over RCCL (collectives move no data "
                                "between GPUs): its GPU + host overhead per step, not a scaling measurement")
+    if world == 1 and not args.no_kg_leg and not args.exchange_at_1:
+        cf_ms = result.get("frontier_forward", {}).get("ms_per_step", ms)
+        result["kg_refresh"] = kg_refresh_legs(model, pkg, layout, cfg, args, dev, len(inter), cf_ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg["nodes"] > 2_000_000:
             log("timing the CPU baseline (oracle restatement on subsampled edge sets, extrapolated) ...")
@@ -502,6 +517,122 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
             result["cpu_baseline"] = base
             result["parity"] = parity
     return result
+
+
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md chip table)
+
+
+def _event_ms(evs: dict, name: str) -> list[float]:
+    return [a.elapsed_time(b) for a, b in evs.get(name, [])]
+
+
+def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_ms: float) -> dict:
+    """The reference epoch's other two phases at this config:
+    TRAIN_KG + update_kg_weights at the reference's B = 512 (main.py:324-345) -- with the fused KG
+    table update (the table's Adam from TransR's compact rows, kgat_adam_rows_f32) and without it
+    (dense [N, d] gradient + Adam, the reference's arithmetic) -- and UPDATE_ATTENTION (main.py:350-361,
+    train mode: MHA dropout on, as the reference runs it).  Kernel times come from HIP events on the
+    launch stream (kernels.KERNEL_EVENTS); rooflines: the table Adam against HBM (24 B per parameter
+    + 4 B per row fused, 28 B per parameter dense), the edge scorer against the fp32 MFMA peak
+    (6 d^2 flop per edge: e_t W_r, W_v, W_o).  epoch_estimate = (interactions // 256 + 1) CF steps
+    (the training step: frontier forward when measured) + (edges // 512 + 1) KG steps + 1 refresh
+    (main.py:297, 324)."""
+    kernels = importlib.import_module(PKG + ".kernels")
+    B = 512
+    n, d = layout.n_nodes, cfg["dim"]
+    E = int(layout.heads.size)
+    rng = np.random.default_rng(11)
+    batches = []
+    for _ in range(args.warmup + args.steps):
+        e = rng.integers(0, E, B)
+        batches.append([torch.from_numpy(np.asarray(x, np.int64)).to(dev)
+                        for x in (layout.heads[e], layout.rels[e], layout.tails[e], rng.integers(0, n, B))])
+
+    def kg_step(b):
+        loss = model(*b, mode=pkg.KGATMode.TRAIN_KG)
+        loss.backward()
+        model.update_kg_weights()
+        return loss
+
+    out = {"batch": B}
+    for tag, fused in (("fused", True), ("unfused", False)):
+        model.fuse_kg_table_update = fused
+        for i in range(args.warmup):
+            kg_step(batches[i])
+        torch.cuda.synchronize()
+        kernels.KERNEL_EVENTS = {}
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            kg_step(batches[args.warmup + i])
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / args.steps * 1e3
+        evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
+        leg = {"ms_per_step": el, "kg_pairs_per_s": B / (el * 1e-3)}
+        for k in ("transr_fwd", "transr_bwd", "adam_rows", "adam_multi"):
+            t = _event_ms(evs, k)
+            if t:
+                leg[f"{k}_avg_ms"] = float(np.mean(t))
+        if fused:
+            t = leg.get("adam_rows_avg_ms")
+            if t:
+                by = 24 * n * d + 4 * n
+                leg["roofline"] = {"kernel": "adam_rows_kernel (table Adam from the compact TransR rows)", "bound": "hbm",
+                                   "bytes_per_launch": by, "achieved": by / (t * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": by / (t * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        else:
+            t = leg.get("adam_multi_avg_ms")
+            if t:
+                # the KG step's gradients: table, relation embeddings, trans matrices (model.py:414-419)
+                by = 28 * (n * d + model._relation_embedding.weight.numel() + model._trans_matrix.numel())
+                leg["roofline"] = {"kernel": "adam_multi_kernel<2> (dense table gradient)", "bound": "hbm",
+                                   "bytes_per_launch": by, "achieved": by / (t * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": by / (t * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        out[tag] = leg
+    model.fuse_kg_table_update = True
+    out["speedup_fused"] = out["unfused"]["ms_per_step"] / out["fused"]["ms_per_step"]
+    # UPDATE_ATTENTION on the whole edge list; A's values are restored afterwards (later legs compare
+    # the timed model with the oracle on the layout's initial values)
+    g = model.graph()
+    saved = g.A.val.detach().clone()
+    att = [torch.from_numpy(np.asarray(x, np.int64)).to(dev) for x in (layout.heads, layout.rels, layout.tails)]
+    att.append(torch.tensor(layout.rel_order))
+    model.train()
+    model(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)  # warm-up (builds the refresh plan)
+    torch.cuda.synchronize()
+    kernels.KERNEL_EVENTS = {}
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        model(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    torch.cuda.synchronize()
+    rms = (time.perf_counter() - t0) / reps * 1e3
+    evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
+    g = model.graph()
+    g.A.val.copy_(saved)
+    g.refresh_transpose()
+    ref = {"ms_per_call": rms, "edges": E, "edges_per_s": E / (rms * 1e-3)}
+    t = _event_ms(evs, "edge_scores")
+    if t:
+        flops = 6.0 * d * d * E
+        ref["edge_scores_avg_ms"] = float(np.mean(t))
+        ref["roofline"] = {"kernel": "edge scorer (e_t W_r, W_v, W_o on the fp32 MFMA)", "bound": "mfma",
+                           "flops_per_launch": flops, "achieved": flops / (float(np.mean(t)) * 1e-3) / 1e12,
+                           "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                           "frac": flops / (float(np.mean(t)) * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFS}
+    t = _event_ms(evs, "row_softmax")
+    if t:
+        by = 8 * g.nnz + 8 * n  # logits read + values written per edge, row pointers
+        ref["row_softmax_avg_ms"] = float(np.mean(t))
+        ref["row_softmax_GBps"] = by / (float(np.mean(t)) * 1e-3) / 1e9
+    out["refresh"] = ref
+    n_cf, n_kg = n_interactions // 256 + 1, E // 512 + 1
+    ep = n_cf * cf_ms + n_kg * out["fused"]["ms_per_step"] + rms
+    out["epoch_estimate"] = {
+        "cf_steps": n_cf, "kg_steps": n_kg, "cf_ms_per_step": cf_ms, "kg_ms_per_step": out["fused"]["ms_per_step"],
+        "refresh_ms": rms, "seconds": ep / 1e3,
+        "what": "one reference epoch (main.py:290-361: CF phase, KG phase, attention refresh; no evaluation) at the "
+                "measured per-step times"}
+    return out
 
 
 def frontier_matches_full(model, pkg, batch) -> dict:
@@ -673,6 +804,8 @@ def main() -> int:
                     help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
     ap.add_argument("--no-frontier-leg", action="store_true",
                     help="skip the second timed run with KGAT.frontier_forward (training-step speed)")
+    ap.add_argument("--no-kg-leg", action="store_true",
+                    help="skip the KG-step / attention-refresh legs and the epoch estimate (c2/c4, N = 1)")
     ap.add_argument("--no-fused-update", action="store_true",
                     help="c2/c4: materialise the table gradient and run Adam as its own pass")
     ap.add_argument("--dry-run", action="store_true",

@@ -13,12 +13,18 @@
 // 64 x 64 quarter as 2 x 2 tiles of v_mfma_f32_32x32x2_f32 (16 accumulators per tile,
 // 64 per lane).  K advances in 16-deep stages through two LDS buffers (register-staged:
 // the next stage's global loads are in flight while the current one is multiplied).
-// Both operands are kept k-contiguous in LDS ([row][k], row pitch 20 floats): lane l
-// of a wave reads its 8 k-values of row (l & 31), half h = l >> 5, with two
-// ds_read_b128 -- with the 80-byte pitch the 16 lanes of a b128 phase hit 16 distinct
-// 4-bank groups (conflict-free).  MFMA step s (s = 0..7) of a stage multiplies k = 8h + s
-// of half h, so a stage sums k in a fixed order: results are deterministic and exact
-// fp32 fma chains (the MFMA rounds once per product), not bit-equal to a library sgemm.
+// MFMA step s (s = 0..7) of a stage multiplies k = 8h + s of half h = lane >> 5, so a
+// stage sums k in a fixed order: results are deterministic and exact fp32 fma chains
+// (the MFMA rounds once per product), not bit-equal to a library sgemm.
+// LDS layout per operand, by its global layout:
+//  * k-contiguous (A, or B^T): [row][k], row pitch 20 floats -- lane l reads its 8
+//    k-values of row (l & 31) with two ds_read_b128; with the 80-byte pitch the 16 lanes
+//    of a b128 phase hit 16 distinct 4-bank groups (conflict-free);
+//  * k-major (A^T, or B: the weight-gradient GEMMs' operands): [k][row], pitch 132 floats --
+//    the global float4 (4 rows of one k) is stored whole (one ds_write_b128, where a
+//    [row][k] image needs four conflicting ds_write_b32), and step s's operand is one
+//    ds_read_b32 per lane: 32 consecutive rows of k = s (lanes 0-31) and of k = 8 + s
+//    (lanes 32-63, 8 pitches = 1056 floats away: the other 32 banks).
 #include "common.hpp"
 #include "gemm.hpp"
 
@@ -26,7 +32,9 @@ namespace kgat {
 
 namespace {
 
-constexpr int kBM = 128, kBN = 128, kBK = 16, kPitch = 20;  // LDS row pitch in floats
+constexpr int kBM = 128, kBN = 128, kBK = 16, kPitch = 20;  // LDS row pitch in floats ([row][k])
+constexpr int kPitchT = kBM + 4;                            // LDS k-row pitch in floats ([k][row])
+constexpr int kStageFloats = kBM * kPitch > kBK * kPitchT ? kBM * kPitch : kBK * kPitchT;
 constexpr int kThreads = 256;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -70,13 +78,22 @@ struct Stage {
       const int idx = t + q * kThreads;
       if (KCONTIG) {
         *reinterpret_cast<float4*>(lds + (idx >> 2) * kPitch + (idx & 3) * 4) = v[q];
-      } else {
-        const int k = idx >> 5, r = (idx & 31) * 4;
-        lds[(r + 0) * kPitch + k] = v[q].x;
-        lds[(r + 1) * kPitch + k] = v[q].y;
-        lds[(r + 2) * kPitch + k] = v[q].z;
-        lds[(r + 3) * kPitch + k] = v[q].w;
+      } else {  // [k][row]: the 4 rows of one k stay together
+        *reinterpret_cast<float4*>(lds + (idx >> 5) * kPitchT + (idx & 31) * 4) = v[q];
       }
+    }
+  }
+
+  // The 8 k-values (k = 8h + s, s = 0..7) of tile row `row` (0..127) for this lane's half h.
+  __device__ __forceinline__ static void read(const float* __restrict__ lds, int row, int h, float (&out)[8]) {
+    if (KCONTIG) {
+      const float4 a = *reinterpret_cast<const float4*>(lds + row * kPitch + 8 * h);
+      const float4 b = *reinterpret_cast<const float4*>(lds + row * kPitch + 8 * h + 4);
+      out[0] = a.x, out[1] = a.y, out[2] = a.z, out[3] = a.w;
+      out[4] = b.x, out[5] = b.y, out[6] = b.z, out[7] = b.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) out[s] = lds[(8 * h + s) * kPitchT + row];
     }
   }
 };
@@ -95,7 +112,7 @@ __device__ __forceinline__ void add_stage(float4& csum, const Stage<KC>& st) {
 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
-  __shared__ float lds[2][2][kBM * kPitch];  // [buffer][A | B][row][k]
+  __shared__ float lds[2][2][kStageFloats];  // [buffer][A | B][operand image]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int tiles_n = static_cast<int>((g.N + kBN - 1) / kBN);
   const int64_t m0 = static_cast<int64_t>(blockIdx.x / tiles_n) * kBM;
@@ -134,26 +151,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
       sa.load(A, g.lda, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * kBK, t);
       sb.load(B, g.ldb, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * kBK, t);
     }
-    float4 fa[2][2], fb[2][2];
+    float fa[2][8], fb[2][8];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const float* pa = &lds[cur][0][(wm + 32 * i + r) * kPitch + 8 * h];
-      const float* pb = &lds[cur][1][(wn + 32 * i + r) * kPitch + 8 * h];
-      fa[i][0] = *reinterpret_cast<const float4*>(pa);
-      fa[i][1] = *reinterpret_cast<const float4*>(pa + 4);
-      fb[i][0] = *reinterpret_cast<const float4*>(pb);
-      fb[i][1] = *reinterpret_cast<const float4*>(pb + 4);
+      Stage<!TA>::read(lds[cur][0], wm + 32 * i + r, h, fa[i]);
+      Stage<TB>::read(lds[cur][1], wn + 32 * i + r, h, fb[i]);
     }
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float a = s < 4 ? fa[i][0][s & 3] : fa[i][1][s & 3];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const float b = s < 4 ? fb[j][0][s & 3] : fb[j][1][s & 3];
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
       }
     }
     if (kt + 1 < nk) {

@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace kgat {
 
@@ -71,7 +72,7 @@ __device__ __forceinline__ void adam_row_step(const SpmmAdam& a, int64_t row, in
 template <int MODE>
 __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t out, int gl, float4 acc,
                                           bool any = false) {
-  if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam) {
+  if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB) {
     if (io.Yc != nullptr) {
       const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
@@ -82,7 +83,7 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     }
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
-  if (MODE == kMaskedAdam) {
+  if (MODE == kMaskedAdam || MODE == kMaskedAdamB) {
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
     return;
   }
@@ -106,7 +107,7 @@ template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
-  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
@@ -167,6 +168,44 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int64_t r_begin = w * S::kRowsPerWave;
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
+  if (MODE == kMaskedAdamB) {
+    // the group's rows' gradients first, then all their Adam loads in flight together
+    constexpr int R = S::kRowsPerGroup;
+    float4 acc[R];
+    bool ok[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int64_t r = r_begin + g + static_cast<int64_t>(k) * S::kGroups;
+      acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      ok[k] = false;
+      if (r < r_end) {
+        const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+        if (end - beg <= A.long_threshold) {  // long rows: the fix-up pass
+          bool any = false;
+          gather_edges<D, true>(A, io, beg, end, base, gl, acc[k], any);
+          ok[k] = true;
+        }
+      }
+    }
+    AdamRow ar[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int64_t r = r_begin + g + static_cast<int64_t>(k) * S::kGroups;
+      if (!ok[k]) continue;
+      if (io.Yc != nullptr) {
+        const int m = io.src_map[io.row0 + r];
+        if (m >= 0) {
+          const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
+          acc[k] = make_float4(o.x + acc[k].x, o.y + acc[k].y, o.z + acc[k].z, o.w + acc[k].w);
+        }
+      }
+      ar[k] = adam_row_load(io.adam, r, gl);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      if (ok[k]) adam_row_step(io.adam, r_begin + g + static_cast<int64_t>(k) * S::kGroups, gl, acc[k], ar[k]);
+    return;
+  }
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
@@ -482,6 +521,12 @@ extern "C" int kgat_spmm_csr_masked_adam_f32(const kgat_csr* A, const int32_t* s
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
   io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps};
+  // KGAT_TU_BATCH=1: the row-batched form (kMaskedAdamB, same bits); default the row-at-a-time one
+  static const int batched = [] {
+    const char* e = getenv("KGAT_TU_BATCH");
+    return e ? atoi(e) : 0;
+  }();
+  if (batched) return dispatch<kMaskedAdamB>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 

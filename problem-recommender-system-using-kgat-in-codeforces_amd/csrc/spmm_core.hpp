@@ -7,7 +7,13 @@
 
 namespace kgat {
 
-enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4, kRows = 5 };
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4, kRows = 5,
+                kMaskedAdamB = 6 };
+
+// kMaskedAdamB: kMaskedAdam with each lane group's rows batched -- the group first gathers the
+// gradients of all its kRowsPerGroup short rows (one accumulator each), then issues every row's
+// p / m / v loads together (3 x kRowsPerGroup float4 in flight per lane instead of 3) and steps
+// them.  Same arithmetic per row (same bits); the choice is KGAT_TU_BATCH (spmm.hip).
 
 // kRows: the dense product A . X on the rows of an output set only (out_rows / out_bits /
 // out_count; -1 entries of out_rows are padding), each written at its own row of Y -- the

@@ -185,6 +185,7 @@ def train(args) -> dict:
     model.build_optimizer(cf_lr=CF_LEARNING_RATE, kg_lr=KG_LEARNING_RATE)
     model.fuse_table_update = True  # the loop below only ever steps right after backward (main.py:312-313)
     model.frontier_forward = True  # TRAIN_CF's forward on the rows its loss reaches (same bits)
+    model.fuse_kg_table_update = True  # the KG step's table Adam from TransR's compact rows (same bits)
     refresh = [torch.from_numpy(np.asarray(x, np.int64)).to(dev)
                for x in (layout.heads, layout.rels, layout.tails, layout.rel_order)]
     train_dict, val_dict = ds.interaction_dict("train"), ds.interaction_dict("validation")

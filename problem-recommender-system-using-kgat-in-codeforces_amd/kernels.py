@@ -38,6 +38,28 @@ def _ld(t: torch.Tensor) -> int:
 # on the launch stream around its kernels.
 SPMM_EVENTS: list | None = None
 
+# Optional per-kernel launch timer (bench.py's KG-step and refresh legs): when set to a dict,
+# the wrappers below that take part append (start_event, end_event) recorded on the launch stream
+# around their launches under their kernel's name.
+KERNEL_EVENTS: dict | None = None
+
+
+def _ev_begin(name: str):
+    if KERNEL_EVENTS is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return name, e0
+
+
+def _ev_end(tok) -> None:
+    if tok is None or KERNEL_EVENTS is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record()
+    KERNEL_EVENTS.setdefault(tok[0], []).append((tok[1], e1))
+
+
 # Edges per chunk of the wide-embedding GEMM edge scorer (scratch = 2 * chunk * d floats).
 EDGE_GEMM_CHUNK = 1 << 20
 
@@ -868,9 +890,11 @@ def transr_fwd(emb, rel_emb, trans, heads, rels, pos, neg, reg: float):
     dev = emb.device
     loss = torch.empty(1, dtype=torch.float32, device=dev)
     work = torch.empty(int(_lib.lib().kgat_transr_work_floats(B, d, k)), dtype=torch.float32, device=dev)
+    tok = _ev_begin("transr_fwd")
     _lib.call("kgat_transr_fwd_ex_f32", emb.data_ptr(), _ld(emb), rel_emb.data_ptr(), trans.data_ptr(), d, k,
               trans.shape[0], heads.data_ptr(), rels.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg), loss.data_ptr(),
               work.data_ptr(), stream_ptr(dev))
+    _ev_end(tok)
     return loss, work
 
 
@@ -885,10 +909,12 @@ def transr_bwd(emb, n_rel: int, k: int, heads, rels, pos, neg, work, grad_out):
     if ws_n < 0:
         raise ValueError("transr_bwd: bad shape")
     ws = torch.empty(ws_n, dtype=torch.float32, device=dev)
+    tok = _ev_begin("transr_bwd")
     _lib.call("kgat_transr_bwd_f32", emb.data_ptr(), _ld(emb), d, k, heads.data_ptr(), rels.data_ptr(),
               pos.data_ptr(), neg.data_ptr(), heads.numel(), n_rel, work.data_ptr(), grad_out.data_ptr(),
               d_emb.data_ptr(), _ld(d_emb), d_rel.data_ptr(), d_trans.data_ptr(), ws.data_ptr(), ws.numel(),
               stream_ptr(dev))
+    _ev_end(tok)
     return d_emb, d_rel, d_trans
 
 
@@ -907,10 +933,12 @@ def transr_bwd_compact(emb, n_rel: int, k: int, heads, rels, pos, neg, work, gra
     if ws_n < 0:
         raise ValueError("transr_bwd: bad shape")
     ws = torch.empty(ws_n, dtype=torch.float32, device=dev)
+    tok = _ev_begin("transr_bwd")
     _lib.call("kgat_transr_bwd_ex_f32", emb.data_ptr(), _ld(emb), d, k, heads.data_ptr(), rels.data_ptr(),
               pos.data_ptr(), neg.data_ptr(), heads.numel(), n_rel, work.data_ptr(), grad_out.data_ptr(),
               Gc.data_ptr(), _ld(Gc), row_map.data_ptr(), d_rel.data_ptr(), d_trans.data_ptr(), ws.data_ptr(),
               ws.numel(), stream_ptr(dev))
+    _ev_end(tok)
     return Gc, d_rel, d_trans
 
 
@@ -925,8 +953,10 @@ def adam_rows(p, m, v, row_map: torch.Tensor, Gc: torch.Tensor, step_size: float
     _req(Gc, "Gc", dim=2)
     if row_map.numel() != p.shape[0] or Gc.shape[1] != p.shape[1]:
         raise ValueError("adam_rows: row_map must cover every row, Gc must be [rows, d]")
+    tok = _ev_begin("adam_rows")
     _lib.call("kgat_adam_rows_f32", p.data_ptr(), m.data_ptr(), v.data_ptr(), p.shape[0], p.shape[1],
               row_map.data_ptr(), Gc.data_ptr(), _ld(Gc), step_size, beta1, beta2, bc2_sqrt, eps, stream_ptr(p.device))
+    _ev_end(tok)
 
 
 def score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out: torch.Tensor, dropout_p: float = 0.0,
@@ -934,6 +964,7 @@ def score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out: torch.Tensor,
     """Edge scores of a plan: out[plan.out_pos[e]] (or out[e]) = logit of edge e; the fused MFMA
     scorer for d <= 128, the chunked GEMM scorer above."""
     d = emb.shape[1]
+    tok = _ev_begin("edge_scores")
     if d not in (16, 32, 64, 128):  # wide embeddings: GEMM path (csrc/attention_gemm.hip)
         chunk = max(16, min(plan.n_edges, EDGE_GEMM_CHUNK))
         work = torch.empty(int(_lib.lib().kgat_edge_logits_gemm_work_floats(chunk, d)), dtype=torch.float32,
@@ -952,6 +983,7 @@ def score_edges(plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, out: torch.Tensor,
                   plan.tile_beg.data_ptr(), plan.n_tiles, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
                   plan.out_pos.data_ptr() if plan.out_pos is not None else None, out.data_ptr(),
                   stream_ptr(emb.device))
+    _ev_end(tok)
 
 
 def edge_logits(graph: DeviceGraph, plan, emb, trans, Wv, bv, Wo, bo, ln_w, ln_b, dropout_p: float = 0.0,
@@ -991,8 +1023,10 @@ def row_softmax(graph: DeviceGraph, slot_logits: torch.Tensor) -> None:
     A = graph.A
     if LONG_THRESHOLD_SOFTMAX != graph_long_threshold():
         raise RuntimeError("row softmax long-row split must match the CSR plan")
+    tok = _ev_begin("row_softmax")
     _lib.call("kgat_row_softmax_ex_f32", A.rowptr.data_ptr(), graph.n_nodes, A.long_rows.data_ptr(), A.n_long,
               slot_logits.data_ptr(), A.val.data_ptr(), stream_ptr(slot_logits.device))
+    _ev_end(tok)
     graph.refresh_transpose()
 
 
@@ -1018,6 +1052,7 @@ def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: flo
 
 def adam_multi(items, beta1: float, beta2: float, eps: float) -> None:
     """One launch per <= 16 tensors: items = [(p, g, m, v, step_size, bc2_sqrt), ...]."""
+    tok = _ev_begin("adam_multi")
     for i in range(0, len(items), _lib.KGAT_ADAM_MAX_TENSORS):
         chunk = items[i:i + _lib.KGAT_ADAM_MAX_TENSORS]
         arr = (_lib.AdamTensor * len(chunk))()
@@ -1029,6 +1064,7 @@ def adam_multi(items, beta1: float, beta2: float, eps: float) -> None:
             a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
             a.n, a.step_size, a.bc2_sqrt = p.numel(), step_size, bc2s
         _lib.call("kgat_adam_multi_f32", arr, len(chunk), beta1, beta2, eps, stream_ptr(chunk[0][0].device))
+    _ev_end(tok)
 
 
 def fill(t: torch.Tensor, value: float) -> torch.Tensor:

@@ -9,9 +9,9 @@ rows [lo_k, hi_k) of A^T -- the in-edges of its nodes, global column ids).
 Forward, per layer (aggregator.py:54-65):
     Xg   = every rank's rows of X_l   all-peer gather (one P2P send + receive per peer,
                                       all in flight together: on a fully connected xGMI
-                                      node each peer pair has its own link), in column
-                                      chunks so chunk c+1 is on the wire while chunk c's
-                                      product runs
+                                      node each peer pair has its own link); optionally in
+                                      column chunks, chunk c+1 on the wire while chunk c's
+                                      product runs (GATHER_CHUNK)
     S_k  = A_loc . Xg                 the single-GPU SpMM on the local rows: per row the
                                       same edges in the same order as one GPU -- bit for bit
     H_k  = biinter(X_k, S_k)          row-local
@@ -21,9 +21,10 @@ Backward ("pull": the transpose of the forward, no reduce-scatter):
       row, zeros elsewhere) gives every rank the compact [dS | dXd] rows of the whole batch;
       dX_k = AT_loc . dS (masked to the batch rows) + dXd -- kgat_spmm_csr_masked_ex_f32
     lower layers: dSg = all-peer gather of dS_l; dX_k = dXd_k + AT_loc . dSg
-  Per output row the single-GPU backward's edges in its order, so the table gradient is the
-  single GPU's bit for bit; only the aggregator weight gradients (per-rank partial sums,
-  all-reduced) are summed in another order.
+  Per output row the single-GPU backward's edges in its order, so the propagated tables and the
+  table gradient are the single GPU's bit for bit at every world size (whole-width gathers);
+  only the aggregator weight gradients (per-rank partial sums, all-reduced) are summed in
+  another order.
 The BPR loss is taken over the GLOBAL batch (every rank's pairs, as data-parallel
 training would): the batch rows are assembled on every rank by one exact all-reduce,
 every rank evaluates the same loss, and each keeps the row gradients of the rows it
@@ -58,9 +59,13 @@ from .graph import GraphLayout, RefreshPlan, _DeviceCSR, degree_weights, stream_
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
 from .optim import FusedAdam
 
-# columns per gathered chunk: chunk c+1 travels while chunk c's SpMM runs (a 256-wide layer in four
-# 64-wide chunks; per output element the sum is the unchunked one, the chunk only splits columns)
-GATHER_CHUNK = int(os.environ.get("KGAT_SHARD_CHUNK", "64"))
+# Columns per gathered chunk (0 = the whole width in one gather): chunk c+1 travels while chunk c's
+# SpMM runs.  Off by default: the SpMM kernel of a narrower width walks a long (hub) row's
+# 512-edge segments in a different interleave (spmm.hip: lane groups of d/4 lanes), so a chunked
+# gather changes the summation order of hub rows -- within tolerance, but no longer the single
+# GPU's bits, which the whole-width gather keeps for every world size (tests/sharded_worker.py).
+# KGAT_SHARD_CHUNK=64 trades that for hiding each layer's SpMM under the next chunk's transfer.
+GATHER_CHUNK = int(os.environ.get("KGAT_SHARD_CHUNK", "0"))
 
 
 # ---------------------------------------------------------------- transport

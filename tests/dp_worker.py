@@ -15,7 +15,9 @@ disagree on the hop mode and must fall back to the dense all-reduce together.  T
 associated differently (A^T . mean(dS) instead of mean(A^T . dS)), so they are compared with the
 Adam tolerance of DESIGN.md §2, and each path's replicas must stay bit-identical.  (F) is (D) with
 ``fuse_table_update``: the merged hop-set terms are handed to update_cf_weights, which runs the union
-product fused with the table's Adam step -- bit-identical to (D).
+product fused with the table's Adam step -- bit-identical to (D).  (G) is (F) with ``frontier_forward``
+(each layer's forward on the rows the loss reaches; it marks the same first hop the exchange
+announces early) -- bit-identical to (F): the data-parallel training step bench.py times at N > 1.
 """
 from __future__ import annotations
 
@@ -46,18 +48,19 @@ def main() -> None:
                         cf_embedding_dim=d0, kg_embedding_dim=d0, message_dropout=[0.1] * len(layer_size))
     models = []
     model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
-    for k in range(6):
+    for k in range(7):
         torch.manual_seed(3)
         m = pkg.KGAT(args)
         m.attach_graph(lay, "cuda")
         rep.broadcast_parameters(m)
         m.train()
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-        m.fuse_table_update = k == 5
+        m.fuse_table_update = k >= 5
+        m.frontier_forward = k == 6
         models.append(m)
     rng = np.random.default_rng(40 + rank)
     failures = []
-    syncs = [None] * 6
+    syncs = [None] * 7
     for step in range(3):
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
@@ -86,8 +89,8 @@ def main() -> None:
             if step == 0:
                 with torch.no_grad():  # a loss evaluation without backward opens no exchange
                     m(*b, mode=pkg.KGATMode.TRAIN_CF)
-    for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop")):
-        got = syncs["ABCDEF".index(tag)].stats
+    for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop"), ("G", "hop")):
+        got = syncs["ABCDEFG".index(tag)].stats
         if got.get(want, 0) != 3:
             failures.append(f"{tag}: table exchange paths {got}, expected 3 x {want}")
     for named in zip(*(m.named_parameters() for m in models)):
@@ -96,6 +99,8 @@ def main() -> None:
             continue
         if not torch.equal(named[3][1].data, named[5][1].data):
             failures.append(f"F {na}: differs from D by {(named[3][1].data - named[5][1].data).abs().max().item():.3e}")
+        if not torch.equal(named[5][1].data, named[6][1].data):
+            failures.append(f"G {na}: differs from F by {(named[5][1].data - named[6][1].data).abs().max().item():.3e}")
         for tag, (_, po) in zip("BCDE", named[1:5]):
             # two ranks: every sum has two operands, so B / C equal A bit for bit; more ranks
             # associate the sums differently (the Adam tolerance, as D / E)
@@ -104,7 +109,7 @@ def main() -> None:
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
             if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
-        for tag, (_, po) in zip("ABCDEF", named):
+        for tag, (_, po) in zip("ABCDEFG", named):
             other = po.data.clone()
             dist.broadcast(other, 0)
             if not torch.equal(other, po.data):

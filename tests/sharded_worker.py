@@ -116,6 +116,7 @@ def main() -> None:
     m(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
     A = ref.graph().A
     close("refreshed A rows", m.shard.local_val, A.val[int(lay.rowptr[lo]):int(lay.rowptr[hi])], 1e-6)
+    exact["refreshed_A"] = torch.equal(m.shard.local_val, A.val[int(lay.rowptr[lo]):int(lay.rowptr[hi])])
     with torch.no_grad():
         tabs_s, tabs_r = m.propagate(), ref.propagate()
     for l, (a, b) in enumerate(zip(tabs_s, tabs_r)):

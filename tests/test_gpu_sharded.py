@@ -92,21 +92,29 @@ def test_sharded_world1_matches_kgat(pkg):
                                    ref(users, items, mode=pkg.KGATMode.PREDICT).cpu().numpy(), atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("world,dims", [(2, "64:64,32"), (2, "256:256,128,64"), (4, "256:256,128,64")])
-def test_sharded_ranks_one_gpu(world, dims):
+@pytest.mark.parametrize("world,dims,chunk", [(2, "64:64,32", 0), (2, "256:256,128,64", 0), (4, "256:256,128,64", 0),
+                                              (3, "256:256,128,64", 64)])
+def test_sharded_ranks_one_gpu(world, dims, chunk):
     """tests/sharded_worker.py on `world` ranks sharing this GPU (gloo, host-staged): the row-sharded
     model vs single-GPU KGAT on the global batch -- at the C2 shape and at C5's (d = 256, layers
-    [256, 128, 64], configs[4]) -- CF and KG loss, gradient shards, Adam, attention refresh, PREDICT."""
-    env = dict(os.environ, SHARDED_WORKER_DIMS=dims)
+    [256, 128, 64], configs[4]) -- CF and KG loss, gradient shards, Adam, attention refresh, PREDICT.
+    With the whole-width gather (chunk 0, the default) the propagated tables, the refreshed values
+    and the table gradients are the single GPU's bit for bit (same rows, same edges, same order);
+    64-column chunks (KGAT_SHARD_CHUNK) change the hub rows' summation order: tolerance only."""
+    env = dict(os.environ, SHARDED_WORKER_DIMS=dims, KGAT_SHARD_CHUNK=str(chunk))
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "sharded_worker.py")]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / f"sharded_world{world}_d{dims.split(':')[0]}.log"
+    log = ROOT / "gpurun_out" / f"sharded_world{world}_d{dims.split(':')[0]}_c{chunk}.log"
     log.parent.mkdir(exist_ok=True)
     log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert p.stdout.count("sharded parity ok") == world, p.stdout[-2000:]
+    if chunk == 0:
+        import re
+        flags = re.findall(r"bit-identical (\{[^}]*\})", p.stdout)  # rank lines may interleave
+        assert len(flags) == world and all("False" not in f for f in flags), flags
 
 
 def test_dp_sharded_grad_sync_world2_matches_allreduce():
@@ -194,3 +202,6 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus):
     assert rec["n_gpus"] == gpus and rec["config"]["parallelism"] == f"dp{gpus}" and rec["config"]["dp_exchange"] == dp
     assert rec["rehearsal"].startswith("gloo") and rec["value"] > 0 and np.isfinite(rec["final_loss"])
     assert sum(rec["dp_table_exchange_steps"].values()) == 4 if dp == "replicated" else True
+    if dp == "replicated":  # the frontier-forward leg (composes with the replicated exchange) ran too
+        fr = rec["frontier_forward"]
+        assert fr["bpr_pairs_per_s"] > 0 and sum(fr["dp_table_exchange_steps"].values()) == 4
