@@ -119,6 +119,13 @@ int kgat_spmm_csr_masked_adam_f32(const kgat_csr *A, const int32_t *src_map, con
                                   float *v, int64_t ldp, int32_t d, float step_size, float beta1, float beta2,
                                   float bc2_sqrt, float eps, float *workspace, int64_t workspace_floats,
                                   void *stream);
+/* ... with a skip flag (device int32, nullable): *skip != 0 when the kernel runs -> p / m / v are
+ * left untouched (kgat_ids_check_ex's bad_dev: the step's ids were out of range). */
+int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                     const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
+                                     float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
+                                     float beta2, float bc2_sqrt, float eps, const int32_t *skip, float *workspace,
+                                     int64_t workspace_floats, void *stream);
 
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
@@ -552,6 +559,9 @@ typedef struct kgat_adam_tensor {
 } kgat_adam_tensor;
 int kgat_adam_multi_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
                         void *stream);
+/* ... with the optimiser skip flag (see kgat_spmm_csr_masked_adam_ex_f32). */
+int kgat_adam_multi_ex_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
+                           const int32_t *skip, void *stream);
 
 /* a9 for the KG step's table (model.py:414-419 after the TransR backward, whose table gradient is
  * nonzero on the <= 3B rows of the batch only): the dense Adam step over p / m / v [n_rows x d]
@@ -560,7 +570,7 @@ int kgat_adam_multi_f32(const kgat_adam_tensor *tensors, int32_t count, float be
  * written.  d % 4 == 0, 16-byte aligned arrays. */
 int kgat_adam_rows_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *row_map,
                        const float *Gc, int64_t ldg, float step_size, float beta1, float beta2, float bc2_sqrt,
-                       float eps, void *stream);
+                       float eps, const int32_t *skip, void *stream);
 
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);
@@ -578,6 +588,12 @@ typedef struct kgat_ids {
   int32_t count;
 } kgat_ids;
 int kgat_ids_check(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *bad, void *stream);
+/* ... that also sets *bad_dev = 1 (device int32, nullable) -- the skip flag the optimiser kernels
+ * read (kgat_adam_multi_ex_f32, kgat_spmm_csr_masked_adam_ex_f32, kgat_adam_rows_f32), so a step
+ * with a bad id moves no parameter although the host learns of it later (no synchronisation);
+ * the caller zeroes it after reporting the error. */
+int kgat_ids_check_ex(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *bad, int32_t *bad_dev,
+                      void *stream);
 
 /* node_map[ids[i]] = i for i < n (ids distinct; negative ids skipped): the node -> compact row
  * map of a row list (the row-sharded backward's global batch rows, whose compact order is the

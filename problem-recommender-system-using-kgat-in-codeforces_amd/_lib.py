@@ -89,6 +89,9 @@ _SIGNATURES = {
     "kgat_spmm_csr_masked_adam_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
                                                      c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp,
                                                      c_i64, c_vp]),
+    "kgat_spmm_csr_masked_adam_ex_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                                        c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
+                                                        c_f32, c_vp, c_vp, c_i64, c_vp]),
     "kgat_map_rank": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_map_bits": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_hop_compact_work_bytes": (c_i64, [c_i64]),
@@ -127,7 +130,7 @@ _SIGNATURES = {
     "kgat_transr_bwd_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                               c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_adam_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32,
-                                          c_f32, c_f32, c_vp]),
+                                          c_f32, c_f32, c_vp, c_vp]),
     "kgat_transr_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                            c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_edge_logits_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -154,6 +157,7 @@ _SIGNATURES = {
     "kgat_sample_kg_batch": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp,
                                             c_vp]),
     "kgat_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp]),
+    "kgat_adam_multi_ex_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "kgat_edge_logits_gemm_work_floats": (c_i64, [c_i64, c_i32]),
     "kgat_edge_logits_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                  c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp,
@@ -178,6 +182,7 @@ _SIGNATURES = {
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
     "kgat_map_build": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_ids_check": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp]),
+    "kgat_ids_check_ex": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp, c_vp]),
     "kgat_gemm_f32": (ctypes.c_int, [c_i32, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
                                      c_i64, c_i64, c_i64, c_i32, c_vp]),
     "kgat_comm_load": (ctypes.c_int, [ctypes.c_char_p]),

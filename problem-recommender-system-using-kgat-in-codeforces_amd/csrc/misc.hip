@@ -45,8 +45,10 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ s
 }
 
 // ids of up to KGAT_IDS_MAX arrays, concatenated into out; out-of-range ids become 0 and set *bad = 1
+// (and *bad_dev = 1 when given: the optimiser kernels' skip flag)
 __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t total, int64_t bound,
-                                                        int64_t* __restrict__ out, int32_t* __restrict__ bad) {
+                                                        int64_t* __restrict__ out, int32_t* __restrict__ bad,
+                                                        int32_t* __restrict__ bad_dev) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   bool flag = false;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
@@ -58,7 +60,10 @@ __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t to
     out[i] = ok ? v : 0;
     flag |= !ok;
   }
-  if (flag) *bad = 1;  // every writer stores 1: no atomic needed (bad may be host-mapped pinned memory)
+  if (flag) {  // every writer stores 1: no atomic needed (bad may be host-mapped pinned memory)
+    *bad = 1;
+    if (bad_dev != nullptr) *bad_dev = 1;
+  }
 }
 
 // node_map[ids[i]] = i (distinct ids; ids[i] < 0 skipped)
@@ -122,7 +127,9 @@ __device__ __forceinline__ void st4(float* p, float4 v) {
 // (all four arrays, four float4 per lane), then the updates, then the stores; V = 2 with
 // non-temporal loads/stores (every byte is touched once per step).
 template <int V>
-__global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps) {
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps,
+                                                         const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;  // the step's ids were out of range: no parameter moves
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t total = T.chunk_off[T.count];
   for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
@@ -198,7 +205,9 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, f
                                                         float* __restrict__ v, int64_t n4, int d4,
                                                         const int32_t* __restrict__ row_map,
                                                         const float* __restrict__ Gc, int64_t ldg, float step_size,
-                                                        float b1, float b2, float bc2s, float eps) {
+                                                        float b1, float b2, float bc2s, float eps,
+                                                        const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t chunks = (n4 + 1023) / 1024;
   for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
@@ -246,6 +255,11 @@ static int adam_variant() {
 
 extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
                                    float eps, void* stream) {
+  return kgat_adam_multi_ex_f32(tensors, count, beta1, beta2, eps, nullptr, stream);
+}
+
+extern "C" int kgat_adam_multi_ex_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
+                                      float eps, const int32_t* skip, void* stream) {
   if (!tensors || count < 1 || count > KGAT_ADAM_MAX_TENSORS) return KGAT_ERR_INVALID;
   kgat::AdamTable T{};
   T.count = count;
@@ -265,9 +279,9 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
   const int grid = static_cast<int>(off < kgat::kCUs * 8 ? off : kgat::kCUs * 8);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (kgat::adam_variant()) {
-    case 1: hipLaunchKernelGGL(kgat::adam_multi_kernel<1>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps); break;
-    case 2: hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps); break;
-    default: hipLaunchKernelGGL(kgat::adam_multi_kernel<0>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps);
+    case 1: hipLaunchKernelGGL(kgat::adam_multi_kernel<1>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip); break;
+    case 2: hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip); break;
+    default: hipLaunchKernelGGL(kgat::adam_multi_kernel<0>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip);
   }
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
@@ -275,7 +289,7 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
 
 extern "C" int kgat_adam_rows_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d, const int32_t* row_map,
                                   const float* Gc, int64_t ldg, float step_size, float beta1, float beta2,
-                                  float bc2_sqrt, float eps, void* stream) {
+                                  float bc2_sqrt, float eps, const int32_t* skip, void* stream) {
   if (!p || !m || !v || !row_map || !Gc || n_rows < 0 || d < 4 || (d & 3) || ldg < d || (ldg & 3)) return KGAT_ERR_INVALID;
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v) |
        reinterpret_cast<uintptr_t>(Gc)) & 15)
@@ -285,7 +299,7 @@ extern "C" int kgat_adam_rows_f32(float* p, float* m, float* v, int64_t n_rows, 
   const int64_t chunks = (n4 + 1023) / 1024;
   const int grid = static_cast<int>(chunks < kgat::kCUs * 8 ? chunks : kgat::kCUs * 8);
   hipLaunchKernelGGL(kgat::adam_rows_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, m, v,
-                     n4, d / 4, row_map, Gc, ldg, step_size, beta1, beta2, bc2_sqrt, eps);
+                     n4, d / 4, row_map, Gc, ldg, step_size, beta1, beta2, bc2_sqrt, eps, skip);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -392,6 +406,11 @@ extern "C" int kgat_gather_f32(const float* src, const int32_t* idx, int64_t n, 
 }
 
 extern "C" int kgat_ids_check(const kgat_ids* ids, int64_t bound, int64_t* out, int32_t* bad, void* stream) {
+  return kgat_ids_check_ex(ids, bound, out, bad, nullptr, stream);
+}
+
+extern "C" int kgat_ids_check_ex(const kgat_ids* ids, int64_t bound, int64_t* out, int32_t* bad, int32_t* bad_dev,
+                                 void* stream) {
   if (!ids || !out || !bad || ids->count < 1 || ids->count > KGAT_IDS_MAX || bound < 0) return KGAT_ERR_INVALID;
   int64_t total = 0;
   for (int k = 0; k < ids->count; ++k) {
@@ -400,7 +419,7 @@ extern "C" int kgat_ids_check(const kgat_ids* ids, int64_t bound, int64_t* out, 
   }
   if (total == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::ids_check_kernel, dim3(kgat::blocks_for(total, 256, kgat::kCUs * 4)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), *ids, total, bound, out, bad);
+                     reinterpret_cast<hipStream_t>(stream), *ids, total, bound, out, bad, bad_dev);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
+  if ((MODE == kMaskedAdam || MODE == kMaskedAdamB) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     // ---- long-row segment: the whole wave, groups take interleaved sub-chunks
@@ -227,6 +228,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   __shared__ float4 red[G][L];
   const int lr = blockIdx.x;
   const int g = threadIdx.x / L, gl = threadIdx.x % L;
+  if ((MODE == kMaskedAdam || MODE == kMaskedAdamB) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
   const int row = A.long_rows[lr];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
   const float4* P = reinterpret_cast<const float4*>(io.part);
@@ -508,6 +510,16 @@ extern "C" int kgat_spmm_csr_masked_adam_f32(const kgat_csr* A, const int32_t* s
                                              const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
                                              int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
                                              float eps, float* workspace, int64_t workspace_floats, void* stream) {
+  return kgat_spmm_csr_masked_adam_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, src_rank, p, m, v, ldp, d, step_size,
+                                          beta1, beta2, bc2_sqrt, eps, nullptr, workspace, workspace_floats, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                                const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                                int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
+                                                float eps, const int32_t* skip, float* workspace,
+                                                int64_t workspace_floats, void* stream) {
   using namespace kgat;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
@@ -520,7 +532,7 @@ extern "C" int kgat_spmm_csr_masked_adam_f32(const kgat_csr* A, const int32_t* s
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
   // KGAT_TU_BATCH=1: the row-batched form (kMaskedAdamB, same bits); default the row-at-a-time one
   static const int batched = [] {
     const char* e = getenv("KGAT_TU_BATCH");

@@ -32,6 +32,7 @@ struct SpmmAdam {
   float* v;
   int64_t ld;  // row stride of p, m, v (floats)
   float step_size, b1, b2, bc2s, eps;
+  const int32_t* skip;  // nullable: *skip != 0 -> the launch leaves p / m / v untouched (bad step ids)
 };
 
 struct SpmmIo {

@@ -250,9 +250,18 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     return out
 
 
+def _skip_ptr(skip: torch.Tensor | None):
+    """The optimiser skip flag (device int32 [1], kgat_ids_check_ex's bad_dev) or None."""
+    if skip is None:
+        return None
+    _req(skip, "skip", dtype=torch.int32, dim=1)
+    return skip.data_ptr()
+
+
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
-                     step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float) -> None:
+                     step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
+                     skip: torch.Tensor | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
     update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
@@ -276,10 +285,10 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("kgat_spmm_csr_masked_adam_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+    _lib.call("kgat_spmm_csr_masked_adam_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
               _rank_ptr(src_rank, src_map), p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
-              bc2_sqrt, eps, ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+              bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
@@ -943,7 +952,7 @@ def transr_bwd_compact(emb, n_rel: int, k: int, heads, rels, pos, neg, work, gra
 
 
 def adam_rows(p, m, v, row_map: torch.Tensor, Gc: torch.Tensor, step_size: float, beta1: float, beta2: float,
-              bc2_sqrt: float, eps: float) -> None:
+              bc2_sqrt: float, eps: float, skip: torch.Tensor | None = None) -> None:
     """Adam over the whole [N, d] table with row r's gradient Gc[row_map[r]] or 0 (kgat_adam_rows_f32)."""
     for t, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
         _req(t, nm, dim=2)
@@ -955,7 +964,8 @@ def adam_rows(p, m, v, row_map: torch.Tensor, Gc: torch.Tensor, step_size: float
         raise ValueError("adam_rows: row_map must cover every row, Gc must be [rows, d]")
     tok = _ev_begin("adam_rows")
     _lib.call("kgat_adam_rows_f32", p.data_ptr(), m.data_ptr(), v.data_ptr(), p.shape[0], p.shape[1],
-              row_map.data_ptr(), Gc.data_ptr(), _ld(Gc), step_size, beta1, beta2, bc2_sqrt, eps, stream_ptr(p.device))
+              row_map.data_ptr(), Gc.data_ptr(), _ld(Gc), step_size, beta1, beta2, bc2_sqrt, eps, _skip_ptr(skip),
+              stream_ptr(p.device))
     _ev_end(tok)
 
 
@@ -1050,8 +1060,9 @@ def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: flo
               beta2, bc2_sqrt, eps, stream_ptr(p.device))
 
 
-def adam_multi(items, beta1: float, beta2: float, eps: float) -> None:
-    """One launch per <= 16 tensors: items = [(p, g, m, v, step_size, bc2_sqrt), ...]."""
+def adam_multi(items, beta1: float, beta2: float, eps: float, skip: torch.Tensor | None = None) -> None:
+    """One launch per <= 16 tensors: items = [(p, g, m, v, step_size, bc2_sqrt), ...]; ``skip``: the
+    optimiser skip flag (nothing moves when it is set)."""
     tok = _ev_begin("adam_multi")
     for i in range(0, len(items), _lib.KGAT_ADAM_MAX_TENSORS):
         chunk = items[i:i + _lib.KGAT_ADAM_MAX_TENSORS]
@@ -1063,7 +1074,8 @@ def adam_multi(items, beta1: float, beta2: float, eps: float) -> None:
                     raise ValueError(f"{nm} must be contiguous")
             a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
             a.n, a.step_size, a.bc2_sqrt = p.numel(), step_size, bc2s
-        _lib.call("kgat_adam_multi_f32", arr, len(chunk), beta1, beta2, eps, stream_ptr(chunk[0][0].device))
+        _lib.call("kgat_adam_multi_ex_f32", arr, len(chunk), beta1, beta2, eps, _skip_ptr(skip),
+                  stream_ptr(chunk[0][0].device))
     _ev_end(tok)
 
 

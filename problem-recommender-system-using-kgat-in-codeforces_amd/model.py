@@ -123,16 +123,22 @@ class _IdGuard:
     nn.Embedding gathers raise IndexError, model.py:188-191, 219-222, 389-391).
 
     Host ids are checked on the host, at once.  Device ids are checked on the device without
-    a host synchronisation (kgat_ids_check: one launch copies them, zeroes any id outside
-    [0, bound) so no kernel reads out of range, and sets a flag in pinned host memory); the flag
-    is read after the call's event and IndexError is raised at the model's next call (or by
-    ``raise_pending(block=True)``) -- the way PyTorch reports a device-side index error.
-    ``update_cf_weights`` / ``update_kg_weights`` wait for the flag (block=True), so a step whose
-    ids were bad raises there, before the optimiser moves any parameter."""
+    a host synchronisation (kgat_ids_check_ex: one launch copies them, zeroes any id outside
+    [0, bound) so no kernel reads out of range, and sets a flag in pinned host memory and one in
+    device memory); the host flag is read after the call's event and IndexError is raised at the
+    model's next call (or by ``raise_pending(block=True)``) -- the way PyTorch reports a
+    device-side index error.  The device flag is the optimiser kernels' skip flag
+    (``update_cf_weights`` / ``update_kg_weights`` pass it): a step whose ids were bad moves no
+    parameter and no Adam moment, although the host learns of it only later; it is cleared when
+    the error is raised."""
 
     def __init__(self):
-        self._host = self._event = None
+        self._host = self._event = self._dev = None
         self._pending = None
+
+    def skip_flag(self) -> torch.Tensor | None:
+        """The device int32 flag the optimiser kernels read (None before any device-id check)."""
+        return self._dev
 
     def raise_pending(self, block: bool = False) -> None:
         if self._pending is None or (not block and not self._event.query()):
@@ -142,7 +148,10 @@ class _IdGuard:
         self._pending = None
         if int(self._host[0]):
             self._host.zero_()
-            raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed)")
+            if self._dev is not None:
+                kernels.fill(self._dev.view(torch.float32), 0.0)  # int32 0 == float 0.0 bits
+            raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed, "
+                             f"and no optimiser step after it moved a parameter)")
 
     def check(self, what: str, ids, bound: int, device, more=()) -> list[torch.Tensor]:
         """int64 device copies of ``ids`` (each as given, flattened), validated against [0, bound);
@@ -162,6 +171,7 @@ class _IdGuard:
             # no copy launch per call)
             self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._event = torch.cuda.Event()
+            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
         outs = []
         for g, b in groups:
             src = [torch.as_tensor(t).to(device).long().reshape(-1).contiguous() for t in g]
@@ -174,8 +184,8 @@ class _IdGuard:
                     d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
                 d.count = len(part)
                 off = sum(sizes[:i])
-                _lib.call("kgat_ids_check", ctypes.byref(d), b, out.data_ptr() + 8 * off, self._host.data_ptr(),
-                          stream_ptr(device))
+                _lib.call("kgat_ids_check_ex", ctypes.byref(d), b, out.data_ptr() + 8 * off, self._host.data_ptr(),
+                          self._dev.data_ptr(), stream_ptr(device))
             outs += list(out[:sum(sizes)].split(sizes))
         self._event.record()
         self._pending = what
@@ -225,8 +235,8 @@ class _TableUpdate:
         self.pending = None
         p = self.param.data
 
-        def run(m, v, step_size, bc2s, b1, b2, eps):
-            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps)
+        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
+            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip)
         return run
 
 
@@ -283,8 +293,8 @@ class _KGTableUpdate:
         self.pending = None
         p, row_map = self.param.data, self._map
 
-        def run(m, v, step_size, bc2s, b1, b2, eps):
-            kernels.adam_rows(p, m, v, row_map, Gc, step_size, b1, b2, bc2s, eps)
+        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
+            kernels.adam_rows(p, m, v, row_map, Gc, step_size, b1, b2, bc2s, eps, skip)
             kernels.frontier_reset(rows, row_map)
         return run
 
@@ -820,9 +830,9 @@ class KGAT(nn.Module):
     def update_cf_weights(self, row_ranges: dict | None = None) -> None:
         """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all.
         A deferred table gradient (fuse_table_update) is stepped by the fused product + Adam."""
-        # a device-side id error of this step's forward surfaces here, before any parameter moves
-        # (one wait on the id check's event: the host stays within the step the GPU runs)
-        self._ids.raise_pending(block=True)
+        # an earlier step's device-side id error surfaces here; this step's own is caught on the
+        # device: its optimiser kernels read the check's flag and leave every parameter as it is
+        self._ids.raise_pending()
         tu = self._table_update
         fused = None
         if tu.pending is not None:
@@ -833,12 +843,12 @@ class KGAT(nn.Module):
                 tu.materialize()
             else:
                 fused = {id(tu.param): tu.launch()}
-        self._cf_optimizer.step(row_ranges, fused=fused)
+        self._cf_optimizer.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
         self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
         """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
-        self._ids.raise_pending(block=True)
+        self._ids.raise_pending()
         self._table_update.materialize()
         ktu = self._kg_table_update
         fused = None
@@ -847,7 +857,7 @@ class KGAT(nn.Module):
                 ktu.materialize()
             else:
                 fused = {id(ktu.param): ktu.launch()}
-        self._kg_optimizer.step(row_ranges, fused=fused)
+        self._kg_optimizer.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
         self._kg_optimizer.zero_grad()
 
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:

@@ -35,7 +35,8 @@ class FusedAdam:
         return st, self.lr / (1.0 - self.beta1 ** t), math.sqrt(1.0 - self.beta2 ** t)
 
     @torch.no_grad()
-    def step(self, row_ranges: dict | None = None, fused: dict | None = None) -> None:
+    def step(self, row_ranges: dict | None = None, fused: dict | None = None,
+             skip: torch.Tensor | None = None) -> None:
         """Every parameter with a gradient in one kgat_adam_multi_f32 launch (per 16 tensors).
 
         ``row_ranges`` {id(param): [(r0, r1), ...]} restricts a parameter's update to those
@@ -45,7 +46,10 @@ class FusedAdam:
         ``fused`` {id(param): launch} steps a parameter whose gradient was never materialised
         (grad None): ``launch(exp_avg, exp_avg_sq, step_size, bc2_sqrt, beta1, beta2, eps)``
         runs the kernel that computes the gradient and applies this step to it
-        (model._TableUpdate: the table's layer-0 A^T product fused with its Adam)."""
+        (model._TableUpdate: the table's layer-0 A^T product fused with its Adam).
+
+        ``skip``: a device int32 flag (the model's device-side id check); when it is set as the
+        kernels run, no parameter or moment moves (the step counters still advance)."""
         items = []
         for p in self.params:
             launch = fused.get(id(p)) if fused else None
@@ -56,7 +60,7 @@ class FusedAdam:
                     raise RuntimeError("FusedAdam: a parameter stepped by a fused launch also has a .grad "
                                        "(materialise the deferred gradient into it first)")
                 st, step_size, bc2s = self._advance(id(p), p.data)
-                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps)
+                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
                 continue
             g = p.grad
             if g is None:
@@ -71,7 +75,7 @@ class FusedAdam:
                 st, step_size, bc2s = self._advance(key, pv)
                 items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
         if items:
-            kernels.adam_multi(items, self.beta1, self.beta2, self.eps)
+            kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         for p in self.params:

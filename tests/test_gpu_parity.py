@@ -1566,22 +1566,43 @@ def test_fused_kg_table_update_bit_identical(pkg, dim, batch):
     assert int((b._kg_table_update.node_map() >= 0).sum()) == 0  # the batch-row map is reset
 
 
-def test_device_id_error_raised_before_update(pkg):
-    """a device-side id out of range raises at update_cf_weights, before the
-    optimiser moves any parameter (the check's flag is waited for there)."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_device_id_error_moves_no_parameter(pkg, fused):
+    """a device-side id out of range moves no parameter.  The check runs on the
+    device without a host synchronisation (kgat_ids_check_ex); its device flag is the optimiser
+    kernels' skip flag, so update_cf_weights / update_kg_weights leave the table, the weights and
+    both Adam moments as they were (with and without the fused table updates), and IndexError is
+    raised at a later call; after it the flag is clear and training steps normally again."""
     graph_mod, _ = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(6000, 60000, seed=11)
     lay = graph_mod.build_layout(U, E, inter, trip)
+    torch.manual_seed(5)
     m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32]))
     m.attach_graph(lay, DEV)
     m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-    before = m._user_entity_embedding.weight.detach().clone()
-    bad = torch.full((16,), U + E + 5, dtype=torch.int64, device=DEV)
+    m.fuse_table_update = m.fuse_kg_table_update = fused
     ok = torch.zeros(16, dtype=torch.int64, device=DEV)
+    m(ok, ok + 1, ok + 2, mode=pkg.KGATMode.TRAIN_CF).backward()  # one good step: moments exist
+    m.update_cf_weights()
+    torch.cuda.synchronize()
+    before = {k: v.detach().clone() for k, v in m.named_parameters() if not v.is_sparse}
+    st = m._cf_optimizer.state[id(m._user_entity_embedding.weight)]
+    mom = (st["exp_avg"].clone(), st["exp_avg_sq"].clone())
+    bad = torch.full((16,), U + E + 5, dtype=torch.int64, device=DEV)
     m(ok, bad, ok, mode=pkg.KGATMode.TRAIN_CF).backward()
+    m.update_cf_weights()  # may or may not raise yet; nothing may move either way
+    torch.cuda.synchronize()
+    for k, v in m.named_parameters():
+        if not v.is_sparse:
+            assert torch.equal(v.detach(), before[k]), k
+    assert torch.equal(st["exp_avg"], mom[0]) and torch.equal(st["exp_avg_sq"], mom[1])
     with pytest.raises(IndexError):
-        m.update_cf_weights()
-    assert torch.equal(m._user_entity_embedding.weight.detach(), before)
+        m.raise_pending(block=True)
+    kg = [ok, ok.clone(), ok + 3, ok + 4]
+    m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
+    m.update_kg_weights()
+    torch.cuda.synchronize()
+    assert not torch.equal(m._user_entity_embedding.weight.detach(), before["_user_entity_embedding.weight"])
 
 
 @pytest.mark.parametrize("layers", [[64], [64, 32], [64, 64], [64, 32, 16]])
