@@ -229,6 +229,10 @@ class _TableUpdate:
         else:
             kernels.add_(self.param.grad, g)
 
+    def discard(self) -> None:
+        """Drop the pending gradient (a step whose update is abandoned: update_cf_weights raised)."""
+        self.pending = None
+
     def launch(self):
         """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...))."""
         graph, src_map, Xc, Yc, rank = self.pending
@@ -286,6 +290,14 @@ class _KGTableUpdate:
             self.param.grad = g
         else:
             kernels.add_(self.param.grad, g)
+
+    def discard(self) -> None:
+        """Drop the pending rows (update_kg_weights raised); the node map is reset for the next step."""
+        if self.pending is None:
+            return
+        rows, _ = self.pending
+        self.pending = None
+        kernels.frontier_reset(rows, self._map)
 
     def launch(self):
         """The table's Adam step on the compact gradient (FusedAdam.step(fused=...))."""
@@ -827,12 +839,24 @@ class KGAT(nn.Module):
         """Raise the IndexError of a device-side id check that has not been reported yet."""
         self._ids.raise_pending(block)
 
+    def _raise_or_abandon(self, opt) -> None:
+        """Report a device-side id error before an optimiser step.  The step it interrupts is
+        abandoned as a whole, as the reference's raising forward leaves no gradient behind: its
+        gradients and deferred table updates are dropped, so no later step sums them in."""
+        try:
+            self._ids.raise_pending()
+        except IndexError:
+            self._table_update.discard()
+            self._kg_table_update.discard()
+            opt.zero_grad()
+            raise
+
     def update_cf_weights(self, row_ranges: dict | None = None) -> None:
         """``row_ranges``: the rows this rank steps (replicas.ShardedGradSync); None = all.
         A deferred table gradient (fuse_table_update) is stepped by the fused product + Adam."""
         # an earlier step's device-side id error surfaces here; this step's own is caught on the
         # device: its optimiser kernels read the check's flag and leave every parameter as it is
-        self._ids.raise_pending()
+        self._raise_or_abandon(self._cf_optimizer)
         tu = self._table_update
         fused = None
         if tu.pending is not None:
@@ -848,7 +872,7 @@ class KGAT(nn.Module):
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
         """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
-        self._ids.raise_pending()
+        self._raise_or_abandon(self._kg_optimizer)
         self._table_update.materialize()
         ktu = self._kg_table_update
         fused = None

@@ -1590,14 +1590,19 @@ def test_device_id_error_moves_no_parameter(pkg, fused):
     mom = (st["exp_avg"].clone(), st["exp_avg_sq"].clone())
     bad = torch.full((16,), U + E + 5, dtype=torch.int64, device=DEV)
     m(ok, bad, ok, mode=pkg.KGATMode.TRAIN_CF).backward()
-    m.update_cf_weights()  # may or may not raise yet; nothing may move either way
+    raised = False
+    try:
+        m.update_cf_weights()  # may or may not raise yet (the flag's event may have fired); nothing may move
+    except IndexError:
+        raised = True
     torch.cuda.synchronize()
     for k, v in m.named_parameters():
         if not v.is_sparse:
             assert torch.equal(v.detach(), before[k]), k
     assert torch.equal(st["exp_avg"], mom[0]) and torch.equal(st["exp_avg_sq"], mom[1])
-    with pytest.raises(IndexError):
-        m.raise_pending(block=True)
+    if not raised:
+        with pytest.raises(IndexError):
+            m.raise_pending(block=True)
     kg = [ok, ok.clone(), ok + 3, ok + 4]
     m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
     m.update_kg_weights()
