@@ -742,10 +742,43 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         "cpu_baseline_note": "not run: the row-sharded config never runs at N = 1 and its CPU step "
                              "(50M x 704 fp32 tables + autograd state) exceeds host RAM",
     }
+    if not args.no_frontier_leg:
+        # the same step with RowShardedKGAT.frontier_forward: the last layer on the batch rows F, layer L-2
+        # on the first hop F + N(F) (this rank's part, marked from its A^T rows), the lower layers whole --
+        # the rows the loss reads, with the whole-shard forward's bits (checked below); not in `value`
+        model.frontier_forward = True
+        fel, fev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
+        model.frontier_forward = False
+        fms = fel / args.steps * 1e3
+        res["frontier_forward"] = {
+            "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
+            "bit_identical_to_full": sharded_frontier_matches_full(model, pkg, batches[0]),
+            "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer L-1 on the batch rows, "
+                    "layer L-2 on F + N(F)); not counted in value (it does not visit every edge)"}
     if whole is not None and rank == 0:
         log("bench-scale parity: eval-mode propagation / CF loss / table gradient vs the oracle on the CPU ...")
         res["parity"] = sharded_parity(model, pkg, batches[0], whole, ckg.n_nodes, cfg)
     return res
+
+
+def sharded_frontier_matches_full(model, pkg, batch) -> dict:
+    """One train-mode CF loss + backward of the row-sharded model with and without frontier_forward (the
+    same step counter, so the same dropout seeds; no optimizer step): the loss, this rank's table
+    gradient rows and every aggregator weight gradient compared bit for bit."""
+    outs, step0 = [], model._step
+    for frontier in (False, True):
+        model.zero_grad(set_to_none=True)
+        model.frontier_forward = frontier
+        model._step = step0
+        loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
+        loss.backward()
+        outs.append([loss.detach().clone()] + [p.grad.detach().clone() for p in model.parameters()
+                                               if not p.is_sparse and p.grad is not None])
+    model.frontier_forward = False
+    model.zero_grad(set_to_none=True)
+    a, b = outs
+    return {"pass": len(a) == len(b) and all(torch.equal(x, y) for x, y in zip(a, b)), "tensors": len(a),
+            "what": "loss + table-shard and aggregator gradients of one train-mode CF step"}
 
 
 def sharded_parity(model, pkg, batch, whole, n: int, cfg: dict) -> dict:

@@ -170,6 +170,15 @@ int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, con
                                   const int32_t *out_count, float *Y, int64_t ldy, int32_t d, float *workspace,
                                   int64_t workspace_floats, void *stream);
 
+/* Rows of A that are in a node set or have an edge into it: hit[r] = 1 iff bit (row0 + r) of
+ * bits or bit col of one of row r's edges is set, else 0 (n_bits: the bitmap's size in nodes,
+ * covering every column and row0 + n_rows).  With A = a shard's rows of A^T and the bitmap of
+ * the batch rows F, the shard's part of the first hop F + N(F) (A^T[j, f] != 0 <=> A[f, j] != 0):
+ * the row set the row-sharded frontier forward computes layer L-2 on.  Long rows are scanned by
+ * their segments (A's long-row plan). */
+int kgat_csr_mark_rows(const kgat_csr *A, const uint32_t *bits, int64_t n_bits, int64_t row0, int32_t *hit,
+                       void *stream);
+
 /* The forward restricted to a hop set (KGAT.frontier_forward; the row set a
  * training step's loss can reach, see model._CFLoss): the dense product
  * Y[r] = (A . X)[r] for the rows r of an output set only -- out_rows[k] for
@@ -313,6 +322,16 @@ int kgat_biinter_fwd_gemm_f32(const float *X, int64_t ldx, const float *S, int64
                               const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
                               int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
                               float *state, float *work, int64_t work_floats, void *stream);
+/* The GEMM forward on the rows rows[0..m) of X / S only (node ids in [0, n_rows), -1 = padding,
+ * skipped): each listed row's H row, state (pre-activations, norm) and dropout draws land at its
+ * own index, bit for bit the whole-table call's; other rows are untouched.  The row-sharded
+ * frontier forward of a wide layer on the first hop.  work: kgat_biinter_gemm_rows_work_floats(m). */
+int64_t kgat_biinter_gemm_rows_work_floats(int64_t m, int32_t d_in, int32_t d_out);
+int kgat_biinter_fwd_gemm_rows_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const int32_t *rows,
+                                   int64_t m, const float *W1, const float *b1, const float *W2, const float *b2,
+                                   float *H, int64_t ldh, int64_t n_rows, int32_t d_in, int32_t d_out,
+                                   float dropout_p, uint64_t seed, float *state, float *work, int64_t work_floats,
+                                   void *stream);
 int kgat_biinter_bwd_gemm_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
                               int64_t ldh, float *state, const float *dH, int64_t lddh, const float *W1,
                               const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds, float *dW1,
@@ -599,6 +618,12 @@ int kgat_ids_check_ex(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t 
  * map of a row list (the row-sharded backward's global batch rows, whose compact order is the
  * host's sorted unique ids).  kgat_frontier_reset(ids, n, node_map) restores -1. */
 int kgat_map_build(const int32_t *ids, int64_t n, int32_t *node_map, void *stream);
+
+/* out[i] = a[i] < 0 ? -1 : (b ? b[a[i]] : a[i]) + offset, -1 where b[a[i]] < 0 (out may alias a
+ * when b is null).  Index plumbing of the row-sharded hop backward: a batch row's compact index
+ * -> its position in a hop list (b = the hop list's node map), local -> global row ids (b null,
+ * offset = the shard's first row). */
+int kgat_map_compose(const int32_t *a, int64_t n, const int32_t *b, int32_t offset, int32_t *out, void *stream);
 
 /* Fill n floats with a value. */
 int kgat_fill_f32(float *dst, int64_t n, float value, void *stream);

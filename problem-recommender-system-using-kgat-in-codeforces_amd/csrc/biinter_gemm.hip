@@ -15,6 +15,7 @@
 //             dW = dA^T U, dB^T M; db = column sums              (gemm_f32 split-K slabs)
 // Dropout draws are the fused kernels' (one 64-bit hash per node, 16-column
 // group of 4 blocks), so both paths drop the same elements.
+#include <cstdlib>
 #include <utility>
 
 #include "common.hpp"
@@ -35,10 +36,10 @@ __device__ __forceinline__ uint32_t gemm_threshold(float p) {
 }
 
 // U = X+S, M = X*S with row pitch d+4 (16-byte aligned rows; the 4 pad columns are written 1, 0, 0, 0
-// and never read)
+// and never read).  rows (nullable): row r of U / M comes from row rows[r] of X / S (-1: zeros).
 __global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
                                                  int64_t lds, float* __restrict__ U, float* __restrict__ M, int64_t n,
-                                                 int d) {
+                                                 int d, const int32_t* __restrict__ rows = nullptr) {
   const int q = d / 4 + 1;  // float4 groups per padded row
   const int64_t total = n * q;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -52,8 +53,10 @@ __global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, in
       *reinterpret_cast<float4*>(M + r * ldu + c) = e;
       continue;
     }
-    const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + c);
-    const float4 s = *reinterpret_cast<const float4*>(S + r * lds + c);
+    const int64_t src = rows != nullptr ? static_cast<int64_t>(rows[r]) : r;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 x = src >= 0 ? *reinterpret_cast<const float4*>(X + src * ldx + c) : z;
+    const float4 s = src >= 0 ? *reinterpret_cast<const float4*>(S + src * lds + c) : z;
     *reinterpret_cast<float4*>(U + r * ldu + c) = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
     *reinterpret_cast<float4*>(M + r * ldu + c) = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
   }
@@ -100,14 +103,23 @@ __global__ __launch_bounds__(256) void wslab_reduce_kernel(const float* __restri
   else db[o] = acc;
 }
 
-// one wave per row; P1/P2 [n, dout] in, P+b written back (the backward's sign source)
+// one wave per row; P1/P2 [n, dout] in, P+b written to P1o/P2o (the backward's sign source; in place
+// when they are P1/P2).  rows (nullable): row r is node rows[r] (-1: padding, nothing written) --
+// its H row, norm, state rows and dropout draws are that node's, as in the whole-table call.
 __global__ __launch_bounds__(256) void epi_fwd_kernel(float* __restrict__ P1, float* __restrict__ P2,
                                                       const float* __restrict__ b1, const float* __restrict__ b2,
                                                       float* __restrict__ H, int64_t ldh, float* __restrict__ norm,
-                                                      int64_t n, int dout, float p, uint64_t seed) {
+                                                      int64_t n, int dout, float p, uint64_t seed,
+                                                      const int32_t* __restrict__ rows = nullptr,
+                                                      float* __restrict__ P1o = nullptr,
+                                                      float* __restrict__ P2o = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (r >= n) return;
+  const int64_t node = rows != nullptr ? static_cast<int64_t>(rows[r]) : r;
+  if (node < 0) return;
+  if (P1o == nullptr) P1o = P1;
+  if (P2o == nullptr) P2o = P2;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t thr = gemm_threshold(p);
   float v[16];
@@ -115,18 +127,18 @@ __global__ __launch_bounds__(256) void epi_fwd_kernel(float* __restrict__ P1, fl
   int cnt = 0;
   for (int c = lane; c < dout; c += 64, ++cnt) {
     const float pa = P1[r * dout + c] + b1[c], pb = P2[r * dout + c] + b2[c];
-    P1[r * dout + c] = pa;
-    P2[r * dout + c] = pb;
+    P1o[node * dout + c] = pa;
+    P2o[node * dout + c] = pb;
     float g = lrelu(pa) + lrelu(pb);
-    if (p > 0.f) g = gemm_keep(seed, r, c, dout, thr) ? g * scale : 0.f;
+    if (p > 0.f) g = gemm_keep(seed, node, c, dout, thr) ? g * scale : 0.f;
     v[cnt] = g;
     sq = fmaf(g, g, sq);
   }
   const float nrm = sqrtf(wave_sum(sq));
   const float inv = 1.f / fmaxf(nrm, kNormEps);
   cnt = 0;
-  for (int c = lane; c < dout; c += 64, ++cnt) H[r * ldh + c] = v[cnt] * inv;
-  if (lane == 0) norm[r] = nrm >= kNormEps ? nrm : -kNormEps;
+  for (int c = lane; c < dout; c += 64, ++cnt) H[node * ldh + c] = v[cnt] * inv;
+  if (lane == 0) norm[node] = nrm >= kNormEps ? nrm : -kNormEps;
 }
 
 // one wave per row: dA, dB written over the P+b state
@@ -229,6 +241,18 @@ inline int64_t wslab_count(int64_t n) { return (n + gemm_chunk(n) - 1) / gemm_ch
     if (int e_ = (call)) return e_;    \
   } while (0)
 
+// The two products of each direction in one dual-GEMM launch (gemm.hip's dual_gemm_kernel: the
+// (X+S, X*S) operands formed at load, dXd / dS formed in the du / dm epilogue -- no U / M arrays,
+// no um / dxs passes; each product the single GEMM's bits).  KGAT_DUAL_GEMM=0: the separate
+// launches (A/B switch).
+inline bool dual_gemm_on() {
+  static const bool on = [] {
+    const char* e = getenv("KGAT_DUAL_GEMM");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 }  // namespace kgat
 
 namespace kgat {
@@ -253,15 +277,28 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   float* slab1 = work + 2 * n * ldu;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
-  // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
-  KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
-  KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
-  hipLaunchKernelGGL(um_kernel, dim3(blocks_for(n * (d_in / 4 + 1), 256, kCUs * 8)), dim3(256), 0,
-                     st, X, ldx, S, lds, U, M, n, d_in);
-  KGAT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
-                     lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
-  KGAT_LAUNCH_CHECK();
+  const bool dual = dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0;
+  if (dual) {
+    // du = dA W1, dm = dB W2, then dXd = du + dm*S, dS = du + dm*X in the epilogue: one launch
+    DualGemm g;
+    g.dxs = true;
+    g.M = n, g.N = d_in, g.K = d_out;
+    g.A1 = dA, g.A2 = dB, g.lda1 = g.lda2 = d_out;
+    g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
+    g.C1 = dXd, g.C2 = dS, g.ldc1 = lddxd, g.ldc2 = ldds;
+    g.X = X, g.S = S, g.ldx = ldx, g.lds = lds;
+    KGAT_GEMM(dual_gemm_f32(g, st));
+  } else {
+    // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
+    KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
+    KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
+    hipLaunchKernelGGL(um_kernel, dim3(blocks_for(n * (d_in / 4 + 1), 256, kCUs * 8)), dim3(256), 0,
+                       st, X, ldx, S, lds, U, M, n, d_in, nullptr);
+    KGAT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
+                       lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
+    KGAT_LAUNCH_CHECK();
+  }
   // [dW | db] = [dA^T U | colsum dA], split over row chunks (deterministic: chunk slabs summed in
   // order): slab_b[d_out, 0:d_in] = dA_b[chunk, d_out]^T . U_b[chunk, d_in], slab_b[:, d_in] = the
   // chunk's column sums of dA, produced by the same GEMM from its A tiles (a [U | 1] operand
@@ -269,14 +306,35 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   const int64_t chunk = gemm_chunk(n);
   const int64_t full = n / chunk, rest = n - full * chunk;
   const int64_t sl_stride = static_cast<int64_t>(ldu) * d_out;
+  if (dual) {
+    // [dW1 | db1], [dW2 | db2] chunk slabs in one launch per batch shape: dA^T (X+S), dB^T (X*S), the
+    // operands formed from X and S at load, the column sums from the dA / dB tiles
+    DualGemm g;
+    g.ta = true, g.b_um = true;
+    g.M = d_out, g.N = d_in;
+    g.lda1 = g.lda2 = d_out, g.ldb1 = ldx, g.ldb2 = lds;
+    g.ldc1 = g.ldc2 = ldu, g.ldcs = ldu;
+    for (int part = 0; part < 2; ++part) {
+      const int64_t nbat = part == 0 ? full : (rest > 0 ? 1 : 0);
+      if (nbat == 0) continue;
+      const int64_t r0 = part == 0 ? 0 : full * chunk;
+      g.K = part == 0 ? chunk : rest, g.batch = nbat;
+      g.A1 = dA + r0 * d_out, g.A2 = dB + r0 * d_out, g.sA1 = g.sA2 = chunk * d_out;
+      g.B1 = X + r0 * ldx, g.B2 = S + r0 * lds, g.sB1 = chunk * ldx, g.sB2 = chunk * lds;
+      g.C1 = slab1 + (part == 0 ? 0 : full) * sl_stride, g.C2 = slab2 + (part == 0 ? 0 : full) * sl_stride;
+      g.sC1 = g.sC2 = sl_stride;
+      g.cs1 = g.C1 + d_in, g.cs2 = g.C2 + d_in, g.sCS1 = g.sCS2 = sl_stride;
+      KGAT_GEMM(dual_gemm_f32(g, st));
+    }
+  }
   for (int mat = 0; mat < 2; ++mat) {
     const float* Um = mat == 0 ? U : M;
     const float* G = mat == 0 ? dA : dB;
     float* sl = mat == 0 ? slab1 : slab2;
-    if (full > 0)
+    if (!dual && full > 0)
       KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, chunk, G, d_out, chunk * d_out, Um, ldu, chunk * ldu, sl, ldu,
                                    sl_stride, sl + d_in, ldu, sl_stride, full, st));
-    if (rest > 0)
+    if (!dual && rest > 0)
       KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, rest, G + full * chunk * d_out, d_out, 0, Um + full * chunk * ldu,
                                    ldu, 0, sl + full * sl_stride, ldu, 0, sl + full * sl_stride + d_in, ldu, 0, 1,
                                    st));
@@ -327,14 +385,58 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   float* P1 = state;
   float* P2 = state + n * d_out;
   float* norm = state + 2 * n * d_out;
-  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
-                     st, X, ldx, S, lds, U, M, n, d_in);
-  KGAT_LAUNCH_CHECK();
-  // P[n, o] = U[n, k] . W[o, k]^T
-  KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
-  KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
+  if (kgat::dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0) {
+    // P1 = (X+S) W1^T, P2 = (X*S) W2^T in one launch, the operands formed at load
+    kgat::DualGemm g;
+    g.tb = true, g.a_um = true;
+    g.M = n, g.N = d_out, g.K = d_in;
+    g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds;
+    g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
+    g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
+    KGAT_GEMM(kgat::dual_gemm_f32(g, st));
+  } else {
+    hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256),
+                       0, st, X, ldx, S, lds, U, M, n, d_in, nullptr);
+    KGAT_LAUNCH_CHECK();
+    // P[n, o] = U[n, k] . W[o, k]^T
+    KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
+    KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
+  }
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh, norm, n, d_out,
                      dropout_p, seed);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int64_t kgat_biinter_gemm_rows_work_floats(int64_t m, int32_t d_in, int32_t d_out) {
+  const int64_t w = kgat_biinter_gemm_work_floats(m, d_in, d_out);
+  return w < 0 ? -1 : w + 2 * m * static_cast<int64_t>(d_out);  // + the compact P1, P2
+}
+
+extern "C" int kgat_biinter_fwd_gemm_rows_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
+                                              const int32_t* rows, int64_t m, const float* W1, const float* b1,
+                                              const float* W2, const float* b2, float* H, int64_t ldh, int64_t n,
+                                              int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
+                                              float* state, float* work, int64_t work_floats, void* stream) {
+  if (!X || !S || !rows || !W1 || !b1 || !W2 || !b2 || !H || !state || n < 0 || m < 0 || !gemm_dims_ok(d_in, d_out))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || (ldx & 3) || (lds & 3) || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return KGAT_ERR_INVALID;
+  if (m == 0) return KGAT_OK;
+  if (!work || work_floats < kgat_biinter_gemm_rows_work_floats(m, d_in, d_out)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int ldu = d_in + 4;
+  float* U = work;
+  float* M = work + m * ldu;
+  float* P1 = work + kgat_biinter_gemm_work_floats(m, d_in, d_out);
+  float* P2 = P1 + m * d_out;
+  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(m * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
+                     st, X, ldx, S, lds, U, M, m, d_in, rows);
+  KGAT_LAUNCH_CHECK();
+  KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
+  KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
+  hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((m + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh,
+                     state + 2 * n * d_out, m, d_out, dropout_p, seed, rows, state, state + n * d_out);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

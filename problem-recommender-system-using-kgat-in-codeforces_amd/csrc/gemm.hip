@@ -210,9 +210,216 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Dual GEMM: two products on the same tile coordinates in one launch,
+//   C1 = op(A1) . op(B1),   C2 = op(A2) . op(B2),
+// each with gemm_kernel's tiling, stage order and MFMA order (so each product has exactly the
+// single kernel's bits).  An operand pair is either two matrices (kSep) or the bi-interaction's
+// (X + S, X * S) formed from one load of X and S (kUM: no U / M array in HBM).  Epilogues:
+// kStore writes C1, C2; kDXS is the bi-interaction backward's dXd = du + dm * S, dS = du + dm * X
+// (C1 = du, C2 = dm; X, S read at the output element), written to C1 / C2.
+enum DualOp { kSep = 0, kUM = 1 };
+enum DualEpi { kStore = 0, kDXS = 1 };
+
+struct DualArgs {
+  const float* A1;
+  const float* A2;
+  int64_t lda1, lda2, sA1, sA2;
+  const float* B1;
+  const float* B2;
+  int64_t ldb1, ldb2, sB1, sB2;
+  float* C1;
+  float* C2;
+  int64_t ldc1, ldc2, sC1, sC2;
+  int64_t M, N, K;
+  float* cs1;  // TA only: column sums of op(A1) / op(A2) over k (nullable)
+  float* cs2;
+  int64_t ldcs, sCS1, sCS2;
+  const float* X;  // kDXS
+  const float* S;
+  int64_t ldx, lds;
+};
+
+// Two stages of one operand pair; kUM turns the loaded (X, S) into (X + S, X * S).
+template <bool KC, int OP>
+struct StagePair {
+  Stage<KC> a, b;
+
+  __device__ __forceinline__ void load(const float* __restrict__ P1, int64_t ld1, const float* __restrict__ P2,
+                                       int64_t ld2, int64_t rows, int64_t K, int64_t r0, int64_t k0, int t) {
+    a.load(P1, ld1, rows, K, r0, k0, t);
+    b.load(P2, ld2, rows, K, r0, k0, t);
+    if (OP == kUM) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float4 x = a.v[q], s = b.v[q];
+        a.v[q] = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
+        b.v[q] = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ l1, float* __restrict__ l2, int t) const {
+    a.store(l1, t);
+    b.store(l2, t);
+  }
+};
+
+template <bool TA, bool TB, int AOP, int BOP, int EPI>
+__global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
+  __shared__ float lds[2][4][kStageFloats];  // [buffer][A1 | A2 | B1 | B2][operand image]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int tiles_n = static_cast<int>((g.N + kBN - 1) / kBN);
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x / tiles_n) * kBM;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x % tiles_n) * kBN;
+  const int64_t z = blockIdx.z;
+  const float* __restrict__ A1 = g.A1 + z * g.sA1;
+  const float* __restrict__ A2 = g.A2 + z * g.sA2;
+  const float* __restrict__ B1 = g.B1 + z * g.sB1;
+  const float* __restrict__ B2 = g.B2 + z * g.sB2;
+
+  StagePair<!TA, AOP> sa;
+  StagePair<TB, BOP> sb;
+  floatx16 acc1[2][2], acc2[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc1[i][j][q] = acc2[i][j][q] = 0.f;
+
+  const int nk = static_cast<int>((g.K + kBK - 1) / kBK);
+  const bool do_cs = TA && g.cs1 != nullptr && n0 == 0;
+  float4 cs1 = make_float4(0.f, 0.f, 0.f, 0.f), cs2 = cs1;
+  sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, 0, t);
+  sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, 0, t);
+  sa.store(lds[0][0], lds[0][1], t);
+  sb.store(lds[0][2], lds[0][3], t);
+  if (do_cs) {
+    add_stage(cs1, sa.a);
+    add_stage(cs2, sa.b);
+  }
+  __syncthreads();
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const int r = lane & 31, h = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * kBK, t);
+      sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * kBK, t);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // product p: its operands' 8 k-values per tile row, then its MFMAs
+      float fa[2][8], fb[2][8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        Stage<!TA>::read(lds[cur][p], wm + 32 * i + r, h, fa[i]);
+        Stage<TB>::read(lds[cur][2 + p], wn + 32 * i + r, h, fb[i]);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (p == 0) acc1[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc1[i][j], 0, 0, 0);
+            else acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc2[i][j], 0, 0, 0);
+          }
+    }
+    if (kt + 1 < nk) {
+      sa.store(lds[cur ^ 1][0], lds[cur ^ 1][1], t);
+      sb.store(lds[cur ^ 1][2], lds[cur ^ 1][3], t);
+      if (do_cs) {
+        add_stage(cs1, sa.a);
+        add_stage(cs2, sa.b);
+      }
+    }
+    __syncthreads();
+  }
+  if (do_cs) {
+    __shared__ float4 cpart[2][kThreads];
+    cpart[0][t] = cs1;
+    cpart[1][t] = cs2;
+    __syncthreads();
+    if (t < 64) {
+      const int which = t >> 5, tt = t & 31;
+      float4 s = cpart[which][tt];
+      for (int j = 1; j < 8; ++j) {
+        const float4 o = cpart[which][tt + 32 * j];
+        s.x += o.x;
+        s.y += o.y;
+        s.z += o.z;
+        s.w += o.w;
+      }
+      float* cs = which == 0 ? g.cs1 + z * g.sCS1 : g.cs2 + z * g.sCS2;
+      const float v[4] = {s.x, s.y, s.z, s.w};
+      for (int i = 0; i < 4; ++i)
+        if (m0 + 4 * tt + i < g.M) cs[(m0 + 4 * tt + i) * g.ldcs] = v[i];
+    }
+  }
+  float* __restrict__ C1 = g.C1 + z * g.sC1;
+  float* __restrict__ C2 = g.C2 + z * g.sC2;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn + 32 * j + r;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (row >= g.M) continue;
+        if (EPI == kDXS) {
+          const float du = acc1[i][j][q], dm = acc2[i][j][q];
+          C1[row * g.ldc1 + col] = fmaf(dm, g.S[row * g.lds + col], du);
+          C2[row * g.ldc2 + col] = fmaf(dm, g.X[row * g.ldx + col], du);
+        } else {
+          C1[row * g.ldc1 + col] = acc1[i][j][q];
+          C2[row * g.ldc2 + col] = acc2[i][j][q];
+        }
+      }
+    }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
+
+int dual_gemm_f32(const DualGemm& d, hipStream_t st) {
+  const int64_t M = d.M, N = d.N, K = d.K;
+  if (M < 0 || N < 0 || K < 0 || d.batch < 0) return KGAT_ERR_INVALID;
+  if (M == 0 || N == 0 || d.batch == 0) return KGAT_OK;
+  if (!d.A1 || !d.A2 || !d.B1 || !d.B2 || !d.C1 || !d.C2 || K == 0) return KGAT_ERR_INVALID;
+  if ((d.lda1 | d.lda2 | d.ldb1 | d.ldb2 | d.sA1 | d.sA2 | d.sB1 | d.sB2) & 3) return KGAT_ERR_INVALID;
+  if (!aligned16(d.A1) || !aligned16(d.A2) || !aligned16(d.B1) || !aligned16(d.B2)) return KGAT_ERR_INVALID;
+  if ((d.ta ? M : K) & 3 || (d.tb ? K : N) & 3) return KGAT_ERR_INVALID;
+  if (d.lda1 < (d.ta ? M : K) || d.lda2 < (d.ta ? M : K) || d.ldb1 < (d.tb ? K : N) || d.ldb2 < (d.tb ? K : N) ||
+      d.ldc1 < N || d.ldc2 < N)
+    return KGAT_ERR_INVALID;
+  if (d.dxs && (!d.X || !d.S || d.ldx < N || d.lds < N || d.batch != 1)) return KGAT_ERR_INVALID;
+  if (d.a_um && d.ta) return KGAT_ERR_INVALID;  // (X+S, X*S) pairs: row-major k-contiguous A only
+  if (d.b_um && d.tb) return KGAT_ERR_INVALID;  // ... and row-major [K, N] B only
+  if ((d.cs1 != nullptr) != (d.cs2 != nullptr) || (d.cs1 && !d.ta)) return KGAT_ERR_INVALID;
+  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  if (tiles > 0x7fffffff || d.batch > 65535) return KGAT_ERR_INVALID;
+  DualArgs g{d.A1, d.A2, d.lda1, d.lda2, d.sA1, d.sA2, d.B1, d.B2, d.ldb1, d.ldb2, d.sB1, d.sB2,
+             d.C1, d.C2, d.ldc1, d.ldc2, d.sC1, d.sC2, M, N, K, d.cs1, d.cs2, d.ldcs, d.sCS1, d.sCS2,
+             d.X, d.S, d.ldx, d.lds};
+  const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(d.batch));
+  // the three forms the bi-interaction uses: forward (UM x W^T), backward du/dm + dXd/dS
+  // epilogue (dA.W), weight gradients (dA^T x UM, split-K batches, column sums)
+  if (!d.ta && d.tb && d.a_um && !d.b_um && !d.dxs)
+    hipLaunchKernelGGL((dual_gemm_kernel<false, true, kUM, kSep, kStore>), grid, dim3(kThreads), 0, st, g);
+  else if (!d.ta && !d.tb && !d.a_um && !d.b_um && d.dxs)
+    hipLaunchKernelGGL((dual_gemm_kernel<false, false, kSep, kSep, kDXS>), grid, dim3(kThreads), 0, st, g);
+  else if (d.ta && !d.tb && !d.a_um && d.b_um && !d.dxs)
+    hipLaunchKernelGGL((dual_gemm_kernel<true, false, kSep, kUM, kStore>), grid, dim3(kThreads), 0, st, g);
+  else if (!d.ta && d.tb && !d.a_um && !d.b_um && !d.dxs)
+    hipLaunchKernelGGL((dual_gemm_kernel<false, true, kSep, kSep, kStore>), grid, dim3(kThreads), 0, st, g);
+  else
+    return KGAT_ERR_UNSUPPORTED_DIM;
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
 
 int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int64_t sA,
              const float* B, int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, int64_t batch,

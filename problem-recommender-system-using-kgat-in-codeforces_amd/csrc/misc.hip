@@ -74,6 +74,18 @@ __global__ __launch_bounds__(256) void map_build_kernel(const int32_t* __restric
     if (ids[i] >= 0) node_map[ids[i]] = static_cast<int32_t>(i);
 }
 
+// out[i] = a[i] < 0 ? -1 : (b ? b[a[i]] : a[i]) + offset  (b[.] < 0 stays -1)
+__global__ __launch_bounds__(256) void map_compose_kernel(const int32_t* __restrict__ a, int64_t n,
+                                                          const int32_t* __restrict__ b, int32_t offset,
+                                                          int32_t* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int32_t x = a[i];
+    const int32_t y = x < 0 ? -1 : (b != nullptr ? b[x] : x);
+    out[i] = y < 0 ? -1 : y + offset;
+  }
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ dst, int64_t n, float value) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = value;
@@ -429,6 +441,16 @@ extern "C" int kgat_map_build(const int32_t* ids, int64_t n, int32_t* node_map, 
   if (n == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::map_build_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), ids, n, node_map);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_map_compose(const int32_t* a, int64_t n, const int32_t* b, int32_t offset, int32_t* out,
+                                void* stream) {
+  if (n < 0 || (n && (!a || !out))) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::map_compose_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), a, n, b, offset, out);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

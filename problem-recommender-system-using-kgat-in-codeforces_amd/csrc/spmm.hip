@@ -320,6 +320,41 @@ __global__ __launch_bounds__(256) void frontier_mark_kernel(kgat_csr A, const in
   }
 }
 
+// hit[r] = 1 for every row r of A that is itself in the set (bit row0 + r of bits) or has an edge
+// into it (bit col): the next row set of the frontier chain, computed by the rows that pull from it
+// (the row-sharded forward marks its rows of the first hop F + N(F) from its rows of A^T).  hit is
+// zeroed by the caller; lanes only ever store 1.  Blocks [0, seg_blocks): one long-row segment per
+// wave (64 lanes over <= seg_len edges); the rest: 16-lane groups, one short row each.
+__global__ __launch_bounds__(256) void csr_mark_rows_kernel(kgat_csr A, const uint32_t* __restrict__ bits,
+                                                            int64_t row0, int32_t* __restrict__ hit,
+                                                            int seg_blocks) {
+  if (static_cast<int>(blockIdx.x) < seg_blocks) {
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= A.n_seg) return;
+    const int row = A.seg_row[s];
+    const int64_t beg = A.seg_beg[s];
+    const int64_t row_end = A.rowptr[row + 1];
+    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+    for (int64_t e = beg + (threadIdx.x & 63); e < end; e += 64)
+      if (bit_of(bits, A.col[e])) {
+        hit[row] = 1;
+        break;
+      }
+    return;
+  }
+  const int64_t r = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 256 + threadIdx.x) >> 4;
+  const int lane = threadIdx.x & 15;
+  if (r >= A.n_rows) return;
+  const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+  if (lane == 0 && bit_of(bits, row0 + r)) hit[r] = 1;
+  if (end - beg > A.long_threshold) return;  // the segment waves scan it
+  for (int64_t e = beg + lane; e < end; e += 16)
+    if (bit_of(bits, A.col[e])) {
+      hit[r] = 1;
+      break;
+    }
+}
+
 struct Popc {
   __device__ int32_t operator()(uint32_t w) const { return __popc(w); }
 };
@@ -656,6 +691,21 @@ extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t
   const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr,
                   out_bits, nullptr, out_rows, out_count};
   return dispatch<kRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int kgat_csr_mark_rows(const kgat_csr* A, const uint32_t* bits, int64_t n_bits, int64_t row0,
+                                  int32_t* hit, void* stream) {
+  if (!A || !bits || !hit || A->n_rows < 0 || row0 < 0 || n_bits < row0 + A->n_rows) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (A->n_rows == 0) return KGAT_OK;
+  if (hipMemsetAsync(hit, 0, static_cast<size_t>(A->n_rows) * sizeof(int32_t), st) != hipSuccess)
+    return KGAT_ERR_INVALID;
+  const int seg_blocks = (A->n_seg + 3) / 4;
+  const int64_t grid = seg_blocks + (A->n_rows + 15) / 16;
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::csr_mark_rows_kernel, dim3(grid), dim3(256), 0, st, *A, bits, row0, hit, seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 extern "C" int kgat_map_rank(const int32_t* node_map, int64_t n, uint64_t* rank, void* stream) {

@@ -120,9 +120,12 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
 
 def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.Tensor,
                       Yc_init: torch.Tensor | None = None, row0: int = 0,
-                      src_bits: torch.Tensor | None = None, src_rank: torch.Tensor | None = None) -> torch.Tensor:
+                      src_bits: torch.Tensor | None = None, src_rank: torch.Tensor | None = None,
+                      row_hit: torch.Tensor | None = None) -> torch.Tensor:
     """Y = B . X for a rectangular block where X[c] = Xc[src_map[c]] (-1 => zero row); with Yc_init,
-    local row r also gets Yc_init[src_map[row0 + r]] (B = rows [row0, ...) of a square matrix)."""
+    local row r also gets Yc_init[src_map[row0 + r]] (B = rows [row0, ...) of a square matrix).
+    ``row_hit`` (int32 [rows of B]): zeroed, then set for every row that gathered an edge or has a
+    Yc row -- the next hop set of the backward chain (kgat_hop_compact lists it)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     _req(out, "out", dim=2)
@@ -137,10 +140,30 @@ def spmm_block_masked(csr, src_map: torch.Tensor, Xc: torch.Tensor, out: torch.T
         return out
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    if row_hit is not None:
+        _req(row_hit, "row_hit", dtype=torch.int32, dim=1)
+        if row_hit.numel() < csr.n_rows:
+            raise ValueError("row_hit shorter than the block")
     _lib.call("kgat_spmm_csr_masked_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
               Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
-              int(row0), out.data_ptr(), _ld(out), d, None, _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map),
+              int(row0), out.data_ptr(), _ld(out), d, row_hit.data_ptr() if row_hit is not None else None,
+              _bits_ptr(src_bits, src_map), _rank_ptr(src_rank, src_map),
               src_map.numel(), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    return out
+
+
+def map_compose(a: torch.Tensor, b: torch.Tensor | None = None, offset: int = 0,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = a[i] < 0 ? -1 : (b[a[i]] if b is given else a[i]) + offset (-1 stays -1), int32."""
+    _req(a, "a", dtype=torch.int32, dim=1)
+    if b is not None:
+        _req(b, "b", dtype=torch.int32, dim=1)
+    out = torch.empty_like(a) if out is None else out
+    _req(out, "out", dtype=torch.int32, dim=1)
+    if out.numel() != a.numel():
+        raise ValueError("map_compose: out size")
+    _lib.call("kgat_map_compose", a.data_ptr(), a.numel(), b.data_ptr() if b is not None else None, int(offset),
+              out.data_ptr(), stream_ptr(a.device))
     return out
 
 
@@ -317,14 +340,25 @@ def hop_compact(graph: DeviceGraph, sync: bool = False, count_host: torch.Tensor
     dev = hit.device
     if sync and count_host is None:
         count_host = host
-    _lib.call("kgat_hop_compact", hit.data_ptr(), hit.numel(), node_map.data_ptr(), rows.data_ptr(),
-              count.data_ptr(), _host_ptr(count_host), work.data_ptr(), work.numel(), stream_ptr(dev))
+    hop_list(hit, node_map, rows, count, work, count_host)
     map_rank(node_map, hb[9])
     if not sync:
         return rows, node_map, count, None
     torch.cuda.current_stream(dev).synchronize()  # the kernel wrote count_host
     n = int(count_host[0])
     return rows[:n], node_map, count, n
+
+
+def hop_list(hit: torch.Tensor, node_map: torch.Tensor, rows: torch.Tensor, count: torch.Tensor, work: torch.Tensor,
+             count_host: torch.Tensor | None = None) -> None:
+    """kgat_hop_compact on explicit buffers: the rows flagged in ``hit`` listed ascending in ``rows``
+    (first count entries), ``node_map`` row -> position or -1, the count on the device (and in the
+    pinned ``count_host``)."""
+    n = hit.numel()
+    if node_map.numel() < n or rows.numel() < max(n, 1) or work.numel() < int(_lib.lib().kgat_hop_compact_work_bytes(n)):
+        raise ValueError("hop_list buffers too small")
+    _lib.call("kgat_hop_compact", hit.data_ptr(), n, node_map.data_ptr(), rows.data_ptr(), count.data_ptr(),
+              _host_ptr(count_host), work.data_ptr(), work.numel(), stream_ptr(hit.device))
 
 
 def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor, count_host: torch.Tensor | None = None):
@@ -441,6 +475,73 @@ def spmm_rows(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor, out_rows: 
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, False, "rows"))
+    return out
+
+
+def spmm_rows_block(csr, X: torch.Tensor, out: torch.Tensor, out_rows: torch.Tensor, out_count: torch.Tensor,
+                    out_bits: torch.Tensor) -> torch.Tensor:
+    """spmm_rows on a rectangular CSR block (a shard's rows of A, global columns): out[r] = (B . X)[r]
+    for r = out_rows[k], k < out_count; other rows of ``out`` untouched."""
+    _req(X, "X", dim=2)
+    _req(out, "out", dim=2)
+    d = X.shape[1]
+    if out.shape[0] != csr.n_rows or out.shape[1] != d:
+        raise ValueError("out shape mismatch")
+    for t, nm in ((out_rows, "out_rows"), (out_count, "out_count")):
+        _req(t, nm, dtype=torch.int32, dim=1)
+    if out_bits.dtype != torch.int32 or out_bits.numel() * 32 < csr.n_rows:
+        raise ValueError("out_bits must be an int32 bitmap covering every row")
+    if csr.n_rows == 0:
+        return out
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=X.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_rows_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out_bits.data_ptr(),
+              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(),
+              stream_ptr(X.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, False, "rows"))
+    return out
+
+
+def csr_mark_rows(csr, bits: torch.Tensor, n_bits: int, row0: int, hit: torch.Tensor) -> torch.Tensor:
+    """hit[r] = 1 iff row r of the block is in the node set ``bits`` (bit row0 + r) or has an edge into
+    it, else 0 (kgat_csr_mark_rows)."""
+    _req(hit, "hit", dtype=torch.int32, dim=1)
+    if bits.dtype != torch.int32 or bits.numel() * 32 < n_bits or hit.numel() < csr.n_rows:
+        raise ValueError("csr_mark_rows: bitmap / flags too small")
+    desc = csr.descriptor()
+    _lib.call("kgat_csr_mark_rows", ctypes.byref(desc), bits.data_ptr(), int(n_bits), int(row0), hit.data_ptr(),
+              stream_ptr(hit.device))
+    return hit
+
+
+def biinter_fwd_gemm_rows(X, S, rows: torch.Tensor, m: int, W1, b1, W2, b2, dropout_p: float, seed: int,
+                          out: torch.Tensor, state: "BiState") -> torch.Tensor:
+    """The wide (GEMM) bi-interaction forward on rows[0..m) of X / S only (kgat_biinter_fwd_gemm_rows_f32):
+    each listed row's H row, pre-activation state and norm land at its own index with the whole-table
+    call's bits (same dropout draws); other rows of ``out`` and the state are untouched."""
+    n, din = X.shape
+    dout = W1.shape[0]
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    if S.shape != X.shape or tuple(out.shape) != (n, dout) or rows.numel() < m:
+        raise ValueError("bi-interaction rows shape mismatch")
+    if state.kind != "gemm" or state.n != n:
+        raise ValueError("bi-interaction state does not match the layer")
+    if m == 0:
+        return out
+    w = int(_lib.lib().kgat_biinter_gemm_rows_work_floats(m, din, dout))
+    if w < 0:
+        raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
+    work = torch.empty(max(w, 1), dtype=torch.float32, device=X.device)
+    _lib.call("kgat_biinter_fwd_gemm_rows_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), rows.data_ptr(), int(m),
+              W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, din, dout,
+              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), state.P.data_ptr(), work.data_ptr(),
+              work.numel(), stream_ptr(X.device))
     return out
 
 

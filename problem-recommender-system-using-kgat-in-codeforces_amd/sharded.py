@@ -56,6 +56,7 @@ from torch import nn
 from . import kernels
 from . import _lib
 from .graph import GraphLayout, RefreshPlan, _DeviceCSR, degree_weights, stream_ptr
+from . import model as _model
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
 from .optim import FusedAdam
 
@@ -267,6 +268,22 @@ class RowShard:
         self.node_map = torch.full((self.n_nodes,), -1, dtype=torch.int32, device=self.device)
         self._ident = None
 
+    def hop_buffers(self):
+        """Scratch of the hop backward (allocated once): local row flags, local row -> hop position,
+        the hop rows (local ids), device count, kgat_hop_compact's scan work."""
+        hb = self.__dict__.get("_hop")
+        if hb is None:
+            n, dev = self.n, self.device
+            work = int(_lib.lib().kgat_hop_compact_work_bytes(n))
+            if work < 0:
+                raise ValueError("shard too large for the hop compaction")
+            hb = self._hop = (torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+                              torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev),
+                              torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                              torch.zeros(1, dtype=torch.int32, device=dev),
+                              torch.empty(max(work, 1), dtype=torch.uint8, device=dev))
+        return hb
+
     def ident(self, n: int) -> torch.Tensor:
         """int32 [0, n) on the device (row list of the pack copies)."""
         if self._ident is None or self._ident.numel() < n:
@@ -309,13 +326,20 @@ class RowShard:
 
 
 def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-                  transpose: bool = False) -> torch.Tensor:
+                  transpose: bool = False, rows=None) -> torch.Tensor:
     """out (+)= csr . Xg, Xg = [N, d] every rank's rows of X (all-peer gather), csr = shard.A (forward)
     or shard.AT (backward).  Column chunks of GATHER_CHUNK: chunk c+1 is on the wire while chunk c's
-    product runs; each product is the single-GPU kernel on the local rows."""
+    product runs; each product is the single-GPU kernel on the local rows.  ``rows`` = (list, device
+    count, bitmap) of local output rows: only those rows are produced (kgat_spmm_csr_rows_f32)."""
     n, d = X.shape
+
+    def product(src, dst):
+        if rows is not None:
+            return kernels.spmm_rows_block(csr, src, dst, *rows)
+        return kernels.spmm_block(csr, src, dst, accumulate=accumulate, transpose=transpose)
+
     if not comm.active:  # one rank: X is the whole table
-        return kernels.spmm_block(csr, X, out, accumulate=accumulate, transpose=transpose)
+        return product(X, out)
     w = min(d, GATHER_CHUNK) if GATHER_CHUNK > 0 else d
     chunks = [(c, min(c + w, d)) for c in range(0, d, w)]
     N, lo, hi = shard.n_nodes, shard.lo, shard.hi
@@ -333,7 +357,7 @@ def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor
         if i + 1 < len(chunks):
             nxt = start(*chunks[i + 1])
         pend.wait()
-        kernels.spmm_block(csr, buf, out[:, c0:c1], accumulate=accumulate, transpose=transpose)
+        product(buf, out[:, c0:c1])
     return out
 
 
@@ -354,6 +378,7 @@ class _BatchRows:
         uniq, inv = np.unique(ids, return_inverse=True)
         self.n = uniq.size
         self.inv = inv.astype(np.int64)
+        self.uniq_np = uniq
         self.uniq = torch.from_numpy(uniq.astype(np.int32)).to(device)   # compact -> global id
         owned = (uniq >= lo) & (uniq < hi)
         self.local_np = np.where(owned, uniq - lo, -1).astype(np.int32)
@@ -385,18 +410,120 @@ class _BatchRows:
         return out
 
 
+def _host_bits(ids: np.ndarray, n: int, device) -> torch.Tensor:
+    """int32 device bitmap of n nodes with the bits of ``ids`` set (host-built: the ids are host data)."""
+    b = np.zeros((n + 31) // 32 + 1, np.uint32)
+    ids = np.asarray(ids, np.int64)
+    ids = ids[ids >= 0]
+    np.bitwise_or.at(b, ids >> 5, (np.uint32(1) << (ids & 31).astype(np.uint32)))
+    return torch.from_numpy(b.view(np.int32)).to(device, non_blocking=True)
+
+
+def _frontier_sets(shard: RowShard, comm, rows, L: int):
+    """The row sets the CF loss reaches, per layer (this rank's part): the last layer's output is read
+    on the batch rows F only (model.py:189-191), layer L-2's on the first hop F + N(F) (the last layer
+    gathers its A rows there).  Returns [set for layer l] with None = the whole shard, else
+    (rows int32 -- the first count valid --, count int32 [1] on the device, int32 bitmap, count):
+    F from the host's batch ids; the first hop marked on the device from this rank's rows of A^T
+    (row j is in it iff j is in F or A^T[j, f] != 0 for some f in F: kgat_csr_mark_rows), kept when
+    the global set holds at most model.HOP_DENSE_FRACTION of the nodes (the counts are all-gathered,
+    one host sync) -- the backward then runs layer L-2 on the same set."""
+    dev = shard.device
+    sets = [None] * L
+    m = rows.n_frontier
+    sets[L - 1] = (rows.frontier, torch.tensor([m], dtype=torch.int32).to(dev, non_blocking=True),
+                   _host_bits(rows.frontier_np, shard.n, dev), m)
+    if L >= 2 and _model.HOP_DENSE_FRACTION > 0:
+        hit, hmap, hrows, count, work = shard.hop_buffers()
+        fb = _host_bits(rows.uniq_np, shard.n_nodes, dev)
+        kernels.csr_mark_rows(shard.AT, fb, shard.n_nodes, shard.lo, hit)
+        kernels.hop_list(hit[:shard.n], hmap, hrows, count, work)
+        counts = comm.all_gather(count).reshape(-1).cpu().numpy().astype(np.int64)
+        if int(counts.sum()) <= _model.HOP_DENSE_FRACTION * shard.n_nodes:
+            bits = torch.empty(2 * ((shard.n + 63) // 64) + 2, dtype=torch.int32, device=dev)
+            kernels.map_bits(hmap[:shard.n], bits)
+            k = comm.rank if comm.active else 0
+            sets[L - 2] = (hrows, count.clone(), bits, int(counts[k]))
+    return sets
+
+
+def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, seeds, dX, rows, bpr, reduce_w,
+               force: bool = False):
+    """Layer l's backward on the global hop set flagged in shard.hop_buffers()'s row flags, if the set
+    is small (every rank decides alike from the all-gathered local counts: one host sync) or ``force``
+    (the frontier forward computed layer l on that set only).
+    Returns (dX_{l}, True) -- dense local rows, the next hop's rows flagged -- or (dX, False): the
+    set is large, the caller runs the layer densely (nothing was computed)."""
+    hit, hmap, hrows, count, work = shard.hop_buffers()
+    dev = dX.device
+    kernels.hop_list(hit[:shard.n], hmap, hrows, count, work)
+    counts = comm.all_gather(count).reshape(-1).cpu().numpy().astype(np.int64)
+    total = int(counts.sum())
+    if not force and total > _model.HOP_DENSE_FRACTION * shard.n_nodes:
+        return dX, False
+    Tc, cu, cp, cn, reg, coef, gout = bpr
+    W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
+    din = W1.shape[1]
+    k = comm.rank if comm.active else 0
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    mine = int(counts[k])
+    # every rank's compact [dS | dXd] hop rows, rank order (= ascending global ids); this rank's
+    # bi-interaction backward writes its own block in place
+    Pg = torch.empty(max(total, 1), 2 * din, dtype=torch.float32, device=dev)
+    ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    own = Pg[int(off[k]):int(off[k + 1])]
+    hr = hrows[:mine] if mine else torch.full((1,), -1, dtype=torch.int32, device=dev)
+    dHc = kernels.gather_rows(dX, hr)
+    dS_out = own[:, :din] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
+    dXd_out = own[:, din:] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
+    _, _, *g = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2, drops[l], seeds[l], dXd=dXd_out,
+                                   dS=dS_out, rows=hr,
+                                   **({} if states[l] is None else {"H": tables[l + 1], "state": states[l]}))
+    reduce_w(l, g)
+    if mine:
+        # the BPR terms of layer l on the batch rows this rank owns (each is in the hop set)
+        kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dXd_out, row_map=kernels.map_compose(rows.local, hmap))
+        kernels.map_compose(hr, None, shard.lo, out=ids[int(off[k]):int(off[k + 1])])
+    pend = [comm.gather_v(own, Pg, off), comm.gather_v(ids[int(off[k]):int(off[k + 1])], ids, off)] \
+        if comm.active else []
+    for p in pend:
+        p.wait()
+    if total:
+        _lib.call("kgat_map_build", ids.data_ptr(), total, shard.node_map.data_ptr(), stream_ptr(dev))
+    out = torch.empty(shard.n, din, dtype=torch.float32, device=dev)
+    kernels.spmm_block_masked(shard.AT, shard.node_map, Pg[:, :din], out, Yc_init=Pg[:, din:], row0=shard.lo,
+                              row_hit=hit if l > 0 else None)
+    if total:
+        kernels.frontier_reset(ids[:total], shard.node_map)
+    return out, True
+
+
 class _ShardedCFLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cu, cp, cn, cfg, X0, *ws):
-        shard, comm, drops, seeds, reg, rows = cfg
+        shard, comm, drops, seeds, reg, rows, frontier = cfg
+        L = len(drops)
         tables, sides, states = [X0], [], []
+        # frontier forward: layers whose output the loss reads on a row set only run on that set (the
+        # rest of their tables is never read: the next layer's A rows, the BPR rows and the backward
+        # all stay inside it); per row the whole-shard call's bits
+        sets = _frontier_sets(shard, comm, rows, L) if frontier else [None] * L
         x = X0
-        for l in range(len(drops)):
+        for l in range(L):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             s = torch.empty(shard.n, x.shape[1], dtype=torch.float32, device=x.device)
-            gathered_spmm(shard, comm, shard.A, x, s)
             st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
-            x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
+            if sets[l] is None:
+                gathered_spmm(shard, comm, shard.A, x, s)
+                x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
+            else:
+                rws, cnt, bits, m = sets[l]
+                gathered_spmm(shard, comm, shard.A, x, s, rows=(rws, cnt, bits))
+                h = torch.empty(shard.n, W1.shape[0], dtype=torch.float32, device=x.device)
+                if st.kind == "gemm":
+                    x = kernels.biinter_fwd_gemm_rows(x, s, rws, m, W1, b1, W2, b2, drops[l], seeds[l], h, st)
+                else:
+                    x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l], h, bits, state=st)
             sides.append(s)
             states.append(st)
             tables.append(x)
@@ -404,11 +531,12 @@ class _ShardedCFLoss(torch.autograd.Function):
         loss, coef = kernels.bpr_fwd(Tc, cu, cp, cn, reg)
         ctx.cfg, ctx.saved = cfg, (tables, sides, states, Tc, coef, ws)
         ctx.ids = (cu, cp, cn)
+        ctx.forced = {l for l in range(L - 1) if sets[l] is not None}
         return loss.view(())
 
     @staticmethod
     def backward(ctx, gout):
-        shard, comm, drops, seeds, reg, rows = ctx.cfg
+        shard, comm, drops, seeds, reg, rows, _frontier = ctx.cfg
         tables, sides, states, Tc, coef, ws = ctx.saved
         cu, cp, cn = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -444,12 +572,24 @@ class _ShardedCFLoss(torch.autograd.Function):
         comm.all_reduce_(P)
         _lib.call("kgat_map_build", rows.uniq.data_ptr(), rows.n, shard.node_map.data_ptr(), stream_ptr(dev))
         dX = torch.empty(shard.n, din, dtype=torch.float32, device=dev)
-        kernels.spmm_block_masked(shard.AT, shard.node_map, P[:, :din], dX, Yc_init=P[:, din:], row0=shard.lo)
+        sparse = L > 1 and _model.HOP_DENSE_FRACTION > 0
+        hit = shard.hop_buffers()[0] if sparse else None
+        kernels.spmm_block_masked(shard.AT, shard.node_map, P[:, :din], dX, Yc_init=P[:, din:], row0=shard.lo,
+                                  row_hit=hit)
         kernels.frontier_reset(rows.uniq, shard.node_map)
         kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dX, row_map=rows.local)
-        # ---- remaining layers densely: dX_l = dXd + AT_loc . (every rank's dS)
+        # ---- lower layers: dX_l is zero outside the hop set the last product flagged (the batch rows
+        # and their A^T neighbours, one hop more per layer).  While the global set holds at most
+        # model.HOP_DENSE_FRACTION of the nodes the layer runs on it (as KGAT's backward does): the
+        # bi-interaction backward on this rank's hop rows, one all-peer gather of every rank's compact
+        # [dS | dXd] hop rows (not the whole dS table), and the A^T product masked to them.  Then densely.
         for l in range(L - 2, -1, -1):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
+            if sparse or l in ctx.forced:
+                dX, sparse = _hop_layer(shard, comm, l, tables, sides, states, ws, drops, seeds, dX, rows,
+                                        (Tc, cu, cp, cn, reg, coef, gout), reduce_w, force=l in ctx.forced)
+                if sparse:
+                    continue
             dXd, dS, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], **saved(l))
             reduce_w(l, g)
             kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dXd, row_map=rows.local)
@@ -528,6 +668,9 @@ class RowShardedKGAT(nn.Module):
             self._aggregator_layers.append(Aggregator(dims[l], dims[l + 1], args.message_dropout[l]))
         self._multi_head_attention = MultiHeadAttention(d, args.kg_embedding_dim)
         self._step = 0
+        # TRAIN_CF's forward on the row sets the loss reads (see _frontier_sets); the driver's
+        # training step turns it on, off = the whole-shard propagation of every layer
+        self.frontier_forward = False
         self.to(device)
 
     # ------------------------------------------------------------------ state
@@ -586,7 +729,8 @@ class RowShardedKGAT(nn.Module):
         rows = _BatchRows(np.concatenate([u, p, q]), self.lo, self.hi, dev)
         cu, cp, cn = (torch.from_numpy(rows.inv[i * B:(i + 1) * B]).to(dev) for i in range(3))
         drops, seeds = self._dropouts()
-        cfg = (self.shard, self.comm, drops, seeds, float(self._regularization_params[0]), rows)
+        cfg = (self.shard, self.comm, drops, seeds, float(self._regularization_params[0]), rows,
+               self.frontier_forward and torch.is_grad_enabled())
         return _ShardedCFLoss.apply(cu, cp, cn, cfg, self._user_entity_embedding_shard, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, pos_tails, neg_tails) -> torch.Tensor:

@@ -132,6 +132,17 @@ def main() -> None:
           ref._user_entity_embedding.weight.grad[lo:hi], ATOL_GRAD)
     exact["cf_table_grad_after_refresh"] = torch.equal(m._user_entity_embedding_shard.grad,
                                                        ref._user_entity_embedding.weight.grad[lo:hi])
+    # the same step with the frontier forward (last layer on the batch rows, layer L-2 on the first hop)
+    full_grads = [p.grad.detach().clone() for p in m.parameters() if not p.is_sparse and p.grad is not None]
+    m.zero_grad(set_to_none=True)
+    m.frontier_forward = True
+    m(*mine, mode=pkg.KGATMode.TRAIN_CF).backward()
+    m.frontier_forward = False
+    close("cf d table shard (frontier forward)", m._user_entity_embedding_shard.grad,
+          ref._user_entity_embedding.weight.grad[lo:hi], ATOL_GRAD)
+    fr_grads = [p.grad.detach().clone() for p in m.parameters() if not p.is_sparse and p.grad is not None]
+    exact["frontier_vs_full"] = len(fr_grads) == len(full_grads) and all(
+        torch.equal(a, b) for a, b in zip(fr_grads, full_grads))
     users = torch.arange(0, 50, device="cuda")
     items = torch.arange(0, 300, device="cuda")
     with torch.no_grad():

@@ -6,6 +6,7 @@ atol 1e-5 on O(1) values, atol 1e-6 on gradients of size ~1e-3).
 """
 from __future__ import annotations
 
+import os
 import sys
 
 import numpy as np
@@ -13,7 +14,7 @@ import pytest
 import torch
 
 from oracle import kgat_cpu as K
-from tests.conftest import KGAT_CASES, golden, load_pkg
+from tests.conftest import KGAT_CASES, ROOT, golden, load_pkg
 
 pytestmark = pytest.mark.gpu
 
@@ -1760,3 +1761,80 @@ def test_fused_table_update_materialises_on_demand(pkg):
         if not pa.is_sparse:
             assert torch.equal(pa, pb), k
     assert torch.equal(a.attentive_matrix.data.coalesce().values(), b.attentive_matrix.data.coalesce().values())
+
+
+def test_dual_gemm_bit_identical_to_separate(tmp_path):
+    """The wide bi-interaction's dual-GEMM launches (gemm.hip dual_gemm_kernel: (X+S, X*S) formed at
+    load, dXd / dS in the du / dm epilogue, both weight-gradient slabs in one launch) give the separate
+    GEMM + um / dxs passes' bits: forward output, pre-activation state, norms and every gradient, at
+    256->256 (7e4 rows, several split-K chunks), 256->128 and 128->128 (tests/dual_gemm_worker.py run
+    with KGAT_DUAL_GEMM=0 and 1; the switch is read once per process)."""
+    import subprocess
+    outs = []
+    for flag in ("0", "1"):
+        path = tmp_path / f"dual{flag}.npz"
+        env = dict(os.environ, KGAT_DUAL_GEMM=flag)
+        env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+        p = subprocess.run([sys.executable, str(ROOT / "tests" / "dual_gemm_worker.py"), str(path)], cwd=ROOT, env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+        outs.append(np.load(path))
+    a, b = outs
+    assert sorted(a.files) == sorted(b.files)
+    for k in a.files:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_biinter_gemm_rows_matches_whole_table(pkg):
+    """kgat_biinter_fwd_gemm_rows_f32 (the row-sharded frontier forward of a wide layer): the listed
+    rows' H, pre-activation state and norm bit for bit the whole-table call's (same dropout draws);
+    unlisted rows untouched."""
+    _, kernels = _mods(pkg)
+    din, dout, n = 256, 128, 4000 + 7
+    g = torch.Generator().manual_seed(3)
+    dv = [t.to(DEV) for t in (torch.randn(n, din, generator=g), torch.randn(n, din, generator=g),
+                              torch.randn(dout, din, generator=g) * 0.1, torch.randn(dout, generator=g) * 0.1,
+                              torch.randn(dout, din, generator=g) * 0.1, torch.randn(dout, generator=g) * 0.1)]
+    st = kernels.BiState(n, DEV, din, dout, kind="gemm")
+    H = kernels.biinter_fwd(*dv, dropout_p=0.1, seed=77, state=st)
+    rows = np.sort(np.random.default_rng(4).choice(n, 333, replace=False))
+    rws = torch.from_numpy(np.concatenate([rows, [-1, -1]]).astype(np.int32)).to(DEV)
+    st2 = kernels.BiState(n, DEV, din, dout, kind="gemm")
+    st2.P.fill_(7.0)
+    H2 = torch.full((n, dout), 5.0, device=DEV)
+    kernels.biinter_fwd_gemm_rows(dv[0], dv[1], rws, rws.numel(), *dv[2:], 0.1, 77, H2, st2)
+    r = torch.from_numpy(rows).to(DEV)
+    assert torch.equal(H2[r], H[r])
+    for a, b in zip(st2.gemm_views(), st.gemm_views()):
+        assert torch.equal(a[r], b[r])
+    other = torch.ones(n, dtype=torch.bool, device=DEV)
+    other[r] = False
+    assert bool((H2[other] == 5.0).all()) and bool((st2.gemm_views()[0][other] == 7.0).all())
+
+
+def test_csr_mark_rows_matches_numpy(pkg):
+    """kgat_csr_mark_rows on a hub-row graph (long rows scanned by segments): row r flagged iff it is
+    in the set or has an edge into it; with a row offset (a shard's rows)."""
+    graph_mod, kernels = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(8000, 120000, seed=21)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    n = lay.n_nodes
+    rng = np.random.default_rng(5)
+    members = rng.choice(n, 40, replace=False)
+    bits = np.zeros((n + 31) // 32 + 1, np.uint32)
+    np.bitwise_or.at(bits, members >> 5, np.uint32(1) << (members & 31).astype(np.uint32))
+    inset = np.zeros(n, bool)
+    inset[members] = True
+    rp, col = lay.rowptr, lay.col
+    lo, hi = 1000, n - 500
+    sh_rp = rp[lo:hi + 1] - rp[lo]
+    sh_col = col[rp[lo]:rp[hi]]
+    csr = graph_mod._DeviceCSR(sh_rp, np.ascontiguousarray(sh_col, np.int32),
+                               torch.ones(sh_col.size, device=DEV), DEV)
+    assert csr.n_long > 0
+    hit = torch.full((hi - lo,), 9, dtype=torch.int32, device=DEV)
+    kernels.csr_mark_rows(csr, torch.from_numpy(bits.view(np.int32)).to(DEV), n, lo, hit)
+    rows = np.repeat(np.arange(hi - lo), np.diff(sh_rp))
+    want = inset[lo:hi].copy()
+    want[rows[inset[sh_col]]] = True
+    np.testing.assert_array_equal(hit.cpu().numpy(), want.astype(np.int32))
