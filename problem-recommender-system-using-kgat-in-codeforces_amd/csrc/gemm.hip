@@ -25,6 +25,8 @@
 //    [row][k] image needs four conflicting ds_write_b32), and step s's operand is one
 //    ds_read_b32 per lane: 32 consecutive rows of k = s (lanes 0-31) and of k = 8 + s
 //    (lanes 32-63, 8 pitches = 1056 floats away: the other 32 banks).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "gemm.hpp"
 
@@ -32,10 +34,17 @@ namespace kgat {
 
 namespace {
 
-constexpr int kBM = 128, kBN = 128, kBK = 16, kPitch = 20;  // LDS row pitch in floats ([row][k])
-constexpr int kPitchT = kBM + 4;                            // LDS k-row pitch in floats ([k][row])
-constexpr int kStageFloats = kBM * kPitch > kBK * kPitchT ? kBM * kPitch : kBK * kPitchT;
+constexpr int kBM = 128, kBN = 128;
+constexpr int kPitchT = kBM + 4;  // LDS k-row pitch in floats ([k][row])
 constexpr int kThreads = 256;
+// k-depth of a stage (one barrier per stage): 16 or 32 (KGAT_GEMM_BK; the sums run in the same
+// k order either way: stage kt, sub-stage u, step s takes k = 32 kt + 16 u + 8 h + s)
+template <int BK>
+struct Tile {
+  static constexpr int kPitch = BK + 4;  // LDS row pitch in floats ([row][k]): conflict-free b128 reads
+  static constexpr int kStageFloats = kBM * kPitch > BK * kPitchT ? kBM * kPitch : BK * kPitchT;
+  static constexpr int kPer = BK / 8;    // float4 per thread per operand stage
+};
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -51,58 +60,62 @@ struct GemmArgs {
   int64_t ldcs, sCS;
 };
 
-// One operand stage: 128 rows x 16 k as 512 float4 (two per thread), and where they go in LDS.
+// One operand stage: 128 rows x BK k as 32 BK float4 (BK/8 per thread), and where they go in LDS.
 // KCONTIG: the operand's k index is its contiguous dimension (A not transposed / B transposed).
-template <bool KCONTIG>
+template <bool KCONTIG, int BK>
 struct Stage {
-  float4 v[2];
+  static constexpr int P = Tile<BK>::kPitch;
+  static constexpr int Q = Tile<BK>::kPer;
+  float4 v[Q];
 
-  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t rows, int64_t K, int64_t r0,
+  __device__ __forceinline__ void load(const float* __restrict__ Pm, int64_t ld, int64_t rows, int64_t K, int64_t r0,
                                        int64_t k0, int t) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
       const int idx = t + q * kThreads;
-      if (KCONTIG) {  // P[r][k]: 4 float4 per row
-        const int64_t r = r0 + (idx >> 2), k = k0 + (idx & 3) * 4;
-        v[q] = (r < rows && k < K) ? *reinterpret_cast<const float4*>(P + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KCONTIG) {  // P[r][k]: BK/4 float4 per row
+        const int64_t r = r0 + idx / (BK / 4), k = k0 + (idx % (BK / 4)) * 4;
+        v[q] = (r < rows && k < K) ? *reinterpret_cast<const float4*>(Pm + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {        // P[k][r]: 32 float4 per k-row
         const int64_t k = k0 + (idx >> 5), r = r0 + (idx & 31) * 4;
-        v[q] = (k < K && r < rows) ? *reinterpret_cast<const float4*>(P + k * ld + r) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[q] = (k < K && r < rows) ? *reinterpret_cast<const float4*>(Pm + k * ld + r) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
 
   __device__ __forceinline__ void store(float* __restrict__ lds, int t) const {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
       const int idx = t + q * kThreads;
       if (KCONTIG) {
-        *reinterpret_cast<float4*>(lds + (idx >> 2) * kPitch + (idx & 3) * 4) = v[q];
+        *reinterpret_cast<float4*>(lds + (idx / (BK / 4)) * P + (idx % (BK / 4)) * 4) = v[q];
       } else {  // [k][row]: the 4 rows of one k stay together
         *reinterpret_cast<float4*>(lds + (idx >> 5) * kPitchT + (idx & 31) * 4) = v[q];
       }
     }
   }
 
-  // The 8 k-values (k = 8h + s, s = 0..7) of tile row `row` (0..127) for this lane's half h.
-  __device__ __forceinline__ static void read(const float* __restrict__ lds, int row, int h, float (&out)[8]) {
+  // The 8 k-values (k = 16 u + 8h + s, s = 0..7) of sub-stage u of tile row `row` (0..127) for
+  // this lane's half h.
+  __device__ __forceinline__ static void read(const float* __restrict__ lds, int row, int h, int u, float (&out)[8]) {
     if (KCONTIG) {
-      const float4 a = *reinterpret_cast<const float4*>(lds + row * kPitch + 8 * h);
-      const float4 b = *reinterpret_cast<const float4*>(lds + row * kPitch + 8 * h + 4);
+      const float4 a = *reinterpret_cast<const float4*>(lds + row * P + 16 * u + 8 * h);
+      const float4 b = *reinterpret_cast<const float4*>(lds + row * P + 16 * u + 8 * h + 4);
       out[0] = a.x, out[1] = a.y, out[2] = a.z, out[3] = a.w;
       out[4] = b.x, out[5] = b.y, out[6] = b.z, out[7] = b.w;
     } else {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) out[s] = lds[(8 * h + s) * kPitchT + row];
+      for (int s = 0; s < 8; ++s) out[s] = lds[(16 * u + 8 * h + s) * kPitchT + row];
     }
   }
 };
 
-// csum += the two float4 of a (k-major, !KCONTIG) stage this thread loaded
-template <bool KC>
-__device__ __forceinline__ void add_stage(float4& csum, const Stage<KC>& st) {
+// csum += the float4s of a (k-major, !KCONTIG) stage this thread loaded (k = (t >> 5) + 8 q: the
+// same k order for any BK)
+template <bool KC, int BK>
+__device__ __forceinline__ void add_stage(float4& csum, const Stage<KC, BK>& st) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < Tile<BK>::kPer; ++q) {
     csum.x += st.v[q].x;
     csum.y += st.v[q].y;
     csum.z += st.v[q].z;
@@ -110,9 +123,9 @@ __device__ __forceinline__ void add_stage(float4& csum, const Stage<KC>& st) {
   }
 }
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, int BK>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
-  __shared__ float lds[2][2][kStageFloats];  // [buffer][A | B][operand image]
+  __shared__ float lds[2][2][Tile<BK>::kStageFloats];  // [buffer][A | B][operand image]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int tiles_n = static_cast<int>((g.N + kBN - 1) / kBN);
   const int64_t m0 = static_cast<int64_t>(blockIdx.x / tiles_n) * kBM;
@@ -121,8 +134,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
   const float* __restrict__ B = g.B + blockIdx.z * g.sB;
   float* __restrict__ C = g.C + blockIdx.z * g.sC;
 
-  Stage<!TA> sa;
-  Stage<TB> sb;
+  Stage<!TA, BK> sa;
+  Stage<TB, BK> sb;
   floatx16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -131,7 +144,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
-  const int nk = static_cast<int>((g.K + kBK - 1) / kBK);
+  const int nk = static_cast<int>((g.K + BK - 1) / BK);
   // TA column sums: this thread's float4 of A^T rows k = (t >> 5) + 8 q (q = 0, 1) of every
   // stage covers columns m0 + 4 (t & 31) .. + 3; summed over its k residues here, combined
   // over the 8 residue threads in order at the end
@@ -148,22 +161,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A, g.lda, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * kBK, t);
-      sb.load(B, g.ldb, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * kBK, t);
-    }
-    float fa[2][8], fb[2][8];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      Stage<!TA>::read(lds[cur][0], wm + 32 * i + r, h, fa[i]);
-      Stage<TB>::read(lds[cur][1], wn + 32 * i + r, h, fb[i]);
+      sa.load(A, g.lda, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * BK, t);
+      sb.load(B, g.ldb, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * BK, t);
     }
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int u = 0; u < BK / 16; ++u) {
+      float fa[2][8], fb[2][8];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        Stage<!TA, BK>::read(lds[cur][0], wm + 32 * i + r, h, u, fa[i]);
+        Stage<TB, BK>::read(lds[cur][1], wn + 32 * i + r, h, u, fb[i]);
+      }
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        }
       }
     }
     if (kt + 1 < nk) {
@@ -241,9 +257,9 @@ struct DualArgs {
 };
 
 // Two stages of one operand pair; kUM turns the loaded (X, S) into (X + S, X * S).
-template <bool KC, int OP>
+template <bool KC, int OP, int BK>
 struct StagePair {
-  Stage<KC> a, b;
+  Stage<KC, BK> a, b;
 
   __device__ __forceinline__ void load(const float* __restrict__ P1, int64_t ld1, const float* __restrict__ P2,
                                        int64_t ld2, int64_t rows, int64_t K, int64_t r0, int64_t k0, int t) {
@@ -251,7 +267,7 @@ struct StagePair {
     b.load(P2, ld2, rows, K, r0, k0, t);
     if (OP == kUM) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < Tile<BK>::kPer; ++q) {
         const float4 x = a.v[q], s = b.v[q];
         a.v[q] = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
         b.v[q] = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
@@ -264,9 +280,9 @@ struct StagePair {
   }
 };
 
-template <bool TA, bool TB, int AOP, int BOP, int EPI>
-__global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
-  __shared__ float lds[2][4][kStageFloats];  // [buffer][A1 | A2 | B1 | B2][operand image]
+template <bool TA, bool TB, int AOP, int BOP, int EPI, int BK>
+__global__ __launch_bounds__(kThreads, 2) void dual_gemm_kernel(DualArgs g) {
+  __shared__ float lds[2][4][Tile<BK>::kStageFloats];  // [buffer][A1 | A2 | B1 | B2][operand image]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int tiles_n = static_cast<int>((g.N + kBN - 1) / kBN);
   const int64_t m0 = static_cast<int64_t>(blockIdx.x / tiles_n) * kBM;
@@ -277,8 +293,8 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
   const float* __restrict__ B1 = g.B1 + z * g.sB1;
   const float* __restrict__ B2 = g.B2 + z * g.sB2;
 
-  StagePair<!TA, AOP> sa;
-  StagePair<TB, BOP> sb;
+  StagePair<!TA, AOP, BK> sa;
+  StagePair<TB, BOP, BK> sb;
   floatx16 acc1[2][2], acc2[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -287,7 +303,7 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc1[i][j][q] = acc2[i][j][q] = 0.f;
 
-  const int nk = static_cast<int>((g.K + kBK - 1) / kBK);
+  const int nk = static_cast<int>((g.K + BK - 1) / BK);
   const bool do_cs = TA && g.cs1 != nullptr && n0 == 0;
   float4 cs1 = make_float4(0.f, 0.f, 0.f, 0.f), cs2 = cs1;
   sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, 0, t);
@@ -304,16 +320,17 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * kBK, t);
-      sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * kBK, t);
+      sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * BK, t);
+      sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * BK, t);
     }
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {  // product p: its operands' 8 k-values per tile row, then its MFMAs
+    for (int up = 0; up < 2 * (BK / 16); ++up) {  // sub-stage u of product p: 8 k-values per tile row, MFMAs
+      const int u = up >> 1, p = up & 1;
       float fa[2][8], fb[2][8];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        Stage<!TA>::read(lds[cur][p], wm + 32 * i + r, h, fa[i]);
-        Stage<TB>::read(lds[cur][2 + p], wn + 32 * i + r, h, fb[i]);
+        Stage<!TA, BK>::read(lds[cur][p], wm + 32 * i + r, h, u, fa[i]);
+        Stage<TB, BK>::read(lds[cur][2 + p], wn + 32 * i + r, h, u, fb[i]);
       }
 #pragma unroll
       for (int s = 0; s < 8; ++s)
@@ -336,7 +353,9 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
     __syncthreads();
   }
   if (do_cs) {
-    __shared__ float4 cpart[2][kThreads];
+    // the operand images are free after the last barrier: the column-sum partials go there (an
+    // array of their own would push the block past 80 KB of LDS, one block per CU)
+    float4(*cpart)[kThreads] = reinterpret_cast<float4(*)[kThreads]>(&lds[0][0][0]);
     cpart[0][t] = cs1;
     cpart[1][t] = cs2;
     __syncthreads();
@@ -358,20 +377,34 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
   }
   float* __restrict__ C1 = g.C1 + z * g.sC1;
   float* __restrict__ C2 = g.C2 + z * g.sC2;
+  const float* __restrict__ Xe = g.X;
+  const float* __restrict__ Se = g.S;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t col = n0 + wn + 32 * j + r;
       if (col >= g.N) continue;
+      float sv[16], xv[16];
+      if (EPI == kDXS) {
+        // the tile's S / X elements all in flight before its first store (a store between two
+        // loads would make each load wait for the previous one's round trip)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int64_t row = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+          const bool ok = row < g.M;
+          sv[q] = ok ? Se[row * g.lds + col] : 0.f;
+          xv[q] = ok ? Xe[row * g.ldx + col] : 0.f;
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t row = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
         if (row >= g.M) continue;
         if (EPI == kDXS) {
           const float du = acc1[i][j][q], dm = acc2[i][j][q];
-          C1[row * g.ldc1 + col] = fmaf(dm, g.S[row * g.lds + col], du);
-          C2[row * g.ldc2 + col] = fmaf(dm, g.X[row * g.ldx + col], du);
+          C1[row * g.ldc1 + col] = fmaf(dm, sv[q], du);
+          C2[row * g.ldc2 + col] = fmaf(dm, xv[q], du);
         } else {
           C1[row * g.ldc1 + col] = acc1[i][j][q];
           C2[row * g.ldc2 + col] = acc2[i][j][q];
@@ -381,6 +414,15 @@ __global__ __launch_bounds__(kThreads, 1) void dual_gemm_kernel(DualArgs g) {
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Stage depth of every GEMM launch: KGAT_GEMM_BK = 16 or 32 (same bits either way).
+int gemm_stage_k() {
+  static const int bk = [] {
+    const char* e = getenv("KGAT_GEMM_BK");
+    return e != nullptr && atoi(e) == 32 ? 32 : 16;
+  }();
+  return bk;
+}
 
 }  // namespace
 
@@ -407,16 +449,21 @@ int dual_gemm_f32(const DualGemm& d, hipStream_t st) {
   const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(d.batch));
   // the three forms the bi-interaction uses: forward (UM x W^T), backward du/dm + dXd/dS
   // epilogue (dA.W), weight gradients (dA^T x UM, split-K batches, column sums)
+// 16-deep stages: the four operand images of two 16-deep buffers are 80 KB, so two blocks (two waves
+// per SIMD, <= 256 registers each) share a CU; 32-deep stages would leave one
+#define KGAT_DUAL_LAUNCH(TA_, TB_, AOP_, BOP_, EPI_) \
+  hipLaunchKernelGGL((dual_gemm_kernel<TA_, TB_, AOP_, BOP_, EPI_, 16>), grid, dim3(kThreads), 0, st, g)
   if (!d.ta && d.tb && d.a_um && !d.b_um && !d.dxs)
-    hipLaunchKernelGGL((dual_gemm_kernel<false, true, kUM, kSep, kStore>), grid, dim3(kThreads), 0, st, g);
+    KGAT_DUAL_LAUNCH(false, true, kUM, kSep, kStore);
   else if (!d.ta && !d.tb && !d.a_um && !d.b_um && d.dxs)
-    hipLaunchKernelGGL((dual_gemm_kernel<false, false, kSep, kSep, kDXS>), grid, dim3(kThreads), 0, st, g);
+    KGAT_DUAL_LAUNCH(false, false, kSep, kSep, kDXS);
   else if (d.ta && !d.tb && !d.a_um && d.b_um && !d.dxs)
-    hipLaunchKernelGGL((dual_gemm_kernel<true, false, kSep, kUM, kStore>), grid, dim3(kThreads), 0, st, g);
+    KGAT_DUAL_LAUNCH(true, false, kSep, kUM, kStore);
   else if (!d.ta && d.tb && !d.a_um && !d.b_um && !d.dxs)
-    hipLaunchKernelGGL((dual_gemm_kernel<false, true, kSep, kSep, kStore>), grid, dim3(kThreads), 0, st, g);
+    KGAT_DUAL_LAUNCH(false, true, kSep, kSep, kStore);
   else
     return KGAT_ERR_UNSUPPORTED_DIM;
+#undef KGAT_DUAL_LAUNCH
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -443,12 +490,19 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
   if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
   GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, accumulate ? 1 : 0, nullptr, 0, 0};
   const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
+#define KGAT_GEMM_LAUNCH(TA_, TB_)                                                                  \
+  do {                                                                                         \
+    if (gemm_stage_k() == 32)                                                                  \
+      hipLaunchKernelGGL((gemm_kernel<TA_, TB_, 32>), grid, dim3(kThreads), 0, st, g);          \
+    else                                                                                       \
+      hipLaunchKernelGGL((gemm_kernel<TA_, TB_, 16>), grid, dim3(kThreads), 0, st, g);          \
+  } while (0)
   if (ta) {
-    if (tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(kThreads), 0, st, g);
-    else hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(kThreads), 0, st, g);
+    if (tb) KGAT_GEMM_LAUNCH(true, true);
+    else KGAT_GEMM_LAUNCH(true, false);
   } else {
-    if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(kThreads), 0, st, g);
-    else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(kThreads), 0, st, g);
+    if (tb) KGAT_GEMM_LAUNCH(false, true);
+    else KGAT_GEMM_LAUNCH(false, false);
   }
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
@@ -464,8 +518,8 @@ int gemm_f32_tn_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t 
   const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
   GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, 0, cs, ldcs, sCS};
-  hipLaunchKernelGGL((gemm_kernel<true, false>), dim3(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch)),
-                     dim3(kThreads), 0, st, g);
+  const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
+  KGAT_GEMM_LAUNCH(true, false);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

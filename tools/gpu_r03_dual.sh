@@ -1,16 +1,22 @@
 #!/bin/bash
-# Dual vs separate wide bi-interaction GEMMs: per-kernel stats and one PMC pass over the dual run.
+# Wide bi-interaction GEMM A/B: dual vs separate launches (KGAT_DUAL_GEMM) x stage depth
+# (KGAT_GEMM_BK 16 / 32), per-kernel stats of each at 300k and 1M rows (256 -> 256), plus C4's
+# 128 -> 128 shape.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/dual
 rm -rf $OUT; mkdir -p $OUT
-for v in 0 1; do
-  KGAT_DUAL_GEMM=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats$v -o run --output-format csv -- \
-    python3 tools/bench_dual.py --rows 300000 > $OUT/b$v.log 2>&1 || { tail -20 $OUT/b$v.log; exit 1; }
-  grep '^{' $OUT/b$v.log
+for shape in "300000 256 256" "1000000 256 256" "1000000 128 128"; do
+  set -- $shape
+  for v in 0 1; do
+    for bk in 16 32; do
+      tag=r$1_${2}x${3}_d${v}_k$bk
+      KGAT_DUAL_GEMM=$v KGAT_GEMM_BK=$bk timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$tag -o run \
+        --output-format csv -- python3 tools/bench_dual.py --rows $1 --din $2 --dout $3 > $OUT/$tag.log 2>&1 \
+        || { tail -20 $OUT/$tag.log; exit 1; }
+      grep '^{' $OUT/$tag.log
+    done
+  done
 done
-CTR="SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
-timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-trace --output-format csv -d $OUT/pmc -o run -- \
-  python3 tools/bench_dual.py --rows 300000 --reps 3 > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
 echo done
