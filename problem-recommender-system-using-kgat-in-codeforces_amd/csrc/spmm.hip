@@ -244,6 +244,139 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   }
 }
 
+// The fused table update (kMaskedAdam) with its two streams on separate waves of a block
+// (KGAT_TU_WS=1): four "gather" waves compute the masked A^T product rows of chunk i (16-lane
+// groups, gather_edges as above, + the Yc row) into an LDS image while four "stream" waves run Adam
+// on chunk i-1 from the other image -- each thread 3 x D/16 float4 of p / m / v in flight, nothing
+// waiting behind a gather.  One barrier per chunk; blocks stride over the chunks (persistent grid);
+// long rows are left to the segment blocks + the fix-up (their Adam runs there).  Same bits as
+// kMaskedAdam: per row the same edges in the same order, then the same adam_elem.
+template <int D, int GW, int SW>
+struct TuShape {
+  static constexpr int kRows = SpmmShape<D>::kRowsPerWave * GW;  // rows per chunk (GW gather waves)
+  static constexpr int kF4 = kRows * D / 4;                       // float4 per chunk image
+  static constexpr int kThreads = 64 * (GW + SW);
+};
+
+template <int D, int GW, int SW>
+__global__ __launch_bounds__(64 * (GW + SW)) void masked_adam_ws_kernel(kgat_csr A, SpmmIo io,
+                                                                                        int seg_blocks,
+                                                                                        int64_t n_chunks) {
+  using S = SpmmShape<D>;
+  using T = TuShape<D, GW, SW>;
+  constexpr int L = S::kLanes;
+  __shared__ float4 img[2][T::kF4];
+  __shared__ int8_t skip_row[2][T::kRows];  // long rows (Adam in the fix-up) and rows past the end
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if (static_cast<int>(blockIdx.x) < seg_blocks) {
+    // long-row segments: one per wave, as spmm_main_kernel's segment waves
+    const int s = blockIdx.x * (GW + SW) + wave;
+    if (s >= A.n_seg) return;
+    const int g = lane / L, gl = lane % L, base = g * L;
+    const int row = A.seg_row[s];
+    const int64_t beg = A.seg_beg[s];
+    const int64_t row_end = A.rowptr[row + 1];
+    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
+    for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
+      const int64_t ce = cb + L < end ? cb + L : end;
+      gather_edges<D, true>(A, io, cb, ce, base, gl, acc, any);
+    }
+#pragma unroll
+    for (int o = L; o < kWave; o <<= 1) {
+      acc.x += __shfl_xor(acc.x, o);
+      acc.y += __shfl_xor(acc.y, o);
+      acc.z += __shfl_xor(acc.z, o);
+      acc.w += __shfl_xor(acc.w, o);
+    }
+    if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
+    return;
+  }
+  const int64_t blk = blockIdx.x - seg_blocks, nblk = gridDim.x - seg_blocks;
+  const bool gather = wave < GW;
+  int it = 0;
+  for (int64_t c = blk;; c += nblk, ++it) {
+    const int buf = it & 1;
+    if (gather && c < n_chunks) {
+      // chunk c: rows [c * kRows, ...), group g of wave w takes rows w*kRowsPerWave + g + k*kGroups
+      const int g = lane / L, gl = lane % L, base = g * L;
+      const int64_t r_begin = c * T::kRows;
+#pragma unroll 1
+      for (int k = 0; k < S::kRowsPerGroup; ++k) {
+        const int lr = wave * S::kRowsPerWave + g + k * S::kGroups;
+        const int64_t r = r_begin + lr;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool skip = r >= A.n_rows;
+        if (!skip) {
+          const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+          skip = end - beg > A.long_threshold;
+          if (!skip) {
+            bool any = false;
+            gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
+            if (io.Yc != nullptr) {
+              const int m = io.src_map[io.row0 + r];
+              if (m >= 0) {
+                const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
+                acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+              }
+            }
+          }
+        }
+        img[buf][lr * L + gl] = acc;
+        if (gl == 0) skip_row[buf][lr] = skip ? 1 : 0;
+      }
+    }
+    if (!gather && it > 0 && c - nblk < n_chunks) {
+      // chunk c - nblk (filled last iteration into the other image): Adam on its rows, float4-linear
+      const int pb = buf ^ 1;
+      const int64_t r0 = (c - nblk) * T::kRows;
+      const int t = threadIdx.x - 64 * GW;
+#pragma unroll 4
+      for (int f = t; f < T::kF4; f += 64 * SW) {
+        const int lr = f / L, gl = f % L;
+        if (skip_row[pb][lr]) continue;
+        adam_row_step(io.adam, r0 + lr, gl, img[pb][f], adam_row_load(io.adam, r0 + lr, gl));
+      }
+    }
+    if (c - nblk >= n_chunks) break;  // block-uniform: every wave leaves after the same iteration
+    __syncthreads();
+  }
+}
+
+template <int D, int GW, int SW>
+static int launch_masked_adam_ws_t(const kgat_csr& A, const SpmmIo& io, int per_cu, hipStream_t st) {
+  using T = TuShape<D, GW, SW>;
+  const int seg_blocks = (A.n_seg + GW + SW - 1) / (GW + SW);
+  const int64_t n_chunks = (A.n_rows + T::kRows - 1) / T::kRows;
+  const int64_t chunk_blocks = std::min<int64_t>(n_chunks, static_cast<int64_t>(per_cu) * kCUs);
+  hipLaunchKernelGGL((masked_adam_ws_kernel<D, GW, SW>), dim3(seg_blocks + chunk_blocks), dim3(T::kThreads), 0, st, A,
+                     io, seg_blocks, n_chunks);
+  KGAT_LAUNCH_CHECK();
+  if (A.n_long > 0) {
+    hipLaunchKernelGGL((spmm_fixup_kernel<D, kMaskedAdam>), dim3(A.n_long), dim3(256), 0, st, A, io);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
+
+// KGAT_TU_WS = 1: 4 gather + 4 stream waves; 2: 6 + 2; 3: 12 + 4 (1024 threads).  KGAT_TU_WS_BLOCKS:
+// blocks per CU (default 4).
+template <int D>
+static int launch_masked_adam_ws(const kgat_csr& A, const SpmmIo& io, int variant, hipStream_t st) {
+  static const int per_cu = [] {
+    const char* e = getenv("KGAT_TU_WS_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
+  switch (variant) {
+    case 2: return launch_masked_adam_ws_t<D, 6, 2>(A, io, per_cu, st);
+    case 3: return launch_masked_adam_ws_t<D, 12, 4>(A, io, per_cu, st);
+    default: return launch_masked_adam_ws_t<D, 4, 4>(A, io, per_cu, st);
+  }
+}
+
 template <int D, int MODE>
 static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
@@ -574,6 +707,20 @@ extern "C" int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr* A, const int32_t
     return e ? atoi(e) : 0;
   }();
   if (batched) return dispatch<kMaskedAdamB>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+  // KGAT_TU_WS=1: gather and Adam on separate waves (masked_adam_ws_kernel, same bits)
+  static const int ws = [] {
+    const char* e = getenv("KGAT_TU_WS");
+    return e ? atoi(e) : 0;
+  }();
+  if (ws) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (d) {
+      case 64: return launch_masked_adam_ws<64>(*A, io, ws, st);
+      case 128: return launch_masked_adam_ws<128>(*A, io, ws, st);
+      case 256: return launch_masked_adam_ws<256>(*A, io, ws, st);
+      default: break;
+    }
+  }
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
