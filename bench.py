@@ -467,7 +467,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         "host_launch_ms_per_step": timed.host_ms_per_step,
         "cpu_baseline": None,
     }
-    if L <= 2 and not args.no_frontier_leg and not args.exchange_at_1:
+    if L <= 3 and not args.no_frontier_leg and not args.exchange_at_1:
         # the same CF step with KGAT.frontier_forward (each layer's forward on the rows the loss can
         # reach only: same loss, gradients and updates bit for bit, tested) -- the training step as
         # driver.py runs it; `value` above stays the full-propagation step.  N > 1: the replicas'
@@ -481,13 +481,14 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         fms = fel / args.steps * 1e3
         # bit identity vs the full forward: checked here at N = 1 (and, with the exchange, in tests/dp_worker.py)
         same = frontier_matches_full(model, pkg, batches[0]) if world == 1 else None
-        est = getattr(model.graph(), "_hop_est", {}).get(0)  # pinned count of the last step's first hop
+        est = getattr(model.graph(), "_hop_est", {}).get(L - 2)  # pinned count of the last step's first hop
         result["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
-            "layer0_rows_last_step": int(est[0][0]) if est is not None and L == 2 else None,
+            "first_hop_rows_last_step": int(est[0][0]) if est is not None and L >= 2 else None,
             "bit_identical_to_full": same,
-            "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer 0 of 2 on F + N(F), the "
-                    "last layer on the batch rows F); not counted in value (it does not visit every edge)"}
+            "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer L-2 on the first hop "
+                    "F + N(F), the last layer on the batch rows F, layer 0 of 3 whole); not counted in value (it "
+                    "does not visit every edge)"}
         if world > 1:
             result["frontier_forward"]["dp_table_exchange_steps"] = fr_exchange
     result["value_note"] = ("value = n_gpus x nnz x L / t_step: each data-parallel replica runs the reference step's "
@@ -560,12 +561,18 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         for i in range(args.warmup):
             kg_step(batches[i])
         torch.cuda.synchronize()
-        kernels.KERNEL_EVENTS = {}
+        # the step time without instrumentation (an event pair around every kernel costs the stream
+        # and the host ~10-20 us each: it would be most of a 0.3 ms step), then the kernels' own times
+        # from an instrumented pass over the same batches
         t0 = time.perf_counter()
         for i in range(args.steps):
             kg_step(batches[args.warmup + i])
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / args.steps * 1e3
+        kernels.KERNEL_EVENTS = {}
+        for i in range(min(args.steps, 8)):
+            kg_step(batches[args.warmup + i])
+        torch.cuda.synchronize()
         evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
         leg = {"ms_per_step": el, "kg_pairs_per_s": B / (el * 1e-3)}
         for k in ("transr_fwd", "transr_bwd", "adam_rows", "adam_multi"):
@@ -599,13 +606,15 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
     model.train()
     model(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)  # warm-up (builds the refresh plan)
     torch.cuda.synchronize()
-    kernels.KERNEL_EVENTS = {}
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
         model(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
     torch.cuda.synchronize()
     rms = (time.perf_counter() - t0) / reps * 1e3
+    kernels.KERNEL_EVENTS = {}
+    model(*att, mode=pkg.KGATMode.UPDATE_ATTENTION)
+    torch.cuda.synchronize()
     evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
     g = model.graph()
     g.A.val.copy_(saved)

@@ -344,6 +344,21 @@ int kgat_biinter_bwd_gemm_f32(const float *X, int64_t ldx, const float *S, int64
  * (no [n, 2*d_out] pre-activation state written) and this GEMM backward.
  * work: float [kgat_biinter_gemm_bits_work_floats]. */
 int64_t kgat_biinter_gemm_bits_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out);
+
+/* The wide backward on the rows rows[0..m) of a layer only (the hop rows of the backward chain),
+ * without gathering them: X, S, H, dH (all [n_rows, *], indexed by node) and the forward's state
+ * are read at each listed node's own row, dXd / dS [m, d_in] are written compactly (row r = node
+ * rows[r]; -1 = padding, zero), the weight gradients sum the listed rows -- the same bits as the
+ * gathered compact call (kgat_biinter_bwd_gemm_f32 / _bits_f32 with key_rows on gathered rows).
+ * state: the GEMM forward's pre-activations + norms (norm, mask null), or null with the fused
+ * forward's norm + mask words (d_out <= 128).  work: kgat_biinter_bwd_gemm_rows_work_floats(m). */
+int64_t kgat_biinter_bwd_gemm_rows_work_floats(int64_t m, int32_t d_in, int32_t d_out);
+int kgat_biinter_bwd_gemm_rows_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
+                                   int64_t ldh, const float *state, const float *norm, const uint64_t *mask,
+                                   const float *dH, int64_t lddh, const int32_t *rows, int64_t m, const float *W1,
+                                   const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds, float *dW1,
+                                   float *db1, float *dW2, float *db2, int64_t n_rows, int32_t d_in, int32_t d_out,
+                                   float dropout_p, uint64_t seed, float *work, int64_t work_floats, void *stream);
 int kgat_biinter_bwd_gemm_bits_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
                                    int64_t ldh, const float *norm, const uint64_t *mask, const float *dH,
                                    int64_t lddh, const float *W1, const float *W2, float *dXd, int64_t lddxd,

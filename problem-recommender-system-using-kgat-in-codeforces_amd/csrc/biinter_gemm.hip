@@ -170,6 +170,57 @@ __global__ __launch_bounds__(256) void epi_bwd_kernel(float* __restrict__ P1, fl
   }
 }
 
+// one wave per output row r of a row list (the hop rows of a layer's backward): node = rows[r]
+// (-1: padding, zero gradient); H, dH, the pre-activation state and the norm read at the node's
+// own row of the whole-table arrays, dA / dB written compactly at r -- epi_bwd_kernel's arithmetic
+// on gathered rows, without the gathers.  bits (nullable): the fused forward's sign/keep words
+// instead of the pre-activations (P1 / P2 unused).
+__global__ __launch_bounds__(256) void epi_bwd_rows_kernel(float* __restrict__ dA, float* __restrict__ dB,
+                                                           const float* __restrict__ P1, const float* __restrict__ P2,
+                                                           const uint64_t* __restrict__ mask,
+                                                           const float* __restrict__ H, int64_t ldh,
+                                                           const float* __restrict__ norm,
+                                                           const float* __restrict__ dH, int64_t lddh,
+                                                           const int32_t* __restrict__ rows, int64_t m, int dout,
+                                                           float p, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (r >= m) return;
+  const int64_t node = rows[r];
+  if (node < 0) {
+    for (int c = lane; c < dout; c += 64) dA[r * dout + c] = dB[r * dout + c] = 0.f;
+    return;
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = gemm_threshold(p);
+  float dot = 0.f;
+  for (int c = lane; c < dout; c += 64) dot = fmaf(H[node * ldh + c], dH[node * lddh + c], dot);
+  dot = wave_sum(dot);
+  const float nr = norm[node];
+  const bool clamped = nr < 0.f;
+  const float inv = clamped ? 1.f / kNormEps : 1.f / nr;
+  const float proj = clamped ? 0.f : dot;
+  const int ng = (dout / 16 + 3) / 4;
+  const int64_t st = node >> 4;
+  const int q = static_cast<int>(node & 15) >> 2, i = static_cast<int>(node & 3);
+  for (int c = lane; c < dout; c += 64) {
+    float dg = (dH[node * lddh + c] - H[node * ldh + c] * proj) * inv;
+    if (mask != nullptr) {
+      const int cb = c >> 4;
+      const uint64_t w = mask[(st * ng + (cb >> 2)) * 64 + q * 16 + (c & 15)];
+      const uint32_t bits = static_cast<uint32_t>(w >> (((cb & 3) * 4 + i) * 3)) & 7u;
+      dg = (bits & 4u) ? dg * scale : 0.f;
+      dA[r * dout + c] = (bits & 1u) ? dg : dg * kLeakySlope;
+      dB[r * dout + c] = (bits & 2u) ? dg : dg * kLeakySlope;
+    } else {
+      if (p > 0.f) dg = gemm_keep(seed, node, c, dout, thr) ? dg * scale : 0.f;
+      const float pa = P1[node * dout + c], pb = P2[node * dout + c];
+      dA[r * dout + c] = pa > 0.f ? dg : dg * kLeakySlope;
+      dB[r * dout + c] = pb > 0.f ? dg : dg * kLeakySlope;
+    }
+  }
+}
+
 // one wave per row: dA, dB from H, dH and the fused forward's saved state (row
 // norm + per-element pre_sum > 0 / pre_mul > 0 / keep bits, kgat_biinter_fwd_f32's
 // mask_out layout, indexed by node = key) instead of the pre-activations
@@ -269,7 +320,8 @@ static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d
 static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* W2,
                          const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
                          float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in, int32_t d_out,
-                         float* work, hipStream_t st) {
+                         float* work, hipStream_t st, const int32_t* rows = nullptr) {
+  // rows (dual GEMM only): row r of dA / dB / dXd / dS is row rows[r] of X / S (-1: zero)
   const int ldu = d_in + 4;
   float* U = work;
   float* M = work + n * ldu;
@@ -277,7 +329,8 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   float* slab1 = work + 2 * n * ldu;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
-  const bool dual = dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0;
+  const bool dual = (dual_gemm_on() || rows != nullptr) && (ldx & 3) == 0 && (lds & 3) == 0;
+  if (rows != nullptr && !dual) return KGAT_ERR_INVALID;
   if (dual) {
     // du = dA W1, dm = dB W2, then dXd = du + dm*S, dS = du + dm*X in the epilogue: one launch
     DualGemm g;
@@ -287,6 +340,7 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
     g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
     g.C1 = dXd, g.C2 = dS, g.ldc1 = lddxd, g.ldc2 = ldds;
     g.X = X, g.S = S, g.ldx = ldx, g.lds = lds;
+    g.erows = rows;
     KGAT_GEMM(dual_gemm_f32(g, st));
   } else {
     // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
@@ -320,7 +374,12 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
       const int64_t r0 = part == 0 ? 0 : full * chunk;
       g.K = part == 0 ? chunk : rest, g.batch = nbat;
       g.A1 = dA + r0 * d_out, g.A2 = dB + r0 * d_out, g.sA1 = g.sA2 = chunk * d_out;
-      g.B1 = X + r0 * ldx, g.B2 = S + r0 * lds, g.sB1 = chunk * ldx, g.sB2 = chunk * lds;
+      if (rows != nullptr) {  // X / S rows through the list: the chunk offsets move the list
+        g.B1 = X, g.B2 = S, g.sB1 = g.sB2 = 0;
+        g.brows = rows + r0, g.sBrows = chunk;
+      } else {
+        g.B1 = X + r0 * ldx, g.B2 = S + r0 * lds, g.sB1 = chunk * ldx, g.sB2 = chunk * lds;
+      }
       g.C1 = slab1 + (part == 0 ? 0 : full) * sl_stride, g.C2 = slab2 + (part == 0 ? 0 : full) * sl_stride;
       g.sC1 = g.sC2 = sl_stride;
       g.cs1 = g.C1 + d_in, g.cs2 = g.C2 + d_in, g.sCS1 = g.sCS2 = sl_stride;
@@ -430,11 +489,22 @@ extern "C" int kgat_biinter_fwd_gemm_rows_f32(const float* X, int64_t ldx, const
   float* M = work + m * ldu;
   float* P1 = work + kgat_biinter_gemm_work_floats(m, d_in, d_out);
   float* P2 = P1 + m * d_out;
-  hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(m * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256), 0,
-                     st, X, ldx, S, lds, U, M, m, d_in, rows);
-  KGAT_LAUNCH_CHECK();
-  KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
-  KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
+  if (kgat::dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0) {
+    // P1 = (X+S) W1^T, P2 = (X*S) W2^T on the listed rows, X / S read through the list at load
+    kgat::DualGemm g;
+    g.tb = true, g.a_um = true;
+    g.M = m, g.N = d_out, g.K = d_in;
+    g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds, g.arows = rows;
+    g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
+    g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
+    KGAT_GEMM(kgat::dual_gemm_f32(g, st));
+  } else {
+    hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(m * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256),
+                       0, st, X, ldx, S, lds, U, M, m, d_in, rows);
+    KGAT_LAUNCH_CHECK();
+    KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
+    KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
+  }
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((m + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh,
                      state + 2 * n * d_out, m, d_out, dropout_p, seed, rows, state, state + n * d_out);
   KGAT_LAUNCH_CHECK();
@@ -464,6 +534,51 @@ extern "C" int kgat_biinter_bwd_gemm_f32(const float* X, int64_t ldx, const floa
   KGAT_LAUNCH_CHECK();
   return kgat::bwd_gemm_tail(X, ldx, S, lds, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in,
                              d_out, work, st);
+}
+
+extern "C" int kgat_biinter_bwd_gemm_rows_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
+                                              const float* H, int64_t ldh, const float* state, const float* norm,
+                                              const uint64_t* mask, const float* dH, int64_t lddh,
+                                              const int32_t* rows, int64_t m, const float* W1, const float* W2,
+                                              float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1,
+                                              float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
+                                              int32_t d_out, float dropout_p, uint64_t seed, float* work,
+                                              int64_t work_floats, void* stream) {
+  // state: the GEMM forward's [P1 + b1 | P2 + b2 | norm] over all n rows (mask null), or null with
+  // norm + mask: the fused forward's saved state (the "bits" kind, d_out <= 128)
+  if (!X || !S || !H || !dH || !rows || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n < 0 || m < 0 ||
+      !gemm_dims_ok(d_in, d_out))
+    return KGAT_ERR_INVALID;
+  if ((state == nullptr) == (mask == nullptr) || (mask != nullptr && (norm == nullptr || d_out > 128)))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || lddh < d_out || lddxd < d_in || ldds < d_in || (ldx & 3) ||
+      (lds & 3) || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return KGAT_ERR_INVALID;
+  if (!work || work_floats < kgat_biinter_bwd_gemm_rows_work_floats(m, d_in, d_out)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (m == 0) return kgat::zero_wgrads(dW1, db1, dW2, db2, d_in, d_out, st);
+  float* dA = work + kgat_biinter_gemm_work_floats(m, d_in, d_out);
+  float* dB = dA + m * d_out;
+  // X / S rows gathered once, compactly: the GEMMs then read contiguous tiles (read through the list
+  // inside the GEMMs -- the dXd / dS epilogue and the k-major weight-gradient loads -- they ran 0.5 ms
+  // slower at 300k rows than this copy costs); H, dH and the state are read through the list
+  float* Xc = dB + m * d_out;
+  float* Sc = Xc + m * static_cast<int64_t>(d_in);
+  if (int e = kgat_gather_rows_f32(X, ldx, rows, m, d_in, Xc, d_in, stream)) return e;
+  if (int e = kgat_gather_rows_f32(S, lds, rows, m, d_in, Sc, d_in, stream)) return e;
+  const float* P1 = state;
+  const float* P2 = state != nullptr ? state + n * d_out : nullptr;
+  const float* nrm = state != nullptr ? state + 2 * n * d_out : norm;
+  hipLaunchKernelGGL(kgat::epi_bwd_rows_kernel, dim3((m + 3) / 4), dim3(256), 0, st, dA, dB, P1, P2, mask, H, ldh, nrm,
+                     dH, lddh, rows, m, d_out, dropout_p, seed);
+  KGAT_LAUNCH_CHECK();
+  return kgat::bwd_gemm_tail(Xc, d_in, Sc, d_in, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, m, d_in,
+                             d_out, work, st);
+}
+
+extern "C" int64_t kgat_biinter_bwd_gemm_rows_work_floats(int64_t m, int32_t d_in, int32_t d_out) {
+  const int64_t w = kgat_biinter_gemm_bits_work_floats(m, d_in, d_out);
+  return w < 0 ? -1 : w + 2 * m * static_cast<int64_t>(d_in);  // + the gathered X, S rows
 }
 
 extern "C" int64_t kgat_biinter_gemm_bits_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {

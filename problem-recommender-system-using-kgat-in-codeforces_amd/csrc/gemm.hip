@@ -68,17 +68,23 @@ struct Stage {
   static constexpr int Q = Tile<BK>::kPer;
   float4 v[Q];
 
+  // idx (nullable): the operand's stored-row index of each logical row -- its m / n row when the
+  // k index is contiguous, its k row otherwise (a row list; -1 = a zero row)
   __device__ __forceinline__ void load(const float* __restrict__ Pm, int64_t ld, int64_t rows, int64_t K, int64_t r0,
-                                       int64_t k0, int t) {
+                                       int64_t k0, int t, const int32_t* __restrict__ ridx = nullptr) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int idx = t + q * kThreads;
       if (KCONTIG) {  // P[r][k]: BK/4 float4 per row
         const int64_t r = r0 + idx / (BK / 4), k = k0 + (idx % (BK / 4)) * 4;
-        v[q] = (r < rows && k < K) ? *reinterpret_cast<const float4*>(Pm + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int64_t rr = (ridx != nullptr && r < rows) ? static_cast<int64_t>(ridx[r]) : r;
+        v[q] = (r < rows && k < K && rr >= 0) ? *reinterpret_cast<const float4*>(Pm + rr * ld + k)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {        // P[k][r]: 32 float4 per k-row
         const int64_t k = k0 + (idx >> 5), r = r0 + (idx & 31) * 4;
-        v[q] = (k < K && r < rows) ? *reinterpret_cast<const float4*>(Pm + k * ld + r) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int64_t kk = (ridx != nullptr && k < K) ? static_cast<int64_t>(ridx[k]) : k;
+        v[q] = (k < K && r < rows && kk >= 0) ? *reinterpret_cast<const float4*>(Pm + kk * ld + r)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -254,6 +260,10 @@ struct DualArgs {
   const float* X;  // kDXS
   const float* S;
   int64_t ldx, lds;
+  const int32_t* arows;  // nullable row lists (-1 = zero row): A's m rows, B's k rows (+ z * sBrows),
+  const int32_t* brows;  // the dXd / dS epilogue's X / S rows
+  int64_t sBrows;
+  const int32_t* erows;
 };
 
 // Two stages of one operand pair; kUM turns the loaded (X, S) into (X + S, X * S).
@@ -262,9 +272,10 @@ struct StagePair {
   Stage<KC, BK> a, b;
 
   __device__ __forceinline__ void load(const float* __restrict__ P1, int64_t ld1, const float* __restrict__ P2,
-                                       int64_t ld2, int64_t rows, int64_t K, int64_t r0, int64_t k0, int t) {
-    a.load(P1, ld1, rows, K, r0, k0, t);
-    b.load(P2, ld2, rows, K, r0, k0, t);
+                                       int64_t ld2, int64_t rows, int64_t K, int64_t r0, int64_t k0, int t,
+                                       const int32_t* __restrict__ ridx = nullptr) {
+    a.load(P1, ld1, rows, K, r0, k0, t, ridx);
+    b.load(P2, ld2, rows, K, r0, k0, t, ridx);
     if (OP == kUM) {
 #pragma unroll
       for (int q = 0; q < Tile<BK>::kPer; ++q) {
@@ -306,8 +317,9 @@ __global__ __launch_bounds__(kThreads, 2) void dual_gemm_kernel(DualArgs g) {
   const int nk = static_cast<int>((g.K + BK - 1) / BK);
   const bool do_cs = TA && g.cs1 != nullptr && n0 == 0;
   float4 cs1 = make_float4(0.f, 0.f, 0.f, 0.f), cs2 = cs1;
-  sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, 0, t);
-  sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, 0, t);
+  const int32_t* __restrict__ brows = g.brows != nullptr ? g.brows + z * g.sBrows : nullptr;
+  sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, 0, t, g.arows);
+  sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, 0, t, brows);
   sa.store(lds[0][0], lds[0][1], t);
   sb.store(lds[0][2], lds[0][3], t);
   if (do_cs) {
@@ -320,8 +332,8 @@ __global__ __launch_bounds__(kThreads, 2) void dual_gemm_kernel(DualArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * BK, t);
-      sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * BK, t);
+      sa.load(A1, g.lda1, A2, g.lda2, g.M, g.K, m0, static_cast<int64_t>(kt + 1) * BK, t, g.arows);
+      sb.load(B1, g.ldb1, B2, g.ldb2, g.N, g.K, n0, static_cast<int64_t>(kt + 1) * BK, t, brows);
     }
 #pragma unroll
     for (int up = 0; up < 2 * (BK / 16); ++up) {  // sub-stage u of product p: 8 k-values per tile row, MFMAs
@@ -392,9 +404,10 @@ __global__ __launch_bounds__(kThreads, 2) void dual_gemm_kernel(DualArgs g) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int64_t row = m0 + wm + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
-          const bool ok = row < g.M;
-          sv[q] = ok ? Se[row * g.lds + col] : 0.f;
-          xv[q] = ok ? Xe[row * g.ldx + col] : 0.f;
+          const int64_t er = (g.erows != nullptr && row < g.M) ? static_cast<int64_t>(g.erows[row]) : row;
+          const bool ok = row < g.M && er >= 0;
+          sv[q] = ok ? Se[er * g.lds + col] : 0.f;
+          xv[q] = ok ? Xe[er * g.ldx + col] : 0.f;
         }
       }
 #pragma unroll
@@ -438,6 +451,7 @@ int dual_gemm_f32(const DualGemm& d, hipStream_t st) {
       d.ldc1 < N || d.ldc2 < N)
     return KGAT_ERR_INVALID;
   if (d.dxs && (!d.X || !d.S || d.ldx < N || d.lds < N || d.batch != 1)) return KGAT_ERR_INVALID;
+  if ((d.arows && d.ta) || (d.brows && d.tb) || (d.erows && !d.dxs)) return KGAT_ERR_INVALID;  // row lists
   if (d.a_um && d.ta) return KGAT_ERR_INVALID;  // (X+S, X*S) pairs: row-major k-contiguous A only
   if (d.b_um && d.tb) return KGAT_ERR_INVALID;  // ... and row-major [K, N] B only
   if ((d.cs1 != nullptr) != (d.cs2 != nullptr) || (d.cs1 && !d.ta)) return KGAT_ERR_INVALID;
@@ -445,7 +459,7 @@ int dual_gemm_f32(const DualGemm& d, hipStream_t st) {
   if (tiles > 0x7fffffff || d.batch > 65535) return KGAT_ERR_INVALID;
   DualArgs g{d.A1, d.A2, d.lda1, d.lda2, d.sA1, d.sA2, d.B1, d.B2, d.ldb1, d.ldb2, d.sB1, d.sB2,
              d.C1, d.C2, d.ldc1, d.ldc2, d.sC1, d.sC2, M, N, K, d.cs1, d.cs2, d.ldcs, d.sCS1, d.sCS2,
-             d.X, d.S, d.ldx, d.lds};
+             d.X, d.S, d.ldx, d.lds, d.arows, d.brows, d.sBrows, d.erows};
   const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(d.batch));
   // the three forms the bi-interaction uses: forward (UM x W^T), backward du/dm + dXd/dS
   // epilogue (dA.W), weight gradients (dA^T x UM, split-K batches, column sums)

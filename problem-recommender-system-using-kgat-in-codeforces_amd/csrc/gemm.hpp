@@ -42,6 +42,13 @@ struct DualGemm {
   const float* X = nullptr;
   const float* S = nullptr;
   int64_t ldx = 0, lds = 0;
+  // row lists (nullable, -1 = a zero row): arows -- A's stored row of each of its M rows (not
+  // transposed A); brows -- B's stored row of each of its K rows (row-major B; batch z reads
+  // brows + z * sBrows); erows -- the dXd / dS epilogue's row of X / S for each output row
+  const int32_t* arows = nullptr;
+  const int32_t* brows = nullptr;
+  int64_t sBrows = 0;
+  const int32_t* erows = nullptr;
 };
 int dual_gemm_f32(const DualGemm& d, hipStream_t st);
 

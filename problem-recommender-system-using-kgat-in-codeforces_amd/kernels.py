@@ -840,10 +840,13 @@ def spmm_biinter_fwd(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0
 
 
 def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,
-                rows: torch.Tensor | None = None, H: torch.Tensor | None = None, state: BiState | None = None):
+                rows: torch.Tensor | None = None, H: torch.Tensor | None = None, state: BiState | None = None,
+                dh_full: bool = False):
     """Returns (dXd, dS, dW1, db1, dW2, db2).  With ``rows`` (int32 [n]), dH/dXd/dS are compact:
     row i belongs to node rows[i] of X and S (-1 = padding).  With the forward's output ``H`` and
-    ``state``, the backward reads them instead of recomputing the forward."""
+    ``state``, the backward reads them instead of recomputing the forward.  ``dh_full`` (with rows):
+    dH is indexed by node ([X rows, d_out]); the wide kinds then read every operand through the row
+    list (kgat_biinter_bwd_gemm_rows_f32: no gathered copies, same bits)."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     _req(dH, "dH", dim=2)
@@ -851,6 +854,12 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     if rows is not None:
         _req(rows, "rows", dtype=torch.int32, dim=1)
         n = rows.numel()
+    if dh_full:
+        if rows is None or dH.shape != (src_rows, dout):
+            raise ValueError("dh_full needs rows and a [nodes, d_out] dH")
+        if state is not None and state.kind in ("gemm", "bits") and H is not None:
+            return _biinter_bwd_rows(X, S, dH, W1, W2, dropout_p, seed, dXd, dS, rows, H, state)
+        dH = gather_rows(dH, rows)
     if dH.shape != (n, dout):
         raise ValueError("dH shape mismatch")
     if (H is None) != (state is None):
@@ -884,6 +893,34 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
               _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), n, din, dout,
               float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
               rows.data_ptr() if rows is not None else None, src_rows, ws.data_ptr(), ws.numel(), stream_ptr(dev))
+    return dXd, dS, dW1, db1, dW2, db2
+
+
+def _biinter_bwd_rows(X, S, dH, W1, W2, p, seed, dXd, dS, rows, H, state):
+    """The wide backward on a row list, every operand read through it (kgat_biinter_bwd_gemm_rows_f32)."""
+    src_rows, din = X.shape
+    dout = W1.shape[0]
+    dev = X.device
+    m = rows.numel()
+    _req(H, "H", dim=2)
+    if H.shape != (src_rows, dout) or state.n != src_rows:
+        raise ValueError("bi-interaction state does not match the layer")
+    dXd = torch.empty(m, din, dtype=torch.float32, device=dev) if dXd is None else dXd
+    dS = torch.empty(m, din, dtype=torch.float32, device=dev) if dS is None else dS
+    dW1, dW2 = torch.empty_like(W1), torch.empty_like(W2)
+    db1 = torch.empty(dout, dtype=torch.float32, device=dev)
+    db2 = torch.empty(dout, dtype=torch.float32, device=dev)
+    w = int(_lib.lib().kgat_biinter_bwd_gemm_rows_work_floats(m, din, dout))
+    if w < 0:
+        raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
+    work = torch.empty(max(w, 1), dtype=torch.float32, device=dev)
+    gemm = state.kind == "gemm"
+    _lib.call("kgat_biinter_bwd_gemm_rows_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
+              state.P.data_ptr() if gemm else None, None if gemm else state.norm.data_ptr(),
+              None if gemm else state.mask.data_ptr(), dH.data_ptr(), _ld(dH), rows.data_ptr(), m,
+              W1.data_ptr(), W2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(),
+              db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), src_rows, din, dout, float(p),
+              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), work.data_ptr(), work.numel(), stream_ptr(dev))
     return dXd, dS, dW1, db1, dW2, db2
 
 

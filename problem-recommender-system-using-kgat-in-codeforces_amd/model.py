@@ -357,52 +357,67 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     return rows, hop, fcount, tok
 
 
+def _tile_forward_ok(din: int, dout: int) -> bool:
+    """Shapes whose forward can run on a row set's 16-row tiles (kgat_biinter_fwd_tiles_f32: the fused
+    kernels with their saved state -- norm + sign/keep words)."""
+    return kernels.fused_supported(din, dout) and dout <= 128 and (
+        kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
+
+
 def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
-    """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1 or 2, every layer
-    with the fused saved state).  The BPR loss reads the batch rows F of every table (model.py:189-191),
-    so the last layer's output is needed on F only, and with 2 layers layer 0's on the first hop
-    F + N(F) (layer 1 gathers its A rows from there) -- the same row sets the backward's hop chain
-    runs on.  Each layer then runs kgat_spmm_csr_rows_f32 on its set's rows and
-    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them (the set's bitmap): every row the step reads gets the
-    full forward's bits (same edges, order and dropout draws), rows outside are never read.  At C2
-    layer 0's set is 1.7 % of the rows (35 % of the edges), layer 1's the ~768 batch rows.
+    """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1, 2 or 3, the
+    restricted layers with the fused kernels' saved state).  The BPR loss reads the batch rows F of
+    every table (model.py:189-191), so the last layer's output is needed on F only, and layer L-2's
+    on the first hop F + N(F) (the last layer gathers its A rows from there) -- the same row sets the
+    backward's hop chain runs on; with 3 layers layer 0 stays whole (its output is read on the second
+    hop, most rows at C4).  Each restricted layer runs kgat_spmm_csr_rows_f32 on its set's rows and
+    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them (the set's bitmap): every row the step
+    reads gets the full forward's bits (same edges, order and dropout draws), rows outside are never
+    read.  At C2 layer 0's set is 1.7 % of the rows (35 % of the edges), layer 1's the ~768 batch rows.
     Returns (tables, sides, states, early) -- early as _early_first_hop's, for the backward -- or
     None when the shapes do not qualify (the full forward runs)."""
     L = len(drops)
-    if L not in (1, 2) or HOP_DENSE_FRACTION <= 0:
+    if L not in (1, 2, 3) or HOP_DENSE_FRACTION <= 0:
         return None
     dims = [X0.shape[1]] + [ws[4 * l].shape[0] for l in range(L)]
-    if not all(kernels.saved_state_supported(dims[l], dims[l + 1]) for l in range(L)):
+    first = max(0, L - 2)  # the first restricted layer
+    if not all(_tile_forward_ok(dims[l], dims[l + 1]) for l in range(first, L)):
         return None
-    if L == 2 and early is None and not _hop_small(graph, 0, graph.n_nodes):
+    if L == 3 and (early is not None or not kernels.fused_supported(dims[0], dims[1])):
+        return None
+    if L >= 2 and early is None and not _hop_small(graph, L - 2, graph.n_nodes):
         return None
     n = graph.n_nodes
     if early is None:
         rows, fcount, tok = _mark_batch(graph, users, pos, neg)
-        hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0) if L == 2 else None)
-        if L == 2:
-            _hop_record(graph, 0)
+        hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, L - 2) if L >= 2 else None)
+        if L >= 2:
+            _hop_record(graph, L - 2)
         early = (rows, hop, fcount, tok)
     rows, hop, fcount, tok = early
     hrows, _, hcount, bits1, fbits = hop
-    # layer l's output row set: the first hop for layer 0 of 2, the batch rows F for the last layer
-    sets = [(hrows, hcount, bits1)] * (L - 1) + [(rows, fcount, fbits)]
+    # layer l's output row set: None = every row (layer 0 of 3), the first hop for layer L-2, the batch
+    # rows F for the last layer
+    sets = [None] * first + [(hrows, hcount, bits1)] * (L - 1 - first) + [(rows, fcount, fbits)]
     tables, sides, states = [X0], [], []
     x = X0
     for l in range(L):
         W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
-        out_rows, out_count, out_bits = sets[l]
         st = kernels.make_state(n, dims[l], dims[l + 1], x.device)
-        s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
-                              out_count, out_bits)
-        x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
-                                      torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device), out_bits,
-                                      state=st)
+        if sets[l] is None:
+            s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st)
+        else:
+            out_rows, out_count, out_bits = sets[l]
+            s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
+                                  out_count, out_bits)
+            x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
+                                          torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device),
+                                          out_bits, state=st)
         sides.append(s)
         states.append(st)
         tables.append(x)
     # L = 1: the backward's last layer needs the batch rows only (no hop set is handed over)
-    return tables, sides, states, (early if L == 2 else (rows, None, fcount, tok))
+    return tables, sides, states, (early if L >= 2 else (rows, None, fcount, tok))
 
 
 def _saved(tables, states, l) -> dict:
@@ -519,9 +534,14 @@ class _CFLoss(torch.autograd.Function):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             fused = states[l] is not None and states[l].kind == "fused"
             compact_dh = pending is not None
+            n_hop = None
             if compact_dh:  # dX is compact over the first hop set
                 hrows, hmap, hcount = pending
                 pending = None
+                if not fused:  # the wide kinds size their compact problem on the host
+                    est = graph._hop_est[l]
+                    est[1].synchronize()
+                    n_hop = int(est[0][0])
             elif sparse and fused:
                 # hop size stays on the device (no host sync); the sparse/dense choice uses the
                 # size this layer's hop set had at the previous step
@@ -548,11 +568,18 @@ class _CFLoss(torch.autograd.Function):
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd_hop(
                         tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], out_rows,
                         dh_compact=compact_dh, out=out)
-                else:
-                    dHc = kernels.gather_rows(dX, hrows)
-                    dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2,
-                                                                        drops[l], seeds[l], rows=hrows,
+                elif compact_dh:
+                    # wide kinds after the first-hop product: dX holds the hop rows compactly
+                    hr = hrows[:n_hop]
+                    dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX[:n_hop], W1, b1, W2,
+                                                                        b2, drops[l], seeds[l], rows=hr,
                                                                         **_saved(tables, states, l))
+                    hrows = hr
+                else:
+                    # wide kinds: H, dH and the state read through the hop list (X / S gathered once)
+                    dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2,
+                                                                        drops[l], seeds[l], rows=hrows,
+                                                                        dh_full=True, **_saved(tables, states, l))
                 kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
                 if l == 0 and hook is not None and hook.replicated:
                     # data-parallel replicas exchange the compact hop-set terms and each computes the

@@ -473,11 +473,11 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
     ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
     own = Pg[int(off[k]):int(off[k + 1])]
     hr = hrows[:mine] if mine else torch.full((1,), -1, dtype=torch.int32, device=dev)
-    dHc = kernels.gather_rows(dX, hr)
     dS_out = own[:, :din] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
     dXd_out = own[:, din:] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
-    _, _, *g = kernels.biinter_bwd(tables[l], sides[l], dHc, W1, b1, W2, b2, drops[l], seeds[l], dXd=dXd_out,
-                                   dS=dS_out, rows=hr,
+    # dX is indexed by local row: the wide kinds read it (and X, S, H, the state) through the hop list
+    _, _, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], dXd=dXd_out,
+                                   dS=dS_out, rows=hr, dh_full=True,
                                    **({} if states[l] is None else {"H": tables[l + 1], "state": states[l]}))
     reduce_w(l, g)
     if mine:

@@ -1611,13 +1611,15 @@ def test_device_id_error_moves_no_parameter(pkg, fused):
     assert not torch.equal(m._user_entity_embedding.weight.detach(), before["_user_entity_embedding.weight"])
 
 
-@pytest.mark.parametrize("layers", [[64], [64, 32], [64, 64], [64, 32, 16]])
-def test_frontier_forward_bit_identical(pkg, layers, monkeypatch):
+@pytest.mark.parametrize("dim,layers", [(64, [64]), (64, [64, 32]), (64, [64, 64]), (64, [64, 32, 16]),
+                                        (128, [128, 64, 32])])
+def test_frontier_forward_bit_identical(pkg, dim, layers, monkeypatch):
     """KGAT.frontier_forward (TRAIN_CF's forward on the rows the loss can reach: layer 0 of 2 on
     the first hop F + N(F), the last layer on the batch rows F -- kgat_spmm_csr_rows_f32 +
     kgat_biinter_fwd_tiles_f32) against the full forward: losses, parameters and both Adam
     moments bit for bit over three train-mode CF steps (dropout on, fused table update on) with a
-    KG step in between, on a hub-row graph; 3 layers fall back to the full forward."""
+    KG step in between, on a hub-row graph; with 3 layers layer 0 stays whole and layers 1 / 2 run
+    on the first hop / the batch rows (C4's shape 128 -> [128, 64, 32]: wide "bits" layers)."""
     graph_mod, _ = _mods(pkg)
     kmod = sys.modules[pkg.__name__ + ".kernels"]
     calls = {"rows": 0}
@@ -1633,7 +1635,7 @@ def test_frontier_forward_bit_identical(pkg, layers, monkeypatch):
     for frontier in (False, True):
         torch.manual_seed(77)
         m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
-                                  message_dropout=[0.1] * len(layers)))
+                                  cf_embedding_dim=dim, kg_embedding_dim=dim, message_dropout=[0.1] * len(layers)))
         m.attach_graph(lay, DEV)
         assert m.graph().A.n_long > 0  # hub rows take the segment + fix-up path
         m.train()
@@ -1656,7 +1658,7 @@ def test_frontier_forward_bit_identical(pkg, layers, monkeypatch):
             m(kg[0], kg[1], kg[2], kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
             m.update_kg_weights()
         assert torch.equal(losses[0], losses[1]), (step, losses)
-    assert calls["rows"] == (3 * len(layers) if len(layers) <= 2 else 0)
+    assert calls["rows"] == 3 * min(len(layers), 2)  # the restricted layers of the three frontier steps
     a, b = models
     for (k, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         if not pa.is_sparse:
@@ -1838,3 +1840,29 @@ def test_csr_mark_rows_matches_numpy(pkg):
     want = inset[lo:hi].copy()
     want[rows[inset[sh_col]]] = True
     np.testing.assert_array_equal(hit.cpu().numpy(), want.astype(np.int32))
+
+
+@pytest.mark.parametrize("din,dout,kind", [(256, 256, "gemm"), (256, 128, "gemm"), (128, 128, "bits"),
+                                           (128, 64, "bits")])
+def test_biinter_bwd_rows_matches_gathered(pkg, din, dout, kind):
+    """kgat_biinter_bwd_gemm_rows_f32 (the hop rows' wide backward read through the row list, dH by
+    node) vs the gathered compact backward (X, S, H, state and dH gathered first): dXd, dS and every
+    weight gradient bit for bit, with -1 padding rows and dropout."""
+    _, kernels = _mods(pkg)
+    n = 5000 + 11
+    g = torch.Generator().manual_seed(din + dout)
+    dv = [t.to(DEV) for t in (torch.randn(n, din, generator=g), torch.randn(n, din, generator=g),
+                              torch.randn(dout, din, generator=g) * 0.1, torch.randn(dout, generator=g) * 0.1,
+                              torch.randn(dout, din, generator=g) * 0.1, torch.randn(dout, generator=g) * 0.1)]
+    rows_np = np.sort(np.random.default_rng(2).choice(n, 1500, replace=False))
+    rows = torch.from_numpy(np.concatenate([rows_np, [-1] * 7]).astype(np.int32)).to(DEV)
+    dHfull = torch.randn(n, dout, generator=g).to(DEV)
+    outs = []
+    for full in (False, True):
+        st = kernels.BiState(n, DEV, din, dout, kind=kind)
+        H = kernels.biinter_fwd(*dv, dropout_p=0.15, seed=21, state=st)
+        dH = dHfull if full else kernels.gather_rows(dHfull, rows)
+        outs.append(kernels.biinter_bwd(dv[0], dv[1], dH, *dv[2:], dropout_p=0.15, seed=21, rows=rows, H=H, state=st,
+                                        dh_full=full))
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i

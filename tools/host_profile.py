@@ -1,4 +1,5 @@
-"""Host-side profile of the CF training step (python tools/host_profile.py [--full]): cProfile over
+"""Host-side profile of the CF training step (python tools/host_profile.py [--full] [--kg [--unfused]]: the
+KG step instead): cProfile over
 200 steps of a small synthetic graph (host launch cost does not depend on the graph size), printing
 the functions with the most own time.  Used to find Python / ctypes overhead in the step's launches."""
 import cProfile
@@ -33,7 +34,20 @@ def main():
     batches = [[torch.from_numpy(rng.integers(0, hi, 256)).to(dev) for hi in (U, int(E * 0.1), int(E * 0.1))]
                for _ in range(16)]
 
+    kg = "--kg" in sys.argv
+    if kg:  # the KG phase's step (main.py:324-345) at the reference's B = 512, fused table update
+        m.fuse_kg_table_update = "--unfused" not in sys.argv
+        n = U + E
+        batches = [[torch.from_numpy(x).to(dev) for x in (lay.heads[e], lay.rels[e], lay.tails[e],
+                                                          rng.integers(0, n, 512))]
+                   for e in (rng.integers(0, lay.heads.size, 512) for _ in range(16))]
+
     def step(b):
+        if kg:
+            loss = m(*b, mode=pkg.KGATMode.TRAIN_KG)
+            loss.backward()
+            m.update_kg_weights()
+            return
         loss = m(*b, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
         m.update_cf_weights()
@@ -47,7 +61,7 @@ def main():
     host = time.perf_counter() - t0
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    print(f"{'full' if full else 'frontier'}: host {host / 200 * 1e3:.3f} ms/step, wall {wall / 200 * 1e3:.3f} ms/step")
+    print(f"{'kg' if kg else ('full' if full else 'frontier')}: host {host / 200 * 1e3:.3f} ms/step, wall {wall / 200 * 1e3:.3f} ms/step")
     pr = cProfile.Profile()
     pr.enable()
     for i in range(200):
