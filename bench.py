@@ -556,8 +556,9 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         return loss
 
     out = {"batch": B}
-    for tag, fused in (("fused", True), ("unfused", False)):
+    for tag, fused, lazy in (("lazy", True, True), ("fused", True, False), ("unfused", False, False)):
         model.fuse_kg_table_update = fused
+        model.lazy_kg_adam = lazy
         for i in range(args.warmup):
             kg_step(batches[i])
         torch.cuda.synchronize()
@@ -575,6 +576,17 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         torch.cuda.synchronize()
         evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
         leg = {"ms_per_step": el, "kg_pairs_per_s": B / (el * 1e-3)}
+        if lazy:
+            # the flush that brings every row current (before the next CF step): here after the leg's
+            # warmup + 2 x steps KG steps, i.e. that many zero-gradient steps replayed for almost every row
+            pend = args.warmup + args.steps + min(args.steps, 8)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            model.flush_kg_table()
+            torch.cuda.synchronize()
+            leg["flush_ms"] = (time.perf_counter() - t1) * 1e3
+            leg["flush_steps_pending"] = pend
+            model.lazy_kg_adam = False
         for k in ("transr_fwd", "transr_bwd", "adam_rows", "adam_multi"):
             t = _event_ms(evs, k)
             if t:
@@ -635,12 +647,21 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         ref["row_softmax_GBps"] = by / (float(np.mean(t)) * 1e-3) / 1e9
     out["refresh"] = ref
     n_cf, n_kg = n_interactions // 256 + 1, E // 512 + 1
+    lz = out["lazy"]
+    # a row's pending zero-gradient steps at the phase's end: ~ the steps since the batch last drew it
+    # (n / 1,536 rows per step on average, at most the phase): the end-of-phase flush scales from the
+    # measured one by that over its pending steps
+    pend_epoch = min(n_kg, n / (3 * B))
+    lz["epoch_flush_ms_estimate"] = lz["flush_ms"] * pend_epoch / lz["flush_steps_pending"]
+    kg_lazy_s = n_kg * lz["ms_per_step"] + lz["epoch_flush_ms_estimate"]
     ep = n_cf * cf_ms + n_kg * out["fused"]["ms_per_step"] + rms
     out["epoch_estimate"] = {
         "cf_steps": n_cf, "kg_steps": n_kg, "cf_ms_per_step": cf_ms, "kg_ms_per_step": out["fused"]["ms_per_step"],
         "refresh_ms": rms, "seconds": ep / 1e3,
+        "seconds_lazy_kg_adam": (n_cf * cf_ms + kg_lazy_s + rms) / 1e3,
         "what": "one reference epoch (main.py:290-361: CF phase, KG phase, attention refresh; no evaluation) at the "
-                "measured per-step times"}
+                "measured per-step times (seconds_lazy_kg_adam: the KG phase with KGAT.lazy_kg_adam, its "
+                "end-of-phase flush included)"}
     return out
 
 
@@ -715,6 +736,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
                               None, comm, dev, shard=shard)
     model.train()
     model.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    model.fuse_table_update = not args.no_fused_update  # layer 0's table product fused with the shard's Adam
     B = cfg["batch"]
     rng = np.random.default_rng(7 + rank)
     batches = []
@@ -781,6 +803,7 @@ def sharded_frontier_matches_full(model, pkg, batch) -> dict:
         model._step = step0
         loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
         loss.backward()
+        model.materialize_table_grad()  # fuse_table_update leaves it to update_cf_weights otherwise
         outs.append([loss.detach().clone()] + [p.grad.detach().clone() for p in model.parameters()
                                                if not p.is_sparse and p.grad is not None])
     model.frontier_forward = False
@@ -800,6 +823,7 @@ def sharded_parity(model, pkg, batch, whole, n: int, cfg: dict) -> dict:
     tables = [t.cpu() for t in model.propagate()]
     loss = model(*batch, mode=pkg.KGATMode.TRAIN_CF)
     loss.backward()
+    model.materialize_table_grad()
     grad = model._user_entity_embedding_shard.grad.detach().cpu()
     state = {k: v.detach().float().cpu().clone() for k, v in model.state_dict().items()
              if k.startswith("_aggregator")}

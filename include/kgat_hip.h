@@ -127,6 +127,17 @@ int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr *A, const int32_t *src_map, 
                                      float beta2, float bc2_sqrt, float eps, const int32_t *skip, float *workspace,
                                      int64_t workspace_floats, void *stream);
 
+/* kgat_spmm_csr_masked_adam_ex_f32 on a row block of a square matrix: A's row r is row yc_row0 + r
+ * of the whole (the Yc_init lookup is Yc_init[src_map[yc_row0 + r]]; src_map covers the whole
+ * matrix), p / m / v the block's own rows.  The row-sharded model's table update: its rows of A^T,
+ * global column ids, the gathered compact [dS | dXd] rows. */
+int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                        const float *Yc_init, int64_t ldyc, int64_t yc_row0,
+                                        const uint64_t *src_rank, float *p, float *m, float *v, int64_t ldp,
+                                        int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
+                                        float eps, const int32_t *skip, float *workspace, int64_t workspace_floats,
+                                        void *stream);
+
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 
@@ -605,6 +616,24 @@ int kgat_adam_multi_ex_f32(const kgat_adam_tensor *tensors, int32_t count, float
 int kgat_adam_rows_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *row_map,
                        const float *Gc, int64_t ldg, float step_size, float beta1, float beta2, float bc2_sqrt,
                        float eps, const int32_t *skip, void *stream);
+
+/* Lazy table Adam for the KG phase (KGAT.lazy_kg_adam): the dense step moves every row each step
+ * (rows outside the batch with a zero gradient); here row r records the last step applied to it
+ * (last[r]) and its skipped zero-gradient steps are replayed in order -- each with its own step size,
+ * bias correction and skip flag, kept in a device history of cap entries (step s at s % cap) -- when
+ * it is next read or updated, or at a flush.  Every element goes through the dense step's sequence of
+ * adam_elem operations: same bits.  d divides 256 (<= 256).
+ * kgat_adam_lazy_catchup_f32: the listed rows (rows null: all n_rows) brought up to step t.
+ * kgat_adam_lazy_rows_f32: step t (>= 1) on the listed rows with their compact gradients Gc[k]
+ * (kgat_frontier_build's order; the rows' skipped steps replayed first), step t's scalars and skip flag
+ * (*skip, nullable) recorded for the other rows.  A caller keeps t - min(last) < cap (flush before). */
+int kgat_adam_lazy_catchup_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *rows,
+                               int64_t n_list, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
+                               int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, void *stream);
+int kgat_adam_lazy_rows_f32(float *p, float *m, float *v, int32_t d, const int32_t *rows, int64_t n_list,
+                            const float *Gc, int64_t ldg, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
+                            int32_t *hist_skip, int32_t cap, float step_size, float beta1, float beta2,
+                            float bc2_sqrt, float eps, const int32_t *skip, void *stream);
 
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);

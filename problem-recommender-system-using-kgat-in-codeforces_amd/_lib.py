@@ -182,6 +182,13 @@ _SIGNATURES = {
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
     "kgat_map_build": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "kgat_map_compose": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "kgat_adam_lazy_catchup_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp,
+                                                  c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_vp]),
+    "kgat_adam_lazy_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
+                                               c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
+    "kgat_spmm_csr_masked_adam_block_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                                           c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32,
+                                                           c_f32, c_f32, c_vp, c_vp, c_i64, c_vp]),
     "kgat_csr_mark_rows": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kgat_biinter_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_biinter_bwd_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),

@@ -3,6 +3,8 @@
 
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace kgat {
@@ -312,6 +314,129 @@ extern "C" int kgat_adam_rows_f32(float* p, float* m, float* v, int64_t n_rows, 
   const int grid = static_cast<int>(chunks < kgat::kCUs * 8 ? chunks : kgat::kCUs * 8);
   hipLaunchKernelGGL(kgat::adam_rows_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p, m, v,
                      n4, d / 4, row_map, Gc, ldg, step_size, beta1, beta2, bc2_sqrt, eps, skip);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+namespace kgat {
+
+// Lazy table Adam (the KG phase's table update on the batch rows only).  The dense step moves every
+// row each step -- rows outside the batch with a zero gradient, which still decays their moments and
+// moves p.  Here a row keeps the number of the last step applied to it (last[row]); the steps it
+// skipped are replayed in order, with their own step size and bias correction (kept on the device,
+// entry s % cap of the history) and the same adam_elem(g = 0) arithmetic, when it is next read or
+// updated, and for every row at a flush.  Each element's sequence of operations is the dense step's,
+// so the values are the same bits.  A row's elements are threads of one block (256 % d == 0).
+struct LazyHist {
+  float* sz;
+  float* bc;
+  int32_t* skip;
+  int32_t cap;
+};
+
+__device__ __forceinline__ void lazy_replay(float& p, float& m, float& v, int32_t from, int32_t to, const LazyHist& h,
+                                            float w1, float b2, float w2, float eps) {
+  for (int32_t s = from + 1; s <= to; ++s) {
+    const int32_t j = s % h.cap;
+    if (h.skip[j] != 0) continue;
+    adam_elem(p, 0.f, m, v, w1, b2, w2, h.sz[j], h.bc[j], eps);
+  }
+}
+
+// rows (nullable = every row): bring the listed rows up to step t (replay only).
+__global__ __launch_bounds__(256) void adam_lazy_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                                float* __restrict__ v, int d,
+                                                                const int32_t* __restrict__ rows, int64_t n_list,
+                                                                int32_t* __restrict__ last, int32_t t, LazyHist h,
+                                                                float b1, float b2, float eps) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t k = i / d;
+  const int c = static_cast<int>(i % d);
+  const int64_t r = k < n_list ? (rows != nullptr ? static_cast<int64_t>(rows[k]) : k) : -1;
+  const int32_t from = r >= 0 ? last[r] : t;
+  if (from < t) {
+    const int64_t o = r * d + c;
+    float pp = p[o], mm = m[o], vv = v[o];
+    lazy_replay(pp, mm, vv, from, t, h, 1.f - b1, b2, 1.f - b2, eps);
+    p[o] = pp;
+    m[o] = mm;
+    v[o] = vv;
+  }
+  __syncthreads();  // every thread of the row has read last[r]
+  if (c == 0 && r >= 0 && from < t) last[r] = t;
+}
+
+// Step t on the listed rows (rows[k] with the compact gradient Gc[k]): the skipped steps first,
+// then step t itself; step t's scalars and skip flag go into the history for the other rows.
+__global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                             float* __restrict__ v, int d,
+                                                             const int32_t* __restrict__ rows, int64_t n_list,
+                                                             const float* __restrict__ Gc, int64_t ldg,
+                                                             int32_t* __restrict__ last, int32_t t, LazyHist h,
+                                                             float step_size, float b1, float b2, float bc2s,
+                                                             float eps, const int32_t* __restrict__ skip) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const bool skipped = skip != nullptr && *skip != 0;
+  if (i == 0) {
+    const int32_t j = t % h.cap;
+    h.sz[j] = step_size;
+    h.bc[j] = bc2s;
+    h.skip[j] = skipped ? 1 : 0;
+  }
+  const int64_t k = i / d;
+  const int c = static_cast<int>(i % d);
+  const int64_t r = k < n_list ? static_cast<int64_t>(rows[k]) : -1;
+  const int32_t from = r >= 0 ? last[r] : t;
+  if (r >= 0 && !skipped) {
+    const float w1 = 1.f - b1, w2 = 1.f - b2;
+    const int64_t o = r * d + c;
+    float pp = p[o], mm = m[o], vv = v[o];
+    lazy_replay(pp, mm, vv, from, t - 1, h, w1, b2, w2, eps);
+    adam_elem(pp, Gc[k * ldg + c], mm, vv, w1, b2, w2, step_size, bc2s, eps);
+    p[o] = pp;
+    m[o] = mm;
+    v[o] = vv;
+  }
+  __syncthreads();
+  if (c == 0 && r >= 0 && !skipped) last[r] = t;
+}
+
+}  // namespace kgat
+
+static bool lazy_args_ok(const float* p, const float* m, const float* v, int32_t d, const int32_t* last,
+                         const float* hsz, const float* hbc, const int32_t* hskip, int32_t cap) {
+  return p && m && v && last && hsz && hbc && hskip && cap > 0 && d > 0 && d <= 256 && (256 % d) == 0;
+}
+
+extern "C" int kgat_adam_lazy_catchup_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
+                                          const int32_t* rows, int64_t n_list, int32_t* last, int32_t t,
+                                          float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
+                                          float beta1, float beta2, float eps, void* stream) {
+  if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || n_rows < 0 || n_list < 0 || t < 0)
+    return KGAT_ERR_INVALID;
+  const int64_t n = rows != nullptr ? n_list : n_rows;
+  if (n == 0) return KGAT_OK;
+  const int64_t blocks = (n * d + 255) / 256;
+  if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::adam_lazy_catchup_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     p, m, v, d, rows, n, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap}, beta1, beta2,
+                     eps);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_adam_lazy_rows_f32(float* p, float* m, float* v, int32_t d, const int32_t* rows, int64_t n_list,
+                                       const float* Gc, int64_t ldg, int32_t* last, int32_t t, float* hist_sz,
+                                       float* hist_bc, int32_t* hist_skip, int32_t cap, float step_size,
+                                       float beta1, float beta2, float bc2_sqrt, float eps, const int32_t* skip,
+                                       void* stream) {
+  if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || !rows || !Gc || n_list < 0 || ldg < d ||
+      t < 1)
+    return KGAT_ERR_INVALID;
+  const int64_t blocks = (std::max<int64_t>(n_list, 1) * d + 255) / 256;  // >= 1 block: the history entry
+  hipLaunchKernelGGL(kgat::adam_lazy_rows_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     p, m, v, d, rows, n_list, Gc, ldg, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap},
+                     step_size, beta1, beta2, bc2_sqrt, eps, skip);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

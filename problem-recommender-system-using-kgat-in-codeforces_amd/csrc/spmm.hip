@@ -688,7 +688,19 @@ extern "C" int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr* A, const int32_t
                                                 int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
                                                 float eps, const int32_t* skip, float* workspace,
                                                 int64_t workspace_floats, void* stream) {
+  return kgat_spmm_csr_masked_adam_block_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, src_rank, p, m, v, ldp, d,
+                                             step_size, beta1, beta2, bc2_sqrt, eps, skip, workspace,
+                                             workspace_floats, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                   int64_t ldxc, const float* Yc_init, int64_t ldyc, int64_t yc_row0,
+                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                                   int32_t d, float step_size, float beta1, float beta2,
+                                                   float bc2_sqrt, float eps, const int32_t* skip, float* workspace,
+                                                   int64_t workspace_floats, void* stream) {
   using namespace kgat;
+  if (yc_row0 < 0) return KGAT_ERR_INVALID;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
@@ -698,7 +710,7 @@ extern "C" int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr* A, const int32_t
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
+  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
   io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
   // KGAT_TU_BATCH=1: the row-batched form (kMaskedAdamB, same bits); default the row-at-a-time one

@@ -273,6 +273,40 @@ def spmm_masked(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_
     return out
 
 
+def spmm_masked_adam_block(csr, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None, row0: int,
+                           p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step_size: float, beta1: float,
+                           beta2: float, bc2_sqrt: float, eps: float, skip: torch.Tensor | None = None) -> None:
+    """spmm_masked_adam on a row block of the transposed graph (a shard's rows of A^T, global columns):
+    block row r is global row row0 + r (its Yc row: Yc_init[src_map[row0 + r]]); p / m / v are the
+    block's rows (kgat_spmm_csr_masked_adam_block_f32)."""
+    _req(src_map, "src_map", dtype=torch.int32, dim=1)
+    _req(Xc, "Xc", dim=2)
+    n, d = csr.n_rows, Xc.shape[1]
+    for t, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _req(t, nm, dim=2)
+        if tuple(t.shape) != (n, d) or not t.is_contiguous():
+            raise ValueError(f"{nm}: contiguous [{n}, {d}] expected, got {tuple(t.shape)}")
+    if Yc_init is not None:
+        _req(Yc_init, "Yc_init", dim=2)
+        if Yc_init.shape[1] != d or row0 < 0 or row0 + n > src_map.numel():
+            raise ValueError("Yc_init width / row0 mismatch")
+    if n == 0:
+        return
+    desc = csr.descriptor()
+    ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
+              int(row0), None, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt, eps,
+              _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, True, "fused_adam"))
+
+
 def _skip_ptr(skip: torch.Tensor | None):
     """The optimiser skip flag (device int32 [1], kgat_ids_check_ex's bad_dev) or None."""
     if skip is None:

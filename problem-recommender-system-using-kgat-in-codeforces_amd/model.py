@@ -299,16 +299,111 @@ class _KGTableUpdate:
         self.pending = None
         kernels.frontier_reset(rows, self._map)
 
-    def launch(self):
-        """The table's Adam step on the compact gradient (FusedAdam.step(fused=...))."""
+    def launch(self, lazy: "_LazyKGAdam | None" = None, opt=None):
+        """The table's Adam step on the compact gradient (FusedAdam.step(fused=...)); with ``lazy`` on the
+        batch rows only (_LazyKGAdam)."""
         rows, Gc = self.pending
         self.pending = None
         p, row_map = self.param.data, self._map
+        if lazy is not None:
+            return lazy.launch(opt, rows, Gc, row_map)
 
         def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
             kernels.adam_rows(p, m, v, row_map, Gc, step_size, b1, b2, bc2s, eps, skip)
             kernels.frontier_reset(rows, row_map)
         return run
+
+
+class _LazyKGAdam:
+    """The KG phase's table Adam on the batch rows only (opt-in: ``KGAT.lazy_kg_adam``; needs the fused KG
+    table update's compact rows).
+
+    The reference's KG step (main.py:334-342, model.py:414-419) runs Adam over the whole table every
+    step: nn.Embedding's dense gradient is zero outside the <= 3B batch rows, yet those rows still move
+    (their moments decay and p takes the step m / (sqrt(v) + eps)).  At C4 that is 24 B of HBM per
+    parameter per step (5 ms) for 1,536 touched rows.  Here each row records the last KG step applied to
+    it and its skipped zero-gradient steps are replayed, in order and with each step's own step size,
+    bias correction and skip flag (a device history), when the row is next read or updated
+    (kgat_adam_lazy_catchup_f32 / kgat_adam_lazy_rows_f32) -- the dense step's exact sequence of
+    adam_elem operations per element, so the same bits.  Anything that reads the whole table (a CF,
+    PREDICT or UPDATE_ATTENTION forward, the CF update, state_dict, propagate) flushes first: every row
+    is brought up to the current step.  Between a KG step and a flush the table's rows outside recent
+    batches and the KG optimiser's moments are behind: call ``KGAT.flush_kg_table()`` before reading
+    ``_user_entity_embedding.weight`` or the KG optimiser's state directly."""
+
+    CAP = 1 << 20  # history entries (steps); a flush is forced before any row falls this far behind
+
+    def __init__(self, param: torch.Tensor):
+        self.param = param
+        self.enabled = False
+        self.last = None
+        self.hist = None
+        self.flushed_at = 0
+        self.dirty = False  # rows behind the current step (a lazy step since the last flush)
+        self._one = None
+
+    def _t(self, opt) -> int:
+        st = opt.state.get(id(self.param))
+        return int(st["step"]) if st is not None else 0
+
+    def ensure(self, opt) -> None:
+        n = self.param.shape[0]
+        if self.last is None or self.last.numel() != n or self.last.device != self.param.device:
+            dev = self.param.device
+            t = self._t(opt)
+            self.last = torch.full((n,), t, dtype=torch.int32, device=dev)
+            self.hist = (torch.zeros(self.CAP, dtype=torch.float32, device=dev),
+                         torch.zeros(self.CAP, dtype=torch.float32, device=dev),
+                         torch.zeros(self.CAP, dtype=torch.int32, device=dev))
+            self._one = torch.ones(1, dtype=torch.int32, device=dev)
+            self.flushed_at = t
+
+    def catch_up(self, opt, rows: torch.Tensor | None = None) -> None:
+        """Bring the listed rows (None: every row) up to the optimiser's current step."""
+        st = opt.state.get(id(self.param))
+        if self.last is None or st is None or (rows is None and not self.dirty):
+            return
+        t = int(st["step"])
+        p = self.param.data
+        n, d = p.shape
+        hs, hb, hk = self.hist
+        _lib.call("kgat_adam_lazy_catchup_f32", p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                  n, d, rows.data_ptr() if rows is not None else None, rows.numel() if rows is not None else 0,
+                  self.last.data_ptr(), t, hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), self.CAP, opt.beta1,
+                  opt.beta2, opt.eps, stream_ptr(p.device))
+        if rows is None:
+            self.flushed_at = t
+            self.dirty = False
+
+    def launch(self, opt, rows: torch.Tensor, Gc: torch.Tensor, row_map: torch.Tensor):
+        """FusedAdam's fused launch for the table: step t on the batch rows only."""
+        p = self.param.data
+
+        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
+            t = self._t(opt)
+            self.dirty = True
+            hs, hb, hk = self.hist
+            _lib.call("kgat_adam_lazy_rows_f32", p.data_ptr(), m.data_ptr(), v.data_ptr(), p.shape[1], rows.data_ptr(),
+                      rows.numel(), Gc.data_ptr(), Gc.stride(0), self.last.data_ptr(), t, hs.data_ptr(), hb.data_ptr(),
+                      hk.data_ptr(), self.CAP, step_size, b1, b2, bc2s, eps,
+                      skip.data_ptr() if skip is not None else None, stream_ptr(p.device))
+            kernels.frontier_reset(rows, row_map)
+        return run
+
+    def dense_step_done(self, opt) -> None:
+        """A dense step t was just applied to every row (caught up before it): record it in the history as
+        applied (skipped by later replays)."""
+        st = opt.state.get(id(self.param))
+        if self.last is None or st is None:
+            return
+        t = int(st["step"])
+        hs, hb, hk = self.hist
+        p = self.param.data
+        dummy = self._one  # no rows listed: the call only writes step t's history entry, with skip = 1
+        _lib.call("kgat_adam_lazy_rows_f32", p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                  p.shape[1], dummy.data_ptr(), 0, p.data_ptr(), p.shape[1], self.last.data_ptr(), t, hs.data_ptr(),
+                  hb.data_ptr(), hk.data_ptr(), self.CAP, 0.0, opt.beta1, opt.beta2, 1.0, opt.eps, self._one.data_ptr(),
+                  stream_ptr(p.device))
 
 
 class _MarkedBatch:
@@ -685,9 +780,38 @@ class KGAT(nn.Module):
         self._ids = _IdGuard()
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
         self._kg_table_update = _KGTableUpdate(self._user_entity_embedding.weight)
+        self._lazy_kg = _LazyKGAdam(self._user_entity_embedding.weight)
         # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
         # (_frontier_forward) -- same loss, gradients and updates, bit for bit
         self.frontier_forward = False
+
+    @property
+    def lazy_kg_adam(self) -> bool:
+        """Opt-in (with ``fuse_kg_table_update``): the KG step's table Adam on the batch rows only, the
+        other rows' zero-gradient steps replayed when they are next read (_LazyKGAdam; same bits)."""
+        return self._lazy_kg.enabled
+
+    @lazy_kg_adam.setter
+    def lazy_kg_adam(self, on: bool) -> None:
+        if not on:
+            self.flush_kg_table()
+            self._lazy_kg.last = None  # every row current: dense steps from here on
+        self._lazy_kg.enabled = bool(on)
+
+    def flush_kg_table(self) -> None:
+        """Bring every table row and the KG optimiser's moments up to the current KG step (lazy_kg_adam)."""
+        if self._lazy_kg.last is not None and getattr(self, "_kg_optimizer", None) is not None:
+            self._lazy_kg.catch_up(self._kg_optimizer)
+
+    def state_dict(self, *args, **kwargs):
+        self.flush_kg_table()
+        return super().state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        self.flush_kg_table()
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._lazy_kg.last = None  # every row is current: restart the lazy state at the next KG step
+        return out
 
     @property
     def fuse_table_update(self) -> bool:
@@ -794,6 +918,7 @@ class KGAT(nn.Module):
     def propagate(self) -> list[torch.Tensor]:
         """The propagated tables [X0, H1, ..., HL] (no autograd state): PREDICT's first half,
         computed once per evaluation by evaluation.evaluate / recommend_topk."""
+        self.flush_kg_table()
         return self._propagate()
 
     def _build_cf_embeddings(self) -> torch.Tensor:
@@ -821,6 +946,14 @@ class KGAT(nn.Module):
                                      more=[((relations,), self._relation_num)])
         ids = [h, r, p, q]
         ktu = self._kg_table_update if torch.is_grad_enabled() else None
+        lazy = self._lazy_kg
+        if lazy.enabled and getattr(self, "_kg_optimizer", None) is not None:
+            # the batch rows TransR reads, brought up to the last KG step (their skipped steps replayed)
+            lazy.ensure(self._kg_optimizer)
+            row_map = self._kg_table_update.node_map()
+            rows, _ = kernels.frontier_build(h, p, q, row_map)
+            lazy.catch_up(self._kg_optimizer, rows)
+            kernels.frontier_reset(rows, row_map)
         return _KGLoss.apply(*ids, float(self._regularization_params[1]), ktu, self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)
 
@@ -884,6 +1017,7 @@ class KGAT(nn.Module):
         # an earlier step's device-side id error surfaces here; this step's own is caught on the
         # device: its optimiser kernels read the check's flag and leave every parameter as it is
         self._raise_or_abandon(self._cf_optimizer)
+        self.flush_kg_table()
         tu = self._table_update
         fused = None
         if tu.pending is not None:
@@ -901,17 +1035,29 @@ class KGAT(nn.Module):
         """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
         self._raise_or_abandon(self._kg_optimizer)
         self._table_update.materialize()
-        ktu = self._kg_table_update
+        ktu, lazy, opt = self._kg_table_update, self._lazy_kg, self._kg_optimizer
         fused = None
         if ktu.pending is not None:
             if (row_ranges and id(ktu.param) in row_ranges) or ktu.param.grad is not None:
                 ktu.materialize()
+            elif lazy.enabled:
+                lazy.ensure(opt)
+                if lazy._t(opt) + 1 - lazy.flushed_at >= lazy.CAP:
+                    lazy.catch_up(opt)  # no row may fall a whole history behind
+                fused = {id(ktu.param): ktu.launch(lazy, opt)}
             else:
                 fused = {id(ktu.param): ktu.launch()}
-        self._kg_optimizer.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
-        self._kg_optimizer.zero_grad()
+        dense_lazy = lazy.last is not None and fused is None and ktu.param.grad is not None
+        if dense_lazy:
+            lazy.catch_up(opt)  # a dense table step follows: every row current first (no-op when clean)
+        opt.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
+        if dense_lazy:
+            lazy.dense_step_done(opt)
+        opt.zero_grad()
 
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:
+        if mode != KGATMode.TRAIN_KG:
+            self.flush_kg_table()  # lazy KG Adam: these modes read the whole table
         if mode != KGATMode.PREDICT:
             # a deferred table gradient refers to this step's hop buffers and A's values (CF) or
             # holds the batch-row map (KG): a new backward or an attention refresh would change them

@@ -447,8 +447,52 @@ def _frontier_sets(shard: RowShard, comm, rows, L: int):
     return sets
 
 
+class _ShardTableUpdate:
+    """The row-sharded CF step's table gradient left as its last product until ``update_cf_weights``
+    (``RowShardedKGAT.fuse_table_update``; the single-GPU model._TableUpdate's idea): with the hop
+    backward, layer 0's table gradient is the masked product AT_loc . dS (+ dXd) of the gathered compact
+    [dS | dXd] hop rows; deferred, the update runs it fused with the shard's Adam step
+    (kgat_spmm_csr_masked_adam_block_f32): each product row is the gradient of its table row and goes
+    straight into that row's Adam -- no [rows, d] gradient written and read back.  Same bits as the
+    product + Adam.  Anything that needs the gradient first (a forward, a KG update) materialises it."""
+
+    def __init__(self):
+        self.pending = None
+
+    def defer(self, shard: RowShard, Pg: torch.Tensor, ids: torch.Tensor, total: int, din: int) -> None:
+        self.pending = (shard, Pg, ids, total, din)  # shard.node_map keeps the gathered ids' map
+
+    def _release(self, shard, ids, total) -> None:
+        if total:
+            kernels.frontier_reset(ids[:total], shard.node_map)
+
+    @torch.no_grad()
+    def materialize(self, param: torch.Tensor) -> None:
+        if self.pending is None:
+            return
+        shard, Pg, ids, total, din = self.pending
+        self.pending = None
+        g = torch.empty(shard.n, din, dtype=torch.float32, device=Pg.device)
+        kernels.spmm_block_masked(shard.AT, shard.node_map, Pg[:, :din], g, Yc_init=Pg[:, din:], row0=shard.lo)
+        self._release(shard, ids, total)
+        if param.grad is None:
+            param.grad = g
+        else:
+            kernels.add_(param.grad, g)
+
+    def launch(self, param: torch.Tensor):
+        shard, Pg, ids, total, din = self.pending
+        self.pending = None
+
+        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
+            kernels.spmm_masked_adam_block(shard.AT, shard.node_map, Pg[:, :din], Pg[:, din:], shard.lo, param.data, m,
+                                           v, step_size, b1, b2, bc2s, eps, skip)
+            self._release(shard, ids, total)
+        return run
+
+
 def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, seeds, dX, rows, bpr, reduce_w,
-               force: bool = False):
+               force: bool = False, defer: _ShardTableUpdate | None = None):
     """Layer l's backward on the global hop set flagged in shard.hop_buffers()'s row flags, if the set
     is small (every rank decides alike from the all-gathered local counts: one host sync) or ``force``
     (the frontier forward computed layer l on that set only).
@@ -490,6 +534,9 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
         p.wait()
     if total:
         _lib.call("kgat_map_build", ids.data_ptr(), total, shard.node_map.data_ptr(), stream_ptr(dev))
+    if l == 0 and defer is not None:
+        defer.defer(shard, Pg, ids, total, din)  # the table's product runs fused with its Adam step
+        return None, True
     out = torch.empty(shard.n, din, dtype=torch.float32, device=dev)
     kernels.spmm_block_masked(shard.AT, shard.node_map, Pg[:, :din], out, Yc_init=Pg[:, din:], row0=shard.lo,
                               row_hit=hit if l > 0 else None)
@@ -501,7 +548,7 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
 class _ShardedCFLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cu, cp, cn, cfg, X0, *ws):
-        shard, comm, drops, seeds, reg, rows, frontier = cfg
+        shard, comm, drops, seeds, reg, rows, frontier, _tu = cfg
         L = len(drops)
         tables, sides, states = [X0], [], []
         # frontier forward: layers whose output the loss reads on a row set only run on that set (the
@@ -536,7 +583,7 @@ class _ShardedCFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        shard, comm, drops, seeds, reg, rows, _frontier = ctx.cfg
+        shard, comm, drops, seeds, reg, rows, _frontier, tu = ctx.cfg
         tables, sides, states, Tc, coef, ws = ctx.saved
         cu, cp, cn = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -587,7 +634,8 @@ class _ShardedCFLoss(torch.autograd.Function):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             if sparse or l in ctx.forced:
                 dX, sparse = _hop_layer(shard, comm, l, tables, sides, states, ws, drops, seeds, dX, rows,
-                                        (Tc, cu, cp, cn, reg, coef, gout), reduce_w, force=l in ctx.forced)
+                                        (Tc, cu, cp, cn, reg, coef, gout), reduce_w, force=l in ctx.forced,
+                                        defer=tu)
                 if sparse:
                     continue
             dXd, dS, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], **saved(l))
@@ -671,6 +719,10 @@ class RowShardedKGAT(nn.Module):
         # TRAIN_CF's forward on the row sets the loss reads (see _frontier_sets); the driver's
         # training step turns it on, off = the whole-shard propagation of every layer
         self.frontier_forward = False
+        # layer 0's table product fused with the shard's Adam step (_ShardTableUpdate); off = the
+        # product in the backward, the table gradient in .grad
+        self.fuse_table_update = False
+        self._table_update = _ShardTableUpdate()
         self.to(device)
 
     # ------------------------------------------------------------------ state
@@ -729,8 +781,9 @@ class RowShardedKGAT(nn.Module):
         rows = _BatchRows(np.concatenate([u, p, q]), self.lo, self.hi, dev)
         cu, cp, cn = (torch.from_numpy(rows.inv[i * B:(i + 1) * B]).to(dev) for i in range(3))
         drops, seeds = self._dropouts()
+        tu = self._table_update if self.fuse_table_update and torch.is_grad_enabled() else None
         cfg = (self.shard, self.comm, drops, seeds, float(self._regularization_params[0]), rows,
-               self.frontier_forward and torch.is_grad_enabled())
+               self.frontier_forward and torch.is_grad_enabled(), tu)
         return _ShardedCFLoss.apply(cu, cp, cn, cfg, self._user_entity_embedding_shard, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, pos_tails, neg_tails) -> torch.Tensor:
@@ -830,15 +883,29 @@ class RowShardedKGAT(nn.Module):
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 
+    def materialize_table_grad(self) -> None:
+        """Write a deferred table gradient (fuse_table_update) into the shard's .grad."""
+        self._table_update.materialize(self._user_entity_embedding_shard)
+
     def update_cf_weights(self) -> None:
-        self._cf_optimizer.step()
+        tu, param = self._table_update, self._user_entity_embedding_shard
+        fused = None
+        if tu.pending is not None:
+            if param.grad is not None:  # another term wrote .grad: the fused launch never reads it
+                tu.materialize(param)
+            else:
+                fused = {id(param): tu.launch(param)}
+        self._cf_optimizer.step(fused=fused)
         self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self) -> None:
+        self.materialize_table_grad()
         self._kg_optimizer.step()
         self._kg_optimizer.zero_grad()
 
     def forward(self, *args, mode: KGATMode):
+        # a deferred table product refers to this step's gathered rows and A^T's values
+        self.materialize_table_grad()
         if mode == KGATMode.TRAIN_CF:
             return self._calc_cf_loss(*args)
         if mode == KGATMode.TRAIN_KG:

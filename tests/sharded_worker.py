@@ -143,6 +143,24 @@ def main() -> None:
     fr_grads = [p.grad.detach().clone() for p in m.parameters() if not p.is_sparse and p.grad is not None]
     exact["frontier_vs_full"] = len(fr_grads) == len(full_grads) and all(
         torch.equal(a, b) for a, b in zip(fr_grads, full_grads))
+    # the table's Adam step fused into its last product (fuse_table_update) vs the unfused step
+    snap = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    s0, res = m._step, []
+    for fuse in (False, True):
+        m.load_state_dict(snap)
+        m.zero_grad(set_to_none=True)
+        m.build_optimizer(1e-3, 1e-4)
+        m.fuse_table_update = fuse
+        m._step = s0
+        m.train()
+        m(*mine, mode=pkg.KGATMode.TRAIN_CF).backward()
+        m.update_cf_weights()
+        st = m._cf_optimizer.state[id(m._user_entity_embedding_shard)]
+        res.append([p.detach().clone() for p in m.parameters()] + [st["exp_avg"].clone(), st["exp_avg_sq"].clone()])
+    m.fuse_table_update = False
+    m.eval()
+    exact["fused_table_update"] = all(torch.equal(a, b) for a, b in zip(*res))
+    m.load_state_dict(snap)
     users = torch.arange(0, 50, device="cuda")
     items = torch.arange(0, 300, device="cuda")
     with torch.no_grad():

@@ -1866,3 +1866,61 @@ def test_biinter_bwd_rows_matches_gathered(pkg, din, dout, kind):
                                         dh_full=full))
     for i, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("dim", [64, 128])
+def test_lazy_kg_adam_bit_identical(pkg, dim):
+    """KGAT.lazy_kg_adam (the KG step's table Adam on the batch rows only, the other rows' zero-gradient
+    steps replayed when next read) vs the dense KG step: over KG phases of several steps between CF steps,
+    a PREDICT in between, a step whose ids are out of range (skipped on the device) and a state_dict at
+    the end, the parameters and both optimisers' moments are equal bit for bit."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(3000, 30000, seed=17)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    n = U + E
+    R = len(lay.rel_order)
+    models = []
+    for lazy in (False, True):
+        torch.manual_seed(3)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=R, layer_size=[dim, 32],
+                                  cf_embedding_dim=dim, kg_embedding_dim=dim))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = m.fuse_kg_table_update = True
+        m.lazy_kg_adam = lazy
+        models.append(m)
+    rng = np.random.default_rng(4)
+    for phase in range(3):
+        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.2), int(E * 0.2))]
+        kgs = [[torch.from_numpy(rng.integers(0, hi, 48)).to(DEV) for hi in (n, R, n, n)] for _ in range(6)]
+        for m in models:
+            torch.manual_seed(50 + phase)
+            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            m.update_cf_weights()
+            for j, kg in enumerate(kgs):
+                if phase == 1 and j == 2:  # a device-side bad id: the step moves nothing
+                    bad = kg[2].clone()
+                    bad[0] = n + 7
+                    m(kg[0], kg[1], bad, kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
+                    torch.cuda.synchronize()  # the check's event has fired: the update reports it, abandons
+                    with pytest.raises(IndexError):
+                        m.update_kg_weights()
+                    continue
+                m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
+                m.update_kg_weights()
+            if phase == 2:
+                with torch.no_grad():
+                    m(ids[0], ids[1], mode=pkg.KGATMode.PREDICT)
+    sa, sb = models[0].state_dict(), models[1].state_dict()
+    for k in sa:
+        if not sa[k].is_sparse:
+            assert torch.equal(sa[k], sb[k]), k
+    for opt in ("_cf_optimizer", "_kg_optimizer"):
+        oa, ob = getattr(models[0], opt), getattr(models[1], opt)
+        for key, st in oa.state.items():
+            pa = [p for p in oa.params if id(p) == key]
+            pb = ob.params[oa.params.index(pa[0])]
+            sb_ = ob.state[id(pb)]
+            assert st["step"] == sb_["step"]
+            assert torch.equal(st["exp_avg"], sb_["exp_avg"]) and torch.equal(st["exp_avg_sq"], sb_["exp_avg_sq"]), opt
