@@ -262,6 +262,7 @@ class _KGTableUpdate:
         self.enabled = False
         self.pending = None
         self._map = None
+        self.marked = None  # the batch rows a TRAIN_KG forward numbered in the map, for its backward
 
     def node_map(self) -> torch.Tensor:
         """node -> compact row of the batch ids (-1 between steps), allocated once."""
@@ -276,6 +277,20 @@ class _KGTableUpdate:
 
     def defer(self, rows: torch.Tensor, Gc: torch.Tensor) -> None:
         self.pending = (rows, Gc)
+
+    def mark(self, heads, pos, neg) -> torch.Tensor:
+        """Number the batch rows in the map (kgat_frontier_build) in the forward -- the lazy Adam's
+        catch-up and the backward's compact gradient use the same rows; a forward whose backward never
+        ran releases its marks here first."""
+        self.release()
+        rows, _ = kernels.frontier_build(heads, pos, neg, self.node_map())
+        self.marked = rows
+        return rows
+
+    def release(self) -> None:
+        if self.marked is not None:
+            kernels.frontier_reset(self.marked, self._map)
+            self.marked = None
 
     @torch.no_grad()
     def materialize(self) -> None:
@@ -725,6 +740,7 @@ class _KGLoss(torch.autograd.Function):
         ctx.save_for_backward(heads, rels, pos, neg, work, emb)
         ctx.shape = (rel_emb.shape[0], rel_emb.shape[1])
         ctx.ktu = ktu
+        ctx.rows = ktu.marked if ktu is not None else None
         return loss.view(())
 
     @staticmethod
@@ -733,13 +749,16 @@ class _KGLoss(torch.autograd.Function):
         n_rel, k = ctx.shape
         gout = gout.reshape(1).to(torch.float32).contiguous()
         ktu, ctx.ktu = ctx.ktu, None
-        if ktu is not None and ktu.wants(heads.numel()):
+        rows = ctx.rows
+        if ktu is not None and rows is not None and ktu.marked is rows and ktu.wants(heads.numel()):
             row_map = ktu.node_map()
-            rows, _ = kernels.frontier_build(heads, pos, neg, row_map)
+            ktu.marked = None  # handed to the table update, which resets the map after its step
             Gc, d_rel, d_trans = kernels.transr_bwd_compact(emb, n_rel, k, heads, rels, pos, neg, work, gout, row_map,
                                                             rows.numel())
             ktu.defer(rows, Gc)
             return None, None, None, None, None, None, None, d_rel, d_trans
+        if ktu is not None:
+            ktu.release()
         d_emb, d_rel, d_trans = kernels.transr_bwd(emb, n_rel, k, heads, rels, pos, neg, work, gout)
         return None, None, None, None, None, None, d_emb, d_rel, d_trans
 
@@ -947,13 +966,14 @@ class KGAT(nn.Module):
         ids = [h, r, p, q]
         ktu = self._kg_table_update if torch.is_grad_enabled() else None
         lazy = self._lazy_kg
-        if lazy.enabled and getattr(self, "_kg_optimizer", None) is not None:
-            # the batch rows TransR reads, brought up to the last KG step (their skipped steps replayed)
-            lazy.ensure(self._kg_optimizer)
-            row_map = self._kg_table_update.node_map()
-            rows, _ = kernels.frontier_build(h, p, q, row_map)
-            lazy.catch_up(self._kg_optimizer, rows)
-            kernels.frontier_reset(rows, row_map)
+        if ktu is not None and ktu.wants(h.numel()):
+            rows = ktu.mark(h, p, q)  # the batch rows, numbered once for the backward's compact gradient
+            if lazy.enabled and getattr(self, "_kg_optimizer", None) is not None:
+                # the rows TransR reads, brought up to the last KG step (their skipped steps replayed)
+                lazy.ensure(self._kg_optimizer)
+                lazy.catch_up(self._kg_optimizer, rows)
+        elif lazy.enabled and lazy.last is not None:
+            self.flush_kg_table()  # an unfused KG step (no compact rows) reads and updates every row
         return _KGLoss.apply(*ids, float(self._regularization_params[1]), ktu, self._user_entity_embedding.weight,
                              self._relation_embedding.weight, self._trans_matrix)
 

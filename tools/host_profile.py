@@ -37,6 +37,7 @@ def main():
     kg = "--kg" in sys.argv
     if kg:  # the KG phase's step (main.py:324-345) at the reference's B = 512, fused table update
         m.fuse_kg_table_update = "--unfused" not in sys.argv
+        m.lazy_kg_adam = "--lazy" in sys.argv
         n = U + E
         batches = [[torch.from_numpy(x).to(dev) for x in (lay.heads[e], lay.rels[e], lay.tails[e],
                                                           rng.integers(0, n, 512))]
