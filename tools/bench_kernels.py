@@ -97,8 +97,11 @@ def gemm_section(args, dev, rec):
     lib = importlib.import_module(PKG + "._lib")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     rows = int(os.environ.get("WIDE_ROWS", "2000000"))
+    # TN: the weight gradients' split-K slabs as biinter_gemm.hip issues them for `rows` rows
+    # (gemm_chunk: ~1024 chunks of ceil(rows / 1024) rounded up to 256 rows, one batch entry each)
+    chunk = max(512, min(65536, ((rows + 1023) // 1024 + 255) // 256 * 256))
     cases = [("NT", rows, 256, 256, 1), ("NN", rows, 256, 256, 1), ("NT", rows, 128, 128, 1), ("NN", rows, 128, 128, 1),
-             ("NT", rows, 128, 256, 1), ("TN", 256, 260, 65536, 32), ("TN", 128, 132, 65536, 32)]
+             ("NT", rows, 128, 256, 1), ("TN", 256, 256, chunk, rows // chunk), ("TN", 128, 128, chunk, rows // chunk)]
     for kind, M, N, Kd, batch in cases:
         ta, tb = kind[0] == "T", kind[1] == "T"
         A = torch.randn(batch, *((Kd, M) if ta else (M, Kd)), device=dev)
