@@ -1030,7 +1030,8 @@ template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
                       float* norm, uint64_t* mask, int64_t node0, hipStream_t st) {
-  // A/B switch (KGAT_FWD_VARIANT): bit 1 = one resident round, bit 2 = 4 waves/SIMD, bit 3 = no prefetch.
+  // A/B switch (KGAT_FWD_VARIANT): bit 1 = one resident round, bit 2 = 4 waves/SIMD, bit 3 = no prefetch,
+  // bit 4 (with 4 = prefetch at 4 waves/SIMD): prefetch at 3 waves/SIMD.
   // Default 8 (measured at C2, 64->64: 795 us vs 809 us for spmm + forward with the prefetch, whose
   // 172 VGPRs allow 2 waves/SIMD; without it 132 VGPRs, 3 waves)
   static int variant = -1;
@@ -1044,7 +1045,10 @@ static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
   hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, PF, W, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S,   \
                      lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, node0)
   switch (variant & 12) {
-    case 4: KGAT_FWD_LAUNCH(true, 4); break;
+    case 4:
+      if (variant & 16) KGAT_FWD_LAUNCH(true, 3);
+      else KGAT_FWD_LAUNCH(true, 4);
+      break;
     case 8: KGAT_FWD_LAUNCH(false, 2); break;
     case 12: KGAT_FWD_LAUNCH(false, 4); break;
     default: KGAT_FWD_LAUNCH(true, 2); break;

@@ -50,12 +50,22 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, float 
   return static_cast<float>(mix_hash(seed, idx) >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
-// Sum over the 16 lanes that share (lane >> 4).
+// v + (v of lane lane' in the same DPP row), lane' given by the DPP control CTRL.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 16 lanes that share (lane >> 4): a butterfly inside the DPP row (no LDS-path
+// ds_bpermute): quad_perm [1,0,3,2] (lane ^ 1), quad_perm [2,3,0,1] (lane ^ 2), row_half_mirror
+// (lane 7 - i: the other quad), row_mirror (lane 15 - i: the other half).  Each level adds the
+// same two partial sums as the xor butterfly (lane ^ 1, ^ 2, ^ 4, ^ 8), so every lane gets the same
+// bits as it.  All 16 lanes of the row must be active.
 __device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+  v = dpp_add<0xB1>(v);
+  v = dpp_add<0x4E>(v);
+  v = dpp_add<0x141>(v);
+  v = dpp_add<0x140>(v);
   return v;
 }
 

@@ -103,6 +103,37 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
 #endif
 constexpr int kRowsUnroll = KGAT_ROWS_U;
 
+// One long-row segment s (the whole wave; groups take interleaved sub-chunks) -> its partial sum in
+// io.part, reduced by the fix-up pass.
+template <int D, int MODE>
+__device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io, int s, int g, int gl, int base) {
+  constexpr int L = SpmmShape<D>::kLanes;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB;
+  if (s >= A.n_seg) return;
+  const int row = A.seg_row[s];
+  if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
+  const int64_t beg = A.seg_beg[s];
+  const int64_t row_end = A.rowptr[row + 1];
+  const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool any = false;
+  // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
+  for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
+    const int64_t ce = cb + L < end ? cb + L : end;
+    gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any);
+  }
+  // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
+  if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
+#pragma unroll
+  for (int o = L; o < kWave; o <<= 1) {
+    acc.x += __shfl_xor(acc.x, o);
+    acc.y += __shfl_xor(acc.y, o);
+    acc.z += __shfl_xor(acc.z, o);
+    acc.w += __shfl_xor(acc.w, o);
+  }
+  if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
@@ -114,31 +145,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   if ((MODE == kMaskedAdam || MODE == kMaskedAdamB) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
-    // ---- long-row segment: the whole wave, groups take interleaved sub-chunks
-    const int s = blockIdx.x * 4 + wave;
-    if (s >= A.n_seg) return;
-    const int row = A.seg_row[s];
-    if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
-    const int64_t beg = A.seg_beg[s];
-    const int64_t row_end = A.rowptr[row + 1];
-    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
-    // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
-    for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
-      const int64_t ce = cb + L < end ? cb + L : end;
-      gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any);
-    }
-    // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
-    if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
-#pragma unroll
-    for (int o = L; o < kWave; o <<= 1) {
-      acc.x += __shfl_xor(acc.x, o);
-      acc.y += __shfl_xor(acc.y, o);
-      acc.z += __shfl_xor(acc.z, o);
-      acc.w += __shfl_xor(acc.w, o);
-    }
-    if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
+    long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base);
     return;
   }
 
@@ -241,6 +248,78 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
     store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
+  }
+}
+
+// The fused table update (kMaskedAdam) with each wave's row metadata fetched up front: the
+// kRowsPerWave + 1 rowptr entries of the wave's rows and their Yc map entries are two coalesced
+// loads at the start (lane j holds row r_begin + j's), handed to the groups by shuffles, so a row's
+// chain starts at its edge chunk instead of behind two dependent single-address loads.  EARLY: the
+// row's p / m / v loads go out before its gather (in flight across it); UM: gathers in flight per
+// group.  Per row the same edges in the same order, the same Yc add and adam_elem: same bits as
+// spmm_main_kernel<D, kMaskedAdam>.  Long rows: the segment blocks + the fix-up, as there.
+template <int D, bool EARLY, int UM, int MINW>
+__global__ __launch_bounds__(256, MINW) void masked_adam_rows_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
+  using S = SpmmShape<D>;
+  constexpr int L = S::kLanes;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane / L, gl = lane % L, base = g * L;
+  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if (static_cast<int>(blockIdx.x) < seg_blocks) {
+    long_segment<D, kMaskedAdam>(A, io, blockIdx.x * 4 + wave, g, gl, base);
+    return;
+  }
+  const int64_t n = A.n_rows;
+  const int64_t r_begin = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kRowsPerWave;
+  const int64_t rl = r_begin + lane;
+  const int64_t rp = (lane <= S::kRowsPerWave && rl <= n) ? A.rowptr[rl] : 0;
+  const int ym = (io.Yc != nullptr && lane < S::kRowsPerWave && rl < n) ? io.src_map[io.row0 + rl] : -1;
+#pragma unroll 1
+  for (int k = 0; k < S::kRowsPerGroup; ++k) {
+    const int j = g + k * S::kGroups;  // the group's row within the wave's rows
+    const int64_t beg = __shfl(rp, j), end = __shfl(rp, j + 1);
+    const int m = __shfl(ym, j);
+    const int64_t r = r_begin + j;
+    if (r >= n || end - beg > A.long_threshold) continue;  // long rows: the fix-up pass
+    AdamRow ar;
+    if (EARLY) ar = adam_row_load(io.adam, r, gl);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
+    gather_edges<D, true, 4, UM>(A, io, beg, end, base, gl, acc, any);
+    if (m >= 0) {
+      const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
+      acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+    }
+    adam_row_step(io.adam, r, gl, acc, EARLY ? ar : adam_row_load(io.adam, r, gl));
+  }
+}
+
+template <int D, bool EARLY, int UM, int MINW = 1>
+static int launch_masked_adam_rows(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
+  using S = SpmmShape<D>;
+  static_assert(S::kRowsPerWave < kWave, "row metadata: one lane per row + 1");
+  const int seg_blocks = (A.n_seg + 3) / 4;
+  const int64_t grid = seg_blocks + (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL((masked_adam_rows_kernel<D, EARLY, UM, MINW>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  if (A.n_long > 0) {
+    hipLaunchKernelGGL((spmm_fixup_kernel<D, kMaskedAdam>), dim3(A.n_long), dim3(256), 0, st, A, io);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
+
+template <int D>
+static int launch_masked_adam_variant(const kgat_csr& A, const SpmmIo& io, int variant, hipStream_t st) {
+  switch (variant) {
+    case 1: return launch_masked_adam_rows<D, false, 4>(A, io, st);
+    case 2: return launch_masked_adam_rows<D, true, 4>(A, io, st);
+    case 3: return launch_masked_adam_rows<D, false, 8>(A, io, st);
+    case 4: return launch_masked_adam_rows<D, true, 8>(A, io, st);
+    case 5: return launch_masked_adam_rows<D, false, 4, 8>(A, io, st);
+    default: return launch_masked_adam_rows<D, true, 4, 6>(A, io, st);
   }
 }
 
@@ -730,6 +809,23 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
       case 64: return launch_masked_adam_ws<64>(*A, io, ws, st);
       case 128: return launch_masked_adam_ws<128>(*A, io, ws, st);
       case 256: return launch_masked_adam_ws<256>(*A, io, ws, st);
+      default: break;
+    }
+  }
+  // KGAT_TU_VARIANT=1..6: masked_adam_rows_kernel (row metadata up front; early Adam loads; 8 gathers
+  // in flight; 5: 8 waves/SIMD forced), same bits
+  static const int tuv = [] {
+    const char* e = getenv("KGAT_TU_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  if (tuv > 0) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (d) {
+      case 16: break;  // 64 rows per wave: no lane left for the metadata's end entry
+      case 32: return launch_masked_adam_variant<32>(*A, io, tuv, st);
+      case 64: return launch_masked_adam_variant<64>(*A, io, tuv, st);
+      case 128: return launch_masked_adam_variant<128>(*A, io, tuv, st);
+      case 256: return launch_masked_adam_variant<256>(*A, io, tuv, st);
       default: break;
     }
   }

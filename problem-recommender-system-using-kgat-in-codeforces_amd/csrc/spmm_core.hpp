@@ -86,7 +86,7 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
 
 // Accumulate edges [beg, end) of one row into acc.  All lanes of the group
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
-template <int D, bool MASKED, int U = 4>
+template <int D, bool MASKED, int U = 4, int UM = 4>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
                                              int gl, float4& acc, bool& any) {
   constexpr int L = SpmmShape<D>::kLanes;
@@ -113,30 +113,40 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
           in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
         }
       }
-      uint64_t hit = (__ballot(in) >> base) & ((L == 64) ? ~0ull : ((1ull << L) - 1));
+      // the group's hit bits in a 32-bit word where they fit (the group's lanes are L <= 32 bits of
+      // the ballot): one v_ffbl per pick instead of the 64-bit scan
+      using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
+      constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
+      HitT hit = static_cast<HitT>(__ballot(in) >> base) & kMask;
       if (hit == 0) continue;
       any = true;
       if (in && io.src_rank == nullptr) mc = io.src_map[mc];
-      // up to four gathers in flight, summed in edge order
+      const uint32_t ldx4u = static_cast<uint32_t>(ldx4);
+      // up to UM gathers in flight, summed in edge order.  A pick past the last hit adds
+      // fma(0, 0, acc) = acc + 0 = acc exactly (acc starts at +0 and an exact-zero sum rounds to
+      // +0, so acc is never -0): the same bits as skipping it, without per-pick selects of acc.
       while (hit) {
-        int jj[4];
+        int jj[UM];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          jj[k] = hit ? __ffsll(static_cast<long long>(hit)) - 1 : -1;
-          hit &= hit ? hit - 1 : 0ull;
+        for (int k = 0; k < UM; ++k) {
+          if constexpr (L <= 32) jj[k] = __ffs(hit) - 1;
+          else jj[k] = __ffsll(static_cast<unsigned long long>(hit)) - 1;
+          hit &= hit - 1;  // 0 stays 0
         }
-        float4 xs[4];
-        float vs[4];
+        float4 xs[UM];
+        float vs[UM];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int src = base + (jj[k] >= 0 ? jj[k] : 0);
+        for (int k = 0; k < UM; ++k) {
+          const bool ok = jj[k] >= 0;
+          const int src = base + (jj[k] & (L - 1));  // a lane of the group either way
           const int c = __shfl(mc, src);
-          vs[k] = __shfl(mv, src);
-          xs[k] = jj[k] >= 0 ? X4[static_cast<int64_t>(c) * ldx4 + gl] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float v = __shfl(mv, src);
+          vs[k] = ok ? v : 0.f;
+          xs[k] = ok ? X4[static_cast<uint64_t>(static_cast<uint32_t>(c)) * ldx4u + gl]
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (jj[k] >= 0) fma4(vs[k], xs[k], acc);
+        for (int k = 0; k < UM; ++k) fma4(vs[k], xs[k], acc);
       }
       continue;
     }
