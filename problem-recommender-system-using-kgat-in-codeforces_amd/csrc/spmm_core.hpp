@@ -77,6 +77,12 @@ __device__ __forceinline__ void fma4(float v, const float4& x, float4& acc) {
   acc.w = fmaf(v, x.w, acc.w);
 }
 
+// float4 offset of row c (a node id or compact row: 0 <= c < 2^31) of a source with ld4 float4 per row:
+// one 32 x 32 -> 64-bit multiply-add instead of a signed 64-bit product
+__device__ __forceinline__ uint64_t row_off(int c, uint32_t ld4) {
+  return static_cast<uint64_t>(static_cast<uint32_t>(c)) * ld4;
+}
+
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x;
   a.y += b.y;
@@ -91,7 +97,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
                                              int gl, float4& acc, bool& any) {
   constexpr int L = SpmmShape<D>::kLanes;
   const float4* X4 = reinterpret_cast<const float4*>(io.X);
-  const int64_t ldx4 = io.ldx / 4;
+  const uint32_t ldx4u = static_cast<uint32_t>(io.ldx / 4);
   for (int64_t cb = beg; cb < end; cb += L) {
     const int n = static_cast<int>(end - cb < L ? end - cb : L);
     int mc = 0;
@@ -121,7 +127,6 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       if (hit == 0) continue;
       any = true;
       if (in && io.src_rank == nullptr) mc = io.src_map[mc];
-      const uint32_t ldx4u = static_cast<uint32_t>(ldx4);
       // up to UM gathers in flight, summed in edge order.  A pick past the last hit adds
       // fma(0, 0, acc) = acc + 0 = acc exactly (acc starts at +0 and an exact-zero sum rounds to
       // +0, so acc is never -0): the same bits as skipping it, without per-pick selects of acc.
@@ -142,7 +147,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
           const int c = __shfl(mc, src);
           const float v = __shfl(mv, src);
           vs[k] = ok ? v : 0.f;
-          xs[k] = ok ? X4[static_cast<uint64_t>(static_cast<uint32_t>(c)) * ldx4u + gl]
+          xs[k] = ok ? X4[row_off(c, ldx4u) + gl]
                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
@@ -163,7 +168,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       for (int k = 0; k < U; ++k) {
         const int ck = __shfl(mc, base + j + k);
         vs[k] = __shfl(mv, base + j + k);
-        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+        xs[k] = X4[row_off(ck, ldx4u) + gl];
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) fma4(vs[k], xs[k], acc);
@@ -175,7 +180,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       for (int k = 0; k < 8; ++k) {
         const int ck = __shfl(mc, base + j + k);
         vs[k] = __shfl(mv, base + j + k);
-        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+        xs[k] = X4[row_off(ck, ldx4u) + gl];
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) fma4(vs[k], xs[k], acc);
@@ -188,7 +193,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
       for (int k = 0; k < 4; ++k) {
         const int ck = __shfl(mc, base + j + k);
         vs[k] = __shfl(mv, base + j + k);
-        xs[k] = X4[static_cast<int64_t>(ck) * ldx4 + gl];
+        xs[k] = X4[row_off(ck, ldx4u) + gl];
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) fma4(vs[k], xs[k], acc);
@@ -197,7 +202,7 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
     for (; j < n; ++j) {
       const int c = __shfl(mc, base + j);
       const float v = __shfl(mv, base + j);
-      fma4(v, X4[static_cast<int64_t>(c) * ldx4 + gl], acc);
+      fma4(v, X4[row_off(c, ldx4u) + gl], acc);
     }
   }
 }
