@@ -138,6 +138,18 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
                                         float eps, const int32_t *skip, float *workspace, int64_t workspace_floats,
                                         void *stream);
 
+/* kgat_spmm_csr_masked_adam_block_f32 on a part of the rows: part 0 every row (= the block call);
+ * part 1 the rows with a gradient term (an edge into the source set, or a Yc row) and the long rows;
+ * part 2 the other short rows, whose gradient is exactly zero: their Adam step with g = +0 (no
+ * workspace needed).  Parts 1 and 2 touch disjoint rows (they may run on two streams at once) and
+ * together give part 0's bits.  Same reference step (model.py:404-413, main.py:312-313). */
+int kgat_spmm_csr_masked_adam_part_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                       const float *Yc_init, int64_t ldyc, int64_t yc_row0,
+                                       const uint64_t *src_rank, float *p, float *m, float *v, int64_t ldp,
+                                       int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
+                                       float eps, const int32_t *skip, int32_t part, float *workspace,
+                                       int64_t workspace_floats, void *stream);
+
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 

@@ -84,6 +84,7 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
   if (MODE == kMaskedAdam || MODE == kMaskedAdamB) {
+    if (io.adam.part == 1 && !any) return;  // no gradient term: masked_adam_zero_kernel steps the row
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
     return;
   }
@@ -247,8 +248,64 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if (threadIdx.x < L) {
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
-    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
+    // long rows are always stepped here (part 0 / 1): the Adam modes pass any = true
+    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t,
+                    MODE == kMaskedAdam || MODE == kMaskedAdamB);
   }
+}
+
+// Part 2 of the fused table update: the short rows whose gradient is exactly zero -- not a Yc row and
+// no edge into the source set (the same membership test as gather_edges, stopping at the first hit) --
+// take their Adam step with g = +0, the value the whole-table launch adds for them (acc = +0, nothing
+// gathered, no Yc row), so the same bits.  Part 1 (spmm_main_kernel<D, kMaskedAdam> with part = 1)
+// steps every other row; the two launches touch disjoint rows and may run concurrently.
+template <int D>
+__global__ __launch_bounds__(256) void masked_adam_zero_kernel(kgat_csr A, SpmmIo io) {
+  using S = SpmmShape<D>;
+  constexpr int L = S::kLanes;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane / L, gl = lane % L, base = g * L;
+  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  const int64_t r_begin = w * S::kRowsPerWave;
+  int64_t r_end = r_begin + S::kRowsPerWave;
+  if (r_end > A.n_rows) r_end = A.n_rows;
+  using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
+  constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
+  for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
+    const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+    if (end - beg > A.long_threshold) continue;                       // part 1 (fix-up)
+    if (io.Yc != nullptr && io.src_map[io.row0 + r] >= 0) continue;  // a Yc row: part 1
+    bool hit = false;
+    for (int64_t cb = beg; cb < end && !hit; cb += L) {
+      const int n = static_cast<int>(end - cb < L ? end - cb : L);
+      bool in = false;
+      if (gl < n) {
+        const int mc = A.col[cb + gl];
+        if (io.src_rank != nullptr) {
+          in = ((io.src_rank[static_cast<uint32_t>(mc) >> 5] >> (mc & 31)) & 1u) != 0;
+        } else {
+          in = io.src_bits != nullptr ? ((io.src_bits[static_cast<uint32_t>(mc) >> 5] >> (mc & 31)) & 1u) != 0
+                                      : io.src_map[mc] >= 0;
+        }
+      }
+      hit = (static_cast<HitT>(__ballot(in) >> base) & kMask) != 0;  // group-uniform
+    }
+    if (hit) continue;  // part 1
+    adam_row_step(io.adam, r, gl, make_float4(0.f, 0.f, 0.f, 0.f), adam_row_load(io.adam, r, gl));
+  }
+}
+
+template <int D>
+static int launch_masked_adam_zero(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
+  using S = SpmmShape<D>;
+  const int64_t grid = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  if (grid == 0) return KGAT_OK;
+  hipLaunchKernelGGL((masked_adam_zero_kernel<D>), dim3(grid), dim3(256), 0, st, A, io);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 // The fused table update (kMaskedAdam) with each wave's row metadata fetched up front: the
@@ -778,8 +835,19 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
                                                    int32_t d, float step_size, float beta1, float beta2,
                                                    float bc2_sqrt, float eps, const int32_t* skip, float* workspace,
                                                    int64_t workspace_floats, void* stream) {
+  return kgat_spmm_csr_masked_adam_part_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, yc_row0, src_rank, p, m, v, ldp, d,
+                                            step_size, beta1, beta2, bc2_sqrt, eps, skip, 0, workspace,
+                                            workspace_floats, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_part_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                  int64_t ldxc, const float* Yc_init, int64_t ldyc, int64_t yc_row0,
+                                                  const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                                  int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
+                                                  float eps, const int32_t* skip, int32_t part, float* workspace,
+                                                  int64_t workspace_floats, void* stream) {
   using namespace kgat;
-  if (yc_row0 < 0) return KGAT_ERR_INVALID;
+  if (yc_row0 < 0 || part < 0 || part > 2) return KGAT_ERR_INVALID;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
@@ -787,11 +855,23 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
     return KGAT_ERR_INVALID;
   if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
   if (A->n_rows == 0) return KGAT_OK;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+  if (part != 2 && A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, part};
+  if (part == 2) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (d) {
+      case 16: return launch_masked_adam_zero<16>(*A, io, st);
+      case 32: return launch_masked_adam_zero<32>(*A, io, st);
+      case 64: return launch_masked_adam_zero<64>(*A, io, st);
+      case 128: return launch_masked_adam_zero<128>(*A, io, st);
+      case 256: return launch_masked_adam_zero<256>(*A, io, st);
+      default: return KGAT_ERR_UNSUPPORTED_DIM;
+    }
+  }
+  if (part == 1) return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
   // KGAT_TU_BATCH=1: the row-batched form (kMaskedAdamB, same bits); default the row-at-a-time one
   static const int batched = [] {
     const char* e = getenv("KGAT_TU_BATCH");

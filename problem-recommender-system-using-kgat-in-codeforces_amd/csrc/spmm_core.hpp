@@ -33,6 +33,10 @@ struct SpmmAdam {
   int64_t ld;  // row stride of p, m, v (floats)
   float step_size, b1, b2, bc2s, eps;
   const int32_t* skip;  // nullable: *skip != 0 -> the launch leaves p / m / v untouched (bad step ids)
+  // the rows this launch steps (kgat_spmm_csr_masked_adam_part_f32): 0 every row; 1 the rows with a
+  // gradient term (a hit or a Yc row) and the long rows; 2 the remaining short rows (zero gradient),
+  // by masked_adam_zero_kernel
+  int part;
 };
 
 struct SpmmIo {

@@ -315,13 +315,35 @@ def _skip_ptr(skip: torch.Tensor | None):
     return skip.data_ptr()
 
 
+def _tu_split_default() -> bool:
+    return os.environ.get("KGAT_TU_SPLIT", "0") != "0"
+
+
+_SIDE_STREAMS: dict = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """One side stream per device (the fused table update's zero-gradient rows)."""
+    key = torch.device(device).index
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return s
+
+
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None) -> None:
+                     skip: torch.Tensor | None = None, split: bool | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).
+
+    ``split`` (default: ``KGAT_TU_SPLIT``): the rows whose gradient is exactly zero (no edge into the
+    source set, no Yc row: ~2/3 of the rows at C2) take their step in a launch of their own on a side
+    stream (kgat_spmm_csr_masked_adam_part_f32 part 2, a pure p / m / v stream) while the current stream
+    runs the product + step of the others (part 1); the current stream then waits for the side one.
+    Disjoint rows, same bits."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -335,6 +357,8 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
         _req(Yc_init, "Yc_init", dim=2)
         if Yc_init.shape[1] != d:
             raise ValueError("Yc_init width mismatch")
+    if split is None:
+        split = _tu_split_default()
     csr = graph.AT
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
@@ -342,10 +366,23 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("kgat_spmm_csr_masked_adam_ex_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-              Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0,
-              _rank_ptr(src_rank, src_map), p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
-              bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
+    rank = _rank_ptr(src_rank, src_map)
+
+    def part(k: int, stream) -> None:
+        _lib.call("kgat_spmm_csr_masked_adam_part_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+                  yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
+                  bc2_sqrt, eps, _skip_ptr(skip), k, ws.data_ptr(), ws.numel(), stream)
+
+    if split:
+        main = torch.cuda.current_stream(Xc.device)
+        side = side_stream(Xc.device)
+        side.wait_stream(main)  # the side launch reads this step's hop set and the skip flag
+        part(2, side.cuda_stream)
+        part(1, main.cuda_stream)
+        main.wait_stream(side)  # every row stepped before anything later on this stream
+    else:
+        part(0, stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))

@@ -1469,6 +1469,52 @@ def test_fused_table_update_bit_identical(pkg, layers):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("layers", [[64, 32], [64, 32, 16]])
+def test_fused_table_update_split_parts_bit_identical(pkg, layers):
+    """The fused table update split in two disjoint row launches (kgat_spmm_csr_masked_adam_part_f32:
+    part 2 = the zero-gradient short rows on a side stream, part 1 = the rest on the current stream)
+    gives the single launch's p / m / v bit for bit, on a hub graph's real pending update (long rows,
+    Yc rows, rows with and without hits), with the skip flag honoured by both parts."""
+    graph_mod, kernels = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=6)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    torch.manual_seed(2024)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
+                              message_dropout=[0.1] * len(layers)))
+    m.attach_graph(lay, DEV)
+    assert m.graph().AT.n_long > 0
+    m.train()
+    m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+    m.fuse_table_update = True
+    rng = np.random.default_rng(5)
+    ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
+    m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+    tu = m._table_update
+    assert tu.pending is not None
+    graph, src_map, Xc, Yc, rank = tu.pending
+    g = torch.Generator(device=DEV).manual_seed(3)
+    p0 = tu.param.data.clone()
+    m0 = torch.rand(p0.shape, generator=g, device=DEV) * 1e-3
+    v0 = torch.rand(p0.shape, generator=g, device=DEV) * 1e-6
+    outs = []
+    for split in (False, True):
+        p, mm, vv = p0.clone(), m0.clone(), v0.clone()
+        kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, mm, vv, 1e-3, 0.9, 0.999, 0.05, 1e-8, split=split)
+        torch.cuda.synchronize()
+        outs.append((p, mm, vv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.equal(outs[1][0], p0)  # the step moved rows
+    # both parts honour the skip flag
+    skip = torch.ones(1, dtype=torch.int32, device=DEV)
+    p, mm, vv = p0.clone(), m0.clone(), v0.clone()
+    kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, mm, vv, 1e-3, 0.9, 0.999, 0.05, 1e-8, skip=skip,
+                             split=True)
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and torch.equal(mm, m0) and torch.equal(vv, v0)
+    tu.discard()
+
+
 def test_fused_table_update_keeps_extra_table_gradient(pkg):
     """with fuse_table_update the CF backward defers the table's gradient, but
     another term of the loss (here an L2 penalty on the whole table) still writes .grad through

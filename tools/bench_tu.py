@@ -102,13 +102,27 @@ def main() -> None:
     digest = [int(t.view(torch.int32).to(torch.int64).sum()) for t in (p1, m1, v1)]
     del p1, m1, v1
     fused = timeit(lambda: K.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, 1e-4, 0.9, 0.999, 0.03, 1e-8))
+    parts = {}
+    if os.environ.get("TU_PARTS"):
+        import ctypes
+        lib = importlib.import_module(PKG + "._lib")
+        csr = graph.AT
+        desc = csr.descriptor()
+        ws = torch.empty(max(1, csr.n_seg * 64), dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        for k in (1, 2):
+            parts[f"part{k}_avg_ms"], parts[f"part{k}_min_ms"] = timeit(lambda: lib.call(
+                "kgat_spmm_csr_masked_adam_part_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
+                Xc.stride(0), Yc.data_ptr() if Yc is not None else None, Yc.stride(0) if Yc is not None else 0, 0,
+                rank.data_ptr() if rank is not None else None, p.data_ptr(), m.data_ptr(), v.data_ptr(), 64, 64, 1e-4,
+                0.9, 0.999, 0.03, 1e-8, None, k, ws.data_ptr(), ws.numel(), st))
     g = torch.randn_like(p)
     dense = timeit(lambda: K.adam_multi([(p.view(-1), g.view(-1), m.view(-1), v.view(-1), 1e-4, 0.03)], 0.9, 0.999,
                                         1e-8))
     tu.discard()
-    print(json.dumps({"tag": a.tag, "env": {k: v for k, v in os.environ.items() if k.startswith("KGAT_")},
+    print(json.dumps({"tag": a.tag, "env": {k: e for k, e in os.environ.items() if k.startswith("KGAT_")},
                       "n_hop": n_hop, "digest": digest, "fused_avg_ms": fused[0], "fused_min_ms": fused[1], "adam_avg_ms": dense[0],
-                      "adam_min_ms": dense[1], "setup_s": round(time.perf_counter() - t0, 1)}), flush=True)
+                      "adam_min_ms": dense[1], **parts, "setup_s": round(time.perf_counter() - t0, 1)}), flush=True)
 
 
 if __name__ == "__main__":
