@@ -186,6 +186,9 @@ def train(args) -> dict:
     model.fuse_table_update = True  # the loop below only ever steps right after backward (main.py:312-313)
     model.frontier_forward = True  # TRAIN_CF's forward on the rows its loss reaches (same bits)
     model.fuse_kg_table_update = True  # the KG step's table Adam from TransR's compact rows (same bits)
+    # ... on the batch rows only, the skipped zero-gradient steps replayed when a row is next read (same bits;
+    # every whole-table reader -- the CF phase, evaluation, state_dict -- flushes first)
+    model.lazy_kg_adam = True
     refresh = [torch.from_numpy(np.asarray(x, np.int64)).to(dev)
                for x in (layout.heads, layout.rels, layout.tails, layout.rel_order)]
     train_dict, val_dict = ds.interaction_dict("train"), ds.interaction_dict("validation")
