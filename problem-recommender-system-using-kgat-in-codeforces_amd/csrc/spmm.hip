@@ -173,9 +173,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   }
 
   // ---- short rows: one group per row
-  int64_t rb = static_cast<int64_t>(blockIdx.x) - seg_blocks;
-  if (io.perm_mul != 0) rb = (rb * io.perm_mul) % (static_cast<int64_t>(gridDim.x) - seg_blocks);
-  const int64_t w = rb * 4 + wave;
+  const int64_t w = static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave;
   const int64_t r_begin = w * S::kRowsPerWave;
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
@@ -515,42 +513,14 @@ static int launch_masked_adam_ws(const kgat_csr& A, const SpmmIo& io, int varian
   }
 }
 
-// A multiplier coprime with nb near nb / golden ratio (0: keep the order): row block b runs in launch slot
-// (b * k) mod nb, so consecutive slots -- and each XCD's share of them -- mix the row ranges.
-static int64_t block_perm(int64_t nb) {
-  if (nb < 3) return 0;
-  int64_t k = static_cast<int64_t>(static_cast<double>(nb) * 0.6180339887) | 1;
-  auto gcd = [](int64_t a, int64_t b) {
-    while (b) {
-      const int64_t t = a % b;
-      a = b;
-      b = t;
-    }
-    return a;
-  };
-  while (k < nb && gcd(k, nb) != 1) k += 2;
-  return k < nb ? k : 0;
-}
-
-static int env_flag(const char* name) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : 0;
-}
-
 template <int D, int MODE>
-static int launch_mode(const kgat_csr& A, const SpmmIo& io_in, hipStream_t st) {
+static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
   int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
   if ((MODE == kMaskedRows || MODE == kRows) && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  SpmmIo io = io_in;
-  // KGAT_TU_PERM / KGAT_SPMM_PERM: the fused table update's / the dense product's row blocks in a
-  // strided order (same bits: every row computed as before)
-  static const int tu_perm = env_flag("KGAT_TU_PERM"), spmm_perm = env_flag("KGAT_SPMM_PERM");
-  if ((MODE == kMaskedAdam && tu_perm) || ((MODE == kOverwrite || MODE == kMasked) && spmm_perm))
-    io.perm_mul = block_perm(row_blocks);
   hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
   KGAT_LAUNCH_CHECK();
   if (A.n_long > 0) {

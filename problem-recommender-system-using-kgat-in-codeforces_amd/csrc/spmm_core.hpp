@@ -59,10 +59,6 @@ struct SpmmIo {
   const int32_t* out_rows;   // k -> r, ascending
   const int32_t* out_count;  // device: the set's size
   SpmmAdam adam;             // kMaskedAdam only
-  // dense row-block order (kMaskedAdam): row block b is processed by launch slot (b * perm_mul) mod
-  // n_blocks -- a multiplier coprime with n_blocks spreads the heavy (user / item) and light (entity)
-  // row ranges over the whole launch and over the XCDs; 0 = in order
-  int64_t perm_mul;
 };
 
 __device__ __forceinline__ bool bit_of(const uint32_t* bits, int64_t i) {
