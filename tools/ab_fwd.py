@@ -4,7 +4,7 @@
     KGAT_FWD_VARIANT=24 python tools/ab_fwd.py out_b.json
     python tools/ab_fwd.py --compare out_a.json out_b.json
 
-Each run times kgat_biinter_fwd_f32 (saved-state form, train-mode dropout) per shape on synthetic
+Each run times kgat_biinter_fwd_f32 (saved-state form, train-mode dropout; AB_P / AB_STATE vary the epilogue) per shape on synthetic
 rows and records a digest of H, the row norms and the state words; --compare checks the digests are
 equal (the variants must produce the same bits) and prints the time ratio.
 """
@@ -38,6 +38,10 @@ def run(out: str) -> None:
     K = importlib.import_module(PKG + ".kernels")
     dev = torch.device("cuda")
     res = {"variant": os.environ.get("KGAT_FWD_VARIANT", "default")}
+    # epilogue-weight probes: AB_P = dropout probability (0 drops the hash and the select), AB_STATE=0
+    # = no saved state (no norm / state-word stores, as in eval)
+    drop_p = float(os.environ.get("AB_P", "0.1"))
+    keep_state = os.environ.get("AB_STATE", "1") != "0"
     only = os.environ.get("AB_SHAPES")
     shapes = [s for s in SHAPES if not only or f"{s[0]}x{s[1]}_n{s[2]}" in only.split(",")]
     for din, dout, n in shapes:
@@ -50,10 +54,12 @@ def run(out: str) -> None:
         b2 = torch.randn(dout, device=dev, generator=g) * 0.1
         H = torch.empty(n, dout, device=dev)
         st = K.BiState(n, dev, din, dout)
-        fn = lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st)  # noqa: E731
+        if not keep_state:
+            st = None
+        fn = lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, drop_p, 5, out=H, state=st)  # noqa: E731
         fn()
         torch.cuda.synchronize()
-        d = digest(H, *([st.norm[:n], st.mask] if st.kind in ("fused", "bits") else []))
+        d = digest(H, *([st.norm[:n], st.mask] if st is not None and st.kind in ("fused", "bits") else []))
         reps = 20
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
