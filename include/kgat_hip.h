@@ -138,18 +138,6 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
                                         float eps, const int32_t *skip, float *workspace, int64_t workspace_floats,
                                         void *stream);
 
-/* kgat_spmm_csr_masked_adam_block_f32 on a part of the rows: part 0 every row (= the block call);
- * part 1 the rows with a gradient term (an edge into the source set, or a Yc row) and the long rows;
- * part 2 the other short rows, whose gradient is exactly zero: their Adam step with g = +0 (no
- * workspace needed).  Parts 1 and 2 touch disjoint rows (they may run on two streams at once) and
- * together give part 0's bits.  Same reference step (model.py:404-413, main.py:312-313). */
-int kgat_spmm_csr_masked_adam_part_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
-                                       const float *Yc_init, int64_t ldyc, int64_t yc_row0,
-                                       const uint64_t *src_rank, float *p, float *m, float *v, int64_t ldp,
-                                       int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
-                                       float eps, const int32_t *skip, int32_t part, float *workspace,
-                                       int64_t workspace_floats, void *stream);
-
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 
@@ -248,18 +236,6 @@ int kgat_biinter_fwd_f32(const float *X, int64_t ldx, const float *S, int64_t ld
                          const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
                          int64_t n_rows, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
                          float *norm_out, uint64_t *mask_out, void *stream);
-
-/* a1 + a2 forward of one layer in one pass (aggregator.py:54-65):
- *   S = A . X (written: the backward reads it), H = bi-interaction(X, S)
- * with kgat_biinter_fwd_f32's saved state (norm_out / mask_out, both or
- * neither).  Bit-identical to kgat_spmm_csr_f32 followed by
- * kgat_biinter_fwd_f32.  A square (n_rows = rows of X); d_in in {16, 32, 64},
- * d_out <= d_in; workspace: n_seg * d_in floats (long-row partials). */
-int kgat_spmm_biinter_fwd_f32(const kgat_csr *A, const float *X, int64_t ldx, float *S, int64_t lds,
-                              const float *W1, const float *b1, const float *W2, const float *b2, float *H,
-                              int64_t ldh, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
-                              float *norm_out, uint64_t *mask_out, float *workspace, int64_t workspace_floats,
-                              void *stream);
 
 /* kgat_biinter_fwd_f32 on the 16-row tiles of the table holding a member of
  * the node set row_bits (uint32 bitmap [ceil(n_rows/32)], e.g. a hop set of

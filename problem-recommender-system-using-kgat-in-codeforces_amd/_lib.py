@@ -78,9 +78,6 @@ _SIGNATURES = {
                                             c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_biinter_fwd_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                                  c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
-    "kgat_spmm_biinter_fwd_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
-                                                 c_vp, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp, c_i64,
-                                                 c_vp]),
     "kgat_biinter_bwd_workspace": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_spmm_csr_masked_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                                 c_i32, c_vp, c_i64, c_vp]),
@@ -189,9 +186,6 @@ _SIGNATURES = {
     "kgat_spmm_csr_masked_adam_block_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_i64,
                                                            c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32,
                                                            c_f32, c_f32, c_vp, c_vp, c_i64, c_vp]),
-    "kgat_spmm_csr_masked_adam_part_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_i64,
-                                                          c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32,
-                                                          c_f32, c_f32, c_vp, c_i32, c_vp, c_i64, c_vp]),
     "kgat_csr_mark_rows": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kgat_biinter_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_biinter_bwd_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),

@@ -11,8 +11,6 @@
 // reads and the k-order of the MFMA chain is (q*K/4 + step) -- any order of a
 // sum is a valid fp32 schedule.  W is staged once per block in LDS with a
 // 4-float pad per row.
-#include <cstdlib>
-
 #include "common.hpp"
 #include "spmm_core.hpp"
 
@@ -109,7 +107,7 @@ __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const floa
 // The forward epilogue of one 16-row sub-tile st: u = X+S and m = X*S in the
 // A-operand layout (lane (q, c): row c, k in [q*KQ, (q+1)*KQ)), W staged in
 // LDS.  Writes H, the row norms and the per-lane state word.  Shared by
-// biinter_fwd_kernel and spmm_bi_fwd_kernel, so both produce the same bits.
+// the whole-table and the tile-list forward, so both produce the same bits.
 template <int DIN, int DOUT, bool SB = true>
 __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const float (&m)[DIN / 4], int64_t st,
                                                int lane, const float* w1s, const float* w2s,
@@ -237,101 +235,6 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
     }
     bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
                               mask_out, node0);
-  }
-}
-
-// Propagation + bi-interaction forward in one pass (aggregator.py:54-65):
-// a wave owns a 16-row sub-tile; its 64/(DIN/4) lane groups gather the
-// sub-tile's S rows (the a1 edge walk of spmm_core.hpp, same order as
-// spmm_main_kernel), store them (saved for the backward) and transpose them
-// through a per-wave LDS tile into the MFMA operand layout; then the
-// sub-tile's epilogue runs as in biinter_fwd_kernel.  Rows longer than
-// long_threshold were produced beforehand by the segment + fix-up passes and
-// are read back from S.  S never makes a second trip through HBM and the
-// MFMA work of one wave overlaps the gathers of the others.
-template <int DIN>
-struct FusedFwdShape {
-  static constexpr int kWaves = 8;                     // 512-thread blocks share one W copy
-  static constexpr int kTile = 16 * (DIN + 4);         // floats of a wave's S tile
-};
-
-template <int DIN, int DOUT>
-__global__ __launch_bounds__(512, 4) void spmm_bi_fwd_kernel(kgat_csr A, const float* __restrict__ X, int64_t ldx,
-                                                          float* __restrict__ S, int64_t lds,
-                                                          const float* __restrict__ W1, const float* __restrict__ b1,
-                                                          const float* __restrict__ W2, const float* __restrict__ b2,
-                                                          float* __restrict__ H, int64_t ldh, float p, uint64_t seed,
-                                                          float* __restrict__ norm_out,
-                                                          uint64_t* __restrict__ mask_out) {
-  using B = BiShape<DIN, DOUT>;
-  using SS = SpmmShape<DIN>;
-  using FS = FusedFwdShape<DIN>;
-  constexpr int L = SS::kLanes, G = SS::kGroups;
-  __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD + FS::kWaves * FS::kTile];
-  float* w1s = smem;
-  float* w2s = smem + DOUT * B::WLD;
-  stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
-  __syncthreads();
-
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
-  const int g = lane / L, gl = lane % L, base = g * L;
-  float* tile = smem + 2 * DOUT * B::WLD + wave * FS::kTile;
-  float bias1[B::NCB], bias2[B::NCB];
-#pragma unroll
-  for (int cb = 0; cb < B::NCB; ++cb) {
-    bias1[cb] = b1[cb * 16 + c];
-    bias2[cb] = b2[cb * 16 + c];
-  }
-  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const uint32_t thr = bi_drop_threshold(p);
-  const int64_t n = A.n_rows;
-  const int64_t nsub = (n + 15) / 16;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * FS::kWaves;
-  const SpmmIo io{X, ldx, S, lds, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr};
-  for (int64_t st = static_cast<int64_t>(blockIdx.x) * FS::kWaves + wave; st < nsub; st += stride) {
-    const int64_t r0 = st * 16;
-    // the sub-tile's own X rows, in the operand layout (issued before the gathers)
-    float xv[B::KQ];
-    load_rows<DIN>(X, ldx, r0 + c, n, q, xv);
-#pragma unroll
-    for (int k = 0; k < 16 / G; ++k) {
-      const int lr = g + k * G;
-      const int64_t r = r0 + lr;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < n) {
-        const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-        float4* srow = reinterpret_cast<float4*>(S + r * lds) + gl;
-        if (end - beg > A.long_threshold) {
-          acc = *srow;  // long row: the fix-up pass wrote it
-        } else {
-          bool any = false;
-          gather_edges<DIN, false, 8>(A, io, beg, end, base, gl, acc, any);
-          *srow = acc;
-        }
-      }
-      *reinterpret_cast<float4*>(tile + lr * (DIN + 4) + gl * 4) = acc;
-    }
-    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
-    float u[B::KQ], m[B::KQ];
-    {
-      const float* sr = tile + c * (DIN + 4) + q * B::KQ;
-#pragma unroll
-      for (int t = 0; t < B::KQ; t += 4) {
-        const float4 sv = *reinterpret_cast<const float4*>(sr + t);
-        u[t] = xv[t] + sv.x;
-        m[t] = xv[t] * sv.x;
-        u[t + 1] = xv[t + 1] + sv.y;
-        m[t + 1] = xv[t + 1] * sv.y;
-        u[t + 2] = xv[t + 2] + sv.z;
-        m[t + 2] = xv[t + 2] * sv.z;
-        u[t + 3] = xv[t + 3] + sv.w;
-        m[t + 3] = xv[t + 3] * sv.w;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // tile reads done before the next sub-tile overwrites it
-    bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
-                              mask_out);
   }
 }
 
@@ -972,21 +875,11 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(const float* __restri
   }
 }
 
-// The backward stages W1/W2 in LDS when they fit beside the tiles (measured
-// at 64x64 on MI355X: 1.05 ms vs 1.66 ms reading W through L1/L2, whose extra
-// registers spill); KGAT_BWD_W_LDS=0 selects the L1/L2 variant for A/B runs.
-static bool bwd_w_in_lds() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("KGAT_BWD_W_LDS");
-    v = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
+// The backward stages W1/W2 in LDS when they fit beside the tiles (measured at 64x64 on MI355X:
+// 1.05 ms vs 1.66 ms reading W through L1/L2, whose extra registers spill).
 template <int DIN, int DOUT>
 static int bwd_grid(int64_t n) {
-  const int lds = (bwd_w_in_lds() ? BwdLds<DIN, DOUT, true>::kTotal : BwdLds<DIN, DOUT, false>::kTotal) * 4;
+  const int lds = BwdLds<DIN, DOUT, true>::kTotal * 4;
   int per_cu = (160 * 1024) / lds;
   if (per_cu < 1) per_cu = 1;
   if (per_cu > 4) per_cu = 4;
@@ -1013,47 +906,16 @@ static int launch_bwd_kernel(int grid, const float* X, int64_t ldx, const float*
 }
 
 template <int DIN, int DOUT>
-static int launch_spmm_fwd(const kgat_csr& A, const float* X, int64_t ldx, float* S, int64_t lds, const float* W1,
-                           const float* b1, const float* W2, const float* b2, float* H, int64_t ldh, float p,
-                           uint64_t seed, float* norm, uint64_t* mask, float* ws, hipStream_t st) {
-  const SpmmIo io{X, ldx, S, lds, ws, nullptr, nullptr, 0, nullptr, 0, nullptr};
-  if (int e = spmm_long_rows(A, io, DIN, st)) return e;
-  const int64_t nsub = (A.n_rows + 15) / 16;
-  const int grid = blocks_for(nsub, FusedFwdShape<DIN>::kWaves, kCUs * 16);
-  hipLaunchKernelGGL((spmm_bi_fwd_kernel<DIN, DOUT>), dim3(grid), dim3(64 * FusedFwdShape<DIN>::kWaves), 0, st, A, X,
-                     ldx, S, lds, W1, b1, W2, b2, H, ldh, p, seed, norm, mask);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
-template <int DIN, int DOUT>
 static int launch_fwd(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* H, int64_t ldh, int64_t n, float p, uint64_t seed,
                       float* norm, uint64_t* mask, int64_t node0, hipStream_t st) {
-  // A/B switch (KGAT_FWD_VARIANT): bit 1 = one resident round, bit 2 = 4 waves/SIMD, bit 3 = no prefetch,
-  // bit 4 (with 4 = prefetch at 4 waves/SIMD): prefetch at 3 waves/SIMD.
-  // Default 8 (measured at C2, 64->64: 795 us vs 809 us for spmm + forward with the prefetch, whose
-  // 172 VGPRs allow 2 waves/SIMD; without it 132 VGPRs, 3 waves)
-  static int variant = -1;
-  if (variant < 0) {
-    const char* e = getenv("KGAT_FWD_VARIANT");
-    variant = e ? atoi(e) : 8;
-  }
+  // no prefetch, 2 waves/SIMD minimum (measured at C2, 64->64: the prefetch's 172 VGPRs allow 2 waves per SIMD,
+  // without it 132; a one-round grid, 4 waves/SIMD and the prefetch at 3 / 4 waves/SIMD measured no faster,
+  // DESIGN.md §5)
   constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
-  const int grid = blocks_for(n, 16 * NWV, ((variant & 2) ? kCUs * 4 : kCUs * 8) * 4 / NWV);
-#define KGAT_FWD_LAUNCH(PF, W)                                                                                   \
-  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, PF, W, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S,   \
-                     lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, node0)
-  switch (variant & 12) {
-    case 4:
-      if (variant & 16) KGAT_FWD_LAUNCH(true, 3);
-      else KGAT_FWD_LAUNCH(true, 4);
-      break;
-    case 8: KGAT_FWD_LAUNCH(false, 2); break;
-    case 12: KGAT_FWD_LAUNCH(false, 4); break;
-    default: KGAT_FWD_LAUNCH(true, 2); break;
-  }
-#undef KGAT_FWD_LAUNCH
+  const int grid = blocks_for(n, 16 * NWV, kCUs * 8 * 4 / NWV);
+  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, false, 2, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S,
+                     lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, node0);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -1166,15 +1028,9 @@ static int launch_bwd(const float* X, int64_t ldx, const float* S, int64_t lds, 
     const int grid = bwd_grid<DIN, DOUT>(n);
     nslab = grid;
     if (ws == nullptr || ws_floats < static_cast<int64_t>(grid) * width) return KGAT_ERR_WORKSPACE;
-    if (bwd_w_in_lds()) {
-      if (int e = launch_bwd_kernel<DIN, DOUT, true>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
-                                                     ldds, ws, n, p, seed, rows, n_src, st))
-        return e;
-    } else {
-      if (int e = launch_bwd_kernel<DIN, DOUT, false>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd,
-                                                      dS, ldds, ws, n, p, seed, rows, n_src, st))
-        return e;
-    }
+    if (int e = launch_bwd_kernel<DIN, DOUT, true>(grid, X, ldx, S, lds, dH, lddh, W1, b1, W2, b2, dXd, lddxd, dS,
+                                                   ldds, ws, n, p, seed, rows, n_src, st))
+      return e;
   }
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, nslab, width, dW1, dW2,
                      db1, db2, DIN, DOUT);
@@ -1312,34 +1168,4 @@ extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float
                          db2, n_max, dropout_p, rows, count, src_rows, dh_compact ? 0 : 1, workspace, workspace_floats, st)
   KGAT_BI_DISPATCH(KGAT_HOP_CALL)
 #undef KGAT_HOP_CALL
-}
-
-extern "C" int kgat_spmm_biinter_fwd_f32(const kgat_csr* A, const float* X, int64_t ldx, float* S, int64_t lds,
-                                         const float* W1, const float* b1, const float* W2, const float* b2, float* H,
-                                         int64_t ldh, int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed,
-                                         float* norm_out, uint64_t* mask_out, float* workspace,
-                                         int64_t workspace_floats, void* stream) {
-  if (!A || !X || !S || !W1 || !b1 || !W2 || !b2 || !H || A->n_rows < 0) return KGAT_ERR_INVALID;
-  if ((norm_out == nullptr) != (mask_out == nullptr) || d_out > 64) return KGAT_ERR_INVALID;
-  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
-    return KGAT_ERR_INVALID;
-  if (ldx < d_in || lds < d_in || ldh < d_out) return KGAT_ERR_INVALID;
-  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
-  if (A->n_rows == 0) return KGAT_OK;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d_in))
-    return KGAT_ERR_WORKSPACE;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define KGAT_SPMM_FWD_CALL(a, b) \
-  kgat::launch_spmm_fwd<a, b>(*A, X, ldx, S, lds, W1, b1, W2, b2, H, ldh, dropout_p, seed, norm_out, mask_out, \
-                              workspace, st)
-  switch (d_in * 1000 + d_out) {
-    case 64064: return KGAT_SPMM_FWD_CALL(64, 64);
-    case 64032: return KGAT_SPMM_FWD_CALL(64, 32);
-    case 64016: return KGAT_SPMM_FWD_CALL(64, 16);
-    case 32032: return KGAT_SPMM_FWD_CALL(32, 32);
-    case 32016: return KGAT_SPMM_FWD_CALL(32, 16);
-    case 16016: return KGAT_SPMM_FWD_CALL(16, 16);
-    default: return KGAT_ERR_UNSUPPORTED_DIM;
-  }
-#undef KGAT_SPMM_FWD_CALL
 }

@@ -37,8 +37,8 @@ namespace {
 constexpr int kBM = 128, kBN = 128;
 constexpr int kPitchT = kBM + 4;  // LDS k-row pitch in floats ([k][row])
 constexpr int kThreads = 256;
-// k-depth of a stage (one barrier per stage): 16 or 32 (KGAT_GEMM_BK; the sums run in the same
-// k order either way: stage kt, sub-stage u, step s takes k = 32 kt + 16 u + 8 h + s)
+// k-depth of a stage (one barrier per stage); the launches use 16 (32 gives the same k order: stage kt,
+// sub-stage u, step s takes k = 32 kt + 16 u + 8 h + s)
 template <int BK>
 struct Tile {
   static constexpr int kPitch = BK + 4;  // LDS row pitch in floats ([row][k]): conflict-free b128 reads
@@ -428,15 +428,6 @@ __global__ __launch_bounds__(kThreads, 2) void dual_gemm_kernel(DualArgs g) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// Stage depth of every GEMM launch: KGAT_GEMM_BK = 16 or 32 (same bits either way).
-int gemm_stage_k() {
-  static const int bk = [] {
-    const char* e = getenv("KGAT_GEMM_BK");
-    return e != nullptr && atoi(e) == 32 ? 32 : 16;
-  }();
-  return bk;
-}
-
 }  // namespace
 
 int dual_gemm_f32(const DualGemm& d, hipStream_t st) {
@@ -504,13 +495,8 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
   if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
   GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, accumulate ? 1 : 0, nullptr, 0, 0};
   const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
-#define KGAT_GEMM_LAUNCH(TA_, TB_)                                                                  \
-  do {                                                                                         \
-    if (gemm_stage_k() == 32)                                                                  \
-      hipLaunchKernelGGL((gemm_kernel<TA_, TB_, 32>), grid, dim3(kThreads), 0, st, g);          \
-    else                                                                                       \
-      hipLaunchKernelGGL((gemm_kernel<TA_, TB_, 16>), grid, dim3(kThreads), 0, st, g);          \
-  } while (0)
+// 16-deep stages (32 measured no faster, same bits: the k order is fixed by the tile)
+#define KGAT_GEMM_LAUNCH(TA_, TB_) hipLaunchKernelGGL((gemm_kernel<TA_, TB_, 16>), grid, dim3(kThreads), 0, st, g)
   if (ta) {
     if (tb) KGAT_GEMM_LAUNCH(true, true);
     else KGAT_GEMM_LAUNCH(true, false);

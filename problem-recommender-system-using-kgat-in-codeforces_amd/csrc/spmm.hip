@@ -30,7 +30,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace kgat {
 
@@ -72,7 +71,7 @@ __device__ __forceinline__ void adam_row_step(const SpmmAdam& a, int64_t row, in
 template <int MODE>
 __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t out, int gl, float4 acc,
                                           bool any = false) {
-  if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB) {
+  if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam) {
     if (io.Yc != nullptr) {
       const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
@@ -83,8 +82,7 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     }
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
-  if (MODE == kMaskedAdam || MODE == kMaskedAdamB) {
-    if (io.adam.part == 1 && !any) return;  // no gradient term: masked_adam_zero_kernel steps the row
+  if (MODE == kMaskedAdam) {
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
     return;
   }
@@ -96,20 +94,16 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
   *y = acc;
 }
 
-// Source rows in flight per lane group in the row-set forward (kRows): its ~10^4 rows leave
-// most of the chip's wave slots empty, so each group keeps more gathers outstanding (the sum
-// stays in edge order: same bits for any value).
-#ifndef KGAT_ROWS_U
-#define KGAT_ROWS_U 4
-#endif
-constexpr int kRowsUnroll = KGAT_ROWS_U;
+// Source rows in flight per lane group in the row-set forward (kRows); 4, 8 and 16 measured
+// alike, the sum stays in edge order for any value.
+constexpr int kRowsUnroll = 4;
 
 // One long-row segment s (the whole wave; groups take interleaved sub-chunks) -> its partial sum in
 // io.part, reduced by the fix-up pass.
 template <int D, int MODE>
 __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io, int s, int g, int gl, int base) {
   constexpr int L = SpmmShape<D>::kLanes;
-  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
   if (s >= A.n_seg) return;
   const int row = A.seg_row[s];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
@@ -139,11 +133,11 @@ template <int D, int MODE>
 __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
-  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam || MODE == kMaskedAdamB;
+  constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
-  if ((MODE == kMaskedAdam || MODE == kMaskedAdamB) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base);
@@ -177,44 +171,6 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int64_t r_begin = w * S::kRowsPerWave;
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
-  if (MODE == kMaskedAdamB) {
-    // the group's rows' gradients first, then all their Adam loads in flight together
-    constexpr int R = S::kRowsPerGroup;
-    float4 acc[R];
-    bool ok[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const int64_t r = r_begin + g + static_cast<int64_t>(k) * S::kGroups;
-      acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      ok[k] = false;
-      if (r < r_end) {
-        const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-        if (end - beg <= A.long_threshold) {  // long rows: the fix-up pass
-          bool any = false;
-          gather_edges<D, true>(A, io, beg, end, base, gl, acc[k], any);
-          ok[k] = true;
-        }
-      }
-    }
-    AdamRow ar[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const int64_t r = r_begin + g + static_cast<int64_t>(k) * S::kGroups;
-      if (!ok[k]) continue;
-      if (io.Yc != nullptr) {
-        const int m = io.src_map[io.row0 + r];
-        if (m >= 0) {
-          const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
-          acc[k] = make_float4(o.x + acc[k].x, o.y + acc[k].y, o.z + acc[k].z, o.w + acc[k].w);
-        }
-      }
-      ar[k] = adam_row_load(io.adam, r, gl);
-    }
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-      if (ok[k]) adam_row_step(io.adam, r_begin + g + static_cast<int64_t>(k) * S::kGroups, gl, acc[k], ar[k]);
-    return;
-  }
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
@@ -236,7 +192,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   __shared__ float4 red[G][L];
   const int lr = blockIdx.x;
   const int g = threadIdx.x / L, gl = threadIdx.x % L;
-  if ((MODE == kMaskedAdam || MODE == kMaskedAdamB) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
   const int row = A.long_rows[lr];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
   const float4* P = reinterpret_cast<const float4*>(io.part);
@@ -248,268 +204,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if (threadIdx.x < L) {
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
-    // long rows are always stepped here (part 0 / 1): the Adam modes pass any = true
-    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t,
-                    MODE == kMaskedAdam || MODE == kMaskedAdamB);
-  }
-}
-
-// Part 2 of the fused table update: the short rows whose gradient is exactly zero -- not a Yc row and
-// no edge into the source set (the same membership test as gather_edges, stopping at the first hit) --
-// take their Adam step with g = +0, the value the whole-table launch adds for them (acc = +0, nothing
-// gathered, no Yc row), so the same bits.  Part 1 (spmm_main_kernel<D, kMaskedAdam> with part = 1)
-// steps every other row; the two launches touch disjoint rows and may run concurrently.
-template <int D>
-__global__ __launch_bounds__(256) void masked_adam_zero_kernel(kgat_csr A, SpmmIo io) {
-  using S = SpmmShape<D>;
-  constexpr int L = S::kLanes;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int g = lane / L, gl = lane % L, base = g * L;
-  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + wave;
-  const int64_t r_begin = w * S::kRowsPerWave;
-  int64_t r_end = r_begin + S::kRowsPerWave;
-  if (r_end > A.n_rows) r_end = A.n_rows;
-  using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
-  constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
-  for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
-    const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-    if (end - beg > A.long_threshold) continue;                       // part 1 (fix-up)
-    if (io.Yc != nullptr && io.src_map[io.row0 + r] >= 0) continue;  // a Yc row: part 1
-    bool hit = false;
-    for (int64_t cb = beg; cb < end && !hit; cb += L) {
-      const int n = static_cast<int>(end - cb < L ? end - cb : L);
-      bool in = false;
-      if (gl < n) {
-        const int mc = A.col[cb + gl];
-        if (io.src_rank != nullptr) {
-          in = ((io.src_rank[static_cast<uint32_t>(mc) >> 5] >> (mc & 31)) & 1u) != 0;
-        } else {
-          in = io.src_bits != nullptr ? ((io.src_bits[static_cast<uint32_t>(mc) >> 5] >> (mc & 31)) & 1u) != 0
-                                      : io.src_map[mc] >= 0;
-        }
-      }
-      hit = (static_cast<HitT>(__ballot(in) >> base) & kMask) != 0;  // group-uniform
-    }
-    if (hit) continue;  // part 1
-    adam_row_step(io.adam, r, gl, make_float4(0.f, 0.f, 0.f, 0.f), adam_row_load(io.adam, r, gl));
-  }
-}
-
-template <int D>
-static int launch_masked_adam_zero(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
-  using S = SpmmShape<D>;
-  const int64_t grid = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
-  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  if (grid == 0) return KGAT_OK;
-  hipLaunchKernelGGL((masked_adam_zero_kernel<D>), dim3(grid), dim3(256), 0, st, A, io);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
-// The fused table update (kMaskedAdam) with each wave's row metadata fetched up front: the
-// kRowsPerWave + 1 rowptr entries of the wave's rows and their Yc map entries are two coalesced
-// loads at the start (lane j holds row r_begin + j's), handed to the groups by shuffles, so a row's
-// chain starts at its edge chunk instead of behind two dependent single-address loads.  EARLY: the
-// row's p / m / v loads go out before its gather (in flight across it); UM: gathers in flight per
-// group.  Per row the same edges in the same order, the same Yc add and adam_elem: same bits as
-// spmm_main_kernel<D, kMaskedAdam>.  Long rows: the segment blocks + the fix-up, as there.
-template <int D, bool EARLY, int UM, int MINW>
-__global__ __launch_bounds__(256, MINW) void masked_adam_rows_kernel(kgat_csr A, SpmmIo io, int seg_blocks) {
-  using S = SpmmShape<D>;
-  constexpr int L = S::kLanes;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int g = lane / L, gl = lane % L, base = g * L;
-  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
-  if (static_cast<int>(blockIdx.x) < seg_blocks) {
-    long_segment<D, kMaskedAdam>(A, io, blockIdx.x * 4 + wave, g, gl, base);
-    return;
-  }
-  const int64_t n = A.n_rows;
-  const int64_t r_begin = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kRowsPerWave;
-  const int64_t rl = r_begin + lane;
-  const int64_t rp = (lane <= S::kRowsPerWave && rl <= n) ? A.rowptr[rl] : 0;
-  const int ym = (io.Yc != nullptr && lane < S::kRowsPerWave && rl < n) ? io.src_map[io.row0 + rl] : -1;
-#pragma unroll 1
-  for (int k = 0; k < S::kRowsPerGroup; ++k) {
-    const int j = g + k * S::kGroups;  // the group's row within the wave's rows
-    const int64_t beg = __shfl(rp, j), end = __shfl(rp, j + 1);
-    const int m = __shfl(ym, j);
-    const int64_t r = r_begin + j;
-    if (r >= n || end - beg > A.long_threshold) continue;  // long rows: the fix-up pass
-    AdamRow ar;
-    if (EARLY) ar = adam_row_load(io.adam, r, gl);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
-    gather_edges<D, true, 4, UM>(A, io, beg, end, base, gl, acc, any);
-    if (m >= 0) {
-      const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
-      acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
-    }
-    adam_row_step(io.adam, r, gl, acc, EARLY ? ar : adam_row_load(io.adam, r, gl));
-  }
-}
-
-template <int D, bool EARLY, int UM, int MINW = 1>
-static int launch_masked_adam_rows(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
-  using S = SpmmShape<D>;
-  static_assert(S::kRowsPerWave < kWave, "row metadata: one lane per row + 1");
-  const int seg_blocks = (A.n_seg + 3) / 4;
-  const int64_t grid = seg_blocks + (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
-  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL((masked_adam_rows_kernel<D, EARLY, UM, MINW>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
-  KGAT_LAUNCH_CHECK();
-  if (A.n_long > 0) {
-    hipLaunchKernelGGL((spmm_fixup_kernel<D, kMaskedAdam>), dim3(A.n_long), dim3(256), 0, st, A, io);
-    KGAT_LAUNCH_CHECK();
-  }
-  return KGAT_OK;
-}
-
-template <int D>
-static int launch_masked_adam_variant(const kgat_csr& A, const SpmmIo& io, int variant, hipStream_t st) {
-  switch (variant) {
-    case 1: return launch_masked_adam_rows<D, false, 4>(A, io, st);
-    case 2: return launch_masked_adam_rows<D, true, 4>(A, io, st);
-    case 3: return launch_masked_adam_rows<D, false, 8>(A, io, st);
-    case 4: return launch_masked_adam_rows<D, true, 8>(A, io, st);
-    case 5: return launch_masked_adam_rows<D, false, 4, 8>(A, io, st);
-    default: return launch_masked_adam_rows<D, true, 4, 6>(A, io, st);
-  }
-}
-
-// The fused table update (kMaskedAdam) with its two streams on separate waves of a block
-// (KGAT_TU_WS=1): four "gather" waves compute the masked A^T product rows of chunk i (16-lane
-// groups, gather_edges as above, + the Yc row) into an LDS image while four "stream" waves run Adam
-// on chunk i-1 from the other image -- each thread 3 x D/16 float4 of p / m / v in flight, nothing
-// waiting behind a gather.  One barrier per chunk; blocks stride over the chunks (persistent grid);
-// long rows are left to the segment blocks + the fix-up (their Adam runs there).  Same bits as
-// kMaskedAdam: per row the same edges in the same order, then the same adam_elem.
-template <int D, int GW, int SW>
-struct TuShape {
-  static constexpr int kRows = SpmmShape<D>::kRowsPerWave * GW;  // rows per chunk (GW gather waves)
-  static constexpr int kF4 = kRows * D / 4;                       // float4 per chunk image
-  static constexpr int kThreads = 64 * (GW + SW);
-};
-
-template <int D, int GW, int SW>
-__global__ __launch_bounds__(64 * (GW + SW)) void masked_adam_ws_kernel(kgat_csr A, SpmmIo io,
-                                                                                        int seg_blocks,
-                                                                                        int64_t n_chunks) {
-  using S = SpmmShape<D>;
-  using T = TuShape<D, GW, SW>;
-  constexpr int L = S::kLanes;
-  __shared__ float4 img[2][T::kF4];
-  __shared__ int8_t skip_row[2][T::kRows];  // long rows (Adam in the fix-up) and rows past the end
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
-  if (static_cast<int>(blockIdx.x) < seg_blocks) {
-    // long-row segments: one per wave, as spmm_main_kernel's segment waves
-    const int s = blockIdx.x * (GW + SW) + wave;
-    if (s >= A.n_seg) return;
-    const int g = lane / L, gl = lane % L, base = g * L;
-    const int row = A.seg_row[s];
-    const int64_t beg = A.seg_beg[s];
-    const int64_t row_end = A.rowptr[row + 1];
-    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool any = false;
-    for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
-      const int64_t ce = cb + L < end ? cb + L : end;
-      gather_edges<D, true>(A, io, cb, ce, base, gl, acc, any);
-    }
-#pragma unroll
-    for (int o = L; o < kWave; o <<= 1) {
-      acc.x += __shfl_xor(acc.x, o);
-      acc.y += __shfl_xor(acc.y, o);
-      acc.z += __shfl_xor(acc.z, o);
-      acc.w += __shfl_xor(acc.w, o);
-    }
-    if (g == 0) reinterpret_cast<float4*>(io.part)[static_cast<int64_t>(s) * L + gl] = acc;
-    return;
-  }
-  const int64_t blk = blockIdx.x - seg_blocks, nblk = gridDim.x - seg_blocks;
-  const bool gather = wave < GW;
-  int it = 0;
-  for (int64_t c = blk;; c += nblk, ++it) {
-    const int buf = it & 1;
-    if (gather && c < n_chunks) {
-      // chunk c: rows [c * kRows, ...), group g of wave w takes rows w*kRowsPerWave + g + k*kGroups
-      const int g = lane / L, gl = lane % L, base = g * L;
-      const int64_t r_begin = c * T::kRows;
-#pragma unroll 1
-      for (int k = 0; k < S::kRowsPerGroup; ++k) {
-        const int lr = wave * S::kRowsPerWave + g + k * S::kGroups;
-        const int64_t r = r_begin + lr;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool skip = r >= A.n_rows;
-        if (!skip) {
-          const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-          skip = end - beg > A.long_threshold;
-          if (!skip) {
-            bool any = false;
-            gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
-            if (io.Yc != nullptr) {
-              const int m = io.src_map[io.row0 + r];
-              if (m >= 0) {
-                const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
-                acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
-              }
-            }
-          }
-        }
-        img[buf][lr * L + gl] = acc;
-        if (gl == 0) skip_row[buf][lr] = skip ? 1 : 0;
-      }
-    }
-    if (!gather && it > 0 && c - nblk < n_chunks) {
-      // chunk c - nblk (filled last iteration into the other image): Adam on its rows, float4-linear
-      const int pb = buf ^ 1;
-      const int64_t r0 = (c - nblk) * T::kRows;
-      const int t = threadIdx.x - 64 * GW;
-#pragma unroll 4
-      for (int f = t; f < T::kF4; f += 64 * SW) {
-        const int lr = f / L, gl = f % L;
-        if (skip_row[pb][lr]) continue;
-        adam_row_step(io.adam, r0 + lr, gl, img[pb][f], adam_row_load(io.adam, r0 + lr, gl));
-      }
-    }
-    if (c - nblk >= n_chunks) break;  // block-uniform: every wave leaves after the same iteration
-    __syncthreads();
-  }
-}
-
-template <int D, int GW, int SW>
-static int launch_masked_adam_ws_t(const kgat_csr& A, const SpmmIo& io, int per_cu, hipStream_t st) {
-  using T = TuShape<D, GW, SW>;
-  const int seg_blocks = (A.n_seg + GW + SW - 1) / (GW + SW);
-  const int64_t n_chunks = (A.n_rows + T::kRows - 1) / T::kRows;
-  const int64_t chunk_blocks = std::min<int64_t>(n_chunks, static_cast<int64_t>(per_cu) * kCUs);
-  hipLaunchKernelGGL((masked_adam_ws_kernel<D, GW, SW>), dim3(seg_blocks + chunk_blocks), dim3(T::kThreads), 0, st, A,
-                     io, seg_blocks, n_chunks);
-  KGAT_LAUNCH_CHECK();
-  if (A.n_long > 0) {
-    hipLaunchKernelGGL((spmm_fixup_kernel<D, kMaskedAdam>), dim3(A.n_long), dim3(256), 0, st, A, io);
-    KGAT_LAUNCH_CHECK();
-  }
-  return KGAT_OK;
-}
-
-// KGAT_TU_WS = 1: 4 gather + 4 stream waves; 2: 6 + 2; 3: 12 + 4 (1024 threads).  KGAT_TU_WS_BLOCKS:
-// blocks per CU (default 4).
-template <int D>
-static int launch_masked_adam_ws(const kgat_csr& A, const SpmmIo& io, int variant, hipStream_t st) {
-  static const int per_cu = [] {
-    const char* e = getenv("KGAT_TU_WS_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 4;
-  }();
-  switch (variant) {
-    case 2: return launch_masked_adam_ws_t<D, 6, 2>(A, io, per_cu, st);
-    case 3: return launch_masked_adam_ws_t<D, 12, 4>(A, io, per_cu, st);
-    default: return launch_masked_adam_ws_t<D, 4, 4>(A, io, per_cu, st);
+    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
   }
 }
 
@@ -835,19 +530,8 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
                                                    int32_t d, float step_size, float beta1, float beta2,
                                                    float bc2_sqrt, float eps, const int32_t* skip, float* workspace,
                                                    int64_t workspace_floats, void* stream) {
-  return kgat_spmm_csr_masked_adam_part_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, yc_row0, src_rank, p, m, v, ldp, d,
-                                            step_size, beta1, beta2, bc2_sqrt, eps, skip, 0, workspace,
-                                            workspace_floats, stream);
-}
-
-extern "C" int kgat_spmm_csr_masked_adam_part_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
-                                                  int64_t ldxc, const float* Yc_init, int64_t ldyc, int64_t yc_row0,
-                                                  const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
-                                                  int32_t d, float step_size, float beta1, float beta2, float bc2_sqrt,
-                                                  float eps, const int32_t* skip, int32_t part, float* workspace,
-                                                  int64_t workspace_floats, void* stream) {
   using namespace kgat;
-  if (yc_row0 < 0 || part < 0 || part > 2) return KGAT_ERR_INVALID;
+  if (yc_row0 < 0) return KGAT_ERR_INVALID;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
@@ -855,61 +539,11 @@ extern "C" int kgat_spmm_csr_masked_adam_part_f32(const kgat_csr* A, const int32
     return KGAT_ERR_INVALID;
   if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
   if (A->n_rows == 0) return KGAT_OK;
-  if (part != 2 && A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, part};
-
-  if (part == 2) {
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (d) {
-      case 16: return launch_masked_adam_zero<16>(*A, io, st);
-      case 32: return launch_masked_adam_zero<32>(*A, io, st);
-      case 64: return launch_masked_adam_zero<64>(*A, io, st);
-      case 128: return launch_masked_adam_zero<128>(*A, io, st);
-      case 256: return launch_masked_adam_zero<256>(*A, io, st);
-      default: return KGAT_ERR_UNSUPPORTED_DIM;
-    }
-  }
-  if (part == 1) return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-  // KGAT_TU_BATCH=1: the row-batched form (kMaskedAdamB, same bits); default the row-at-a-time one
-  static const int batched = [] {
-    const char* e = getenv("KGAT_TU_BATCH");
-    return e ? atoi(e) : 0;
-  }();
-  if (batched) return dispatch<kMaskedAdamB>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-  // KGAT_TU_WS=1: gather and Adam on separate waves (masked_adam_ws_kernel, same bits)
-  static const int ws = [] {
-    const char* e = getenv("KGAT_TU_WS");
-    return e ? atoi(e) : 0;
-  }();
-  if (ws) {
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (d) {
-      case 64: return launch_masked_adam_ws<64>(*A, io, ws, st);
-      case 128: return launch_masked_adam_ws<128>(*A, io, ws, st);
-      case 256: return launch_masked_adam_ws<256>(*A, io, ws, st);
-      default: break;
-    }
-  }
-  // KGAT_TU_VARIANT=1..6: masked_adam_rows_kernel (row metadata up front; early Adam loads; 8 gathers
-  // in flight; 5: 8 waves/SIMD forced), same bits
-  static const int tuv = [] {
-    const char* e = getenv("KGAT_TU_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  if (tuv > 0) {
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    switch (d) {
-      case 16: break;  // 64 rows per wave: no lane left for the metadata's end entry
-      case 32: return launch_masked_adam_variant<32>(*A, io, tuv, st);
-      case 64: return launch_masked_adam_variant<64>(*A, io, tuv, st);
-      case 128: return launch_masked_adam_variant<128>(*A, io, tuv, st);
-      case 256: return launch_masked_adam_variant<256>(*A, io, tuv, st);
-      default: break;
-    }
-  }
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 

@@ -7,13 +7,7 @@
 
 namespace kgat {
 
-enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4, kRows = 5,
-                kMaskedAdamB = 6 };
-
-// kMaskedAdamB: kMaskedAdam with each lane group's rows batched -- the group first gathers the
-// gradients of all its kRowsPerGroup short rows (one accumulator each), then issues every row's
-// p / m / v loads together (3 x kRowsPerGroup float4 in flight per lane instead of 3) and steps
-// them.  Same arithmetic per row (same bits); the choice is KGAT_TU_BATCH (spmm.hip).
+enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, kMaskedAdam = 4, kRows = 5 };
 
 // kRows: the dense product A . X on the rows of an output set only (out_rows / out_bits /
 // out_count; -1 entries of out_rows are padding), each written at its own row of Y -- the
@@ -33,10 +27,6 @@ struct SpmmAdam {
   int64_t ld;  // row stride of p, m, v (floats)
   float step_size, b1, b2, bc2s, eps;
   const int32_t* skip;  // nullable: *skip != 0 -> the launch leaves p / m / v untouched (bad step ids)
-  // the rows this launch steps (kgat_spmm_csr_masked_adam_part_f32): 0 every row; 1 the rows with a
-  // gradient term (a hit or a Yc row) and the long rows; 2 the remaining short rows (zero gradient),
-  // by masked_adam_zero_kernel
-  int part;
 };
 
 struct SpmmIo {

@@ -637,9 +637,8 @@ extern "C" int kgat_transr_fwd_ex_f32(const float* emb, int64_t ld_emb, const fl
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // the chunked MFMA form where W_r is big enough for its re-reads to dominate (d >= 128); the
   // per-sample kernel otherwise (and for shapes without an instantiation)
-  static const bool force_valu = getenv("KGAT_TRANSR_VALU") != nullptr;  // A/B switch
   bool done = false;
-  if (!force_valu && d >= 128 && (ld_emb & 3) == 0 && (reinterpret_cast<uintptr_t>(emb) & 15) == 0 &&
+  if (d >= 128 && (ld_emb & 3) == 0 && (reinterpret_cast<uintptr_t>(emb) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(trans) & 15) == 0 && n_rel <= 65535 * 64 && (batch + 15) / 16 <= 65535) {
     if (d == 128) done = launch_fwd_mfma_d<128>(k, n_rel, emb, ld_emb, rel_emb, trans, heads, rels, pos, neg, batch, reg, work, st);
     else if (d == 256) done = launch_fwd_mfma_d<256>(k, n_rel, emb, ld_emb, rel_emb, trans, heads, rels, pos, neg, batch, reg, work, st);

@@ -315,35 +315,13 @@ def _skip_ptr(skip: torch.Tensor | None):
     return skip.data_ptr()
 
 
-def _tu_split_default() -> bool:
-    return os.environ.get("KGAT_TU_SPLIT", "0") != "0"
-
-
-_SIDE_STREAMS: dict = {}
-
-
-def side_stream(device) -> torch.cuda.Stream:
-    """One side stream per device (the fused table update's zero-gradient rows)."""
-    key = torch.device(device).index
-    s = _SIDE_STREAMS.get(key)
-    if s is None:
-        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
-    return s
-
-
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None, split: bool | None = None) -> None:
+                     skip: torch.Tensor | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).
-
-    ``split`` (default: ``KGAT_TU_SPLIT``): the rows whose gradient is exactly zero (no edge into the
-    source set, no Yc row: ~2/3 of the rows at C2) take their step in a launch of their own on a side
-    stream (kgat_spmm_csr_masked_adam_part_f32 part 2, a pure p / m / v stream) while the current stream
-    runs the product + step of the others (part 1); the current stream then waits for the side one.
-    Disjoint rows, same bits."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -357,8 +335,6 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
         _req(Yc_init, "Yc_init", dim=2)
         if Yc_init.shape[1] != d:
             raise ValueError("Yc_init width mismatch")
-    if split is None:
-        split = _tu_split_default()
     csr = graph.AT
     desc = csr.descriptor()
     ws = torch.empty(max(1, csr.n_seg * d), dtype=torch.float32, device=Xc.device)
@@ -369,20 +345,9 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
     rank = _rank_ptr(src_rank, src_map)
 
-    def part(k: int, stream) -> None:
-        _lib.call("kgat_spmm_csr_masked_adam_part_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-                  yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
-                  bc2_sqrt, eps, _skip_ptr(skip), k, ws.data_ptr(), ws.numel(), stream)
-
-    if split:
-        main = torch.cuda.current_stream(Xc.device)
-        side = side_stream(Xc.device)
-        side.wait_stream(main)  # the side launch reads this step's hop set and the skip flag
-        part(2, side.cuda_stream)
-        part(1, main.cuda_stream)
-        main.wait_stream(side)  # every row stepped before anything later on this stream
-    else:
-        part(0, stream_ptr(Xc.device))
+    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
+              eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
@@ -714,12 +679,11 @@ def fused_supported(d_in: int, d_out: int) -> bool:
 # C4's wide fused shapes (d_out > 64 or d_in * d_out > 4096: no saved-state fused backward) run the
 # fused MFMA forward keeping its norm + sign/keep bits and the GEMM backward from those bits
 # (kgat_biinter_bwd_gemm_bits_f32) -- instead of the rocBLAS forward with its [n, 2*d_out]
-# pre-activation state.  KGAT_BITS_WIDE=0 restores the GEMM forward.
-BITS_WIDE = os.environ.get("KGAT_BITS_WIDE", "1") != "0"
+# pre-activation state.
 
 
 def bits_supported(d_in: int, d_out: int) -> bool:
-    return BITS_WIDE and fused_supported(d_in, d_out) and d_out <= 128 and not saved_state_supported(d_in, d_out)
+    return fused_supported(d_in, d_out) and d_out <= 128 and not saved_state_supported(d_in, d_out)
 
 
 class BiState:
@@ -808,106 +772,32 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
     return out
 
 
-# Row blocks of the pipelined layer forward (0 = one spmm launch, then one biinter_fwd launch).
-FWD_PIPELINE_BLOCKS = int(os.environ.get("KGAT_FWD_BLOCKS", "0"))
-FWD_PIPELINE_MIN_ROWS = 1 << 16
-
-
 def propagate_layer(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
                     state: BiState | None = None):
     """One KGAT layer forward (aggregator.py:54-65): S = A . X, H = biinter(X, S); returns (S, H).
+    (Row-block pipelining of the two launches on two streams and a one-pass propagation +
+    bi-interaction kernel both measured slower)"""
+    S = spmm(graph, X)
+    return S, biinter_fwd(X, S, W1, b1, W2, b2, dropout_p, seed, state=state)
 
-    For fused shapes on large graphs the rows are cut into FWD_PIPELINE_BLOCKS blocks of equal
-    edge count: block b's propagation (kgat_spmm_csr_f32 on a row view of A, current stream)
-    overlaps block b-1's bi-interaction (kgat_biinter_fwd_rows_f32, a second stream) -- the
-    gather is fabric-bound, the bi-interaction MFMA-bound.  Same bits as the two whole launches."""
+
+def biinter_fwd_rows(X, S, W1, b1, W2, b2, r0: int, n_rows: int, H, dropout_p: float = 0.0, seed: int = 0,
+                     state: BiState | None = None) -> None:
+    """kgat_biinter_fwd_rows_f32: the fused forward of rows [r0, r0 + n_rows) of the whole-table
+    call (X, S, H whole tables; r0 a multiple of 16; the dropout draws and the saved state of those
+    rows exactly the whole call's)."""
     n, din = X.shape
     dout = W1.shape[0]
-    k = FWD_PIPELINE_BLOCKS
-    fused = fused_supported(din, dout) and (state is None or state.kind == "fused")
-    if k <= 1 or not fused or n < FWD_PIPELINE_MIN_ROWS or not X.is_cuda:
-        S = spmm(graph, X)
-        return S, biinter_fwd(X, S, W1, b1, W2, b2, dropout_p, seed, state=state)
-    for t, nm in ((X, "X"), (W1, "W1"), (W2, "W2")):
-        _req(t, nm, dim=2)
-    if n != graph.n_nodes or W1.shape != (dout, din) or W2.shape != (dout, din) or b1.numel() != dout:
-        raise ValueError("layer shape mismatch")
-    if not (W1.is_contiguous() and W2.is_contiguous()):
-        raise ValueError("W must be contiguous")
-    if state is not None and (state.norm.numel() < n or state.mask.numel() < (n + 15) // 16 * 64 or dout > 64):
-        raise ValueError("bi-interaction state too small or d_out > 64")
-    dev = X.device
-    S = torch.empty(n, din, dtype=torch.float32, device=dev)
-    H = torch.empty(n, dout, dtype=torch.float32, device=dev)
-    main = torch.cuda.current_stream(dev)
-    side = graph.side_stream()
+    if r0 % 16 or r0 < 0 or n_rows < 0 or r0 + n_rows > n or (state is not None and not saved_state_supported(din, dout)):
+        raise ValueError("biinter_fwd_rows: r0 a multiple of 16 inside the table; state only for saved-state shapes")
+    if S.shape != X.shape or H.shape != (n, dout) or W1.shape != (dout, din) or not fused_supported(din, dout):
+        raise ValueError("bi-interaction shape mismatch")
     ldx, lds, ldh = _ld(X), _ld(S), _ld(H)
-    seed64 = ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF)
-    ev = SPMM_EVENTS
-    for view in graph.row_blocks(k):
-        r0, nb = view.r0, view.n_rows
-        desc = view.descriptor()
-        ws = torch.empty(max(1, view.n_seg * din), dtype=torch.float32, device=dev)
-        if ev is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(main)
-        _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), ldx, S.data_ptr() + 4 * r0 * lds, lds, din, 0,
-                  ws.data_ptr(), ws.numel(), main.cuda_stream)
-        if ev is not None:
-            e1.record(main)
-            ev.append((e0, e1, din, False, ("block", nb, int(view.nnz))))
-        ready = torch.cuda.Event()
-        ready.record(main)
-        side.wait_event(ready)
-        _lib.call("kgat_biinter_fwd_rows_f32", X.data_ptr() + 4 * r0 * ldx, ldx, S.data_ptr() + 4 * r0 * lds, lds,
-                  W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), H.data_ptr() + 4 * r0 * ldh, ldh, nb, r0,
-                  din, dout, float(dropout_p), seed64,
-                  state.norm.data_ptr() + 4 * r0 if state is not None else None,
-                  state.mask.data_ptr() + 8 * (r0 // 16) * 64 if state is not None else None, side.cuda_stream)
-    done = torch.cuda.Event()
-    done.record(side)
-    main.wait_event(done)
-    return S, H
-
-
-# (d_in, d_out) pairs of the fused propagation + bi-interaction forward (kgat_spmm_biinter_fwd_f32)
-SPMM_FUSED_SHAPES = {(64, 64), (64, 32), (64, 16), (32, 32), (32, 16), (16, 16)}
-
-
-def spmm_biinter_fwd(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
-                     state: BiState | None = None):
-    """S = A . X and H = biinter(X, S) in one pass; returns (S, H).  Same bits as spmm + biinter_fwd."""
-    for t, nm in ((X, "X"), (W1, "W1"), (W2, "W2")):
-        _req(t, nm, dim=2)
-    n, din = X.shape
-    dout = W1.shape[0]
-    if n != graph.n_nodes or W1.shape != (dout, din) or W2.shape != (dout, din) or b1.numel() != dout:
-        raise ValueError("fused forward shape mismatch")
-    if (din, dout) not in SPMM_FUSED_SHAPES:
-        raise ValueError(f"no fused propagation forward for {din}->{dout}")
-    if not (W1.is_contiguous() and W2.is_contiguous()):
-        raise ValueError("W must be contiguous")
-    if state is not None and (state.kind != "fused" or state.norm.numel() < n
-                              or state.mask.numel() < (n + 15) // 16 * 64):
-        raise ValueError("bi-interaction state does not match the layer")
-    S = torch.empty(n, din, dtype=torch.float32, device=X.device)
-    H = torch.empty(n, dout, dtype=torch.float32, device=X.device)
-    csr = graph.A
-    desc = csr.descriptor()
-    ws = torch.empty(max(1, csr.n_seg * din), dtype=torch.float32, device=X.device)
-    ev = SPMM_EVENTS
-    if ev is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-    _lib.call("kgat_spmm_biinter_fwd_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), S.data_ptr(), _ld(S),
-              W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), H.data_ptr(), _ld(H), din, dout,
-              float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
-              state.norm.data_ptr() if state is not None else None,
-              state.mask.data_ptr() if state is not None else None, ws.data_ptr(), ws.numel(), stream_ptr(X.device))
-    if ev is not None:
-        e1.record()
-        ev.append((e0, e1, din, False, "fused"))
-    return S, H
+    _lib.call("kgat_biinter_fwd_rows_f32", X.data_ptr() + 4 * r0 * ldx, ldx, S.data_ptr() + 4 * r0 * lds, lds,
+              W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), H.data_ptr() + 4 * r0 * ldh, ldh, n_rows,
+              r0, din, dout, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              state.norm.data_ptr() + 4 * r0 if state is not None else None,
+              state.mask.data_ptr() + 8 * (r0 // 16) * 64 if state is not None else None, stream_ptr(X.device))
 
 
 def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,

@@ -355,7 +355,6 @@ class _LazyKGAdam:
         self.hist = None
         self.flushed_at = 0
         self.dirty = False  # rows behind the current step (a lazy step since the last flush)
-        self._one = None
 
     def _t(self, opt) -> int:
         st = opt.state.get(id(self.param))
@@ -367,10 +366,11 @@ class _LazyKGAdam:
             dev = self.param.device
             t = self._t(opt)
             self.last = torch.full((n,), t, dtype=torch.int32, device=dev)
-            self.hist = (torch.zeros(self.CAP, dtype=torch.float32, device=dev),
-                         torch.zeros(self.CAP, dtype=torch.float32, device=dev),
-                         torch.zeros(self.CAP, dtype=torch.int32, device=dev))
-            self._one = torch.ones(1, dtype=torch.int32, device=dev)
+            if self.hist is None or self.hist[0].device != dev:
+                # entries are written by the step that owns them before any replay reads them
+                self.hist = (torch.zeros(self.CAP, dtype=torch.float32, device=dev),
+                             torch.zeros(self.CAP, dtype=torch.float32, device=dev),
+                             torch.zeros(self.CAP, dtype=torch.int32, device=dev))
             self.flushed_at = t
 
     def catch_up(self, opt, rows: torch.Tensor | None = None) -> None:
@@ -406,19 +406,12 @@ class _LazyKGAdam:
         return run
 
     def dense_step_done(self, opt) -> None:
-        """A dense step t was just applied to every row (caught up before it): record it in the history as
-        applied (skipped by later replays)."""
-        st = opt.state.get(id(self.param))
-        if self.last is None or st is None:
-            return
-        t = int(st["step"])
-        hs, hb, hk = self.hist
-        p = self.param.data
-        dummy = self._one  # no rows listed: the call only writes step t's history entry, with skip = 1
-        _lib.call("kgat_adam_lazy_rows_f32", p.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                  p.shape[1], dummy.data_ptr(), 0, p.data_ptr(), p.shape[1], self.last.data_ptr(), t, hs.data_ptr(),
-                  hb.data_ptr(), hk.data_ptr(), self.CAP, 0.0, opt.beta1, opt.beta2, 1.0, opt.eps, self._one.data_ptr(),
-                  stream_ptr(p.device))
+        """A dense step t was just applied to every row (each caught up before it): every row is current at
+        t, so the per-row record restarts there (the next lazy step re-creates it, ``ensure``).  Keeping the
+        old record would leave every row's last[] at its pre-dense value, and after 2^20 such steps the ring
+        slots a replay still needs would be overwritten."""
+        self.last = None
+        self.dirty = False
 
 
 class _MarkedBatch:
@@ -1012,6 +1005,11 @@ class KGAT(nn.Module):
 
     # ------------------------------------------------------------- optimizers
     def build_optimizer(self, cf_lr: float, kg_lr: float) -> None:
+        # lazy KG Adam: the replays still owed are the old optimiser's steps -- apply them, then restart
+        # the per-row step record at the new optimiser's t = 0 (a stale last[r] would skip its steps)
+        self.flush_kg_table()
+        self._lazy_kg.last = None
+        self._lazy_kg.dirty = False
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 

@@ -109,6 +109,7 @@ class ShardedGradSync:
         self.bounds: list[tuple[int, int]] = []
         self._early = None  # (gradient tensor, [work handles]) of the hooked table gradient
         self._announced = None  # this step's early (flag, hop count) all-gather: (device, pinned host, event)
+        self.discarded = 0  # announcements dropped because their forward's backward never ran
 
     def attach(self, model) -> "ShardedGradSync":
         """Overlap the table gradient's exchange with its computation: the CF backward then
@@ -145,12 +146,24 @@ class ShardedGradSync:
         return torch.cat(parts)
 
     def _gather_info(self, sparse: bool, count: torch.Tensor | None, dev):
-        """[G] int32 in rank order: each rank's layer-0 hop count, -1 for a rank whose backward is dense."""
+        """[G, 2] int32 in rank order: each rank's layer-0 hop count (-1 for a rank whose backward is
+        dense) and its count of discarded announcements (compared across ranks by _split_info)."""
+        info = torch.full((2,), self.discarded, dtype=torch.int32, device=dev)
         if sparse:
-            info = count.reshape(1).to(torch.int32)
+            info[:1].copy_(count.reshape(1))
         else:
-            info = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        return self._all_gather(info)
+            info[:1].fill_(-1)
+        return self._all_gather(info).view(-1, 2)
+
+    @staticmethod
+    def _split_info(both: torch.Tensor, host: list[int]) -> tuple[torch.Tensor, list[int]]:
+        """(device [G] hop counts, host counts) of a _gather_info result; raises when the ranks dropped
+        different numbers of announced forwards (their all-gathers would pair up different steps)."""
+        counts, dropped = host[0::2], host[1::2]
+        if len(set(dropped)) > 1:
+            raise RuntimeError(f"ShardedGradSync: the ranks discarded different numbers of announced TRAIN_CF "
+                               f"forwards (no backward ran): {dropped} -- every rank must run the same steps")
+        return both[:, 0].contiguous(), counts
 
     def announce(self, sparse: bool, count: torch.Tensor | None) -> None:
         """All-gather this step's (hop flag, layer-0 hop count) early -- from the forward, when the
@@ -159,7 +172,12 @@ class ShardedGradSync:
         # A grad-enabled TRAIN_CF forward whose backward never ran (a loss only logged) left its
         # announcement open.  Every rank runs the same program, so every rank dropped the same
         # forward and made the same all-gather: the stale announcement is simply discarded.  That
-        # forward's own backward cannot run later -- model._mark_batch marked its token stale.
+        # forward's own backward cannot run later -- model._mark_batch marked its token stale.  That is
+        # only safe while the ranks dropped the same forwards; the count is compared across ranks at the
+        # next exchange (_agree), so diverging control flow raises instead of pairing up other steps'
+        # all-gathers.
+        if self._announced is not None:
+            self.discarded += 1
         self._announced = None
         both = self._gather_info(sparse, count, count.device)
         host = torch.empty(tuple(both.shape), dtype=torch.int32, pin_memory=True)
@@ -175,7 +193,7 @@ class ShardedGradSync:
         if ann is None:
             return None
         ann[2].synchronize()
-        counts = ann[1].tolist()
+        counts = ann[1].reshape(-1).tolist()[0::2]
         return max(1, max(counts)) if all(c >= 0 for c in counts) else None
 
     def _agree(self, sparse: bool, count: torch.Tensor | None, dev) -> tuple[torch.Tensor, list[int], bool]:
@@ -186,11 +204,12 @@ class ShardedGradSync:
         if ann is not None:
             both, host_t, ev = ann
             ev.synchronize()
-            host = host_t.tolist()
+            host = host_t.reshape(-1).tolist()
         else:
             both = self._gather_info(sparse, count, dev)
-            host = both.cpu().tolist()  # the gather sizes
-        return both, host, all(c >= 0 for c in host)
+            host = both.reshape(-1).cpu().tolist()  # the gather sizes
+        counts_dev, counts = self._split_info(both, host)
+        return counts_dev, counts, all(c >= 0 for c in counts)
 
     def table_grad_hop(self, graph, hmap, hrows, hcount, dSc, dXdc, rank_words, deferral=None, packed=None):
         """The mean table gradient from this rank's compact layer-0 hop-set terms (model._CFLoss):

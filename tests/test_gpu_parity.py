@@ -576,37 +576,11 @@ def test_cf_hop_chain_matches_dense_backward(pkg, layers):
         np.testing.assert_allclose(sp[k].cpu().numpy(), de[k].cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=k)
 
 
-@pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (32, 16), (16, 16)])
-def test_spmm_biinter_fused_forward_bit_identical(pkg, din, dout):
-    """kgat_spmm_biinter_fwd_f32 (propagation + bi-interaction in one pass, long hub rows via the
-    segment pass) against kgat_spmm_csr_f32 + kgat_biinter_fwd_f32: S, H, norms and state words
-    bit for bit, with and without dropout; ragged last sub-tile (n % 16 != 0)."""
-    graph_mod, kernels = _mods(pkg)
-    lay, _ = random_graph(graph_mod, 3001, 12, hubs=6, hub_deg=2000, seed=din + dout)
-    g = graph_mod.DeviceGraph(lay, DEV)
-    assert g.A.n_long > 0
-    torch.manual_seed(din * dout)
-    X = torch.randn(lay.n_nodes, din, device=DEV)
-    W1, W2 = torch.randn(dout, din, device=DEV) * 0.2, torch.randn(dout, din, device=DEV) * 0.2
-    b1, b2 = torch.randn(dout, device=DEV) * 0.1, torch.randn(dout, device=DEV) * 0.1
-    for p in (0.0, 0.1):
-        st_a = kernels.make_state(lay.n_nodes, din, dout, DEV)
-        st_b = kernels.make_state(lay.n_nodes, din, dout, DEV)
-        S_ref = kernels.spmm(g, X)
-        H_ref = kernels.biinter_fwd(X, S_ref, W1, b1, W2, b2, p, 99, state=st_a)
-        S, H = kernels.spmm_biinter_fwd(g, X, W1, b1, W2, b2, p, 99, state=st_b)
-        assert torch.equal(S, S_ref)
-        assert torch.equal(H, H_ref)
-        n = lay.n_nodes
-        assert torch.equal(st_a.norm[:n], st_b.norm[:n])
-        assert torch.equal(st_a.mask[:(n + 15) // 16 * 64], st_b.mask[:(n + 15) // 16 * 64])
-
-
 @pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (32, 16)])
-def test_propagate_layer_pipelined_bit_identical(pkg, din, dout):
-    """The row-block pipelined layer forward (propagation of block b on the current stream while
-    block b-1's bi-interaction runs on a second stream, dropout drawn by global node id) gives the
-    same S, H and saved state as one spmm launch followed by one biinter_fwd launch."""
+def test_biinter_fwd_row_blocks_bit_identical(pkg, din, dout):
+    """kgat_biinter_fwd_rows_f32 (kernels.biinter_fwd_rows) on row blocks of the table -- 16-aligned
+    starts, a ragged last block, dropout drawn by global node id -- gives the whole-table launch's H and
+    saved state (norms, sign/keep words) bit for bit."""
     graph_mod, kernels = _mods(pkg)
     lay, _ = random_graph(graph_mod, 5003, 10, hubs=5, hub_deg=1500, seed=din)
     g = graph_mod.DeviceGraph(lay, DEV)
@@ -615,20 +589,16 @@ def test_propagate_layer_pipelined_bit_identical(pkg, din, dout):
     X = torch.randn(n, din, device=DEV)
     W1, W2 = torch.randn(dout, din, device=DEV) * 0.2, torch.randn(dout, din, device=DEV) * 0.2
     b1, b2 = torch.randn(dout, device=DEV) * 0.1, torch.randn(dout, device=DEV) * 0.1
-    old = (kernels.FWD_PIPELINE_BLOCKS, kernels.FWD_PIPELINE_MIN_ROWS)
-    try:
-        kernels.FWD_PIPELINE_MIN_ROWS = 0
-        outs = {}
-        for k in (1, 7):
-            kernels.FWD_PIPELINE_BLOCKS = k
-            st = kernels.make_state(n, din, dout, DEV)
-            S, H = kernels.propagate_layer(g, X, W1, b1, W2, b2, 0.1, 1234, state=st)
-            outs[k] = (S, H, st.norm[:n].clone(), st.mask[:(n + 15) // 16 * 64].clone())
-        assert len(g.row_blocks(7)) > 1
-    finally:
-        kernels.FWD_PIPELINE_BLOCKS, kernels.FWD_PIPELINE_MIN_ROWS = old
-    for a, b in zip(outs[1], outs[7]):
-        assert torch.equal(a, b)
+    st = kernels.make_state(n, din, dout, DEV)
+    S, H = kernels.propagate_layer(g, X, W1, b1, W2, b2, 0.1, 1234, state=st)
+    st2 = kernels.make_state(n, din, dout, DEV)
+    H2 = torch.full_like(H, 7.0)
+    bounds = [0, 1008, 1024, 2512, n]
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        kernels.biinter_fwd_rows(X, S, W1, b1, W2, b2, r0, r1 - r0, H2, 0.1, 1234, state=st2)
+    assert torch.equal(H, H2)
+    assert torch.equal(st.norm[:n], st2.norm[:n])
+    assert torch.equal(st.mask[:(n + 15) // 16 * 64], st2.mask[:(n + 15) // 16 * 64])
 
 
 def test_row_softmax_short_and_long_rows(pkg):
@@ -1469,52 +1439,6 @@ def test_fused_table_update_bit_identical(pkg, layers):
     assert torch.equal(grads[0], grads[1])
 
 
-@pytest.mark.parametrize("layers", [[64, 32], [64, 32, 16]])
-def test_fused_table_update_split_parts_bit_identical(pkg, layers):
-    """The fused table update split in two disjoint row launches (kgat_spmm_csr_masked_adam_part_f32:
-    part 2 = the zero-gradient short rows on a side stream, part 1 = the rest on the current stream)
-    gives the single launch's p / m / v bit for bit, on a hub graph's real pending update (long rows,
-    Yc rows, rows with and without hits), with the skip flag honoured by both parts."""
-    graph_mod, kernels = _mods(pkg)
-    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=6)
-    lay = graph_mod.build_layout(U, E, inter, trip)
-    torch.manual_seed(2024)
-    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=layers,
-                              message_dropout=[0.1] * len(layers)))
-    m.attach_graph(lay, DEV)
-    assert m.graph().AT.n_long > 0
-    m.train()
-    m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-    m.fuse_table_update = True
-    rng = np.random.default_rng(5)
-    ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
-    m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
-    tu = m._table_update
-    assert tu.pending is not None
-    graph, src_map, Xc, Yc, rank = tu.pending
-    g = torch.Generator(device=DEV).manual_seed(3)
-    p0 = tu.param.data.clone()
-    m0 = torch.rand(p0.shape, generator=g, device=DEV) * 1e-3
-    v0 = torch.rand(p0.shape, generator=g, device=DEV) * 1e-6
-    outs = []
-    for split in (False, True):
-        p, mm, vv = p0.clone(), m0.clone(), v0.clone()
-        kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, mm, vv, 1e-3, 0.9, 0.999, 0.05, 1e-8, split=split)
-        torch.cuda.synchronize()
-        outs.append((p, mm, vv))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-    assert not torch.equal(outs[1][0], p0)  # the step moved rows
-    # both parts honour the skip flag
-    skip = torch.ones(1, dtype=torch.int32, device=DEV)
-    p, mm, vv = p0.clone(), m0.clone(), v0.clone()
-    kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, mm, vv, 1e-3, 0.9, 0.999, 0.05, 1e-8, skip=skip,
-                             split=True)
-    torch.cuda.synchronize()
-    assert torch.equal(p, p0) and torch.equal(mm, m0) and torch.equal(vv, v0)
-    tu.discard()
-
-
 def test_fused_table_update_keeps_extra_table_gradient(pkg):
     """with fuse_table_update the CF backward defers the table's gradient, but
     another term of the loss (here an L2 penalty on the whole table) still writes .grad through
@@ -1937,13 +1861,16 @@ def test_lazy_kg_adam_bit_identical(pkg, dim):
         m.lazy_kg_adam = lazy
         models.append(m)
     rng = np.random.default_rng(4)
-    for phase in range(3):
+    for phase in range(4):
         ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.2), int(E * 0.2))]
         kgs = [[torch.from_numpy(rng.integers(0, hi, 48)).to(DEV) for hi in (n, R, n, n)] for _ in range(6)]
         for m in models:
             torch.manual_seed(50 + phase)
             m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            if phase == 3:  # the device skip flag set while a CF step is in flight
+                m._ids.skip_flag().fill_(1)
             m.update_cf_weights()
+            m._ids.skip_flag().zero_()
             for j, kg in enumerate(kgs):
                 if phase == 1 and j == 2:  # a device-side bad id: the step moves nothing
                     bad = kg[2].clone()
@@ -1954,10 +1881,19 @@ def test_lazy_kg_adam_bit_identical(pkg, dim):
                         m.update_kg_weights()
                     continue
                 m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
+                if phase >= 2 and j in (1, 4):
+                    # the skip flag set on the device while the step is in flight (the host has not seen it):
+                    # the lazy path's history entry (skip = 1) and the dense step move nothing alike, and
+                    # both advance Adam's step counter
+                    m._ids.skip_flag().fill_(1)
                 m.update_kg_weights()
+                m._ids.skip_flag().zero_()
             if phase == 2:
                 with torch.no_grad():
                     m(ids[0], ids[1], mode=pkg.KGATMode.PREDICT)
+                # a second build_optimizer mid-training: the lazy replays still owed under the old
+                # optimiser are applied first, and the new optimiser's steps restart every row at t = 0
+                m.build_optimizer(cf_lr=1e-3, kg_lr=2e-4)
     sa, sb = models[0].state_dict(), models[1].state_dict()
     for k in sa:
         if not sa[k].is_sparse:

@@ -165,6 +165,26 @@ def test_dp_replicated_exchange_wide_layer0_world2():
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_exchange_paths_c4_shape(world):
+    """C4's exact shape (d = 128, layers [128, 64, 32], configs[3]) through every
+    data-parallel exchange path of tests/dp_worker.py on `world` ranks sharing this GPU (gloo) -- the
+    3-layer sharded table exchange bench.py runs for C4 (row-block reduce-scatter, owned-row Adam,
+    all-gather), with and without the backward overlap (attach), and with frontier_forward + the fused
+    table update on (path H, bit-identical to C); replicas identical on every path, B / C bit-equal to
+    the all-reduce path A at world 2."""
+    env = dict(os.environ, DP_WORKER_DIMS="128:128,64,32")
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    log = ROOT / "gpurun_out" / f"dp_world{world}_c4shape.log"
+    log.parent.mkdir(exist_ok=True)
+    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert p.stdout.count(": OK") == world, p.stdout[-2000:]
+
+
 def test_rccl_world1_collectives_match_gloo():
     """every collective of replicas.py / sharded.py through RCCL (backend "nccl",
     world 1 on the box's GPU, forced) vs the gloo / no-exchange paths (tests/rccl_worker.py)."""
@@ -180,11 +200,13 @@ def test_rccl_world1_collectives_match_gloo():
     assert "rccl world1: OK" in p.stdout, p.stdout[-2000:]
 
 
-@pytest.mark.parametrize("dp,gpus", [("replicated", 2), ("sharded", 2), ("replicated", 4)])
-def test_bench_two_ranks_gloo_rehearsal(dp, gpus):
+@pytest.mark.parametrize("dp,gpus,config,scale", [("replicated", 2, "small", 0.2), ("sharded", 2, "small", 0.2),
+                                                  ("replicated", 4, "small", 0.2), ("sharded", 2, "c4", 0.01)])
+def test_bench_two_ranks_gloo_rehearsal(dp, gpus, config, scale):
     """bench.py --gpus 2 end to end (launch, process group, DP replicas with the table exchange, timing,
     max-over-ranks, one JSON line) with both ranks on this one GPU over gloo (KGAT_BENCH_BACKEND):
-    the N-rank path the driver's multi-GPU run takes, minus RCCL."""
+    the N-rank path the driver's multi-GPU run takes, minus RCCL -- also at C4's shape (d = 128,
+    [128, 64, 32], 1 % scale) with the sharded exchange and its frontier leg."""
     import json
     import subprocess
     import sys
@@ -192,7 +214,7 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus):
     env = dict(os.environ, KGAT_BENCH_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--config", "small", "--scale", "0.2",
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--config", config, "--scale", str(scale),
                         "--steps", "3", "--warmup", "1", "--dp", dp], cwd=ROOT, env=env, capture_output=True,
                        text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -202,6 +224,9 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus):
     assert rec["n_gpus"] == gpus and rec["config"]["parallelism"] == f"dp{gpus}" and rec["config"]["dp_exchange"] == dp
     assert rec["rehearsal"].startswith("gloo") and rec["value"] > 0 and np.isfinite(rec["final_loss"])
     assert sum(rec["dp_table_exchange_steps"].values()) == 4 if dp == "replicated" else True
-    if dp == "replicated":  # the frontier-forward leg (composes with the replicated exchange) ran too
-        fr = rec["frontier_forward"]
-        assert fr["bpr_pairs_per_s"] > 0 and sum(fr["dp_table_exchange_steps"].values()) == 4
+    fr = rec["frontier_forward"]  # the frontier-forward leg (composes with either exchange) ran too
+    assert fr["bpr_pairs_per_s"] > 0
+    if dp == "replicated":
+        assert sum(fr["dp_table_exchange_steps"].values()) == 4
+    if config == "c4":
+        assert rec["config"]["embed_dim"] == 128 and rec["config"]["layer_size"] == [128, 64, 32]

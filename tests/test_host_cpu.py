@@ -32,23 +32,21 @@ def test_header_symbols_are_bound_and_exported():
     assert b"invalid" in lib.kgat_strerror(1001)
 
 
-def test_masked_adam_part_rejects_bad_arguments():
-    """kgat_spmm_csr_masked_adam_part_f32 validates before it touches the device: a part outside 0..2, a
-    negative yc_row0 and a null table are refused with KGAT_ERR_INVALID (host-side checks only)."""
+def test_masked_adam_block_rejects_bad_arguments():
+    """kgat_spmm_csr_masked_adam_block_f32 validates before it touches the device: a negative yc_row0
+    and a null table are refused with KGAT_ERR_INVALID (host-side checks only)."""
     lib = _lib.lib()
     desc = _lib.CSR()
     fake = ctypes.c_void_p(16)  # never dereferenced: the argument checks fail first
-    args = dict(part=0, row0=0, p=fake)
+    args = dict(row0=0, p=fake)
 
     def call(**kw):
         a = {**args, **kw}
-        return lib.kgat_spmm_csr_masked_adam_part_f32(ctypes.byref(desc), fake, fake, 64, None, 0, a["row0"], None,
-                                                      a["p"], fake, fake, 64, 64, 1e-3, 0.9, 0.999, 1.0, 1e-8, None,
-                                                      a["part"], None, 0, None)
+        return lib.kgat_spmm_csr_masked_adam_block_f32(ctypes.byref(desc), fake, fake, 64, None, 0, a["row0"], None,
+                                                       a["p"], fake, fake, 64, 64, 1e-3, 0.9, 0.999, 1.0, 1e-8, None,
+                                                       None, 0, None)
     invalid = 1001
     assert b"invalid" in lib.kgat_strerror(invalid)
-    assert call(part=3) == invalid
-    assert call(part=-1) == invalid
     assert call(row0=-1) == invalid
     assert call(p=None) == invalid
 

@@ -101,3 +101,42 @@ def test_sharded_grad_sync_world2():
         assert p.exitcode == 0
     assert all(r[1] for r in res), res
     assert all(r[2] for r in res), res
+
+
+def _discard_worker(rank: int, world: int, port: str, q) -> None:
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
+    try:
+        pkg = load_pkg()
+        rep = __import__(pkg.__name__ + ".replicas", fromlist=["replicas"])
+        sync = rep.ShardedGradSync([], replicate_table=True)
+        out = []
+        for discarded in ((0, 0), (1, 1), (1, 2)):
+            sync.discarded = discarded[rank]
+            both = sync._gather_info(True, torch.tensor([10 + rank], dtype=torch.int32), "cpu")
+            try:
+                dev, host = sync._split_info(both, both.reshape(-1).tolist())
+                out.append((dev.tolist(), host))
+            except RuntimeError as e:
+                out.append(str(e)[:80])
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_announce_discards_compared_across_ranks():
+    """the replicated exchange's (hop count, discarded announcements) all-gather -- equal
+    discard counts pass the counts through in rank order; unequal ones (ranks whose control flow
+    diverged) raise instead of pairing up different steps' collectives."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _rendezvous()
+    procs = [ctx.Process(target=_discard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, out in res:
+        assert out[0] == ([10, 11], [10, 11]) and out[1] == ([10, 11], [10, 11]), out
+        assert isinstance(out[2], str) and "discarded different" in out[2], out

@@ -213,8 +213,6 @@ def fused_section(args, K, g, n, dev, rec):
             K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st)
 
         rec(f"spmm+biinter_fwd_{din}x{dout}", timeit(two, args.reps))
-        rec(f"spmm_biinter_fused_{din}x{dout}",
-            timeit(lambda: K.spmm_biinter_fwd(g, X, W1, b1, W2, b2, 0.1, 5, state=st), args.reps))
 
 
 def attention_section(args, K, lay, U, E, dev, rec):
