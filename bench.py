@@ -57,6 +57,11 @@ PKG = "problem-recommender-system-using-kgat-in-codeforces_amd"
 CONFIGS = {
     "c2": dict(nodes=1_000_000, triples=10_000_000, dim=64, layers=[64, 32], batch=256, mode="dp",
                workload="synthetic CKG 1M entities / 10M triples, embed_dim=64, 2 KGAT layers (BASELINE configs[1])"),
+    "c3": dict(users=5000, dim=128, layers=[128, 64, 32], batch=256, mode="dp", codeforces=True,
+               nfm=dict(embedding_dim=128, hidden_dim=[128, 64, 32], batch=1024, predict_users=64),
+               workload="synthetic full-shaped Codeforces (5,000 users, 9,500 problems, 1,913 contests, 37 tags, 28 "
+                        "ratings; driver.synthetic_codeforces, train split), embed_dim=128, 3 KGAT layers + NFM head "
+                        "(configs[2])"),
     "c4": dict(nodes=10_000_000, triples=100_000_000, dim=128, layers=[128, 64, 32], batch=256, mode="dp",
                workload="synthetic CKG 10M entities / 100M triples, embed_dim=128, 3 KGAT layers (configs[3])"),
     "c5": dict(nodes=50_000_000, triples=500_000_000, dim=256, layers=[256, 128, 64], batch=256, mode="sharded",
@@ -400,7 +405,17 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     replicas = importlib.import_module(PKG + ".replicas")
     t0 = time.perf_counter()
     log(f"generating the synthetic CKG ({cfg['workload']}) ...")
-    U, E, inter, trip = graph_mod.synthetic_ckg(cfg["nodes"], cfg["triples"], seed=2024)
+    ds = None
+    if cfg.get("codeforces"):
+        # C3: the Codeforces-shaped dataset driver.py trains on (no real data here), its train split
+        driver = importlib.import_module(PKG + ".driver")
+        ci, trip, E = driver.synthetic_codeforces(users=cfg["users"], seed=2024)
+        U = cfg["users"]
+        tr, va, te = driver.split_interactions(ci, U)
+        ds = driver.Dataset(U, E, 9500, tr, va, te, trip)
+        inter = tr
+    else:
+        U, E, inter, trip = graph_mod.synthetic_ckg(cfg["nodes"], cfg["triples"], seed=2024)
     log(f"  {time.perf_counter() - t0:.1f}s; building the layout ...")
     layout = graph_mod.build_layout(U, E, inter, trip)
     log(f"graph: N={layout.n_nodes} interactions={len(inter)} kg={len(trip)} nnz={layout.nnz} "
@@ -427,7 +442,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     su = inter[order]
     ustart = np.searchsorted(su[:, 0], np.arange(U + 1))
     have = np.nonzero(np.diff(ustart) > 0)[0]
-    n_items = max(1, int(E * 0.1))
+    n_items = ds.item_num if ds is not None else max(1, int(E * 0.1))
     batches = []
     for _ in range(args.warmup + args.steps):
         u = rng.choice(have, B, replace=len(have) < B)
@@ -436,8 +451,9 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                         for x in (u, su[k, 1], rng.integers(0, n_items, B))])
     params = [p for p in model.parameters() if not p.is_sparse and p.requires_grad]
     dp_mode = args.dp if args.dp != "auto" else ("replicated" if L <= 2 else "sharded")
-    sync = replicas.ShardedGradSync(params, replicate_table=dp_mode == "replicated",
-                                    force=args.exchange_at_1).attach(model)
+    # sharded mode: each owner's block Adam + broadcast pipelined inside the backward (ShardedGradSync.pipeline)
+    sync = replicas.ShardedGradSync(params, replicate_table=dp_mode == "replicated", force=args.exchange_at_1,
+                                    pipeline=dp_mode == "sharded").attach(model)
 
     def step(b):
         loss = model(*b, mode=pkg.KGATMode.TRAIN_CF)
@@ -504,8 +520,10 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     if world == 1 and not args.no_kg_leg and not args.exchange_at_1:
         cf_ms = result.get("frontier_forward", {}).get("ms_per_step", ms)
         result["kg_refresh"] = kg_refresh_legs(model, pkg, layout, cfg, args, dev, len(inter), cf_ms)
+    if ds is not None and cfg.get("nfm") and world == 1:
+        result["nfm"] = nfm_legs(ds, cfg, args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if cfg["nodes"] > 2_000_000:
+        if cfg.get("nodes", 0) > 2_000_000:
             log("timing the CPU baseline (oracle restatement on subsampled edge sets, extrapolated) ...")
             result["cpu_baseline"] = cpu_extrapolated(layout, cfg)
         else:
@@ -556,9 +574,11 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         return loss
 
     out = {"batch": B}
-    for tag, fused, lazy in (("lazy", True, True), ("fused", True, False), ("unfused", False, False)):
+    for tag, fused, lazy, cap in (("captured", True, True, True), ("lazy", True, True, False),
+                                  ("fused", True, False, False), ("unfused", False, False, False)):
         model.fuse_kg_table_update = fused
         model.lazy_kg_adam = lazy
+        model.capture_kg_step = cap
         for i in range(args.warmup):
             kg_step(batches[i])
         torch.cuda.synchronize()
@@ -576,6 +596,9 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         torch.cuda.synchronize()
         evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
         leg = {"ms_per_step": el, "kg_pairs_per_s": B / (el * 1e-3)}
+        if cap:
+            leg["graph_replays"] = model._kg_graph.replays
+            model.capture_kg_step = False
         if lazy:
             # the flush that brings every row current (before the next CF step): here after the leg's
             # warmup + 2 x steps KG steps, i.e. that many zero-gradient steps replayed for almost every row
@@ -647,7 +670,7 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         ref["row_softmax_GBps"] = by / (float(np.mean(t)) * 1e-3) / 1e9
     out["refresh"] = ref
     n_cf, n_kg = n_interactions // 256 + 1, E // 512 + 1
-    lz = out["lazy"]
+    lz = out["captured"]
     # a row's pending zero-gradient steps at the phase's end: ~ the steps since the batch last drew it
     # (n / 1,536 rows per step on average, at most the phase): the end-of-phase flush scales from the
     # measured one by that over its pending steps
@@ -661,8 +684,129 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         "seconds": (n_cf * cf_ms + kg_lazy_s + rms) / 1e3, "seconds_fused_kg_dense_adam": ep_fused / 1e3,
         "what": "one reference epoch (main.py:290-361: CF phase, KG phase, attention refresh; no evaluation) at the "
                 "measured per-step times, as driver.py trains: frontier-forward CF steps, KG steps with "
-                "KGAT.lazy_kg_adam (its end-of-phase flush included); seconds_fused_kg_dense_adam: the KG steps "
-                "with the whole-table Adam every step"}
+                "KGAT.lazy_kg_adam and KGAT.capture_kg_step (the step replayed as HIP graphs; its end-of-phase flush "
+                "included); seconds_eager_lazy_kg: the same KG steps launched eagerly; seconds_fused_kg_dense_adam: "
+                "the KG steps with the whole-table Adam every step"}
+    out["epoch_estimate"]["seconds_eager_lazy_kg"] = (n_cf * cf_ms + n_kg * out["lazy"]["ms_per_step"]
+                                                       + lz["epoch_flush_ms_estimate"] + rms) / 1e3
+    return out
+
+
+def nfm_legs(ds, cfg, args, dev) -> dict:
+    """C3's NFM head (src/model/NFM/main.py:281-301, model.py:73-129) on the same Codeforces-shaped data:
+    the train step (B pairs: positive and negative feature batches, loss, backward, Adam) and PREDICT on
+    the users x all items grid of NFM/preprocess.py:309-334, batches built on the device (NFMBatcher)
+    before timing.  Parity: loss, every gradient and a grid's scores vs oracle/kgat_cpu.py on the same
+    weights and rows.  Rooflines: the PREDICT kernel (nfm_fwd: feature pooling + MLP + heads) against the
+    fp32 MFMA peak (2 sum d_l d_(l+1) flop per row) and against HBM (k (4d + 8) + 4d bytes per
+    row at k gathered features).  CPU baseline: the oracle's train step and PREDICT."""
+    pkg = importlib.import_module(PKG)
+    from oracle import kgat_cpu as K
+
+    nc = cfg["nfm"]
+    B, d, hidden = nc["batch"], nc["embedding_dim"], nc["hidden_dim"]
+    U, I, E = ds.user_num, ds.item_num, ds.entity_num
+    trip = ds.triplets
+    fh, ft = trip[trip[:, 0] < I, 0], trip[trip[:, 0] < I, 2]  # problem-headed triplets (NFM/preprocess.py:166)
+    batcher = pkg.NFMBatcher(U, I, E, fh, ft, ds.interaction_dict("train"), dev, train_batch_size=B, seed=2024)
+    torch.manual_seed(2024)
+    model = pkg.NFM(pkg.NFMArgs(user_num=U, item_num=I, entity_num=E, embedding_dim=d, hidden_dim=hidden,
+                                message_dropout=[0.1] * len(hidden))).to(dev)
+    model.build_optimizer(lr=1e-4)  # NFM/main.py:33-38
+    model.train()
+    train = [batcher.generate_train_batch() for _ in range(args.warmup + args.steps)]
+    users = list(range(nc["predict_users"]))
+    grid = batcher.generate_test_batch(users)
+    rows = grid.shape[0]
+    nnz_grid = int(grid.rowptr[-1].item())
+
+    def step(b):
+        loss = model(b[0], b[1], mode=pkg.NFMMode.TRAIN)
+        loss.backward()
+        model.update_weights()
+        return loss
+
+    for b in train[:args.warmup]:
+        step(b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in train[args.warmup:]:
+        loss = step(b)
+    torch.cuda.synchronize()
+    tr_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    model.eval()
+    with torch.no_grad():
+        model(grid, mode=pkg.NFMMode.PREDICT)  # warm-up
+        torch.cuda.synchronize()
+        reps = 10
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            model(grid, mode=pkg.NFMMode.PREDICT)
+        e1.record()
+        torch.cuda.synchronize()
+    pr_ms = e0.elapsed_time(e1) / reps
+    dims = [d, *hidden]
+    flops_row = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:])) + 2 * dims[-1]
+    k_row = nnz_grid / rows
+    bytes_row = k_row * (4 * d + 8) + 4 * d
+    out = {"config": {"embedding_dim": d, "hidden_dim": hidden, "train_batch": B, "users": U, "items": I,
+                      "features": U + E, "predict_rows": rows, "predict_users": len(users),
+                      "features_per_row": k_row},
+           "train": {"ms_per_step": tr_ms, "pairs_per_s": B / (tr_ms * 1e-3), "final_loss": float(loss.item()),
+                     "what": "NFM TRAIN step (pos + neg batches of B rows, loss, backward, Adam; dropout 0.1), "
+                             "batches pre-built on the device"},
+           "predict": {"ms_per_call": pr_ms, "rows_per_s": rows / (pr_ms * 1e-3),
+                       "roofline": {"kernel": "nfm_fwd_kernel (pooling + MLP + heads)", "bound": "mfma",
+                                    "flops_per_row": flops_row, "achieved": flops_row * rows / (pr_ms * 1e-3) / 1e12,
+                                    "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                    "frac": flops_row * rows / (pr_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFS,
+                                    "hbm_bytes_per_row": bytes_row,
+                                    "hbm_frac": bytes_row * rows / (pr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "note": "the call's HIP-event time (one kernel launch + its output allocation); "
+                                            "the feature table (%.0f MB) is L2 / Infinity-Cache resident, so the gather "
+                                            "bytes are an upper bound on HBM traffic" % ((U + E) * d * 4 / 1e6)}}}
+    # parity: the timed model's weights, one train batch (eval mode: dropout off) and 4 users' grid rows
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.named_parameters()}
+    xp, xn = (x.to_sparse_coo().cpu() for x in train[0])
+    ref = K.nfm_loss(params, xp, xn, lam=1e-5)
+    ref.backward()
+    model.zero_grad(set_to_none=True)
+    got = model(train[0][0], train[0][1], mode=pkg.NFMMode.TRAIN)
+    got.backward()
+    gerr = max(float((p.grad.cpu() - params[k].grad).abs().max()) for k, p in model.named_parameters())
+    gscale = max(float(params[k].grad.abs().max()) for k in params)
+    small = batcher.generate_test_batch(users[:4])
+    with torch.no_grad():
+        sc = model(small, mode=pkg.NFMMode.PREDICT).cpu()
+        want = K.nfm_score({k: v.detach() for k, v in params.items()}, small.to_sparse_coo().cpu())
+    serr = float((sc - want).abs().max())
+    lrel = abs(float(got) - float(ref)) / max(abs(float(ref)), 1e-30)
+    model.zero_grad(set_to_none=True)
+    out["parity"] = {"loss_rel": lrel, "max_abs_grad": gerr, "max_abs_grad_ref": gscale, "max_abs_score": serr,
+                     "tolerance": {"loss_rel": 1e-4, "grad_rel_to_max": 1e-4, "score": 1e-4},
+                     "pass": bool(lrel <= 1e-4 and gerr <= 1e-4 * max(gscale, 1e-30) + 1e-7 and serr <= 1e-4),
+                     "what": "eval-mode NFM loss + every gradient on one B-pair train batch and PREDICT scores of 4 "
+                             "users x all items vs oracle/kgat_cpu.py (nfm_loss / nfm_score) on the timed weights"}
+    if not args.no_cpu_baseline:
+        torch.set_num_threads(min(64, os.cpu_count() or 1))
+        ts = []
+        for b in train[:3]:
+            xp, xn = (x.to_sparse_coo().cpu() for x in b)
+            pc = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+            t1 = time.perf_counter()
+            K.nfm_loss(pc, xp, xn).backward()
+            ts.append(time.perf_counter() - t1)
+        gx = grid.to_sparse_coo().cpu()
+        t1 = time.perf_counter()
+        with torch.no_grad():
+            K.nfm_score({k: v.detach() for k, v in params.items()}, gx)
+        pcpu = time.perf_counter() - t1
+        out["cpu_baseline"] = {"train_ms_per_step": float(np.median(ts)) * 1e3, "predict_ms_per_call": pcpu * 1e3,
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": "oracle/kgat_cpu.py nfm_loss + backward on 3 of the timed train batches "
+                                         "(median; no optimiser step) and nfm_score on the timed PREDICT grid"}
+    model.train()
     return out
 
 
@@ -885,7 +1029,10 @@ def main() -> int:
     global EVENT_EVERY
     EVENT_EVERY = max(1, args.event_every)
     cfg = dict(CONFIGS[args.config])
-    if args.scale != 1.0:
+    if args.scale != 1.0 and cfg.get("codeforces"):
+        cfg["users"] = max(100, int(cfg["users"] * args.scale))
+        cfg["workload"] += f" scaled x{args.scale:g} ({cfg['users']:,} users)"
+    elif args.scale != 1.0:
         cfg["nodes"] = max(1000, int(cfg["nodes"] * args.scale))
         cfg["triples"] = max(5000, int(cfg["triples"] * args.scale))
         cfg["workload"] += f" scaled x{args.scale:g} ({cfg['nodes']:,} nodes / {cfg['triples']:,} triples)"

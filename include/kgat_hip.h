@@ -623,6 +623,28 @@ int kgat_adam_lazy_rows_f32(float *p, float *m, float *v, int32_t d, const int32
                             int32_t *hist_skip, int32_t cap, float step_size, float beta1, float beta2,
                             float bc2_sqrt, float eps, const int32_t *skip, void *stream);
 
+/* The KG step captured as a HIP graph (KGAT.capture_kg_step; main.py:324-345, model.py:204-261,
+ * 414-419): a graph replays the kernel arguments it was captured with, so a step's scalars live on
+ * the device.  t_dev (int32 [1]) holds the optimiser's step number: kgat_step_advance adds 1 (the
+ * graph's first update node); the _sched variants read t = *t_dev and the step's size and
+ * sqrt(1 - beta2^t) from the schedule tables sched_sz[t] / sched_bc[t] (float, > t entries, filled by
+ * the host with the by-value launches' own float values: lr / (1 - beta1^t), sqrt(1 - beta2^t)).
+ * Otherwise each is kgat_adam_multi_ex_f32 (every tensor at step t), kgat_adam_lazy_catchup_f32 and
+ * kgat_adam_lazy_rows_f32, bit for bit. */
+int kgat_step_advance(int32_t *t_dev, void *stream);
+int kgat_adam_multi_sched_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
+                              const int32_t *skip, const int32_t *t_dev, const float *sched_sz, const float *sched_bc,
+                              void *stream);
+int kgat_adam_lazy_catchup_sched_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *rows,
+                                     int64_t n_list, int32_t *last, const int32_t *t_dev, float *hist_sz,
+                                     float *hist_bc, int32_t *hist_skip, int32_t cap, float beta1, float beta2,
+                                     float eps, void *stream);
+int kgat_adam_lazy_rows_sched_f32(float *p, float *m, float *v, int32_t d, const int32_t *rows, int64_t n_list,
+                                  const float *Gc, int64_t ldg, int32_t *last, float *hist_sz, float *hist_bc,
+                                  int32_t *hist_skip, int32_t cap, const int32_t *t_dev, const float *sched_sz,
+                                  const float *sched_bc, float beta1, float beta2, float eps, const int32_t *skip,
+                                  void *stream);
+
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);
 

@@ -112,6 +112,20 @@ extern "C" int kgat_version(void) { return 1; }
 
 namespace kgat {
 
+// A captured optimiser step's scalars on the device (a HIP graph replays the same kernel arguments every
+// step): t = *t (advanced by kgat_step_advance inside the graph), step size and sqrt(1 - beta2^t) =
+// sz[t] / bc[t] -- tables the host filled with FusedAdam's own expressions, so the same floats the
+// by-value launches get.  t == nullptr: the by-value arguments.
+struct StepSched {
+  const int32_t* t;
+  const float* sz;
+  const float* bc;
+};
+
+__global__ void step_advance_kernel(int32_t* __restrict__ t) {
+  if (threadIdx.x == 0) t[0] = t[0] + 1;
+}
+
 // Every tensor of one optimiser step in ONE launch: the tensor table travels in
 // the kernel arguments; block b works on chunk b of the concatenated float4
 // index space (tensor chosen by a scan of <= 16 chunk offsets).
@@ -142,16 +156,20 @@ __device__ __forceinline__ void st4(float* p, float4 v) {
 // non-temporal loads/stores (every byte is touched once per step).
 template <int V>
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps,
-                                                         const int32_t* __restrict__ skip) {
+                                                         const int32_t* __restrict__ skip, StepSched sched) {
   if (skip != nullptr && *skip != 0) return;  // the step's ids were out of range: no parameter moves
   const float w1 = 1.f - b1, w2 = 1.f - b2;
+  // a captured step (kgat_adam_multi_sched_f32): every tensor's step size and bias correction are step t's
+  // entries of the host-computed schedule, t read on the device
+  const int32_t ts = sched.t != nullptr ? *sched.t : 0;
   const int64_t total = T.chunk_off[T.count];
   for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
     int i = 0;
     while (i + 1 < T.count && T.chunk_off[i + 1] <= c) ++i;
     const kgat_adam_tensor& a = T.t[i];
     const int64_t base = (c - T.chunk_off[i]) * kAdamChunk;
-    const float step_size = a.step_size, bc2s = a.bc2_sqrt;
+    const float step_size = sched.t != nullptr ? sched.sz[ts] : a.step_size;
+    const float bc2s = sched.t != nullptr ? sched.bc[ts] : a.bc2_sqrt;
     if (V >= 1 && base + kAdamChunk <= a.n) {
       float4 pp[4], mm[4], vv[4], gg[4];
 #pragma unroll
@@ -264,7 +282,15 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
 
 extern "C" int kgat_adam_multi_ex_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
                                       float eps, const int32_t* skip, void* stream) {
+  return kgat_adam_multi_sched_f32(tensors, count, beta1, beta2, eps, skip, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int kgat_adam_multi_sched_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
+                                         float eps, const int32_t* skip, const int32_t* t_dev, const float* sched_sz,
+                                         const float* sched_bc, void* stream) {
   if (!tensors || count < 1 || count > KGAT_ADAM_MAX_TENSORS) return KGAT_ERR_INVALID;
+  if (t_dev != nullptr && (!sched_sz || !sched_bc)) return KGAT_ERR_INVALID;
+  const kgat::StepSched sched{t_dev, sched_sz, sched_bc};
   kgat::AdamTable T{};
   T.count = count;
   int64_t off = 0;
@@ -283,7 +309,7 @@ extern "C" int kgat_adam_multi_ex_f32(const kgat_adam_tensor* tensors, int32_t c
   const int grid = static_cast<int>(off < kgat::kCUs * 8 ? off : kgat::kCUs * 8);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // the <2> access pattern: C2 table (64M parameters) 314 us vs 346 us for <0> / <1> on the same box
-  hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip);
+  hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip, sched);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -335,7 +361,8 @@ __global__ __launch_bounds__(256) void adam_lazy_catchup_kernel(float* __restric
                                                                 float* __restrict__ v, int d,
                                                                 const int32_t* __restrict__ rows, int64_t n_list,
                                                                 int32_t* __restrict__ last, int32_t t, LazyHist h,
-                                                                float b1, float b2, float eps) {
+                                                                float b1, float b2, float eps, StepSched sched) {
+  if (sched.t != nullptr) t = *sched.t;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const int64_t k = i / d;
   const int c = static_cast<int>(i % d);
@@ -361,7 +388,13 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
                                                              const float* __restrict__ Gc, int64_t ldg,
                                                              int32_t* __restrict__ last, int32_t t, LazyHist h,
                                                              float step_size, float b1, float b2, float bc2s,
-                                                             float eps, const int32_t* __restrict__ skip) {
+                                                             float eps, const int32_t* __restrict__ skip,
+                                                             StepSched sched) {
+  if (sched.t != nullptr) {
+    t = *sched.t;
+    step_size = sched.sz[t];
+    bc2s = sched.bc[t];
+  }
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const bool skipped = skip != nullptr && *skip != 0;
   if (i == 0) {
@@ -395,10 +428,9 @@ static bool lazy_args_ok(const float* p, const float* m, const float* v, int32_t
   return p && m && v && last && hsz && hbc && hskip && cap > 0 && d > 0 && d <= 256 && (256 % d) == 0;
 }
 
-extern "C" int kgat_adam_lazy_catchup_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
-                                          const int32_t* rows, int64_t n_list, int32_t* last, int32_t t,
-                                          float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
-                                          float beta1, float beta2, float eps, void* stream) {
+static int lazy_catchup(float* p, float* m, float* v, int64_t n_rows, int32_t d, const int32_t* rows, int64_t n_list,
+                        int32_t* last, int32_t t, const int32_t* t_dev, float* hist_sz, float* hist_bc,
+                        int32_t* hist_skip, int32_t cap, float beta1, float beta2, float eps, void* stream) {
   if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || n_rows < 0 || n_list < 0 || t < 0)
     return KGAT_ERR_INVALID;
   const int64_t n = rows != nullptr ? n_list : n_rows;
@@ -407,7 +439,40 @@ extern "C" int kgat_adam_lazy_catchup_f32(float* p, float* m, float* v, int64_t 
   if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(kgat::adam_lazy_catchup_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      p, m, v, d, rows, n, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap}, beta1, beta2,
-                     eps);
+                     eps, kgat::StepSched{t_dev, nullptr, nullptr});
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_adam_lazy_catchup_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
+                                          const int32_t* rows, int64_t n_list, int32_t* last, int32_t t,
+                                          float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
+                                          float beta1, float beta2, float eps, void* stream) {
+  return lazy_catchup(p, m, v, n_rows, d, rows, n_list, last, t, nullptr, hist_sz, hist_bc, hist_skip, cap, beta1,
+                      beta2, eps, stream);
+}
+
+extern "C" int kgat_adam_lazy_catchup_sched_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d,
+                                                const int32_t* rows, int64_t n_list, int32_t* last,
+                                                const int32_t* t_dev, float* hist_sz, float* hist_bc,
+                                                int32_t* hist_skip, int32_t cap, float beta1, float beta2, float eps,
+                                                void* stream) {
+  if (!t_dev) return KGAT_ERR_INVALID;
+  return lazy_catchup(p, m, v, n_rows, d, rows, n_list, last, 0, t_dev, hist_sz, hist_bc, hist_skip, cap, beta1,
+                      beta2, eps, stream);
+}
+
+static int lazy_rows(float* p, float* m, float* v, int32_t d, const int32_t* rows, int64_t n_list, const float* Gc,
+                     int64_t ldg, int32_t* last, int32_t t, float* hist_sz, float* hist_bc, int32_t* hist_skip,
+                     int32_t cap, float step_size, float beta1, float beta2, float bc2_sqrt, float eps,
+                     const int32_t* skip, kgat::StepSched sched, void* stream) {
+  if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || !rows || !Gc || n_list < 0 || ldg < d ||
+      (sched.t == nullptr && t < 1))
+    return KGAT_ERR_INVALID;
+  const int64_t blocks = (std::max<int64_t>(n_list, 1) * d + 255) / 256;  // >= 1 block: the history entry
+  hipLaunchKernelGGL(kgat::adam_lazy_rows_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     p, m, v, d, rows, n_list, Gc, ldg, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap},
+                     step_size, beta1, beta2, bc2_sqrt, eps, skip, sched);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -417,13 +482,23 @@ extern "C" int kgat_adam_lazy_rows_f32(float* p, float* m, float* v, int32_t d, 
                                        float* hist_bc, int32_t* hist_skip, int32_t cap, float step_size,
                                        float beta1, float beta2, float bc2_sqrt, float eps, const int32_t* skip,
                                        void* stream) {
-  if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || !rows || !Gc || n_list < 0 || ldg < d ||
-      t < 1)
-    return KGAT_ERR_INVALID;
-  const int64_t blocks = (std::max<int64_t>(n_list, 1) * d + 255) / 256;  // >= 1 block: the history entry
-  hipLaunchKernelGGL(kgat::adam_lazy_rows_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     p, m, v, d, rows, n_list, Gc, ldg, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap},
-                     step_size, beta1, beta2, bc2_sqrt, eps, skip);
+  return lazy_rows(p, m, v, d, rows, n_list, Gc, ldg, last, t, hist_sz, hist_bc, hist_skip, cap, step_size, beta1,
+                   beta2, bc2_sqrt, eps, skip, kgat::StepSched{nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int kgat_adam_lazy_rows_sched_f32(float* p, float* m, float* v, int32_t d, const int32_t* rows,
+                                             int64_t n_list, const float* Gc, int64_t ldg, int32_t* last,
+                                             float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
+                                             const int32_t* t_dev, const float* sched_sz, const float* sched_bc,
+                                             float beta1, float beta2, float eps, const int32_t* skip, void* stream) {
+  if (!t_dev || !sched_sz || !sched_bc) return KGAT_ERR_INVALID;
+  return lazy_rows(p, m, v, d, rows, n_list, Gc, ldg, last, 0, hist_sz, hist_bc, hist_skip, cap, 0.f, beta1, beta2,
+                   0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc}, stream);
+}
+
+extern "C" int kgat_step_advance(int32_t* t, void* stream) {
+  if (!t) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::step_advance_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), t);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -16,6 +16,7 @@ from enum import IntEnum
 from typing import Any
 
 import ctypes
+import math
 
 import numpy as np
 import torch
@@ -153,10 +154,11 @@ class _IdGuard:
             raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed, "
                              f"and no optimiser step after it moved a parameter)")
 
-    def check(self, what: str, ids, bound: int, device, more=()) -> list[torch.Tensor]:
+    def check(self, what: str, ids, bound: int, device, more=(), outs=None) -> list[torch.Tensor]:
         """int64 device copies of ``ids`` (each as given, flattened), validated against [0, bound);
         ``more`` = further (ids, bound) groups of the same call, checked under the same flag so a
-        call raises (for an earlier call's device ids) at most once, before it runs."""
+        call raises (for an earlier call's device ids) at most once, before it runs.  ``outs``: one
+        preallocated int64 buffer per group (device ids; a captured step's static inputs)."""
         self.raise_pending()
         groups = [(list(ids), int(bound))] + [(list(i), int(b)) for i, b in more]
         flat = [torch.as_tensor(t) for g, _ in groups for t in g]
@@ -172,11 +174,16 @@ class _IdGuard:
             self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._event = torch.cuda.Event()
             self._dev = torch.zeros(1, dtype=torch.int32, device=device)
-        outs = []
-        for g, b in groups:
+        given, outs = outs, []
+        for gi, (g, b) in enumerate(groups):
             src = [torch.as_tensor(t).to(device).long().reshape(-1).contiguous() for t in g]
             sizes = [t.numel() for t in src]
-            out = torch.empty(max(sum(sizes), 1), dtype=torch.int64, device=device)
+            if given is not None:
+                out = given[gi]
+                if out.dtype != torch.int64 or not out.is_contiguous() or out.numel() < sum(sizes):
+                    raise ValueError("id check: preallocated buffer too small")
+            else:
+                out = torch.empty(max(sum(sizes), 1), dtype=torch.int64, device=device)
             for i in range(0, len(src), _lib.KGAT_IDS_MAX):
                 part = src[i:i + _lib.KGAT_IDS_MAX]
                 d = _lib.Ids()
@@ -412,6 +419,236 @@ class _LazyKGAdam:
         slots a replay still needs would be overwritten."""
         self.last = None
         self.dirty = False
+
+
+class _KGStepGraph:
+    """The KG step captured as three HIP graphs (opt-in: ``KGAT.capture_kg_step``; with the fused KG
+    table update and the lazy KG Adam, as driver.py trains).
+
+    The reference KG step is ``loss = model(h, r, t+, t-, mode=TRAIN_KG); loss.backward();
+    model.update_kg_weights()`` (main.py:334-342; model.py:204-261, 414-419).  Eagerly that is ~10
+    launches wrapped in ~0.2 ms of Python, ctypes and autograd work for ~0.12 ms of kernels at C2.
+    Here each of the three calls replays one graph captured once per shape:
+      forward  -- frontier_build (the batch rows' map), the lazy Adam catch-up of those rows, TransR
+                  forward (loss + the backward's work buffer);
+      backward -- TransR backward: the table gradient's compact rows, d_rel, d_trans;
+      update   -- kgat_step_advance (the device step counter), the lazy table Adam on the batch rows,
+                  the Adam of the relation embeddings and trans matrices, frontier_reset.
+    Only the id check (2 launches copying the caller's ids into the graphs' static buffers) and the
+    loss copy run outside.  A graph replays its captured kernel arguments, so the step's scalars live
+    on the device: t_dev (advanced by the update graph) indexes schedule tables of the step size and
+    sqrt(1 - beta2^t) that the host fills with FusedAdam's own expressions -- the same floats the eager
+    launches get -- and the host keeps the optimiser's step counters in step.  The gradients of the
+    three parameters stay in the graph's buffers between backward and update (``.grad`` stays None, as
+    with the fused table updates); anything that needs them materialises them.  Same bits as the
+    eager step (tests/test_gpu_parity.py::test_captured_kg_step_bit_identical)."""
+
+    SCHED = 1 << 16  # initial schedule entries (steps); doubled (and the graphs recaptured) when t reaches them
+
+    def __init__(self, model: "KGAT"):
+        self.model = model
+        self.enabled = False
+        self.key = None
+        self.g = None       # (forward, backward, update) graphs
+        self.buf = None     # static tensors of the captured step
+        self.pending = None  # "fwd" after a forward replay, "bwd" after a backward replay
+        self.t_dev_value = None  # the host's view of t_dev
+        self._sched = None  # (key, sz, bc)
+        self.replays = 0
+
+    # ---------------------------------------------------------------- eligibility
+    def _states(self, opt):
+        m = self.model
+        ps = (m._user_entity_embedding.weight, m._relation_embedding.weight, m._trans_matrix)
+        sts = [opt.state.get(id(p)) for p in ps]
+        return ps, sts
+
+    def usable(self, ids, opt) -> bool:
+        m = self.model
+        if not (self.enabled and m._kg_table_update.enabled and m._lazy_kg.enabled and opt is not None):
+            return False
+        B = ids[0].numel()
+        if B == 0 or not all(torch.is_tensor(t) and t.is_cuda and t.numel() == B for t in ids):
+            return False
+        if not m._kg_table_update.wants(B) or m._lazy_kg.last is None or m._ids.skip_flag() is None:
+            return False
+        ps, sts = self._states(opt)
+        if any(st is None for st in sts) or len({int(st["step"]) for st in sts}) != 1:
+            return False  # the first KG step (and a state restored out of step) runs eagerly
+        return not any(p.grad is not None for p in ps)
+
+    # ---------------------------------------------------------------- schedule + capture
+    def _schedule(self, opt, dev, need: int):
+        """Device tables of step t's step size and sqrt(1 - beta2^t) for t < len >= need."""
+        key = (id(opt), opt.lr, opt.beta1, opt.beta2, str(dev))
+        if self._sched is None or self._sched[0] != key or self._sched[1].numel() < need:
+            size = self.SCHED
+            while size < need:
+                size *= 2
+            # FusedAdam._advance's expressions, evaluated per t in Python floats, then rounded to float32 as
+            # ctypes rounds the by-value arguments
+            lr, b1, b2 = opt.lr, opt.beta1, opt.beta2
+            sz = np.array([0.0] + [lr / (1.0 - b1 ** t) for t in range(1, size)], dtype=np.float32)
+            bc = np.array([0.0] + [math.sqrt(1.0 - b2 ** t) for t in range(1, size)], dtype=np.float32)
+            self._sched = (key, torch.from_numpy(sz).to(dev), torch.from_numpy(bc).to(dev))
+        return self._sched[1], self._sched[2]
+
+    def _key(self, B, opt):
+        m = self.model
+        ps, sts = self._states(opt)
+        lz = m._lazy_kg
+        return (B, id(opt), opt.beta1, opt.beta2, opt.eps, float(m._regularization_params[1]),
+                self._sched[1].data_ptr(), self._sched[2].data_ptr(),
+                *(p.data_ptr() for p in ps), *(st[k].data_ptr() for st in sts for k in ("exp_avg", "exp_avg_sq")),
+                lz.last.data_ptr(), *(h.data_ptr() for h in lz.hist), m._kg_table_update.node_map().data_ptr(),
+                m._ids.skip_flag().data_ptr())
+
+    def _capture(self, B, opt):
+        m = self.model
+        dev = m._user_entity_embedding.weight.device
+        sz, bc = self._sched[1], self._sched[2]
+        ps, sts = self._states(opt)
+        emb, rel, trans = (p.data for p in ps)
+        lz = m._lazy_kg
+        hs, hb, hk = lz.hist
+        row_map = m._kg_table_update.node_map()
+        skip = m._ids.skip_flag()
+        n, d = emb.shape
+        n_rel, k = rel.shape
+        reg = float(m._regularization_params[1])
+        b = {"hpq": torch.zeros(3 * B, dtype=torch.int64, device=dev),
+             "rels": torch.zeros(B, dtype=torch.int64, device=dev),
+             "gout": torch.ones(1, dtype=torch.float32, device=dev),
+             "t": torch.zeros(1, dtype=torch.int32, device=dev)}
+        h, p, q = b["hpq"][:B], b["hpq"][B:2 * B], b["hpq"][2 * B:]
+        r = b["rels"]
+        ev = (kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS)
+        kernels.KERNEL_EVENTS = kernels.SPMM_EVENTS = None  # no event records inside a capture
+        pool = torch.cuda.graph_pool_handle()
+        g = [torch.cuda.CUDAGraph() for _ in range(3)]
+        try:
+            torch.cuda.synchronize(dev)
+            with torch.cuda.graph(g[0], pool=pool):
+                rows, _ = kernels.frontier_build(h, p, q, row_map)
+                st_ = stream_ptr(dev)
+                _lib.call("kgat_adam_lazy_catchup_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
+                          sts[0]["exp_avg_sq"].data_ptr(), n, d, rows.data_ptr(), rows.numel(), lz.last.data_ptr(),
+                          b["t"].data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP, opt.beta1, opt.beta2,
+                          opt.eps, st_)
+                loss, work = kernels.transr_fwd(emb, rel, trans, h, r, p, q, reg)
+            with torch.cuda.graph(g[1], pool=pool):
+                Gc, d_rel, d_trans = kernels.transr_bwd_compact(emb, n_rel, k, h, r, p, q, work, b["gout"], row_map,
+                                                                rows.numel())
+            with torch.cuda.graph(g[2], pool=pool):
+                st_ = stream_ptr(dev)
+                _lib.call("kgat_step_advance", b["t"].data_ptr(), st_)
+                _lib.call("kgat_adam_lazy_rows_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
+                          sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
+                          Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,
+                          b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), opt.beta1, opt.beta2, opt.eps,
+                          skip.data_ptr(), st_)
+                arr = (_lib.AdamTensor * 2)()
+                for a, (pp, gg, stt) in zip(arr, ((rel, d_rel, sts[1]), (trans, d_trans, sts[2]))):
+                    a.p, a.g, a.m, a.v = pp.data_ptr(), gg.data_ptr(), stt["exp_avg"].data_ptr(), stt["exp_avg_sq"].data_ptr()
+                    a.n, a.step_size, a.bc2_sqrt = pp.numel(), 0.0, 0.0
+                _lib.call("kgat_adam_multi_sched_f32", arr, 2, opt.beta1, opt.beta2, opt.eps, skip.data_ptr(),
+                          b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), st_)
+                kernels.frontier_reset(rows, row_map)
+        finally:
+            kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS = ev
+        b.update(rows=rows, loss=loss, work=work, Gc=Gc, d_rel=d_rel, d_trans=d_trans)
+        self.g, self.buf = g, b
+        self.t_dev_value = None
+        self.key = self._key(B, opt)
+
+    # ---------------------------------------------------------------- the three calls
+    def forward(self, ids, opt) -> torch.Tensor:
+        """Replay the forward graph on the caller's ids (heads, relations, positive, negative tails)."""
+        m = self.model
+        B = ids[0].numel()
+        t = int(self._states(opt)[1][0]["step"])
+        self._schedule(opt, m._user_entity_embedding.weight.device, t + 2)
+        if self.key != self._key(B, opt):
+            self._capture(B, opt)
+        b = self.buf
+        dev = b["t"].device
+        n = m._user_num + m._entity_num
+        m._ids.check("TRAIN_KG ids", (ids[0], ids[2], ids[3]), n, dev, more=[((ids[1],), m._relation_num)],
+                     outs=(b["hpq"], b["rels"]))
+        if self.t_dev_value != t:
+            b["t"].fill_(t)  # eager steps ran since the last replay
+            self.t_dev_value = t
+        self.g[0].replay()
+        self.pending = "fwd"
+        self.replays += 1
+        return b["loss"]
+
+    def backward(self, gout: torch.Tensor) -> None:
+        if self.pending != "fwd":
+            raise RuntimeError("TRAIN_KG backward: the captured step's forward buffers were reused by a later "
+                               "TRAIN_KG forward before this backward ran")
+        self.buf["gout"].copy_(gout.reshape(1))
+        self.g[1].replay()
+        self.pending = "bwd"
+
+    def update(self, opt) -> None:
+        """The update graph: the host advances the three optimiser states' step counters as FusedAdam does."""
+        m = self.model
+        lz = m._lazy_kg
+        if lz._t(opt) + 1 - lz.flushed_at >= lz.CAP:
+            lz.catch_up(opt)  # no row may fall a whole history behind
+        ps, _ = self._states(opt)
+        for p in ps:
+            opt._advance(id(p), p.data)
+        lz.dirty = True
+        self.g[2].replay()
+        self.t_dev_value = int(self._states(opt)[1][0]["step"])
+        self.pending = None
+
+    def release(self) -> None:
+        """A forward whose backward never ran (or a step abandoned after it): the batch rows' map is reset."""
+        if self.pending is not None:
+            kernels.frontier_reset(self.buf["rows"], self.model._kg_table_update.node_map())
+            self.pending = None
+
+    @torch.no_grad()
+    def materialize(self) -> None:
+        """The pending step's gradients into ``.grad`` (the table: its compact rows scattered into a zero
+        [N, d] gradient, as the fused KG update's materialisation); the map is reset."""
+        if self.pending == "fwd":
+            self.release()
+            return
+        if self.pending != "bwd":
+            return
+        m = self.model
+        b = self.buf
+        emb = m._user_entity_embedding.weight
+        g = kernels.zeros(tuple(emb.shape), emb.device)
+        kernels.scatter_rows(g, b["rows"], b["Gc"][:b["rows"].numel()], accumulate=False)
+        for p, gg in ((emb, g), (m._relation_embedding.weight, b["d_rel"].clone()),
+                      (m._trans_matrix, b["d_trans"].clone())):
+            if p.grad is None:
+                p.grad = gg
+            else:
+                kernels.add_(p.grad, gg)
+        self.release()
+
+
+class _KGGraphLoss(torch.autograd.Function):
+    """The captured KG step's loss node: forward replays the forward graph (its loss copied out, so a
+    kept loss survives the next step), backward replays the backward graph (gradients stay in the
+    graph's buffers for the update graph)."""
+
+    @staticmethod
+    def forward(ctx, step, ids, opt, emb, rel_emb, trans):
+        ctx.step = step
+        return step.forward(ids, opt).clone().view(())
+
+    @staticmethod
+    def backward(ctx, gout):
+        ctx.step.backward(gout.to(torch.float32))
+        ctx.step = None
+        return None, None, None, None, None, None
 
 
 class _MarkedBatch:
@@ -793,6 +1030,7 @@ class KGAT(nn.Module):
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
         self._kg_table_update = _KGTableUpdate(self._user_entity_embedding.weight)
         self._lazy_kg = _LazyKGAdam(self._user_entity_embedding.weight)
+        self._kg_graph = _KGStepGraph(self)
         # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
         # (_frontier_forward) -- same loss, gradients and updates, bit for bit
         self.frontier_forward = False
@@ -853,6 +1091,20 @@ class KGAT(nn.Module):
         """Write a deferred table gradient (CF or KG step) into ``_user_entity_embedding.weight.grad``."""
         self._table_update.materialize()
         self._kg_table_update.materialize()
+        self._kg_graph.materialize()
+
+    @property
+    def capture_kg_step(self) -> bool:
+        """Opt-in (with ``fuse_kg_table_update`` and ``lazy_kg_adam``): TRAIN_KG's forward, its backward and
+        ``update_kg_weights`` each replay one captured HIP graph (_KGStepGraph; same bits)."""
+        return self._kg_graph.enabled
+
+    @capture_kg_step.setter
+    def capture_kg_step(self, on: bool) -> None:
+        if not on:
+            self._kg_graph.materialize()
+            self._kg_graph.g = self._kg_graph.buf = self._kg_graph.key = None
+        self._kg_graph.enabled = bool(on)
 
     # ------------------------------------------------------------------ graph
     def graph(self) -> DeviceGraph:
@@ -954,6 +1206,13 @@ class KGAT(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("KGAT runs on the MI355X HIP path only: move the model to a GPU first")
         n = self._user_num + self._entity_num
+        step, opt = self._kg_graph, getattr(self, "_kg_optimizer", None)
+        if step.enabled and torch.is_grad_enabled():
+            step.release()  # a dropped captured forward's batch-row marks
+            ids = tuple(torch.as_tensor(t) for t in (heads, relations, positive_tails, negative_tails))
+            if step.usable(ids, opt):
+                return _KGGraphLoss.apply(step, ids, opt, self._user_entity_embedding.weight,
+                                          self._relation_embedding.weight, self._trans_matrix)
         h, p, q, r = self._ids.check("TRAIN_KG ids", (heads, positive_tails, negative_tails), n, dev,
                                      more=[((relations,), self._relation_num)])
         ids = [h, r, p, q]
@@ -1026,6 +1285,7 @@ class KGAT(nn.Module):
         except IndexError:
             self._table_update.discard()
             self._kg_table_update.discard()
+            self._kg_graph.release()
             opt.zero_grad()
             raise
 
@@ -1053,6 +1313,16 @@ class KGAT(nn.Module):
         """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
         self._raise_or_abandon(self._kg_optimizer)
         self._table_update.materialize()
+        step = self._kg_graph
+        if step.pending == "bwd":
+            ps, _ = step._states(self._kg_optimizer)
+            if row_ranges or any(p.grad is not None for p in ps):
+                step.materialize()  # another gradient joined this step's: the eager update sums them
+            else:
+                step.update(self._kg_optimizer)
+                self._kg_optimizer.zero_grad()
+                return
+        step.release()
         ktu, lazy, opt = self._kg_table_update, self._lazy_kg, self._kg_optimizer
         fused = None
         if ktu.pending is not None:
@@ -1081,6 +1351,7 @@ class KGAT(nn.Module):
             # holds the batch-row map (KG): a new backward or an attention refresh would change them
             self._table_update.materialize()
             self._kg_table_update.materialize()
+            self._kg_graph.materialize()
         if mode == KGATMode.TRAIN_CF:
             return self._calc_cf_loss(*args)
         if mode == KGATMode.TRAIN_KG:

@@ -95,9 +95,16 @@ class ShardedGradSync:
     after the optimizer step all-gathers the owned blocks of the parameters."""
 
     def __init__(self, params, big_bytes: int = SMALL_BUCKET_BYTES, replicate_table: bool = False,
-                 force: bool = False):
-        """``force``: run the collectives even on a world of one rank (tests: RCCL at world 1)."""
+                 force: bool = False, pipeline: bool = False):
+        """``force``: run the collectives even on a world of one rank (tests: RCCL at world 1).
+        ``pipeline`` (with attach, sharded mode): the table's owned-block Adam and the broadcast of the
+        updated block run inside the backward, block by block (see _owner_step)."""
         self.force = bool(force)
+        self.pipeline = bool(pipeline)
+        self._model = None
+        self._bcast: list = []   # this step's block broadcasts (work handles), waited by gather()
+        self._stepped = set()    # main blocks whose owner step + broadcast were issued this step
+        self._side = None
         self.params = list(params)
         self.big_bytes = int(big_bytes)
         self.replicate_table = bool(replicate_table)
@@ -127,6 +134,7 @@ class ShardedGradSync:
         self._table = table
         self.bounds = [(k * s, (k + 1) * s) for k in range(n)] + ([(s * n, rows)] if s * n < rows else [])
         self.replicated = self.replicate_table
+        self._model = model
         model._table_grad_hook = self
         return self
 
@@ -275,12 +283,52 @@ class ShardedGradSync:
         n = world()
         if self._early is None or self._early[0] is not grad:
             self._early = (grad, [])
+            self._bcast, self._stepped = [], set()
         r0, r1 = self.bounds[k]
         view = grad[r0:r1]
         if k < n and _is_nccl():
             self._early[1].append(dist.reduce(view, dst=k, async_op=True))
         else:  # the tail rows (every rank steps them), and gloo (no CUDA reduce): all-reduce
             self._early[1].append(dist.all_reduce(view, async_op=True))
+        if self.pipeline and 1 <= k <= n:
+            # block k-1's owner step + broadcast, issued behind block k's reduce (the same collective order
+            # on every rank); it runs while the next blocks are computed
+            self._owner_step(k - 1)
+
+    def _side_stream(self, dev) -> torch.cuda.Stream:
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=dev)
+        return self._side
+
+    def _owner_step(self, j: int) -> None:
+        """Pipelined sharded exchange (``pipeline``): the owner of main block j (rank j) takes its Adam step on
+        the block as soon as the block's reduce lands -- on a side stream, behind that reduce only -- and
+        broadcasts the updated rows; every other rank receives them into its replica.  Block j's wire time
+        then overlaps blocks j+1.. of the backward product instead of following the whole update (the
+        all-gather of gather()).  Per element: the same mean (the reduced sum / G) and the same Adam step with
+        the owned block's own state -- the bits of the reduce-scatter / owned-row Adam / all-gather path."""
+        n = world()
+        rank = _rank()
+        grad = self._early[0]
+        p = self._table
+        r0, r1 = self.bounds[j]
+        self._stepped.add(j)
+        if rank == j:
+            model = self._model
+            opt = model._cf_optimizer
+            side = self._side_stream(grad.device)
+            with torch.cuda.stream(side):
+                self._early[1][j].wait()  # the side stream waits for the reduce; the compute stream does not
+                gv = grad[r0:r1]
+                gv.div_(n)
+                from . import kernels
+                st, step_size, bc2s = opt._advance((id(p), r0, r1), p.data[r0:r1])
+                kernels.adam_multi([(p.data[r0:r1], gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s)],
+                                   opt.beta1, opt.beta2, opt.eps, model._ids.skip_flag())
+                self._bcast.append(dist.broadcast(p.data[r0:r1], src=j, async_op=True))
+            grad.record_stream(side)
+        else:
+            self._bcast.append(dist.broadcast(p.data[r0:r1], src=j, async_op=True))
 
     def reduce(self) -> dict | None:
         n = world()
@@ -305,12 +353,25 @@ class ShardedGradSync:
                 g.div_(n)
                 continue
             if early is not None and p is self._table and len(early[1]) == len(self.bounds):
+                s = self.bounds[0][1]
+                main = s * n
+                if self.pipeline:
+                    if g.data_ptr() != early[0].data_ptr():
+                        raise RuntimeError("ShardedGradSync(pipeline): autograd copied the table gradient")
+                    for j in range(n):
+                        if j not in self._stepped:
+                            self._owner_step(j)
+                    rr = []
+                    if main < g.shape[0]:  # the tail rows: all-reduced, every rank steps them
+                        early[1][n].wait()
+                        g[main:].div_(n)
+                        rr.append((main, g.shape[0]))
+                    ranges[id(p)] = rr  # the owned block was stepped by _owner_step
+                    continue
                 for w in early[1]:
                     w.wait()
                 if g.data_ptr() != early[0].data_ptr():  # autograd kept a copy: take the reduced tensor
                     g.copy_(early[0])
-                s = self.bounds[0][1]
-                main = s * n
                 g[rank * s:(rank + 1) * s].div_(n)
                 rr = [(rank * s, (rank + 1) * s)]
                 if main < g.shape[0]:
@@ -357,6 +418,9 @@ class ShardedGradSync:
         n = world()
         if n == 1 and not self.force:
             return
+        bc, self._bcast, self._stepped = self._bcast, [], set()
+        for w in bc:  # the pipelined blocks' broadcasts: the current stream waits for the last of them
+            w.wait()
         rank = _rank()
         for p, s, main in self._big:
             full = p.data[:main]

@@ -48,7 +48,7 @@ def main() -> None:
                         cf_embedding_dim=d0, kg_embedding_dim=d0, message_dropout=[0.1] * len(layer_size))
     models = []
     model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
-    for k in range(8):
+    for k in range(9):
         torch.manual_seed(3)
         m = pkg.KGAT(args)
         m.attach_graph(lay, "cuda")
@@ -56,11 +56,11 @@ def main() -> None:
         m.train()
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
         m.fuse_table_update = k >= 5
-        m.frontier_forward = k >= 6
+        m.frontier_forward = k in (6, 7)
         models.append(m)
     rng = np.random.default_rng(40 + rank)
     failures = []
-    syncs = [None] * 8
+    syncs = [None] * 9
     for step in range(3):
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
@@ -68,7 +68,7 @@ def main() -> None:
             torch.manual_seed(1000 * step + rank)  # same dropout for every path, per rank
             if k and syncs[k] is None:
                 params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
-                syncs[k] = rep.ShardedGradSync(params, replicate_table=3 <= k <= 6)
+                syncs[k] = rep.ShardedGradSync(params, replicate_table=3 <= k <= 6, pipeline=k == 8)
                 if k >= 2:
                     syncs[k].attach(m)
             frac = model_mod.HOP_DENSE_FRACTION
@@ -90,7 +90,7 @@ def main() -> None:
                 with torch.no_grad():  # a loss evaluation without backward opens no exchange
                     m(*b, mode=pkg.KGATMode.TRAIN_CF)
     for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop"), ("G", "hop")):
-        got = syncs["ABCDEFGH".index(tag)].stats
+        got = syncs["ABCDEFGHI".index(tag)].stats
         # 2 layers: the layer-0 hop set is the first hop (small); 3 layers: the second hop, which may
         # cross HOP_DENSE_FRACTION -- then every rank agrees on the dense exchange
         if (got.get(want, 0) != 3) if len(layer_size) == 2 else (sum(got.values()) != 3):
@@ -105,6 +105,8 @@ def main() -> None:
             failures.append(f"G {na}: differs from F by {(named[5][1].data - named[6][1].data).abs().max().item():.3e}")
         if not torch.equal(named[2][1].data, named[7][1].data):
             failures.append(f"H {na}: differs from C by {(named[2][1].data - named[7][1].data).abs().max().item():.3e}")
+        if not torch.equal(named[2][1].data, named[8][1].data):
+            failures.append(f"I {na}: differs from C by {(named[2][1].data - named[8][1].data).abs().max().item():.3e}")
         for tag, (_, po) in zip("BCDE", named[1:5]):
             # two ranks: every sum has two operands, so B / C equal A bit for bit; more ranks
             # associate the sums differently (the Adam tolerance, as D / E)
@@ -113,7 +115,7 @@ def main() -> None:
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
             if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
-        for tag, (_, po) in zip("ABCDEFGH", named):
+        for tag, (_, po) in zip("ABCDEFGHI", named):
             other = po.data.clone()
             dist.broadcast(other, 0)
             if not torch.equal(other, po.data):

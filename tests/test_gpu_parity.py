@@ -1907,3 +1907,80 @@ def test_lazy_kg_adam_bit_identical(pkg, dim):
                 continue
             assert sa_["step"] == sb_["step"], opt
             assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
+
+
+@pytest.mark.parametrize("dim", [64, 128])
+def test_captured_kg_step_bit_identical(pkg, dim):
+    """KGAT.capture_kg_step (TRAIN_KG forward, backward and update_kg_weights each one replayed HIP graph,
+    the step's scalars on the device) vs the eager lazy KG step: over KG phases between CF steps -- with a
+    step whose ids are out of range, the skip flag set while a step is in flight, a dropped loss (forward
+    without backward), two backwards before one update, a PREDICT and a second build_optimizer -- the
+    losses, parameters and both optimisers' states are equal bit for bit, and the graphs did replay."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(3000, 30000, seed=17)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    n = U + E
+    R = len(lay.rel_order)
+    models = []
+    for cap in (False, True):
+        torch.manual_seed(3)
+        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=R, layer_size=[dim, 32],
+                                  cf_embedding_dim=dim, kg_embedding_dim=dim))
+        m.attach_graph(lay, DEV)
+        m.train()
+        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
+        m.fuse_table_update = m.fuse_kg_table_update = m.lazy_kg_adam = True
+        m.capture_kg_step = cap
+        models.append(m)
+    rng = np.random.default_rng(4)
+    for phase in range(4):
+        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.2), int(E * 0.2))]
+        kgs = [[torch.from_numpy(rng.integers(0, hi, 48)).to(DEV) for hi in (n, R, n, n)] for _ in range(8)]
+        losses = []
+        for m in models:
+            torch.manual_seed(50 + phase)
+            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            m.update_cf_weights()
+            out = []
+            for j, kg in enumerate(kgs):
+                if phase == 1 and j == 2:  # a device-side bad id: the step moves nothing, the update raises
+                    bad = kg[2].clone()
+                    bad[0] = n + 7
+                    m(kg[0], kg[1], bad, kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
+                    torch.cuda.synchronize()
+                    with pytest.raises(IndexError):
+                        m.update_kg_weights()
+                    continue
+                if phase == 2 and j == 3:  # a dropped loss: its batch-row marks are released by the next forward
+                    out.append(m(*kg, mode=pkg.KGATMode.TRAIN_KG).detach().clone())
+                    continue
+                loss = m(*kg, mode=pkg.KGATMode.TRAIN_KG)
+                loss.backward()
+                if phase == 3 and j == 5:  # two backwards, one update (gradient accumulation)
+                    kg2 = kgs[(j + 1) % len(kgs)]
+                    m(*kg2, mode=pkg.KGATMode.TRAIN_KG).backward()
+                if phase >= 2 and j in (1, 6):
+                    m._ids.skip_flag().fill_(1)  # set on the device while the step is in flight
+                m.update_kg_weights()
+                m._ids.skip_flag().zero_()
+                out.append(loss.detach().clone())
+            losses.append(torch.stack(out))
+            if phase == 2:
+                with torch.no_grad():
+                    m(ids[0], ids[1], mode=pkg.KGATMode.PREDICT)
+                m.build_optimizer(cf_lr=1e-3, kg_lr=2e-4)
+        assert torch.equal(losses[0], losses[1]), phase
+    assert models[1]._kg_graph.replays >= 20 and models[0]._kg_graph.replays == 0
+    sa, sb = models[0].state_dict(), models[1].state_dict()
+    for k in sa:
+        if not sa[k].is_sparse:
+            assert torch.equal(sa[k], sb[k]), k
+    for opt in ("_cf_optimizer", "_kg_optimizer"):
+        oa, ob = getattr(models[0], opt), getattr(models[1], opt)
+        for pa, pb in zip(oa.params, ob.params):
+            sa_, sb_ = oa.state.get(id(pa)), ob.state.get(id(pb))
+            assert (sa_ is None) == (sb_ is None), opt
+            if sa_ is None:
+                continue
+            assert sa_["step"] == sb_["step"], opt
+            assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
