@@ -94,19 +94,26 @@ def compulsory_bytes(n: int, nnz: int, d: int) -> int:
 
 
 def sharded_bytes_per_gpu(cfg: dict, world: int) -> float:
-    """Planned HBM per rank of the row-sharded mode (sharded.RowShardedKGAT), largest shard ~1.15x the mean.
-    Per node row (fp32): X0, its gradient and CF Adam m/v (4d), layer outputs H_l and sides S_l,
-    three backward temporaries of the widest layer; per edge: the local rows of A and of A^T
-    (col + val each) and the refresh's two position maps (24 B); per node of the whole graph: two
-    gathered column chunks in flight (sharded.GATHER_CHUNK columns each) and the batch-row map."""
+    """Planned HBM per rank of the row-sharded mode (sharded.RowShardedKGAT) -- the buffers its step allocates,
+    largest shard ~1.15x the mean.  Per local node row (fp32): X0, its gradient and the CF Adam m / v (4d),
+    the layer outputs H_l and sides S_l, the wide (GEMM) layers' pre-activation state (2 d_out + 1 per
+    layer), three backward temporaries of the widest layer.  Per local edge: the rows of A and of A^T (col
+    + val each) and the refresh's two position maps (24 B).  Per node of the whole graph: the gathered
+    layer inputs -- the pipelined forward keeps layer l's gathered input and layer l+1's, being posted
+    block by block, alive together (sharded._layer_pipelined): max_l (d_l + d_(l+1)) floats -- and the
+    batch-row map."""
+    import importlib as _il
+    kern = _il.import_module(PKG + ".kernels")
     d, layers = cfg["dim"], cfg["layers"]
     dims = [d, *layers]
-    per_row = 4 * (4 * d + sum(layers) + sum(dims[:-1]) + 3 * max(dims))
+    gemm_state = sum(2 * b + 1 for a, b in zip(dims[:-1], dims[1:]) if not kern.fused_supported(a, b))
+    per_row = 4 * (4 * d + sum(layers) + sum(dims[:-1]) + gemm_state + 3 * max(dims))
     nnz = 2 * cfg["triples"]
     per_rank_rows = 1.15 * cfg["nodes"] / world
     per_rank_edges = 1.15 * nnz / world
-    chunk = min(d, 64)
-    return per_row * per_rank_rows + 24 * per_rank_edges + (2 * 4 * chunk + 4) * cfg["nodes"]
+    pairs = [dims[l] + dims[l + 1] for l in range(len(layers) - 1)] or [d]
+    gathered = 4 * max(pairs) if world > 1 else 0
+    return per_row * per_rank_rows + 24 * per_rank_edges + (gathered + 4) * cfg["nodes"]
 
 
 def min_gpus(cfg: dict) -> int:

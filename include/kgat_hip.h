@@ -762,6 +762,14 @@ int kgat_comm_ring_exchange(kgat_comm *comm, const void *send, void *recv, int64
  * one receive per peer in a single RCCL group -- on a fully connected xGMI node every peer pair
  * has its own link, so all seven links carry rows concurrently (no ring hop). */
 int kgat_comm_allgatherv(kgat_comm *comm, const void *send, void *recv, const int64_t *offsets, void *stream);
+/* The same gather with every rank's block placed anywhere: rank r's nbytes[r] bytes land at
+ * recv + dst_off[r] (world entries each, the same on every rank; blocks must not overlap).  The
+ * row-sharded forward posts each finished row block of a layer's output with it (rank r's block b =
+ * rows [lo_r + a_rb, lo_r + a_r(b+1)) of the next layer's gathered input), so the next layer's wire
+ * time runs under this layer's remaining blocks.  World <= KGAT_COMM_MAX_WORLD. */
+#define KGAT_COMM_MAX_WORLD 64
+int kgat_comm_gather_at(kgat_comm *comm, const void *send, void *recv, const int64_t *dst_off, const int64_t *nbytes,
+                        void *stream);
 /* All-to-all with per-peer sizes: send[send_off[p], send_off[p+1]) goes to rank p, rank p's block
  * lands in recv[recv_off[p], recv_off[p+1]) (byte offsets, world + 1 each); the own block is
  * copied on the stream.  The row-sharded attention refresh moves A's refreshed values to the

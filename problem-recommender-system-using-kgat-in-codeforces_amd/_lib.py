@@ -219,6 +219,7 @@ _SIGNATURES = {
     "kgat_comm_reduce_scatter_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_comm_ring_exchange": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_comm_allgatherv": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp]),
+    "kgat_comm_gather_at": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_vp]),
     "kgat_comm_alltoallv": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_vp]),
     "kgat_synth_open": (ctypes.c_int, [c_i64, c_i64, c_u64, ctypes.c_double, ctypes.c_int, ctypes.POINTER(c_vp)]),
     "kgat_synth_close": (None, [c_vp]),

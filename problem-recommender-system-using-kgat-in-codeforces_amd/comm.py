@@ -136,6 +136,20 @@ class RcclComm:
         _lib.call("kgat_comm_allgatherv", self._h, send.data_ptr(), out.data_ptr(), offs, st)
         return self._end()
 
+    def gather_at(self, send: torch.Tensor, out: torch.Tensor, starts, sizes) -> _Done:
+        """Rank r's ``sizes[r]`` rows land in out[starts[r]:starts[r] + sizes[r]] (kgat_comm_gather_at);
+        ``send`` = this rank's rows.  The pipelined row-sharded forward's block post."""
+        self._check(out, "out")
+        row = out.stride(0) * out.element_size()
+        offs = (ctypes.c_int64 * self.world)(*[int(a) * row for a in starts])
+        nb = (ctypes.c_int64 * self.world)(*[int(z) * row for z in sizes])
+        if int(sizes[self.rank]):
+            self._check(send, "send")
+        st = self._begin(send, out)
+        _lib.call("kgat_comm_gather_at", self._h, send.data_ptr() if int(sizes[self.rank]) else None, out.data_ptr(),
+                  offs, nb, st)
+        return self._end()
+
     def all_to_all_v(self, send: torch.Tensor, send_off, recv: torch.Tensor, recv_off) -> None:
         """send[send_off[p]:send_off[p+1]] -> rank p, rank p's block -> recv[recv_off[p]:...] (1-D,
         element offsets; kgat_comm_alltoallv); the caller's stream is ordered after it."""

@@ -183,17 +183,18 @@ extern "C" int kgat_comm_ring_exchange(kgat_comm* c, const void* send, void* rec
   return e1 ? e1 : e2 ? e2 : e3;
 }
 
-extern "C" int kgat_comm_allgatherv(kgat_comm* c, const void* send, void* recv, const int64_t* offsets, void* stream) {
+extern "C" int kgat_comm_gather_at(kgat_comm* c, const void* send, void* recv, const int64_t* dst_off,
+                                   const int64_t* nbytes, void* stream) {
   using namespace kgat;
-  if (c == nullptr || offsets == nullptr || recv == nullptr) return KGAT_ERR_INVALID;
+  if (c == nullptr || dst_off == nullptr || nbytes == nullptr || recv == nullptr) return KGAT_ERR_INVALID;
   for (int r = 0; r < c->world; ++r)
-    if (offsets[r + 1] < offsets[r]) return KGAT_ERR_INVALID;
+    if (nbytes[r] < 0 || dst_off[r] < 0) return KGAT_ERR_INVALID;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   char* out = static_cast<char*>(recv);
-  const int64_t mine = offsets[c->rank + 1] - offsets[c->rank];
+  const int64_t mine = nbytes[c->rank];
   if (mine > 0 && send == nullptr) return KGAT_ERR_INVALID;
-  if (mine > 0 && send != out + offsets[c->rank] &&
-      hipMemcpyAsync(out + offsets[c->rank], send, static_cast<size_t>(mine), hipMemcpyDeviceToDevice, st) !=
+  if (mine > 0 && send != out + dst_off[c->rank] &&
+      hipMemcpyAsync(out + dst_off[c->rank], send, static_cast<size_t>(mine), hipMemcpyDeviceToDevice, st) !=
           hipSuccess)
     return KGAT_ERR_INVALID;
   if (c->world == 1) return KGAT_OK;
@@ -201,13 +202,25 @@ extern "C" int kgat_comm_allgatherv(kgat_comm* c, const void* send, void* recv, 
   int err = KGAT_OK;
   for (int p = 0; p < c->world && !err; ++p) {
     if (p == c->rank) continue;
-    const int64_t theirs = offsets[p + 1] - offsets[p];
     if (mine > 0) err = status(g_rccl.send(send, static_cast<size_t>(mine), ncclUint8, p, c->comm, st));
-    if (!err && theirs > 0)
-      err = status(g_rccl.recv(out + offsets[p], static_cast<size_t>(theirs), ncclUint8, p, c->comm, st));
+    if (!err && nbytes[p] > 0)
+      err = status(g_rccl.recv(out + dst_off[p], static_cast<size_t>(nbytes[p]), ncclUint8, p, c->comm, st));
   }
   const int e2 = status(g_rccl.group_end());
   return err ? err : e2;
+}
+
+extern "C" int kgat_comm_allgatherv(kgat_comm* c, const void* send, void* recv, const int64_t* offsets, void* stream) {
+  using namespace kgat;
+  if (c == nullptr || offsets == nullptr || recv == nullptr) return KGAT_ERR_INVALID;
+  if (c->world > KGAT_COMM_MAX_WORLD) return KGAT_ERR_INVALID;
+  int64_t off[KGAT_COMM_MAX_WORLD], len[KGAT_COMM_MAX_WORLD];
+  for (int r = 0; r < c->world; ++r) {
+    if (offsets[r + 1] < offsets[r]) return KGAT_ERR_INVALID;
+    off[r] = offsets[r];
+    len[r] = offsets[r + 1] - offsets[r];
+  }
+  return kgat_comm_gather_at(c, send, recv, off, len, stream);
 }
 
 extern "C" int kgat_comm_alltoallv(kgat_comm* c, const void* send, const int64_t* send_off, void* recv,

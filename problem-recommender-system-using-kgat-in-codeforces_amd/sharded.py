@@ -55,7 +55,7 @@ from torch import nn
 
 from . import kernels
 from . import _lib
-from .graph import GraphLayout, RefreshPlan, _DeviceCSR, degree_weights, stream_ptr
+from .graph import GraphLayout, RefreshPlan, _CSRRowView, _DeviceCSR, degree_weights, stream_ptr
 from . import model as _model
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
 from .optim import FusedAdam
@@ -115,33 +115,40 @@ class Comm:
         """Start the all-peer gather: rank r's rows land in out[bounds[r]:bounds[r+1]] on every rank
         (send = this rank's rows; it may be that slice of ``out`` itself).  One send and one receive
         per peer, all in one batch."""
-        lo, hi = int(bounds[self.rank]), int(bounds[self.rank + 1])
-        own = out[lo:hi]
-        if send.data_ptr() != own.data_ptr():
+        b = [int(x) for x in bounds]
+        return self.gather_at(send, out, b[:-1], [hi - lo for lo, hi in zip(b[:-1], b[1:])])
+
+    def gather_at(self, send: torch.Tensor, out: torch.Tensor, starts, sizes) -> _Pending:
+        """Start an all-peer gather of blocks placed anywhere: rank r's ``sizes[r]`` rows land in
+        out[starts[r]:starts[r] + sizes[r]] on every rank (send = this rank's rows; it may be its own
+        slice of ``out``).  The pipelined forward posts each finished row block of a layer with it."""
+        k = self.rank
+        lo, n_own = int(starts[k]), int(sizes[k])
+        own = out[lo:lo + n_own]
+        if n_own and send.data_ptr() != own.data_ptr():
             own.copy_(send)
         if not self.active or self.world == 1:
             return _Pending([])
-        peers = [r for r in range(self.world) if r != self.rank]
+        peers = [r for r in range(self.world) if r != k]
         if self.host:
-            s = own.detach().cpu()
-            bufs = {r: torch.empty((int(bounds[r + 1]) - int(bounds[r]), *out.shape[1:]), dtype=out.dtype)
-                    for r in peers}
+            s = own.detach().cpu() if n_own else None
+            bufs = {r: torch.empty((int(sizes[r]), *out.shape[1:]), dtype=out.dtype) for r in peers}
             ops = []
             for r in peers:
-                if s.shape[0]:
+                if n_own:
                     ops.append(dist.P2POp(dist.isend, s, self._glob(r), self.group))
                 if bufs[r].shape[0]:
                     ops.append(dist.P2POp(dist.irecv, bufs[r], self._glob(r), self.group))
             works = dist.batch_isend_irecv(ops) if ops else []
-            return _Pending(works, [(out[int(bounds[r]):int(bounds[r + 1])], bufs[r]) for r in peers
+            return _Pending(works, [(out[int(starts[r]):int(starts[r]) + int(sizes[r])], bufs[r]) for r in peers
                                     if bufs[r].shape[0]])
         ops = []
         for r in peers:
-            if hi > lo:
+            if n_own:
                 ops.append(dist.P2POp(dist.isend, own, self._glob(r), self.group))
-            a, b = int(bounds[r]), int(bounds[r + 1])
-            if b > a:
-                ops.append(dist.P2POp(dist.irecv, out[a:b], self._glob(r), self.group))
+            a, z = int(starts[r]), int(sizes[r])
+            if z:
+                ops.append(dist.P2POp(dist.irecv, out[a:a + z], self._glob(r), self.group))
         return _Pending(dist.batch_isend_irecv(ops) if ops else [])
 
     def all_to_all_v(self, send: torch.Tensor, send_off, recv: torch.Tensor, recv_off) -> None:
@@ -326,7 +333,7 @@ class RowShard:
 
 
 def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-                  transpose: bool = False, rows=None) -> torch.Tensor:
+                  transpose: bool = False, rows=None, pre=None) -> torch.Tensor:
     """out (+)= csr . Xg, Xg = [N, d] every rank's rows of X (all-peer gather), csr = shard.A (forward)
     or shard.AT (backward).  Column chunks of GATHER_CHUNK: chunk c+1 is on the wire while chunk c's
     product runs; each product is the single-GPU kernel on the local rows.  ``rows`` = (list, device
@@ -340,6 +347,8 @@ def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor
 
     if not comm.active:  # one rank: X is the whole table
         return product(X, out)
+    if pre is not None:  # gathered by the previous (pipelined) layer's block posts
+        return product(_gathered(shard, comm, X, pre), out)
     w = min(d, GATHER_CHUNK) if GATHER_CHUNK > 0 else d
     chunks = [(c, min(c + w, d)) for c in range(0, d, w)]
     N, lo, hi = shard.n_nodes, shard.lo, shard.hi
@@ -359,6 +368,70 @@ def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor
         pend.wait()
         product(buf, out[:, c0:c1])
     return out
+
+
+class _RowBlocks:
+    """The pipelined forward's row blocks: every rank's shard cut into K blocks at 16-row boundaries (the
+    bi-interaction's sub-tiles), from the shard sizes alone -- every rank knows every rank's blocks, so
+    block b's all-peer post pairs up on every rank.  This rank's blocks carry a row view of A (its own
+    long-row plan: a row never spans two blocks, so each row's edges are summed exactly as in the whole
+    launch), the row list and the tile bitmap of the block."""
+
+    def __init__(self, shard: RowShard, K: int):
+        dev = shard.device
+        self.K = K
+        cuts = []
+        for n in (int(z) for z in shard.sizes):
+            c = [min(n, (n * b // K) // 16 * 16) for b in range(K)] + [n]
+            cuts.append(list(np.maximum.accumulate(c)))
+        self.cuts = cuts
+        mine = cuts[shard.rank]
+        self.mine = mine
+        self.views, self.rows, self.bits = [], [], []
+        for a, b in zip(mine[:-1], mine[1:]):
+            self.views.append(_CSRRowView(shard.A, a, b, dev) if b > a else None)
+            self.rows.append(torch.arange(a, b, dtype=torch.int32, device=dev) if b > a else None)
+            w = np.zeros((shard.n + 31) // 32 + 1, np.uint32)
+            for t in range(a // 16, (b + 15) // 16):  # the block's 16-row tiles: half-words of the bitmap
+                w[t >> 1] |= np.uint32(0xFFFF) << np.uint32(16 * (t & 1))
+            self.bits.append(torch.from_numpy(w.view(np.int32)).to(dev) if b > a else None)
+        bounds = shard.bounds
+        self.starts = [[int(bounds[r]) + cuts[r][b] for r in range(shard.world)] for b in range(K)]
+        self.sizes = [[cuts[r][b + 1] - cuts[r][b] for r in range(shard.world)] for b in range(K)]
+
+
+def _gathered(shard: RowShard, comm, X: torch.Tensor, pre) -> torch.Tensor:
+    """[N, d] every rank's rows of X: the blocks a pipelined layer already posted (``pre`` = (buffer,
+    pending posts)), else one whole-width all-peer gather."""
+    if pre is not None:
+        buf, pends = pre
+        for pd in pends:
+            pd.wait()
+        return buf
+    return gather_table(shard, comm, X)
+
+
+def _layer_pipelined(shard: RowShard, comm, blocks: _RowBlocks, Xg: torch.Tensor, x: torch.Tensor, W1, b1, W2, b2,
+                     drop: float, seed: int, st, s: torch.Tensor):
+    """One whole-shard layer forward computed in row blocks, each block's output rows posted to every peer
+    (the next layer's gathered input) as soon as they exist: the next layer's gather travels under this
+    layer's remaining blocks instead of after the layer.  Per row: the SpMM of its edges in order (a row
+    view of A), the bi-interaction with its own dropout draws and state (the tile-list / row-list kernels)
+    -- the whole launch's bits.  Returns (this rank's output rows, (next gathered buffer, pending posts))."""
+    dout = W1.shape[0]
+    h = torch.empty(shard.n, dout, dtype=torch.float32, device=x.device)
+    nxt = torch.empty(shard.n_nodes, dout, dtype=torch.float32, device=x.device)
+    pends = []
+    for b in range(blocks.K):
+        a0, a1 = blocks.mine[b], blocks.mine[b + 1]
+        if a1 > a0:
+            kernels.spmm_block(blocks.views[b], Xg, s[a0:a1])
+            if st.kind == "gemm":
+                kernels.biinter_fwd_gemm_rows(x, s, blocks.rows[b], a1 - a0, W1, b1, W2, b2, drop, seed, h, st)
+            else:
+                kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drop, seed, h, blocks.bits[b], state=st)
+        pends.append(comm.gather_at(h[a0:a1], nxt, blocks.starts[b], blocks.sizes[b]))
+    return h, (nxt, pends)
 
 
 def gather_table(shard: RowShard, comm, X: torch.Tensor) -> torch.Tensor:
@@ -548,7 +621,7 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
 class _ShardedCFLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cu, cp, cn, cfg, X0, *ws):
-        shard, comm, drops, seeds, reg, rows, frontier, _tu = cfg
+        shard, comm, drops, seeds, reg, rows, frontier, _tu, blocks = cfg
         L = len(drops)
         tables, sides, states = [X0], [], []
         # frontier forward: layers whose output the loss reads on a row set only run on that set (the
@@ -556,16 +629,22 @@ class _ShardedCFLoss(torch.autograd.Function):
         # all stay inside it); per row the whole-shard call's bits
         sets = _frontier_sets(shard, comm, rows, L) if frontier else [None] * L
         x = X0
+        pre = None  # the next layer's gathered input, posted block by block by a pipelined layer
         for l in range(L):
             W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
             s = torch.empty(shard.n, x.shape[1], dtype=torch.float32, device=x.device)
             st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
-            if sets[l] is None:
-                gathered_spmm(shard, comm, shard.A, x, s)
+            if sets[l] is None and blocks is not None and l + 1 < L and comm.active:
+                x, pre = _layer_pipelined(shard, comm, blocks, _gathered(shard, comm, x, pre), x, W1, b1, W2, b2,
+                                          drops[l], seeds[l], st, s)
+            elif sets[l] is None:
+                gathered_spmm(shard, comm, shard.A, x, s, pre=pre)
+                pre = None
                 x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             else:
                 rws, cnt, bits, m = sets[l]
-                gathered_spmm(shard, comm, shard.A, x, s, rows=(rws, cnt, bits))
+                gathered_spmm(shard, comm, shard.A, x, s, rows=(rws, cnt, bits), pre=pre)
+                pre = None
                 h = torch.empty(shard.n, W1.shape[0], dtype=torch.float32, device=x.device)
                 if st.kind == "gemm":
                     x = kernels.biinter_fwd_gemm_rows(x, s, rws, m, W1, b1, W2, b2, drops[l], seeds[l], h, st)
@@ -583,7 +662,7 @@ class _ShardedCFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        shard, comm, drops, seeds, reg, rows, _frontier, tu = ctx.cfg
+        shard, comm, drops, seeds, reg, rows, _frontier, tu, _blocks = ctx.cfg
         tables, sides, states, Tc, coef, ws = ctx.saved
         cu, cp, cn = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -723,7 +802,19 @@ class RowShardedKGAT(nn.Module):
         # product in the backward, the table gradient in .grad
         self.fuse_table_update = False
         self._table_update = _ShardTableUpdate()
+        # row blocks of the pipelined forward (each finished block's output posted to the peers while the
+        # next block computes; same bits); 0 = whole-shard launches, the next layer gathered after them
+        self.pipeline_blocks = 4
         self.to(device)
+
+    def _blocks(self) -> _RowBlocks | None:
+        K = int(self.pipeline_blocks)
+        if K <= 1 or GATHER_CHUNK > 0:
+            return None
+        cached = self.__dict__.get("_row_blocks")
+        if cached is None or cached.K != K:
+            cached = self._row_blocks = _RowBlocks(self.shard, K)
+        return cached
 
     # ------------------------------------------------------------------ state
     @torch.no_grad()
@@ -763,13 +854,23 @@ class RowShardedKGAT(nn.Module):
     def propagate(self) -> list[torch.Tensor]:
         """This rank's rows of [X0, H1, ..., HL] (no autograd state)."""
         drops, seeds = self._dropouts()
+        blocks = self._blocks()
+        L = len(self._aggregator_layers)
         with torch.no_grad():
             x = self._user_entity_embedding_shard.detach()
             tables = [x]
+            pre = None
             for l, agg in enumerate(self._aggregator_layers):
+                ws = [w.detach() for w in agg.weights()]
                 s = torch.empty(self.shard.n, x.shape[1], dtype=torch.float32, device=x.device)
-                gathered_spmm(self.shard, self.comm, self.shard.A, x, s)
-                x = kernels.biinter_fwd(x, s, *[w.detach() for w in agg.weights()], drops[l], seeds[l])
+                if blocks is not None and l + 1 < L and self.comm.active:
+                    st = kernels.make_state(x.shape[0], ws[0].shape[1], ws[0].shape[0], x.device)
+                    x, pre = _layer_pipelined(self.shard, self.comm, blocks, _gathered(self.shard, self.comm, x, pre),
+                                              x, *ws, drops[l], seeds[l], st, s)
+                else:
+                    gathered_spmm(self.shard, self.comm, self.shard.A, x, s, pre=pre)
+                    pre = None
+                    x = kernels.biinter_fwd(x, s, *ws, drops[l], seeds[l])
                 tables.append(x)
         return tables
 
@@ -783,7 +884,7 @@ class RowShardedKGAT(nn.Module):
         drops, seeds = self._dropouts()
         tu = self._table_update if self.fuse_table_update and torch.is_grad_enabled() else None
         cfg = (self.shard, self.comm, drops, seeds, float(self._regularization_params[0]), rows,
-               self.frontier_forward and torch.is_grad_enabled(), tu)
+               self.frontier_forward and torch.is_grad_enabled(), tu, self._blocks())
         return _ShardedCFLoss.apply(cu, cp, cn, cfg, self._user_entity_embedding_shard, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, pos_tails, neg_tails) -> torch.Tensor:

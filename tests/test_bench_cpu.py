@@ -28,17 +28,20 @@ def test_gpus_2_launches_two_ranks():
 
 
 def test_c5_refuses_one_gpu_cleanly():
-    p = _run("--config", "c5", "--gpus", "1")
-    assert p.returncode == 2
-    assert "needs >= 4 GPUs" in p.stderr
-    assert not p.stdout.strip()
+    """C5's planned per-rank HBM (bench.sharded_bytes_per_gpu: the buffers the pipelined row-sharded step
+    allocates) exceeds one GPU's budget below 8 ranks: refused before anything touches a GPU."""
+    for g in ("1", "4"):
+        p = _run("--config", "c5", "--gpus", g, *(["--dry-run"] if g != "1" else []))
+        assert p.returncode != 0, (g, p.stderr[-2000:])  # 2 (one rank) / the launcher's failure (ranks)
+        assert "needs >= 8 GPUs" in p.stderr
+        assert not any(x.startswith("{") for x in p.stdout.splitlines())
 
 
-def test_c5_world4_dry_run_accepted():
-    p = _run("--config", "c5", "--gpus", "4", "--dry-run")
+def test_c5_world8_dry_run_accepted():
+    p = _run("--config", "c5", "--gpus", "8", "--dry-run")
     assert p.returncode == 0, p.stderr[-2000:]
     rec = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
-    assert rec["ranks_joined"] == 4 and rec["mode"] == "sharded"
+    assert rec["ranks_joined"] == 8 and rec["mode"] == "sharded" and rec["min_gpus"] == 8
 
 
 def test_cpu_extrapolated_baseline_small():
