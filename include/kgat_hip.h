@@ -358,6 +358,17 @@ int kgat_biinter_bwd_gemm_rows_f32(const float *X, int64_t ldx, const float *S, 
                                    const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds, float *dW1,
                                    float *db1, float *dW2, float *db2, int64_t n_rows, int32_t d_in, int32_t d_out,
                                    float dropout_p, uint64_t seed, float *work, int64_t work_floats, void *stream);
+/* ... in two calls on the same work buffer: phases 1 = the operand gathers, the epilogue and the
+ * dXd / dS GEMM; phases 2 = the weight gradients (reads what phase 1 left in work); 3 = both.  The
+ * row-sharded backward posts dS / dXd to its peers between the two, so the weight-gradient GEMMs run
+ * under that gather.  Same bits as one call. */
+int kgat_biinter_bwd_gemm_rows_ex_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
+                                      int64_t ldh, const float *state, const float *norm, const uint64_t *mask,
+                                      const float *dH, int64_t lddh, const int32_t *rows, int64_t m, const float *W1,
+                                      const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds,
+                                      float *dW1, float *db1, float *dW2, float *db2, int64_t n_rows, int32_t d_in,
+                                      int32_t d_out, float dropout_p, uint64_t seed, float *work,
+                                      int64_t work_floats, int32_t phases, void *stream);
 int kgat_biinter_bwd_gemm_bits_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H,
                                    int64_t ldh, const float *norm, const uint64_t *mask, const float *dH,
                                    int64_t lddh, const float *W1, const float *W2, float *dXd, int64_t lddxd,

@@ -201,6 +201,10 @@ _SIGNATURES = {
                                                       c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
                                                       c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp,
                                                       c_i64, c_vp]),
+    "kgat_biinter_bwd_gemm_rows_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                                      c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                                      c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp,
+                                                      c_i64, c_i32, c_vp]),
     "kgat_biinter_fwd_gemm_rows_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                                       c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp,
                                                       c_i64, c_vp]),

@@ -320,8 +320,9 @@ static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d
 static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* W2,
                          const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
                          float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in, int32_t d_out,
-                         float* work, hipStream_t st, const int32_t* rows = nullptr) {
-  // rows (dual GEMM only): row r of dA / dB / dXd / dS is row rows[r] of X / S (-1: zero)
+                         float* work, hipStream_t st, const int32_t* rows = nullptr, int phases = 3) {
+  // rows (dual GEMM only): row r of dA / dB / dXd / dS is row rows[r] of X / S (-1: zero).
+  // phases: bit 1 the dXd / dS GEMM, bit 2 the weight gradients (work keeps what the second needs)
   const int ldu = d_in + 4;
   float* U = work;
   float* M = work + n * ldu;
@@ -331,7 +332,8 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
   const bool dual = (dual_gemm_on() || rows != nullptr) && (ldx & 3) == 0 && (lds & 3) == 0;
   if (rows != nullptr && !dual) return KGAT_ERR_INVALID;
-  if (dual) {
+  if (phases != 3 && !dual) return KGAT_ERR_INVALID;
+  if (dual && (phases & 1)) {
     // du = dA W1, dm = dB W2, then dXd = du + dm*S, dS = du + dm*X in the epilogue: one launch
     DualGemm g;
     g.dxs = true;
@@ -342,7 +344,7 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
     g.X = X, g.S = S, g.ldx = ldx, g.lds = lds;
     g.erows = rows;
     KGAT_GEMM(dual_gemm_f32(g, st));
-  } else {
+  } else if (!dual) {
     // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
     KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
     KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
@@ -353,6 +355,7 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
                        lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
     KGAT_LAUNCH_CHECK();
   }
+  if (!(phases & 2)) return KGAT_OK;
   // [dW | db] = [dA^T U | colsum dA], split over row chunks (deterministic: chunk slabs summed in
   // order): slab_b[d_out, 0:d_in] = dA_b[chunk, d_out]^T . U_b[chunk, d_in], slab_b[:, d_in] = the
   // chunk's column sums of dA, produced by the same GEMM from its A tiles (a [U | 1] operand
@@ -544,6 +547,20 @@ extern "C" int kgat_biinter_bwd_gemm_rows_f32(const float* X, int64_t ldx, const
                                               float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
                                               int32_t d_out, float dropout_p, uint64_t seed, float* work,
                                               int64_t work_floats, void* stream) {
+  return kgat_biinter_bwd_gemm_rows_ex_f32(X, ldx, S, lds, H, ldh, state, norm, mask, dH, lddh, rows, m, W1, W2, dXd,
+                                           lddxd, dS, ldds, dW1, db1, dW2, db2, n, d_in, d_out, dropout_p, seed, work,
+                                           work_floats, 3, stream);
+}
+
+extern "C" int kgat_biinter_bwd_gemm_rows_ex_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
+                                                 const float* H, int64_t ldh, const float* state, const float* norm,
+                                                 const uint64_t* mask, const float* dH, int64_t lddh,
+                                                 const int32_t* rows, int64_t m, const float* W1, const float* W2,
+                                                 float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1,
+                                                 float* db1, float* dW2, float* db2, int64_t n, int32_t d_in,
+                                                 int32_t d_out, float dropout_p, uint64_t seed, float* work,
+                                                 int64_t work_floats, int32_t phases, void* stream) {
+  if (phases < 1 || phases > 3) return KGAT_ERR_INVALID;
   // state: the GEMM forward's [P1 + b1 | P2 + b2 | norm] over all n rows (mask null), or null with
   // norm + mask: the fused forward's saved state (the "bits" kind, d_out <= 128)
   if (!X || !S || !H || !dH || !rows || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 || n < 0 || m < 0 ||
@@ -564,16 +581,18 @@ extern "C" int kgat_biinter_bwd_gemm_rows_f32(const float* X, int64_t ldx, const
   // slower at 300k rows than this copy costs); H, dH and the state are read through the list
   float* Xc = dB + m * d_out;
   float* Sc = Xc + m * static_cast<int64_t>(d_in);
-  if (int e = kgat_gather_rows_f32(X, ldx, rows, m, d_in, Xc, d_in, stream)) return e;
-  if (int e = kgat_gather_rows_f32(S, lds, rows, m, d_in, Sc, d_in, stream)) return e;
-  const float* P1 = state;
-  const float* P2 = state != nullptr ? state + n * d_out : nullptr;
-  const float* nrm = state != nullptr ? state + 2 * n * d_out : norm;
-  hipLaunchKernelGGL(kgat::epi_bwd_rows_kernel, dim3((m + 3) / 4), dim3(256), 0, st, dA, dB, P1, P2, mask, H, ldh, nrm,
-                     dH, lddh, rows, m, d_out, dropout_p, seed);
-  KGAT_LAUNCH_CHECK();
+  if (phases & 1) {
+    if (int e = kgat_gather_rows_f32(X, ldx, rows, m, d_in, Xc, d_in, stream)) return e;
+    if (int e = kgat_gather_rows_f32(S, lds, rows, m, d_in, Sc, d_in, stream)) return e;
+    const float* P1 = state;
+    const float* P2 = state != nullptr ? state + n * d_out : nullptr;
+    const float* nrm = state != nullptr ? state + 2 * n * d_out : norm;
+    hipLaunchKernelGGL(kgat::epi_bwd_rows_kernel, dim3((m + 3) / 4), dim3(256), 0, st, dA, dB, P1, P2, mask, H, ldh,
+                       nrm, dH, lddh, rows, m, d_out, dropout_p, seed);
+    KGAT_LAUNCH_CHECK();
+  }
   return kgat::bwd_gemm_tail(Xc, d_in, Sc, d_in, W1, W2, dA, dB, dXd, lddxd, dS, ldds, dW1, db1, dW2, db2, m, d_in,
-                             d_out, work, st);
+                             d_out, work, st, nullptr, phases);
 }
 
 extern "C" int64_t kgat_biinter_bwd_gemm_rows_work_floats(int64_t m, int32_t d_in, int32_t d_out) {

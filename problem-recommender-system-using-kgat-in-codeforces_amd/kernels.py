@@ -802,12 +802,14 @@ def biinter_fwd_rows(X, S, W1, b1, W2, b2, r0: int, n_rows: int, H, dropout_p: f
 
 def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, dXd=None, dS=None,
                 rows: torch.Tensor | None = None, H: torch.Tensor | None = None, state: BiState | None = None,
-                dh_full: bool = False):
+                dh_full: bool = False, split: bool = False):
     """Returns (dXd, dS, dW1, db1, dW2, db2).  With ``rows`` (int32 [n]), dH/dXd/dS are compact:
     row i belongs to node rows[i] of X and S (-1 = padding).  With the forward's output ``H`` and
     ``state``, the backward reads them instead of recomputing the forward.  ``dh_full`` (with rows):
     dH is indexed by node ([X rows, d_out]); the wide kinds then read every operand through the row
-    list (kgat_biinter_bwd_gemm_rows_f32: no gathered copies, same bits)."""
+    list (kgat_biinter_bwd_gemm_rows_f32: no gathered copies, same bits).  ``split`` (that wide row-list
+    case only): returns (dXd, dS, finish), finish() -> (dW1, db1, dW2, db2) -- the weight gradients run
+    when the caller has started what depends on dXd / dS only."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     _req(dH, "dH", dim=2)
@@ -819,8 +821,11 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
         if rows is None or dH.shape != (src_rows, dout):
             raise ValueError("dh_full needs rows and a [nodes, d_out] dH")
         if state is not None and state.kind in ("gemm", "bits") and H is not None:
-            return _biinter_bwd_rows(X, S, dH, W1, W2, dropout_p, seed, dXd, dS, rows, H, state)
+            return _biinter_bwd_rows(X, S, dH, W1, W2, dropout_p, seed, dXd, dS, rows, H, state, split=split)
         dH = gather_rows(dH, rows)
+    if split:
+        out = biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p, seed, dXd, dS, rows, H, state)
+        return out[0], out[1], lambda: out[2:]
     if dH.shape != (n, dout):
         raise ValueError("dH shape mismatch")
     if (H is None) != (state is None):
@@ -857,8 +862,10 @@ def biinter_bwd(X, S, dH, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
     return dXd, dS, dW1, db1, dW2, db2
 
 
-def _biinter_bwd_rows(X, S, dH, W1, W2, p, seed, dXd, dS, rows, H, state):
-    """The wide backward on a row list, every operand read through it (kgat_biinter_bwd_gemm_rows_f32)."""
+def _biinter_bwd_rows(X, S, dH, W1, W2, p, seed, dXd, dS, rows, H, state, split: bool = False):
+    """The wide backward on a row list, every operand read through it (kgat_biinter_bwd_gemm_rows_f32).
+    ``split``: returns (dXd, dS, finish) after the dXd / dS half (kgat_biinter_bwd_gemm_rows_ex_f32 phase
+    1); finish() runs the weight gradients (phase 2) and returns (dW1, db1, dW2, db2) -- same bits."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     dev = X.device
@@ -876,12 +883,22 @@ def _biinter_bwd_rows(X, S, dH, W1, W2, p, seed, dXd, dS, rows, H, state):
         raise ValueError(f"unsupported bi-interaction shape {din}->{dout}")
     work = torch.empty(max(w, 1), dtype=torch.float32, device=dev)
     gemm = state.kind == "gemm"
-    _lib.call("kgat_biinter_bwd_gemm_rows_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
-              state.P.data_ptr() if gemm else None, None if gemm else state.norm.data_ptr(),
-              None if gemm else state.mask.data_ptr(), dH.data_ptr(), _ld(dH), rows.data_ptr(), m,
-              W1.data_ptr(), W2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(),
-              db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), src_rows, din, dout, float(p),
-              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), work.data_ptr(), work.numel(), stream_ptr(dev))
+
+    def call(phases):
+        _lib.call("kgat_biinter_bwd_gemm_rows_ex_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(),
+                  _ld(H), state.P.data_ptr() if gemm else None, None if gemm else state.norm.data_ptr(),
+                  None if gemm else state.mask.data_ptr(), dH.data_ptr(), _ld(dH), rows.data_ptr(), m,
+                  W1.data_ptr(), W2.data_ptr(), dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(),
+                  db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(), src_rows, din, dout, float(p),
+                  ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), work.data_ptr(), work.numel(), phases, stream_ptr(dev))
+    if split:
+        call(1)
+
+        def finish():
+            call(2)
+            return dW1, db1, dW2, db2
+        return dXd, dS, finish
+    call(3)
     return dXd, dS, dW1, db1, dW2, db2
 
 

@@ -931,6 +931,9 @@ class _CFLoss(torch.autograd.Function):
                         kernels.spmm_block_masked(view, hmap, dSc, dX[view.r0:view.r0 + view.n_rows],
                                                   Yc_init=dXdc, row0=view.r0, src_rank=rank)
                         hook.block_ready(k, dX)
+                    # the exchange owns the table gradient now (its blocks are in flight): autograd gets
+                    # none (it would copy the whole [N, d] tensor), ShardedGradSync.reduce hands it over
+                    dX = None
                 elif l == 0 and tu is not None and tu.defer(graph, hmap, dSc, dXdc, rank):
                     dX = None  # computed fused with the table's Adam step by update_cf_weights
                 else:
@@ -949,6 +952,7 @@ class _CFLoss(torch.autograd.Function):
                 for k, view in enumerate(graph.transpose_row_blocks(hook.bounds)):
                     kernels.spmm_block(view, dS, dXd[view.r0:view.r0 + view.n_rows], accumulate=True)
                     hook.block_ready(k, dXd)
+                dXd = None  # owned by the exchange (see the hop branch)
             else:
                 kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
             wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]

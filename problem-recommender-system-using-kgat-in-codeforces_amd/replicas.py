@@ -341,6 +341,13 @@ class ShardedGradSync:
         early, self._early = self._early, None
         done, self._done = self._done, None
         for p in self.params:
+            if early is not None and p is self._table and not self.replicated:
+                # the attached backward left the table gradient to this exchange (model._CFLoss returns none
+                # to autograd: its blocks were already in flight)
+                if p.grad is not None:
+                    raise RuntimeError("ShardedGradSync: another gradient reached the table after its exchange "
+                                       "started (backward a second loss before reduce())")
+                p.grad = early[0]
             g = p.grad
             if g is None:
                 continue
@@ -356,8 +363,6 @@ class ShardedGradSync:
                 s = self.bounds[0][1]
                 main = s * n
                 if self.pipeline:
-                    if g.data_ptr() != early[0].data_ptr():
-                        raise RuntimeError("ShardedGradSync(pipeline): autograd copied the table gradient")
                     for j in range(n):
                         if j not in self._stepped:
                             self._owner_step(j)
@@ -370,8 +375,6 @@ class ShardedGradSync:
                     continue
                 for w in early[1]:
                     w.wait()
-                if g.data_ptr() != early[0].data_ptr():  # autograd kept a copy: take the reduced tensor
-                    g.copy_(early[0])
                 g[rank * s:(rank + 1) * s].div_(n)
                 rr = [(rank * s, (rank + 1) * s)]
                 if main < g.shape[0]:

@@ -592,17 +592,19 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
     hr = hrows[:mine] if mine else torch.full((1,), -1, dtype=torch.int32, device=dev)
     dS_out = own[:, :din] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
     dXd_out = own[:, din:] if mine else torch.empty(1, din, dtype=torch.float32, device=dev)
-    # dX is indexed by local row: the wide kinds read it (and X, S, H, the state) through the hop list
-    _, _, *g = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], dXd=dXd_out,
-                                   dS=dS_out, rows=hr, dh_full=True,
-                                   **({} if states[l] is None else {"H": tables[l + 1], "state": states[l]}))
-    reduce_w(l, g)
+    # dX is indexed by local row: the wide kinds read it (and X, S, H, the state) through the hop list.
+    # The dXd / dS half first: the rows go to the peers while the weight-gradient GEMMs (which nothing
+    # downstream waits for) run under the transfer
+    _, _, wgrads = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2, drops[l], seeds[l], dXd=dXd_out,
+                                       dS=dS_out, rows=hr, dh_full=True, split=True,
+                                       **({} if states[l] is None else {"H": tables[l + 1], "state": states[l]}))
     if mine:
         # the BPR terms of layer l on the batch rows this rank owns (each is in the hop set)
         kernels.bpr_bwd(Tc, l, cu, cp, cn, reg, coef, gout, dXd_out, row_map=kernels.map_compose(rows.local, hmap))
         kernels.map_compose(hr, None, shard.lo, out=ids[int(off[k]):int(off[k + 1])])
     pend = [comm.gather_v(own, Pg, off), comm.gather_v(ids[int(off[k]):int(off[k + 1])], ids, off)] \
         if comm.active else []
+    reduce_w(l, list(wgrads()))
     for p in pend:
         p.wait()
     if total:
