@@ -293,14 +293,14 @@ class ShardedGradSync:
         if self.pipeline and 1 <= k <= n:
             # block k-1's owner step + broadcast, issued behind block k's reduce (the same collective order
             # on every rank); it runs while the next blocks are computed
-            self._owner_step(k - 1)
+            self._owner_step(k - 1, self._early)
 
     def _side_stream(self, dev) -> torch.cuda.Stream:
         if self._side is None:
             self._side = torch.cuda.Stream(device=dev)
         return self._side
 
-    def _owner_step(self, j: int) -> None:
+    def _owner_step(self, j: int, early) -> None:
         """Pipelined sharded exchange (``pipeline``): the owner of main block j (rank j) takes its Adam step on
         the block as soon as the block's reduce lands -- on a side stream, behind that reduce only -- and
         broadcasts the updated rows; every other rank receives them into its replica.  Block j's wire time
@@ -309,7 +309,7 @@ class ShardedGradSync:
         the owned block's own state -- the bits of the reduce-scatter / owned-row Adam / all-gather path."""
         n = world()
         rank = _rank()
-        grad = self._early[0]
+        grad = early[0]
         p = self._table
         r0, r1 = self.bounds[j]
         self._stepped.add(j)
@@ -318,7 +318,7 @@ class ShardedGradSync:
             opt = model._cf_optimizer
             side = self._side_stream(grad.device)
             with torch.cuda.stream(side):
-                self._early[1][j].wait()  # the side stream waits for the reduce; the compute stream does not
+                early[1][j].wait()  # the side stream waits for the reduce; the compute stream does not
                 gv = grad[r0:r1]
                 gv.div_(n)
                 from . import kernels
@@ -365,7 +365,7 @@ class ShardedGradSync:
                 if self.pipeline:
                     for j in range(n):
                         if j not in self._stepped:
-                            self._owner_step(j)
+                            self._owner_step(j, early)
                     rr = []
                     if main < g.shape[0]:  # the tail rows: all-reduced, every rank steps them
                         early[1][n].wait()
