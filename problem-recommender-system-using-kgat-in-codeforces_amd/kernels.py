@@ -114,7 +114,8 @@ def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False
               int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
     if ev is not None:
         e1.record()
-        ev.append((e0, e1, d, transpose, ("block", int(csr.n_rows), int(csr.col.numel()), bool(accumulate))))
+        nnz = csr.nnz if hasattr(csr, "nnz") else csr.col.numel()  # a row view (_CSRRowView) or a whole CSR
+        ev.append((e0, e1, d, transpose, ("block", int(csr.n_rows), int(nnz), bool(accumulate))))
     return out
 
 
