@@ -102,6 +102,8 @@ __device__ __forceinline__ void nfm_layer(const NfmNet& N, const NfmLds& plan, c
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) acc[nb] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int wp = WLDS ? plan.w_pitch[l] : 0;
+  // global weights (too large for LDS): 16-byte fragment loads where the rows allow them
+  const bool w4 = !WLDS && (din & 3) == 0 && (reinterpret_cast<uintptr_t>(N.W[l]) & 15) == 0;
   const float* wlds = WLDS ? smem + plan.w_off[l] + cl * wp + 4 * g : nullptr;
   const float* a_row = tile + cl * P + 4 * g;
   for (int k0 = 0; k0 < kpad; k0 += 16) {  // one A fragment feeds NB interleaved MFMA chains
@@ -115,10 +117,14 @@ __device__ __forceinline__ void nfm_layer(const NfmNet& N, const NfmLds& plan, c
       } else {
         const int n = nbc * 16 + cl, kk = k0 + 4 * g;
         const float* wr = N.W[l] + static_cast<int64_t>(n < dout ? n : 0) * din;
-        b4[nb].x = (n < dout && kk < din) ? wr[kk] : 0.f;
-        b4[nb].y = (n < dout && kk + 1 < din) ? wr[kk + 1] : 0.f;
-        b4[nb].z = (n < dout && kk + 2 < din) ? wr[kk + 2] : 0.f;
-        b4[nb].w = (n < dout && kk + 3 < din) ? wr[kk + 3] : 0.f;
+        if (w4 && n < dout && kk + 3 < din) {
+          b4[nb] = *reinterpret_cast<const float4*>(wr + kk);  // one 16-byte load (L1 / L2 resident weights)
+        } else {
+          b4[nb].x = (n < dout && kk < din) ? wr[kk] : 0.f;
+          b4[nb].y = (n < dout && kk + 1 < din) ? wr[kk + 1] : 0.f;
+          b4[nb].z = (n < dout && kk + 2 < din) ? wr[kk + 2] : 0.f;
+          b4[nb].w = (n < dout && kk + 3 < din) ? wr[kk + 3] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -150,7 +156,14 @@ __device__ __forceinline__ void nfm_layer(const NfmNet& N, const NfmLds& plan, c
   wave_lds_sync();
 }
 
-template <int NC, bool WLDS>
+// Column j of pooling slot k of lane cl: V4 (d % 4 == 0, 16-byte aligned rows) -- each lane loads float4s,
+// slots 4f..4f+3 = columns 4 cl + 64 f + t; otherwise one float per slot, columns cl + 16 k.
+template <bool V4>
+__device__ __forceinline__ int pool_col(int cl, int k) {
+  return V4 ? 4 * cl + 64 * (k >> 2) + (k & 3) : cl + 16 * k;
+}
+
+template <int NC, bool WLDS, bool V4>
 __device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan, const float* smem, float* tile,
                                              int64_t row0, const int64_t* __restrict__ rowptr,
                                              const int64_t* __restrict__ col, const float* __restrict__ val,
@@ -168,8 +181,9 @@ __device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan
   float colm[NC];
 #pragma unroll
   for (int k = 0; k < NC; ++k) {  // this lane's pooling columns, clamped to the row (exact x*v*1 when inside)
-    colk[k] = cl + 16 * k < d ? cl + 16 * k : d - 1;
-    colm[k] = cl + 16 * k < d ? 1.f : 0.f;
+    const int j = pool_col<V4>(cl, k);
+    colk[k] = j < d ? j : d - 1;
+    colm[k] = j < d ? 1.f : 0.f;
   }
   // round rr pools row rr*4 + g; lane cl holds entry beg + cl (past the end: x = 0),
   // and the next round's entries are loaded while this round's rows are fetched
@@ -211,8 +225,20 @@ __device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan
           const uint32_t c = static_cast<uint32_t>(__shfl(c_l, src));
           xb[u] = k0 + u < 16 ? __shfl(x_l, src) : 0.f;
           const float* v = N.V + static_cast<uint64_t>(c) * static_cast<uint32_t>(N.ldv);
+          if constexpr (V4) {
 #pragma unroll
-          for (int k = 0; k < NC; ++k) vb[u][k] = v[colk[k]];  // unconditional: columns clamped, masked below
+            for (int f = 0; f < NC / 4; ++f) {  // one 16-byte load per 4 columns (the row's bytes in 1/4 the loads)
+              const int c4 = 4 * cl + 64 * f;
+              const float4 x4 = c4 < d ? *reinterpret_cast<const float4*>(v + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+              vb[u][4 * f] = x4.x;
+              vb[u][4 * f + 1] = x4.y;
+              vb[u][4 * f + 2] = x4.z;
+              vb[u][4 * f + 3] = x4.w;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < NC; ++k) vb[u][k] = v[colk[k]];  // unconditional: columns clamped, masked below
+          }
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u)
@@ -230,7 +256,7 @@ __device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan
     float* ar = act && r < rows ? act + r * aw : nullptr;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      const int j = cl + 16 * k;
+      const int j = pool_col<V4>(cl, k);
       if (j < dpad) {
         const float z = j < d ? 0.5f * (s[k] * s[k] - q[k]) : 0.f;
         tile[m * P + j] = z;
@@ -267,7 +293,7 @@ __device__ __forceinline__ void nfm_fwd_tile(const NfmNet& N, const NfmLds& plan
   wave_lds_sync();  // the tile is free for the wave's next rows
 }
 
-template <int NC, bool WLDS>
+template <int NC, bool WLDS, bool V4>
 __global__ __launch_bounds__(256, NC <= 4 ? 3 : NC <= 8 ? 2 : 1) void nfm_fwd_kernel(NfmNet N, NfmLds plan, const int64_t* __restrict__ rowptr,
                                                       const int64_t* __restrict__ col, const float* __restrict__ val,
                                                       int64_t rows, float* __restrict__ act, float* __restrict__ y) {
@@ -298,7 +324,7 @@ __global__ __launch_bounds__(256, NC <= 4 ? 3 : NC <= 8 ? 2 : 1) void nfm_fwd_ke
   // persistent: the block walks 64-row groups (the staged weights serve them all)
   for (int64_t grp = blockIdx.x; grp * 64 < rows; grp += gridDim.x) {
     const int64_t row0 = grp * 64 + wv * 16;
-    if (row0 < rows) nfm_fwd_tile<NC, WLDS>(N, plan, smem, tile, row0, rowptr, col, val, rows, act, y);
+    if (row0 < rows) nfm_fwd_tile<NC, WLDS, V4>(N, plan, smem, tile, row0, rowptr, col, val, rows, act, y);
   }
 }
 
@@ -714,10 +740,14 @@ extern "C" int kgat_nfm_fwd_f32(const kgat_nfm* net, const int64_t* rowptr, cons
   const size_t lds = sizeof(float) * static_cast<size_t>(plan.total);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nc = dmax <= 64 ? 4 : dmax <= 128 ? 8 : 16;
+  // float4 pooling loads where the feature rows allow them (bit-identical: per column the same sums)
+  const bool v4 = (N.dims[0] & 3) == 0 && (N.ldv & 3) == 0 && (reinterpret_cast<uintptr_t>(N.V) & 15) == 0;
   using Fn = void (*)(kgat::NfmNet, kgat::NfmLds, const int64_t*, const int64_t*, const float*, int64_t, float*, float*);
-  Fn fn = nc == 4    ? (plan.wlds ? kgat::nfm_fwd_kernel<4, true> : kgat::nfm_fwd_kernel<4, false>)
-          : nc == 8  ? (plan.wlds ? kgat::nfm_fwd_kernel<8, true> : kgat::nfm_fwd_kernel<8, false>)
-                     : (plan.wlds ? kgat::nfm_fwd_kernel<16, true> : kgat::nfm_fwd_kernel<16, false>);
+#define KGAT_NFM_FN(NCV, W) (v4 ? kgat::nfm_fwd_kernel<NCV, W, true> : kgat::nfm_fwd_kernel<NCV, W, false>)
+  Fn fn = nc == 4    ? (plan.wlds ? KGAT_NFM_FN(4, true) : KGAT_NFM_FN(4, false))
+          : nc == 8  ? (plan.wlds ? KGAT_NFM_FN(8, true) : KGAT_NFM_FN(8, false))
+                     : (plan.wlds ? KGAT_NFM_FN(16, true) : KGAT_NFM_FN(16, false));
+#undef KGAT_NFM_FN
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
