@@ -678,6 +678,10 @@ int kgat_ids_check(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *ba
  * the caller zeroes it after reporting the error. */
 int kgat_ids_check_ex(const kgat_ids *ids, int64_t bound, int64_t *out, int32_t *bad, int32_t *bad_dev,
                       void *stream);
+/* ... with one bound per array (bounds[k] for ids->ptr[k]): the KG step's heads / tails (node count) and
+ * relations (relation count) checked and copied in one launch (the captured step's static input). */
+int kgat_ids_check_multi(const kgat_ids *ids, const int64_t *bounds, int64_t *out, int32_t *bad, int32_t *bad_dev,
+                         void *stream);
 
 /* node_map[ids[i]] = i for i < n (ids distinct; negative ids skipped): the node -> compact row
  * map of a row list (the row-sharded backward's global batch rows, whose compact order is the

@@ -210,6 +210,7 @@ _SIGNATURES = {
                                                       c_i64, c_vp]),
     "kgat_ids_check": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp]),
     "kgat_ids_check_ex": (ctypes.c_int, [ctypes.POINTER(Ids), c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "kgat_ids_check_multi": (ctypes.c_int, [ctypes.POINTER(Ids), ctypes.POINTER(c_i64), c_vp, c_vp, c_vp, c_vp]),
     "kgat_gemm_f32": (ctypes.c_int, [c_i32, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
                                      c_i64, c_i64, c_i64, c_i32, c_vp]),
     "kgat_comm_load": (ctypes.c_int, [ctypes.c_char_p]),

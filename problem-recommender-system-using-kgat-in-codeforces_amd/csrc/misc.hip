@@ -48,7 +48,11 @@ __global__ __launch_bounds__(256) void gather_kernel(const float* __restrict__ s
 
 // ids of up to KGAT_IDS_MAX arrays, concatenated into out; out-of-range ids become 0 and set *bad = 1
 // (and *bad_dev = 1 when given: the optimiser kernels' skip flag)
-__global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t total, int64_t bound,
+struct IdBounds {
+  int64_t b[KGAT_IDS_MAX];
+};
+
+__global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t total, IdBounds bounds,
                                                         int64_t* __restrict__ out, int32_t* __restrict__ bad,
                                                         int32_t* __restrict__ bad_dev) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -58,7 +62,7 @@ __global__ __launch_bounds__(256) void ids_check_kernel(kgat_ids ids, int64_t to
     int64_t off = i;
     while (k + 1 < ids.count && off >= ids.n[k]) off -= ids.n[k++];
     const int64_t v = ids.ptr[k][off];
-    const bool ok = v >= 0 && v < bound;
+    const bool ok = v >= 0 && v < bounds.b[k];
     out[i] = ok ? v : 0;
     flag |= !ok;
   }
@@ -610,15 +614,25 @@ extern "C" int kgat_ids_check(const kgat_ids* ids, int64_t bound, int64_t* out, 
 
 extern "C" int kgat_ids_check_ex(const kgat_ids* ids, int64_t bound, int64_t* out, int32_t* bad, int32_t* bad_dev,
                                  void* stream) {
-  if (!ids || !out || !bad || ids->count < 1 || ids->count > KGAT_IDS_MAX || bound < 0) return KGAT_ERR_INVALID;
+  if (!ids || ids->count < 1 || ids->count > KGAT_IDS_MAX) return KGAT_ERR_INVALID;
+  int64_t b[KGAT_IDS_MAX];
+  for (int k = 0; k < ids->count; ++k) b[k] = bound;
+  return kgat_ids_check_multi(ids, b, out, bad, bad_dev, stream);
+}
+
+extern "C" int kgat_ids_check_multi(const kgat_ids* ids, const int64_t* bounds, int64_t* out, int32_t* bad,
+                                    int32_t* bad_dev, void* stream) {
+  if (!ids || !bounds || !out || !bad || ids->count < 1 || ids->count > KGAT_IDS_MAX) return KGAT_ERR_INVALID;
+  kgat::IdBounds bb{};
   int64_t total = 0;
   for (int k = 0; k < ids->count; ++k) {
-    if (ids->n[k] < 0 || (ids->n[k] && !ids->ptr[k])) return KGAT_ERR_INVALID;
+    if (ids->n[k] < 0 || (ids->n[k] && !ids->ptr[k]) || bounds[k] < 0) return KGAT_ERR_INVALID;
     total += ids->n[k];
+    bb.b[k] = bounds[k];
   }
   if (total == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::ids_check_kernel, dim3(kgat::blocks_for(total, 256, kgat::kCUs * 4)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), *ids, total, bound, out, bad, bad_dev);
+                     reinterpret_cast<hipStream_t>(stream), *ids, total, bb, out, bad, bad_dev);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

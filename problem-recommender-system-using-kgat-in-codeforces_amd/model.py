@@ -198,6 +198,24 @@ class _IdGuard:
         self._pending = what
         return outs
 
+    def check_multi(self, what: str, ts, bounds, out: torch.Tensor, device) -> None:
+        """The captured KG step's check: ``ts`` (<= KGAT_IDS_MAX int64 contiguous 1-D device tensors) checked
+        against their own bounds (a ctypes int64 array) and copied, concatenated, into the preallocated ``out``
+        in one launch (kgat_ids_check_multi)."""
+        self.raise_pending()
+        if self._host is None:
+            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._event = torch.cuda.Event()
+            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+        d = _lib.Ids()
+        for k, t in enumerate(ts):
+            d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
+        d.count = len(ts)
+        _lib.call("kgat_ids_check_multi", ctypes.byref(d), bounds, out.data_ptr(), self._host.data_ptr(),
+                  self._dev.data_ptr(), stream_ptr(device))
+        self._event.record()
+        self._pending = what
+
 
 class _TableUpdate:
     """The CF step's table gradient left unmaterialised until ``update_cf_weights`` (opt-in:
@@ -422,26 +440,28 @@ class _LazyKGAdam:
 
 
 class _KGStepGraph:
-    """The KG step captured as three HIP graphs (opt-in: ``KGAT.capture_kg_step``; with the fused KG
-    table update and the lazy KG Adam, as driver.py trains).
+    """The KG step captured as HIP graphs (opt-in: ``KGAT.capture_kg_step``; with the fused KG table update
+    and the lazy KG Adam, as driver.py trains).
 
     The reference KG step is ``loss = model(h, r, t+, t-, mode=TRAIN_KG); loss.backward();
-    model.update_kg_weights()`` (main.py:334-342; model.py:204-261, 414-419).  Eagerly that is ~10
+    model.update_kg_weights()`` (main.py:334-342; model.py:204-261, 414-419).  Eagerly that is ~13
     launches wrapped in ~0.2 ms of Python, ctypes and autograd work for ~0.12 ms of kernels at C2.
-    Here each of the three calls replays one graph captured once per shape:
-      forward  -- frontier_build (the batch rows' map), the lazy Adam catch-up of those rows, TransR
-                  forward (loss + the backward's work buffer);
-      backward -- TransR backward: the table gradient's compact rows, d_rel, d_trans;
-      update   -- kgat_step_advance (the device step counter), the lazy table Adam on the batch rows,
-                  the Adam of the relation embeddings and trans matrices, frontier_reset.
-    Only the id check (2 launches copying the caller's ids into the graphs' static buffers) and the
-    loss copy run outside.  A graph replays its captured kernel arguments, so the step's scalars live
-    on the device: t_dev (advanced by the update graph) indexes schedule tables of the step size and
-    sqrt(1 - beta2^t) that the host fills with FusedAdam's own expressions -- the same floats the eager
-    launches get -- and the host keeps the optimiser's step counters in step.  The gradients of the
-    three parameters stay in the graph's buffers between backward and update (``.grad`` stays None, as
-    with the fused table updates); anything that needs them materialises them.  Same bits as the
-    eager step (tests/test_gpu_parity.py::test_captured_kg_step_bit_identical)."""
+    Here the forward and the update each replay one graph captured once per shape:
+      forward -- frontier_build (the batch rows' map), the lazy Adam catch-up of those rows, TransR
+                 forward (loss + the backward's work buffer);
+      update  -- TransR backward (the table gradient's compact rows, d_rel, d_trans), kgat_step_advance
+                 (the device step counter), the lazy table Adam on the batch rows, the Adam of the
+                 relation embeddings and trans matrices, frontier_reset.
+    ``loss.backward()`` only copies its upstream gradient into the graphs' input (the backward kernels
+    run in the update graph, so one replay fewer); a third graph -- the TransR backward alone -- serves
+    anything that needs the gradients before the update (``materialize``).  Outside the graphs: one id
+    check (kgat_ids_check_multi: the caller's ids checked and copied into the static inputs) and the loss
+    copy.  A graph replays its captured kernel arguments, so the step's scalars live on the device:
+    t_dev (advanced by the update graph) indexes schedule tables of the step size and sqrt(1 - beta2^t)
+    that the host fills with FusedAdam's own expressions -- the same floats the eager launches get -- and
+    the host keeps the optimiser's step counters in step.  The three parameters' ``.grad`` stay None
+    between backward and update, as with the fused table updates.  Same bits as the eager step
+    (tests/test_gpu_parity.py::test_captured_kg_step_bit_identical)."""
 
     SCHED = 1 << 16  # initial schedule entries (steps); doubled (and the graphs recaptured) when t reaches them
 
@@ -449,11 +469,12 @@ class _KGStepGraph:
         self.model = model
         self.enabled = False
         self.key = None
-        self.g = None       # (forward, backward, update) graphs
+        self.g = None       # {"fwd", "bwd", "upd"} graphs
         self.buf = None     # static tensors of the captured step
-        self.pending = None  # "fwd" after a forward replay, "bwd" after a backward replay
+        self.pending = None  # "fwd" after a forward replay, "bwd" once backward copied its gradient in
         self.t_dev_value = None  # the host's view of t_dev
         self._sched = None  # (key, sz, bc)
+        self._bounds = (ctypes.c_int64 * _lib.KGAT_IDS_MAX)()
         self.replays = 0
 
     # ---------------------------------------------------------------- eligibility
@@ -463,19 +484,23 @@ class _KGStepGraph:
         sts = [opt.state.get(id(p)) for p in ps]
         return ps, sts
 
-    def usable(self, ids, opt) -> bool:
+    def usable(self, ids, opt):
+        """The three parameters' KG optimiser states when the captured step applies, else None."""
         m = self.model
         if not (self.enabled and m._kg_table_update.enabled and m._lazy_kg.enabled and opt is not None):
-            return False
+            return None
         B = ids[0].numel()
-        if B == 0 or not all(torch.is_tensor(t) and t.is_cuda and t.numel() == B for t in ids):
-            return False
+        if B == 0 or not all(torch.is_tensor(t) and t.is_cuda and t.dtype == torch.int64 and t.dim() == 1
+                             and t.is_contiguous() and t.numel() == B for t in ids):
+            return None
         if not m._kg_table_update.wants(B) or m._lazy_kg.last is None or m._ids.skip_flag() is None:
-            return False
+            return None
         ps, sts = self._states(opt)
         if any(st is None for st in sts) or len({int(st["step"]) for st in sts}) != 1:
-            return False  # the first KG step (and a state restored out of step) runs eagerly
-        return not any(p.grad is not None for p in ps)
+            return None  # the first KG step (and a state restored out of step) runs eagerly
+        if any(p.grad is not None for p in ps):
+            return None
+        return ps, sts
 
     # ---------------------------------------------------------------- schedule + capture
     def _schedule(self, opt, dev, need: int):
@@ -493,21 +518,21 @@ class _KGStepGraph:
             self._sched = (key, torch.from_numpy(sz).to(dev), torch.from_numpy(bc).to(dev))
         return self._sched[1], self._sched[2]
 
-    def _key(self, B, opt):
+    def _key(self, B, opt, ps, sts):
+        """Everything the graphs captured by address: a change (another optimiser, reallocated state or
+        parameters, a new lazy record) recaptures them."""
         m = self.model
-        ps, sts = self._states(opt)
         lz = m._lazy_kg
-        return (B, id(opt), opt.beta1, opt.beta2, opt.eps, float(m._regularization_params[1]),
+        return (B, opt.beta1, opt.beta2, opt.eps, float(m._regularization_params[1]),
                 self._sched[1].data_ptr(), self._sched[2].data_ptr(),
                 *(p.data_ptr() for p in ps), *(st[k].data_ptr() for st in sts for k in ("exp_avg", "exp_avg_sq")),
                 lz.last.data_ptr(), *(h.data_ptr() for h in lz.hist), m._kg_table_update.node_map().data_ptr(),
                 m._ids.skip_flag().data_ptr())
 
-    def _capture(self, B, opt):
+    def _capture(self, B, opt, ps, sts):
         m = self.model
         dev = m._user_entity_embedding.weight.device
         sz, bc = self._sched[1], self._sched[2]
-        ps, sts = self._states(opt)
         emb, rel, trans = (p.data for p in ps)
         lz = m._lazy_kg
         hs, hb, hk = lz.hist
@@ -516,93 +541,97 @@ class _KGStepGraph:
         n, d = emb.shape
         n_rel, k = rel.shape
         reg = float(m._regularization_params[1])
-        b = {"hpq": torch.zeros(3 * B, dtype=torch.int64, device=dev),
-             "rels": torch.zeros(B, dtype=torch.int64, device=dev),
+        b = {"ids": torch.zeros(4 * B, dtype=torch.int64, device=dev),  # heads | pos | neg | relations
              "gout": torch.ones(1, dtype=torch.float32, device=dev),
              "t": torch.zeros(1, dtype=torch.int32, device=dev)}
-        h, p, q = b["hpq"][:B], b["hpq"][B:2 * B], b["hpq"][2 * B:]
-        r = b["rels"]
+        h, p, q, r = b["ids"].split(B)
         ev = (kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS)
         kernels.KERNEL_EVENTS = kernels.SPMM_EVENTS = None  # no event records inside a capture
         pool = torch.cuda.graph_pool_handle()
-        g = [torch.cuda.CUDAGraph() for _ in range(3)]
+        g = {key: torch.cuda.CUDAGraph() for key in ("fwd", "bwd", "upd")}
+
+        def update_kernels(Gc, d_rel, d_trans):
+            st_ = stream_ptr(dev)
+            _lib.call("kgat_step_advance", b["t"].data_ptr(), st_)
+            _lib.call("kgat_adam_lazy_rows_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
+                      sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
+                      Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,
+                      b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), opt.beta1, opt.beta2, opt.eps,
+                      skip.data_ptr(), st_)
+            arr = (_lib.AdamTensor * 2)()
+            for a, (pp, gg, stt) in zip(arr, ((rel, d_rel, sts[1]), (trans, d_trans, sts[2]))):
+                a.p, a.g, a.m, a.v = pp.data_ptr(), gg.data_ptr(), stt["exp_avg"].data_ptr(), stt["exp_avg_sq"].data_ptr()
+                a.n, a.step_size, a.bc2_sqrt = pp.numel(), 0.0, 0.0
+            _lib.call("kgat_adam_multi_sched_f32", arr, 2, opt.beta1, opt.beta2, opt.eps, skip.data_ptr(),
+                      b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), st_)
+            kernels.frontier_reset(rows, row_map)
+
         try:
             torch.cuda.synchronize(dev)
-            with torch.cuda.graph(g[0], pool=pool):
+            with torch.cuda.graph(g["fwd"], pool=pool):
                 rows, _ = kernels.frontier_build(h, p, q, row_map)
-                st_ = stream_ptr(dev)
                 _lib.call("kgat_adam_lazy_catchup_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
                           sts[0]["exp_avg_sq"].data_ptr(), n, d, rows.data_ptr(), rows.numel(), lz.last.data_ptr(),
                           b["t"].data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP, opt.beta1, opt.beta2,
-                          opt.eps, st_)
+                          opt.eps, stream_ptr(dev))
                 loss, work = kernels.transr_fwd(emb, rel, trans, h, r, p, q, reg)
-            with torch.cuda.graph(g[1], pool=pool):
-                Gc, d_rel, d_trans = kernels.transr_bwd_compact(emb, n_rel, k, h, r, p, q, work, b["gout"], row_map,
-                                                                rows.numel())
-            with torch.cuda.graph(g[2], pool=pool):
-                st_ = stream_ptr(dev)
-                _lib.call("kgat_step_advance", b["t"].data_ptr(), st_)
-                _lib.call("kgat_adam_lazy_rows_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
-                          sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
-                          Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,
-                          b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), opt.beta1, opt.beta2, opt.eps,
-                          skip.data_ptr(), st_)
-                arr = (_lib.AdamTensor * 2)()
-                for a, (pp, gg, stt) in zip(arr, ((rel, d_rel, sts[1]), (trans, d_trans, sts[2]))):
-                    a.p, a.g, a.m, a.v = pp.data_ptr(), gg.data_ptr(), stt["exp_avg"].data_ptr(), stt["exp_avg_sq"].data_ptr()
-                    a.n, a.step_size, a.bc2_sqrt = pp.numel(), 0.0, 0.0
-                _lib.call("kgat_adam_multi_sched_f32", arr, 2, opt.beta1, opt.beta2, opt.eps, skip.data_ptr(),
-                          b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), st_)
-                kernels.frontier_reset(rows, row_map)
+            with torch.cuda.graph(g["bwd"], pool=pool):
+                grads = kernels.transr_bwd_compact(emb, n_rel, k, h, r, p, q, work, b["gout"], row_map, rows.numel())
+            with torch.cuda.graph(g["upd"], pool=pool):
+                update_kernels(*kernels.transr_bwd_compact(emb, n_rel, k, h, r, p, q, work, b["gout"], row_map,
+                                                           rows.numel()))
         finally:
             kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS = ev
-        b.update(rows=rows, loss=loss, work=work, Gc=Gc, d_rel=d_rel, d_trans=d_trans)
+        b.update(rows=rows, loss=loss, work=work, Gc=grads[0], d_rel=grads[1], d_trans=grads[2])
         self.g, self.buf = g, b
         self.t_dev_value = None
-        self.key = self._key(B, opt)
+        self.key = self._key(B, opt, ps, sts)
 
     # ---------------------------------------------------------------- the three calls
-    def forward(self, ids, opt) -> torch.Tensor:
+    def forward(self, ids, opt, ps, sts) -> torch.Tensor:
         """Replay the forward graph on the caller's ids (heads, relations, positive, negative tails)."""
         m = self.model
         B = ids[0].numel()
-        t = int(self._states(opt)[1][0]["step"])
+        t = int(sts[0]["step"])
         self._schedule(opt, m._user_entity_embedding.weight.device, t + 2)
-        if self.key != self._key(B, opt):
-            self._capture(B, opt)
+        if self.key != self._key(B, opt, ps, sts):
+            self._capture(B, opt, ps, sts)
         b = self.buf
         dev = b["t"].device
         n = m._user_num + m._entity_num
-        m._ids.check("TRAIN_KG ids", (ids[0], ids[2], ids[3]), n, dev, more=[((ids[1],), m._relation_num)],
-                     outs=(b["hpq"], b["rels"]))
+        bd = self._bounds
+        bd[0] = bd[1] = bd[2] = n
+        bd[3] = m._relation_num
+        m._ids.check_multi("TRAIN_KG ids", (ids[0], ids[2], ids[3], ids[1]), bd, b["ids"], dev)
         if self.t_dev_value != t:
             b["t"].fill_(t)  # eager steps ran since the last replay
             self.t_dev_value = t
-        self.g[0].replay()
+        self.g["fwd"].replay()
         self.pending = "fwd"
         self.replays += 1
         return b["loss"]
 
     def backward(self, gout: torch.Tensor) -> None:
+        """The upstream gradient into the graphs' input; the TransR backward runs in the update graph."""
         if self.pending != "fwd":
             raise RuntimeError("TRAIN_KG backward: the captured step's forward buffers were reused by a later "
                                "TRAIN_KG forward before this backward ran")
         self.buf["gout"].copy_(gout.reshape(1))
-        self.g[1].replay()
         self.pending = "bwd"
 
     def update(self, opt) -> None:
-        """The update graph: the host advances the three optimiser states' step counters as FusedAdam does."""
+        """The update graph (TransR backward + the three Adam steps): the host advances the optimiser
+        states' step counters as FusedAdam does."""
         m = self.model
         lz = m._lazy_kg
-        if lz._t(opt) + 1 - lz.flushed_at >= lz.CAP:
+        ps, sts = self._states(opt)
+        if int(sts[0]["step"]) + 1 - lz.flushed_at >= lz.CAP:
             lz.catch_up(opt)  # no row may fall a whole history behind
-        ps, _ = self._states(opt)
         for p in ps:
             opt._advance(id(p), p.data)
         lz.dirty = True
-        self.g[2].replay()
-        self.t_dev_value = int(self._states(opt)[1][0]["step"])
+        self.g["upd"].replay()
+        self.t_dev_value = int(sts[0]["step"])
         self.pending = None
 
     def release(self) -> None:
@@ -613,8 +642,8 @@ class _KGStepGraph:
 
     @torch.no_grad()
     def materialize(self) -> None:
-        """The pending step's gradients into ``.grad`` (the table: its compact rows scattered into a zero
-        [N, d] gradient, as the fused KG update's materialisation); the map is reset."""
+        """The pending step's gradients into ``.grad`` (the backward graph; the table's compact rows
+        scattered into a zero [N, d] gradient, as the fused KG update's materialisation); the map is reset."""
         if self.pending == "fwd":
             self.release()
             return
@@ -622,6 +651,7 @@ class _KGStepGraph:
             return
         m = self.model
         b = self.buf
+        self.g["bwd"].replay()
         emb = m._user_entity_embedding.weight
         g = kernels.zeros(tuple(emb.shape), emb.device)
         kernels.scatter_rows(g, b["rows"], b["Gc"][:b["rows"].numel()], accumulate=False)
@@ -636,19 +666,18 @@ class _KGStepGraph:
 
 class _KGGraphLoss(torch.autograd.Function):
     """The captured KG step's loss node: forward replays the forward graph (its loss copied out, so a
-    kept loss survives the next step), backward replays the backward graph (gradients stay in the
-    graph's buffers for the update graph)."""
+    kept loss survives the next step), backward hands the upstream gradient to the update graph."""
 
     @staticmethod
-    def forward(ctx, step, ids, opt, emb, rel_emb, trans):
+    def forward(ctx, step, ids, opt, states, emb, rel_emb, trans):
         ctx.step = step
-        return step.forward(ids, opt).clone().view(())
+        return step.forward(ids, opt, *states).clone().view(())
 
     @staticmethod
     def backward(ctx, gout):
         ctx.step.backward(gout.to(torch.float32))
         ctx.step = None
-        return None, None, None, None, None, None
+        return None, None, None, None, None, None, None
 
 
 class _MarkedBatch:
@@ -1214,8 +1243,9 @@ class KGAT(nn.Module):
         if step.enabled and torch.is_grad_enabled():
             step.release()  # a dropped captured forward's batch-row marks
             ids = tuple(torch.as_tensor(t) for t in (heads, relations, positive_tails, negative_tails))
-            if step.usable(ids, opt):
-                return _KGGraphLoss.apply(step, ids, opt, self._user_entity_embedding.weight,
+            states = step.usable(ids, opt)
+            if states is not None:
+                return _KGGraphLoss.apply(step, ids, opt, states, self._user_entity_embedding.weight,
                                           self._relation_embedding.weight, self._trans_matrix)
         h, p, q, r = self._ids.check("TRAIN_KG ids", (heads, positive_tails, negative_tails), n, dev,
                                      more=[((relations,), self._relation_num)])

@@ -6,6 +6,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k nfm > gpurun_out/r04_nfm_tests.log 2>&1 || { tail -30 gpurun_out/r04_nfm_tests.log; exit 1; }
+tail -1 gpurun_out/r04_nfm_tests.log
 timeout -k 10 600 python -u bench.py > gpurun_out/r04_c2_bench.log 2>&1 || { tail -30 gpurun_out/r04_c2_bench.log; exit 1; }
 tail -1 gpurun_out/r04_c2_bench.log | cut -c1-600
 timeout -k 10 600 python -u bench.py --config c3 > gpurun_out/r04_c3_bench.log 2>&1 || { tail -30 gpurun_out/r04_c3_bench.log; exit 1; }

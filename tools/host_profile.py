@@ -1,4 +1,5 @@
-"""Host-side profile of the CF training step (python tools/host_profile.py [--full] [--kg [--unfused]]: the
+"""Host-side profile of the CF training step (python tools/host_profile.py [--full] [--kg [--unfused | --lazy |
+--captured]]: the
 KG step instead): cProfile over
 200 steps of a small synthetic graph (host launch cost does not depend on the graph size), printing
 the functions with the most own time.  Used to find Python / ctypes overhead in the step's launches."""
@@ -37,7 +38,8 @@ def main():
     kg = "--kg" in sys.argv
     if kg:  # the KG phase's step (main.py:324-345) at the reference's B = 512, fused table update
         m.fuse_kg_table_update = "--unfused" not in sys.argv
-        m.lazy_kg_adam = "--lazy" in sys.argv
+        m.lazy_kg_adam = "--lazy" in sys.argv or "--captured" in sys.argv
+        m.capture_kg_step = "--captured" in sys.argv
         n = U + E
         batches = [[torch.from_numpy(x).to(dev) for x in (lay.heads[e], lay.rels[e], lay.tails[e],
                                                           rng.integers(0, n, 512))]
