@@ -88,6 +88,10 @@ def spmm_bytes(n: int, nnz: int, d: int, accumulate: bool) -> int:
     return 8 * (n + 1) + nnz * (8 + 4 * d) + 4 * n * d * (2 if accumulate else 1)
 
 
+CACHE_RESIDENT_BYTES = 64 << 20  # tables up to this size are served from L2 / the Infinity Cache (256 MiB)
+L2_GATHER_PEAK_GBS = 18800.0      # MI355X_MICROARCH.md: gathered rows served from the XCDs' L2, chip-wide
+
+
 def compulsory_bytes(n: int, nnz: int, d: int) -> int:
     """Bytes one SpMM launch cannot avoid: rowptr, col+val, every source row read once, output written."""
     return 8 * (n + 1) + 8 * nnz + 8 * n * d
@@ -308,7 +312,8 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(acc[1], acc[2], d, a), compulsory_bytes(acc[1], acc[2], d)))
         elif acc is False:
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(n, nnz, d, False), compulsory_bytes(n, nnz, d)))
-    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc not in ("masked", "fused_adam")]
+    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events
+           if tr and acc not in ("masked", "fused_adam", "reach")]
     masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc in ("masked", "fused_adam")]
     fused = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if acc == "fused_adam"]
     # the layer-0 launches (d0 wide; the row-sharded mode's gathered column chunks are narrower)
@@ -344,6 +349,14 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
                     "this kernel build) / live HIP-event launch time; the SURVEY §8d algorithmic formula prices "
                     "every gathered row as an HBM read although Zipf hub rows are served from L2 / the Infinity "
                     "Cache, so algorithmic_frac can exceed 1; compulsory = each source row read once"}
+    if 4 * n * d0 <= CACHE_RESIDENT_BYTES:
+        # a table this small stays in the XCDs' L2s and the Infinity Cache: the gathers never reach HBM
+        # after the first touch, so the HBM fraction says nothing; the bound is the cache's row-gather rate
+        roof["cache_roofline"] = {
+            "level": "L2 / Infinity Cache", "achieved": algo_gbs, "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
+            "frac": algo_gbs / L2_GATHER_PEAK_GBS, "table_bytes": 4 * n * d0,
+            "peak_source": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': rows shared by every workgroup "
+                           "(the XCD's L2) 16.8-18.8 TB/s chip-wide; the upper figure is the peak used"}
     spmm = {"fwd_launches": len(fwd), "bwd_launches": len(bwd), "fwd_avg_ms": avg_ms,
             "bwd_avg_ms": float(np.mean([t for t, _ in bwd])) if bwd else None,
             "bwd_masked_launches": len(masked), "bwd_masked_ms_per_step": sum(masked) / steps,
@@ -514,6 +527,30 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                     "does not visit every edge)"}
         if world > 1:
             result["frontier_forward"]["dp_table_exchange_steps"] = fr_exchange
+        else:
+            # + KGAT.lazy_cf_adam (the table Adam on the rows the step reads and reaches only, the others'
+            # zero-gradient steps replayed when next read; same bits, tests/test_gpu_parity.py) -- the
+            # training step driver.py runs
+            model.frontier_forward = model.lazy_cf_adam = True
+            lel, lev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            model.flush_cf_table()
+            torch.cuda.synchronize()
+            flush_ms = (time.perf_counter() - t1) * 1e3
+            model.frontier_forward = model.lazy_cf_adam = False
+            lms = lel / args.steps * 1e3
+
+            def ev_ms(tag):
+                t = [e0.elapsed_time(e1) for e0, e1, _d, _tr, acc in lev if acc == tag]
+                return float(np.mean(t)) if t else None
+            result["frontier_forward"]["lazy_cf_adam"] = {
+                "ms_per_step": lms, "bpr_pairs_per_s": B / (lms * 1e-3), "speedup_vs_dense_update": fms / lms,
+                "table_update_avg_ms": ev_ms("fused_adam"), "reach_catchup_avg_ms": ev_ms("reach"),
+                "flush_ms": flush_ms, "flush_steps_pending": args.warmup + args.steps,
+                "what": "frontier CF step with the lazy table Adam: the forward brings the rows it reads current "
+                        "(kgat_lazy_reach_catchup_f32), the fused product + Adam steps the rows its product reaches "
+                        "(kgat_spmm_csr_masked_adam_lazy_f32); flush_ms: every row brought current after the leg"}
     result["value_note"] = ("value = n_gpus x nnz x L / t_step: each data-parallel replica runs the reference step's "
                             "full propagation over every edge for its own 256-pair batch (weak scaling; replicas "
                             "repeat the same graph's work); bpr_pairs_per_s (and frontier_forward.bpr_pairs_per_s, "
@@ -525,8 +562,17 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         result["rehearsal"] = ("the N-rank table exchange forced at world 1 over RCCL (collectives move no data "
                                "between GPUs): its GPU + host overhead per step, not a scaling measurement")
     if world == 1 and not args.no_kg_leg and not args.exchange_at_1:
-        cf_ms = result.get("frontier_forward", {}).get("ms_per_step", ms)
+        fr = result.get("frontier_forward", {})
+        cf_ms = fr.get("lazy_cf_adam", fr).get("ms_per_step", ms)
         result["kg_refresh"] = kg_refresh_legs(model, pkg, layout, cfg, args, dev, len(inter), cf_ms)
+        lz_cf = fr.get("lazy_cf_adam")
+        if lz_cf is not None:
+            # the CF phase ends with one flush of the rows still owed steps (measured after the leg's
+            # warm-up + timed steps; rows are reached every few steps, so the epoch's is of that order)
+            ep = result["kg_refresh"]["epoch_estimate"]
+            ep["cf_flush_ms"] = lz_cf["flush_ms"]
+            ep["seconds"] += lz_cf["flush_ms"] / 1e3
+            ep["seconds_eager_lazy_kg"] += lz_cf["flush_ms"] / 1e3
     if ds is not None and cfg.get("nfm") and world == 1:
         result["nfm"] = nfm_legs(ds, cfg, args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -568,8 +614,11 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
     n, d = layout.n_nodes, cfg["dim"]
     E = int(layout.heads.size)
     rng = np.random.default_rng(11)
+    # a KG step is ~0.1-0.3 ms: time at least 100 of them (the default 20 would be ~3 ms of work, short
+    # enough for the clock ramp after the previous leg's sync to show); 32 distinct batches, cycled
+    steps = max(args.steps, 100)
     batches = []
-    for _ in range(args.warmup + args.steps):
+    for _ in range(32):
         e = rng.integers(0, E, B)
         batches.append([torch.from_numpy(np.asarray(x, np.int64)).to(dev)
                         for x in (layout.heads[e], layout.rels[e], layout.tails[e], rng.integers(0, n, B))])
@@ -587,19 +636,19 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         model.lazy_kg_adam = lazy
         model.capture_kg_step = cap
         for i in range(args.warmup):
-            kg_step(batches[i])
+            kg_step(batches[i % 32])
         torch.cuda.synchronize()
         # the step time without instrumentation (an event pair around every kernel costs the stream
         # and the host ~10-20 us each: it would be most of a 0.3 ms step), then the kernels' own times
         # from an instrumented pass over the same batches
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            kg_step(batches[args.warmup + i])
+        for i in range(steps):
+            kg_step(batches[(args.warmup + i) % 32])
         torch.cuda.synchronize()
-        el = (time.perf_counter() - t0) / args.steps * 1e3
+        el = (time.perf_counter() - t0) / steps * 1e3
         kernels.KERNEL_EVENTS = {}
-        for i in range(min(args.steps, 8)):
-            kg_step(batches[args.warmup + i])
+        for i in range(8):
+            kg_step(batches[(args.warmup + i) % 32])
         torch.cuda.synchronize()
         evs, kernels.KERNEL_EVENTS = kernels.KERNEL_EVENTS, None
         leg = {"ms_per_step": el, "kg_pairs_per_s": B / (el * 1e-3)}
@@ -609,7 +658,7 @@ def kg_refresh_legs(model, pkg, layout, cfg, args, dev, n_interactions: int, cf_
         if lazy:
             # the flush that brings every row current (before the next CF step): here after the leg's
             # warmup + 2 x steps KG steps, i.e. that many zero-gradient steps replayed for almost every row
-            pend = args.warmup + args.steps + min(args.steps, 8)
+            pend = args.warmup + steps + 8
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             model.flush_kg_table()

@@ -90,6 +90,28 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = p + (-step_size) * (m / (sqrtf(v) / bc2s + eps));
 }
 
+// Lazy table Adam (a table's Adam on the rows a step touches only).  The dense step moves every row
+// each step -- rows with a zero gradient too, which still decays their moments and moves p.  Here a
+// row keeps the number of the last step applied to it (last[row]); the steps it skipped are replayed
+// in order, with their own step size and bias correction (kept on the device, entry s % cap of the
+// history) and the same adam_elem(g = 0) arithmetic, when it is next read or updated, and for every
+// row at a flush.  Each element's sequence of operations is the dense step's: the same bits.
+struct LazyHist {
+  float* sz;
+  float* bc;
+  int32_t* skip;
+  int32_t cap;
+};
+
+__device__ __forceinline__ void lazy_replay(float& p, float& m, float& v, int32_t from, int32_t to, const LazyHist& h,
+                                            float w1, float b2, float w2, float eps) {
+  for (int32_t s = from + 1; s <= to; ++s) {
+    const int32_t j = s % h.cap;
+    if (h.skip[j] != 0) continue;
+    adam_elem(p, 0.f, m, v, w1, b2, w2, h.sz[j], h.bc[j], eps);
+  }
+}
+
 inline int blocks_for(int64_t work, int per_block, int cap) {
   int64_t b = (work + per_block - 1) / per_block;
   if (b < 1) b = 1;

@@ -337,29 +337,8 @@ extern "C" int kgat_adam_rows_f32(float* p, float* m, float* v, int64_t n_rows, 
 
 namespace kgat {
 
-// Lazy table Adam (the KG phase's table update on the batch rows only).  The dense step moves every
-// row each step -- rows outside the batch with a zero gradient, which still decays their moments and
-// moves p.  Here a row keeps the number of the last step applied to it (last[row]); the steps it
-// skipped are replayed in order, with their own step size and bias correction (kept on the device,
-// entry s % cap of the history) and the same adam_elem(g = 0) arithmetic, when it is next read or
-// updated, and for every row at a flush.  Each element's sequence of operations is the dense step's,
-// so the values are the same bits.  A row's elements are threads of one block (256 % d == 0).
-struct LazyHist {
-  float* sz;
-  float* bc;
-  int32_t* skip;
-  int32_t cap;
-};
-
-__device__ __forceinline__ void lazy_replay(float& p, float& m, float& v, int32_t from, int32_t to, const LazyHist& h,
-                                            float w1, float b2, float w2, float eps) {
-  for (int32_t s = from + 1; s <= to; ++s) {
-    const int32_t j = s % h.cap;
-    if (h.skip[j] != 0) continue;
-    adam_elem(p, 0.f, m, v, w1, b2, w2, h.sz[j], h.bc[j], eps);
-  }
-}
-
+// Lazy table Adam of the KG phase (common.hpp's LazyHist / lazy_replay): the batch rows only.  A
+// row's elements are threads of one block (256 % d == 0).
 // rows (nullable = every row): bring the listed rows up to step t (replay only).
 __global__ __launch_bounds__(256) void adam_lazy_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
                                                                 float* __restrict__ v, int d,

@@ -64,6 +64,29 @@ __device__ __forceinline__ void adam_row_step(const SpmmAdam& a, int64_t row, in
   __builtin_nontemporal_store(r.v, reinterpret_cast<floatx4*>(a.v + o));
 }
 
+// Lazy step t on one row segment: its skipped steps replayed first (rows the forward's
+// kgat_lazy_reach_catchup_f32 brought current replay none), then step t with gradient g.
+__device__ __forceinline__ void adam_row_lazy(const SpmmAdam& a, int64_t row, int gl, float4 g) {
+  const int32_t from = a.last[row];
+  AdamRow r = adam_row_load(a, row, gl);
+  const float w1 = 1.f - a.b1, w2 = 1.f - a.b2;
+  const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float pk = r.p[k], mk = r.m[k], vk = r.v[k];
+    lazy_replay(pk, mk, vk, from, a.t - 1, a.hist, w1, a.b2, w2, a.eps);
+    adam_elem(pk, gg[k], mk, vk, w1, a.b2, w2, a.step_size, a.bc2s, a.eps);
+    r.p[k] = pk;
+    r.m[k] = mk;
+    r.v[k] = vk;
+  }
+  const int64_t o = row * a.ld + 4 * gl;
+  __builtin_nontemporal_store(r.p, reinterpret_cast<floatx4*>(a.p + o));
+  __builtin_nontemporal_store(r.m, reinterpret_cast<floatx4*>(a.m + o));
+  __builtin_nontemporal_store(r.v, reinterpret_cast<floatx4*>(a.v + o));
+  if (gl == 0) a.last[row] = a.t;  // the group's lanes (one wave) all read last[row] above
+}
+
 // Final write of one output row segment (lane gl) in the five modes: row is
 // the (global-id) row of A, out the row of Y it lands in (row, or its position
 // in the output set for kMaskedRows).  kMaskedAdam writes no Y: the row is the
@@ -83,6 +106,10 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
   if (MODE == kMaskedAdam) {
+    if (io.adam.last != nullptr) {
+      if (any) adam_row_lazy(io.adam, row, gl, acc);
+      return;
+    }
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
     return;
   }
@@ -137,7 +164,17 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
-  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if (MODE == kMaskedAdam) {
+    const bool skipped = io.adam.skip != nullptr && *io.adam.skip != 0;
+    if (io.adam.last != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+      // step t's scalars and skip flag, for the rows whose step t is replayed later
+      const int32_t j = io.adam.t % io.adam.hist.cap;
+      io.adam.hist.sz[j] = io.adam.step_size;
+      io.adam.hist.bc[j] = io.adam.bc2s;
+      io.adam.hist.skip[j] = skipped ? 1 : 0;
+    }
+    if (skipped) return;
+  }
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base);
@@ -204,7 +241,9 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if (threadIdx.x < L) {
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
-    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
+    // a long row is always stepped by the lazy update (its segments' hits are not collected; a
+    // zero row's step t is the replay's adam_elem(g = 0) either way)
+    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t, MODE == kMaskedAdam);
   }
 }
 
@@ -543,8 +582,121 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                  int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                                  const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                                  int32_t d, float step_size, float beta1, float beta2,
+                                                  float bc2_sqrt, float eps, const int32_t* skip, int32_t* last,
+                                                  int32_t t, float* hist_sz, float* hist_bc, int32_t* hist_skip,
+                                                  int32_t cap, float* workspace, int64_t workspace_floats,
+                                                  void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
+    return KGAT_ERR_INVALID;
+  if (!last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1) return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
+      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
+            nullptr, nullptr, nullptr, nullptr};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, last, t,
+                     LazyHist{hist_sz, hist_bc, hist_skip, cap}};
+  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace kgat {
+
+// The lazy CF table Adam's forward half: the rows the frontier forward's first restricted layer reads
+// -- its output set S (set_bits) and every column of A's rows S, i.e. every row of A^T with an edge
+// into S -- brought up to step t (their skipped steps replayed, LazyHist).  Rows already at t are
+// passed over without a scan; a row of A^T longer than the long-row threshold is brought up to t
+// without one (a current row is read the same by anyone).  Groups of D/4 lanes, one row at a time,
+// the membership scan a ballot per D/4 edges that stops at the first hit.
+template <int D>
+__global__ __launch_bounds__(256) void lazy_reach_kernel(kgat_csr AT, const uint32_t* __restrict__ set_bits,
+                                                         float* __restrict__ p, float* __restrict__ m,
+                                                         float* __restrict__ v, int64_t ld, int32_t* __restrict__ last,
+                                                         int32_t t, LazyHist h, float b1, float b2, float eps) {
+  using S = SpmmShape<D>;
+  constexpr int L = S::kLanes;
+  using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
+  constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
+  const int lane = threadIdx.x & 63;
+  const int g = lane / L, gl = lane % L, base = g * L;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int64_t r_begin = w * S::kRowsPerWave;
+  const int64_t r_end = r_begin + S::kRowsPerWave < AT.n_rows ? r_begin + S::kRowsPerWave : AT.n_rows;
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
+    const int32_t from = last[r];
+    if (from >= t) continue;
+    bool in = bit_of(set_bits, r);
+    if (!in) {
+      const int64_t beg = AT.rowptr[r], end = AT.rowptr[r + 1];
+      if (end - beg > AT.long_threshold) {
+        in = true;
+      } else {
+        for (int64_t cb = beg; cb < end && !in; cb += L) {
+          const bool hit = cb + gl < end && bit_of(set_bits, AT.col[cb + gl]);
+          in = (static_cast<HitT>(__ballot(hit) >> base) & kMask) != 0;
+        }
+      }
+    }
+    if (!in) continue;
+    float4* P = reinterpret_cast<float4*>(p + r * ld) + gl;
+    float4* M = reinterpret_cast<float4*>(m + r * ld) + gl;
+    float4* V = reinterpret_cast<float4*>(v + r * ld) + gl;
+    float4 pp = *P, mm = *M, vv = *V;
+    lazy_replay(pp.x, mm.x, vv.x, from, t, h, w1, b2, w2, eps);
+    lazy_replay(pp.y, mm.y, vv.y, from, t, h, w1, b2, w2, eps);
+    lazy_replay(pp.z, mm.z, vv.z, from, t, h, w1, b2, w2, eps);
+    lazy_replay(pp.w, mm.w, vv.w, from, t, h, w1, b2, w2, eps);
+    *P = pp;
+    *M = mm;
+    *V = vv;
+    if (gl == 0) last[r] = t;  // the group's lanes (one wave) all read last[r] above
+  }
+}
+
+template <int D>
+static int launch_reach(const kgat_csr& AT, const uint32_t* bits, float* p, float* m, float* v, int64_t ld,
+                        int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, hipStream_t st) {
+  const int64_t blocks = (AT.n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
+  if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(lazy_reach_kernel<D>, dim3(blocks), dim3(256), 0, st, AT, bits, p, m, v, ld, last, t, h, b1, b2,
+                     eps);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+}  // namespace kgat
+
+extern "C" int kgat_lazy_reach_catchup_f32(const kgat_csr* AT, const uint32_t* set_bits, float* p, float* m, float* v,
+                                           int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
+                                           float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
+                                           float eps, void* stream) {
+  using namespace kgat;
+  if (!AT || !set_bits || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 0 ||
+      AT->n_rows < 0 || ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
+    return KGAT_ERR_INVALID;
+  if (AT->n_rows == 0 || t == 0) return KGAT_OK;
+  const LazyHist h{hist_sz, hist_bc, hist_skip, cap};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (d) {
+    case 16: return launch_reach<16>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 32: return launch_reach<32>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 64: return launch_reach<64>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 128: return launch_reach<128>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 256: return launch_reach<256>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    default: return KGAT_ERR_UNSUPPORTED_DIM;
+  }
 }
 
 extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {

@@ -319,10 +319,12 @@ def _skip_ptr(skip: torch.Tensor | None):
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None) -> None:
+                     skip: torch.Tensor | None = None, lazy: tuple | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).  ``lazy``
+    = (last int32 [N], t, (hist_sz, hist_bc, hist_skip), cap): step t on the rows the product reaches
+    only (kgat_spmm_csr_masked_adam_lazy_f32, model._LazyTableAdam)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -346,12 +348,52 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
     rank = _rank_ptr(src_rank, src_map)
 
-    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-              yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
-              eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    if lazy is not None:
+        last, t, (hs, hb, hk), cap = lazy
+        _req(last, "last", dtype=torch.int32, dim=1)
+        if last.numel() != n or min(h.numel() for h in (hs, hb, hk)) < cap:
+            raise ValueError("lazy: last must cover every row, the history cap entries")
+        _lib.call("kgat_spmm_csr_masked_adam_lazy_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+                  yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
+                  eps, _skip_ptr(skip), last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap),
+                  ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    else:
+        _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
+                  _ld(Xc), yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
+                  beta2, bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
+
+
+def lazy_reach_catchup(graph: DeviceGraph, set_bits: torch.Tensor, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                       last: torch.Tensor, t: int, hist: tuple, cap: int, beta1: float, beta2: float,
+                       eps: float) -> None:
+    """The rows of the transposed graph in the set (set_bits: bit r <=> row r) or with an edge into it, and
+    every long row, brought up to step t: their skipped zero-gradient Adam steps replayed from the device
+    history (kgat_lazy_reach_catchup_f32; model._LazyTableAdam)."""
+    n, d = p.shape
+    for x, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _req(x, nm, dim=2)
+        if tuple(x.shape) != (n, d) or not x.is_contiguous():
+            raise ValueError(f"{nm}: contiguous [{n}, {d}] expected")
+    _req(last, "last", dtype=torch.int32, dim=1)
+    if n != graph.n_nodes or last.numel() != n or set_bits.numel() * 32 < n:
+        raise ValueError("lazy_reach_catchup: the table, last[] and set_bits must cover every node")
+    hs, hb, hk = hist
+    if min(h.numel() for h in (hs, hb, hk)) < cap:
+        raise ValueError("lazy_reach_catchup: the history holds cap entries")
+    desc = graph.AT.descriptor()
+    ev = SPMM_EVENTS
+    if ev is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("kgat_lazy_reach_catchup_f32", ctypes.byref(desc), set_bits.data_ptr(), p.data_ptr(), m.data_ptr(),
+              v.data_ptr(), d, d, last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap), beta1,
+              beta2, eps, stream_ptr(p.device))
+    if ev is not None:
+        e1.record()
+        ev.append((e0, e1, d, True, "reach"))
 
 
 def _host_ptr(t: torch.Tensor | None):

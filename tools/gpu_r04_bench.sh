@@ -13,7 +13,7 @@ tail -1 gpurun_out/r04_c2_bench.log | cut -c1-600
 timeout -k 10 600 python -u bench.py --config c3 > gpurun_out/r04_c3_bench.log 2>&1 || { tail -30 gpurun_out/r04_c3_bench.log; exit 1; }
 tail -1 gpurun_out/r04_c3_bench.log | cut -c1-600
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_c2 -o run --output-format csv -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-parity > gpurun_out/r04_prof_c2.log 2>&1 || { tail -20 gpurun_out/r04_prof_c2.log; exit 1; }
+  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-parity --no-kg-leg --no-frontier-leg > gpurun_out/r04_prof_c2.log 2>&1 || { tail -20 gpurun_out/r04_prof_c2.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_c3 -o run --output-format csv -- \
-  python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-parity > gpurun_out/r04_prof_c3.log 2>&1 || { tail -20 gpurun_out/r04_prof_c3.log; exit 1; }
+  python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-parity --no-kg-leg --no-frontier-leg > gpurun_out/r04_prof_c3.log 2>&1 || { tail -20 gpurun_out/r04_prof_c3.log; exit 1; }
 echo done
