@@ -140,24 +140,33 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
 
 /* Lazy form of kgat_spmm_csr_masked_adam_ex_f32 (the CF phase's table Adam on the rows the step
  * touches; replaces the dense torch.optim.Adam step of model.py:404-413 over the whole table): Adam
- * step t (>= 1) on the rows whose product gathered an edge or has a Yc_init row, and on every long
- * row, each after replaying its skipped steps last[r]+1 .. t-1 from the device history (hist_*[s %
- * cap]: step size, sqrt(1 - beta2^s), skip flag); last[r] = t for them.  Step t's scalars and skip
- * flag are written to the history; the other rows (gradient exactly 0) stay behind until replayed
- * (kgat_lazy_reach_catchup_f32, kgat_adam_lazy_catchup_f32).  Same bits as the dense step. */
+ * step t (>= 1) on the rows stamped t (stamp[r] == t, kgat_rows_stamp: the source set and every row
+ * with an edge into it -- outside them the gradient is exactly 0), each after replaying its skipped
+ * steps last[r]+1 .. t-1 from the device history (hist_*[s % cap]: step size, sqrt(1 - beta2^s),
+ * skip flag); last[r] = t for them.  Step t's scalars and skip flag are written to the history; the
+ * other rows stay behind until replayed (kgat_adam_lazy_stamped_f32, kgat_adam_lazy_catchup_f32).
+ * Same bits as the dense step. */
 int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
                                        const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
                                        float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
-                                       float beta2, float bc2_sqrt, float eps, const int32_t *skip, int32_t *last,
-                                       int32_t t, float *hist_sz, float *hist_bc, int32_t *hist_skip, int32_t cap,
-                                       float *workspace, int64_t workspace_floats, void *stream);
+                                       float beta2, float bc2_sqrt, float eps, const int32_t *skip,
+                                       const int32_t *stamp, int32_t *last, int32_t t, float *hist_sz,
+                                       float *hist_bc, int32_t *hist_skip, int32_t cap, float *workspace,
+                                       int64_t workspace_floats, void *stream);
 
-/* The lazy CF table Adam's forward half: every row of AT (the transposed graph) that is in the set
- * (set_bits: bit r <=> row r) or has an edge into it -- the rows the frontier forward's layer on the
- * set reads --, and every long row of AT, brought up to step t (skipped steps replayed, last[r] = t). */
-int kgat_lazy_reach_catchup_f32(const kgat_csr *AT, const uint32_t *set_bits, float *p, float *m, float *v,
-                                int64_t ldp, int32_t d, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
-                                int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, void *stream);
+/* stamp[r] = s for every row r = rows[k], k < *count (device; -1 entries skipped), and every column
+ * of A's rows in the set (set_bits: the same rows as a bitmap, for the long rows' segments) -- the
+ * rows a layer computed on the set reads, and (A^T's view) the rows where A^T . dS over the set can
+ * be nonzero.  max_rows: the list's capacity (sizes the grid). */
+int kgat_rows_stamp(const kgat_csr *A, const int32_t *rows, const int32_t *count, int64_t max_rows,
+                    const uint32_t *set_bits, int32_t *stamp, int32_t s, void *stream);
+
+/* The lazy CF table Adam's forward half: every row stamped t that is behind step t - 1 brought up to
+ * it (skipped steps replayed from the history, last[r] = t - 1) -- the rows the frontier forward reads
+ * are current before it reads them. */
+int kgat_adam_lazy_stamped_f32(const int32_t *stamp, int64_t n_rows, float *p, float *m, float *v, int64_t ldp,
+                               int32_t d, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
+                               int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, void *stream);
 
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);

@@ -107,7 +107,7 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
   }
   if (MODE == kMaskedAdam) {
     if (io.adam.last != nullptr) {
-      if (any) adam_row_lazy(io.adam, row, gl, acc);
+      adam_row_lazy(io.adam, row, gl, acc);  // a stamped row (the others never get here)
       return;
     }
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
@@ -119,6 +119,12 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
   }
   *y = acc;
+}
+
+// The lazy table update passes over the rows not stamped with its step (gradient exactly 0).
+template <int MODE>
+__device__ __forceinline__ bool lazy_pass(const SpmmIo& io, int64_t row) {
+  return MODE == kMaskedAdam && io.adam.stamp != nullptr && io.adam.stamp[row] != io.adam.t;
 }
 
 // Source rows in flight per lane group in the row-set forward (kRows); 4, 8 and 16 measured
@@ -134,6 +140,7 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
   if (s >= A.n_seg) return;
   const int row = A.seg_row[s];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
+  if (lazy_pass<MODE>(io, row)) return;
   const int64_t beg = A.seg_beg[s];
   const int64_t row_end = A.rowptr[row + 1];
   const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
@@ -209,6 +216,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
+    if (lazy_pass<MODE>(io, r)) continue;
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -232,6 +240,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
   const int row = A.long_rows[lr];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
+  if (lazy_pass<MODE>(io, row)) return;
   const float4* P = reinterpret_cast<const float4*>(io.part);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int s_end = A.long_seg_off[lr + 1];
@@ -241,9 +250,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if (threadIdx.x < L) {
     float4 t = red[0][gl];
     for (int k = 1; k < G; ++k) add4(t, red[k][gl]);
-    // a long row is always stepped by the lazy update (its segments' hits are not collected; a
-    // zero row's step t is the replay's adam_elem(g = 0) either way)
-    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t, MODE == kMaskedAdam);
+    store_row<MODE>(io, row, MODE == kMaskedRows ? io.out_map[row] : row, gl, t);
   }
 }
 
@@ -582,7 +589,7 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}, nullptr};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -590,14 +597,14 @@ extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32
                                                   int64_t ldxc, const float* Yc_init, int64_t ldyc,
                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
                                                   int32_t d, float step_size, float beta1, float beta2,
-                                                  float bc2_sqrt, float eps, const int32_t* skip, int32_t* last,
-                                                  int32_t t, float* hist_sz, float* hist_bc, int32_t* hist_skip,
-                                                  int32_t cap, float* workspace, int64_t workspace_floats,
-                                                  void* stream) {
+                                                  float bc2_sqrt, float eps, const int32_t* skip,
+                                                  const int32_t* stamp, int32_t* last, int32_t t, float* hist_sz,
+                                                  float* hist_bc, int32_t* hist_skip, int32_t cap, float* workspace,
+                                                  int64_t workspace_floats, void* stream) {
   using namespace kgat;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
-  if (!last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1) return KGAT_ERR_INVALID;
+  if (!stamp || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1) return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
       (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
     return KGAT_ERR_INVALID;
@@ -607,94 +614,126 @@ extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
   io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, last, t,
-                     LazyHist{hist_sz, hist_bc, hist_skip, cap}};
+                     LazyHist{hist_sz, hist_bc, hist_skip, cap}, stamp};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
 namespace kgat {
 
-// The lazy CF table Adam's forward half: the rows the frontier forward's first restricted layer reads
-// -- its output set S (set_bits) and every column of A's rows S, i.e. every row of A^T with an edge
-// into S -- brought up to step t (their skipped steps replayed, LazyHist).  Rows already at t are
-// passed over without a scan; a row of A^T longer than the long-row threshold is brought up to t
-// without one (a current row is read the same by anyone).  Groups of D/4 lanes, one row at a time,
-// the membership scan a ballot per D/4 edges that stops at the first hit.
+// The lazy CF table Adam's marks: stamp[r] = s for every row r of the set (rows[0 .. *count)) and every
+// column of A's rows in the set -- the rows the frontier forward's layer on the set reads, and the rows
+// of A^T with an edge into it, i.e. where the table gradient A^T . dS can be nonzero.  Every writer
+// stores the same value (no atomics, no clearing: a stamp of an older step never equals s).  Blocks
+// [0, seg_blocks): one long-row segment per wave (its row's set bit decides); the rest: 16-lane groups
+// striding over the list's short rows.
+__global__ __launch_bounds__(256) void rows_stamp_kernel(kgat_csr A, const int32_t* __restrict__ rows,
+                                                         const int32_t* __restrict__ count,
+                                                         const uint32_t* __restrict__ set_bits,
+                                                         int32_t* __restrict__ stamp, int32_t s, int seg_blocks) {
+  const int lane = threadIdx.x & 63;
+  if (static_cast<int>(blockIdx.x) < seg_blocks) {
+    const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sg >= A.n_seg) return;
+    const int row = A.seg_row[sg];
+    if (!bit_of(set_bits, row)) return;
+    const int64_t beg = A.seg_beg[sg];
+    const int64_t row_end = A.rowptr[row + 1];
+    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+    for (int64_t e = beg + lane; e < end; e += kWave) stamp[A.col[e]] = s;
+    return;
+  }
+  constexpr int L = 16;
+  const int g = lane / L, gl = lane % L;
+  const int64_t cnt = *count;
+  const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * (kWave / L);
+  for (int64_t k = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + (threadIdx.x >> 6)) * (kWave / L) + g;
+       k < cnt; k += stride) {
+    const int32_t r = rows[k];
+    if (r < 0) continue;
+    if (gl == 0) stamp[r] = s;
+    const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+    if (end - beg > A.long_threshold) continue;  // its segments' waves
+    for (int64_t e = beg + gl; e < end; e += L) stamp[A.col[e]] = s;
+  }
+}
+
+// The lazy CF table Adam's forward half: every row stamped t (rows_stamp_kernel) that is behind step t
+// brought up to it (its skipped steps replayed, LazyHist).  Groups of D/4 lanes, one row at a time.
 template <int D>
-__global__ __launch_bounds__(256) void lazy_reach_kernel(kgat_csr AT, const uint32_t* __restrict__ set_bits,
-                                                         float* __restrict__ p, float* __restrict__ m,
-                                                         float* __restrict__ v, int64_t ld, int32_t* __restrict__ last,
-                                                         int32_t t, LazyHist h, float b1, float b2, float eps) {
+__global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __restrict__ stamp, int64_t n_rows,
+                                                           float* __restrict__ p, float* __restrict__ m,
+                                                           float* __restrict__ v, int64_t ld,
+                                                           int32_t* __restrict__ last, int32_t t, LazyHist h,
+                                                           float b1, float b2, float eps) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
-  using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
-  constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
   const int lane = threadIdx.x & 63;
-  const int g = lane / L, gl = lane % L, base = g * L;
+  const int g = lane / L, gl = lane % L;
   const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int64_t r_begin = w * S::kRowsPerWave;
-  const int64_t r_end = r_begin + S::kRowsPerWave < AT.n_rows ? r_begin + S::kRowsPerWave : AT.n_rows;
+  const int64_t r_end = r_begin + S::kRowsPerWave < n_rows ? r_begin + S::kRowsPerWave : n_rows;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
+    if (stamp[r] != t) continue;
     const int32_t from = last[r];
-    if (from >= t) continue;
-    bool in = bit_of(set_bits, r);
-    if (!in) {
-      const int64_t beg = AT.rowptr[r], end = AT.rowptr[r + 1];
-      if (end - beg > AT.long_threshold) {
-        in = true;
-      } else {
-        for (int64_t cb = beg; cb < end && !in; cb += L) {
-          const bool hit = cb + gl < end && bit_of(set_bits, AT.col[cb + gl]);
-          in = (static_cast<HitT>(__ballot(hit) >> base) & kMask) != 0;
-        }
-      }
-    }
-    if (!in) continue;
+    if (from >= t - 1) continue;
     float4* P = reinterpret_cast<float4*>(p + r * ld) + gl;
     float4* M = reinterpret_cast<float4*>(m + r * ld) + gl;
     float4* V = reinterpret_cast<float4*>(v + r * ld) + gl;
     float4 pp = *P, mm = *M, vv = *V;
-    lazy_replay(pp.x, mm.x, vv.x, from, t, h, w1, b2, w2, eps);
-    lazy_replay(pp.y, mm.y, vv.y, from, t, h, w1, b2, w2, eps);
-    lazy_replay(pp.z, mm.z, vv.z, from, t, h, w1, b2, w2, eps);
-    lazy_replay(pp.w, mm.w, vv.w, from, t, h, w1, b2, w2, eps);
+    lazy_replay(pp.x, mm.x, vv.x, from, t - 1, h, w1, b2, w2, eps);
+    lazy_replay(pp.y, mm.y, vv.y, from, t - 1, h, w1, b2, w2, eps);
+    lazy_replay(pp.z, mm.z, vv.z, from, t - 1, h, w1, b2, w2, eps);
+    lazy_replay(pp.w, mm.w, vv.w, from, t - 1, h, w1, b2, w2, eps);
     *P = pp;
     *M = mm;
     *V = vv;
-    if (gl == 0) last[r] = t;  // the group's lanes (one wave) all read last[r] above
+    if (gl == 0) last[r] = t - 1;  // the group's lanes (one wave) all read last[r] above
   }
 }
 
 template <int D>
-static int launch_reach(const kgat_csr& AT, const uint32_t* bits, float* p, float* m, float* v, int64_t ld,
-                        int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, hipStream_t st) {
-  const int64_t blocks = (AT.n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
+static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v, int64_t ld,
+                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, hipStream_t st) {
+  const int64_t blocks = (n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
   if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(lazy_reach_kernel<D>, dim3(blocks), dim3(256), 0, st, AT, bits, p, m, v, ld, last, t, h, b1, b2,
-                     eps);
+  hipLaunchKernelGGL(lazy_stamped_kernel<D>, dim3(blocks), dim3(256), 0, st, stamp, n_rows, p, m, v, ld, last, t, h,
+                     b1, b2, eps);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
 
 }  // namespace kgat
 
-extern "C" int kgat_lazy_reach_catchup_f32(const kgat_csr* AT, const uint32_t* set_bits, float* p, float* m, float* v,
-                                           int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
-                                           float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
-                                           float eps, void* stream) {
+extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int32_t* count, int64_t max_rows,
+                               const uint32_t* set_bits, int32_t* stamp, int32_t s, void* stream) {
   using namespace kgat;
-  if (!AT || !set_bits || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 0 ||
-      AT->n_rows < 0 || ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
+  if (!A || !rows || !count || !set_bits || !stamp || max_rows < 0 || A->n_rows < 0) return KGAT_ERR_INVALID;
+  const int seg_blocks = (A->n_seg + 3) / 4;
+  const int64_t list_blocks = std::min<int64_t>(std::max<int64_t>((max_rows + 15) / 16, 1), 2048);
+  hipLaunchKernelGGL(rows_stamp_kernel, dim3(seg_blocks + list_blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_adam_lazy_stamped_f32(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v,
+                                          int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
+                                          float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
+                                          float eps, void* stream) {
+  using namespace kgat;
+  if (!stamp || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || n_rows < 0 ||
+      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
     return KGAT_ERR_INVALID;
-  if (AT->n_rows == 0 || t == 0) return KGAT_OK;
+  if (n_rows == 0) return KGAT_OK;
   const LazyHist h{hist_sz, hist_bc, hist_skip, cap};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (d) {
-    case 16: return launch_reach<16>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 32: return launch_reach<32>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 64: return launch_reach<64>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 128: return launch_reach<128>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 256: return launch_reach<256>(*AT, set_bits, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
     default: return KGAT_ERR_UNSUPPORTED_DIM;
   }
 }

@@ -323,8 +323,8 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
     update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).  ``lazy``
-    = (last int32 [N], t, (hist_sz, hist_bc, hist_skip), cap): step t on the rows the product reaches
-    only (kgat_spmm_csr_masked_adam_lazy_f32, model._LazyTableAdam)."""
+    = (stamp int32 [N], last int32 [N], t, (hist_sz, hist_bc, hist_skip), cap): step t on the rows
+    stamped t only (kgat_spmm_csr_masked_adam_lazy_f32, model._LazyTableAdam)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -349,14 +349,15 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     rank = _rank_ptr(src_rank, src_map)
 
     if lazy is not None:
-        last, t, (hs, hb, hk), cap = lazy
+        stamp, last, t, (hs, hb, hk), cap = lazy
         _req(last, "last", dtype=torch.int32, dim=1)
-        if last.numel() != n or min(h.numel() for h in (hs, hb, hk)) < cap:
-            raise ValueError("lazy: last must cover every row, the history cap entries")
+        _req(stamp, "stamp", dtype=torch.int32, dim=1)
+        if last.numel() != n or stamp.numel() != n or min(h.numel() for h in (hs, hb, hk)) < cap:
+            raise ValueError("lazy: last / stamp must cover every row, the history cap entries")
         _lib.call("kgat_spmm_csr_masked_adam_lazy_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
                   yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
-                  eps, _skip_ptr(skip), last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap),
-                  ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+                  eps, _skip_ptr(skip), stamp.data_ptr(), last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(),
+                  hk.data_ptr(), int(cap), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     else:
         _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
                   _ld(Xc), yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
@@ -366,31 +367,35 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
         ev.append((e0, e1, d, True, "fused_adam"))
 
 
-def lazy_reach_catchup(graph: DeviceGraph, set_bits: torch.Tensor, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
-                       last: torch.Tensor, t: int, hist: tuple, cap: int, beta1: float, beta2: float,
-                       eps: float) -> None:
-    """The rows of the transposed graph in the set (set_bits: bit r <=> row r) or with an edge into it, and
-    every long row, brought up to step t: their skipped zero-gradient Adam steps replayed from the device
-    history (kgat_lazy_reach_catchup_f32; model._LazyTableAdam)."""
+def lazy_mark_catchup(graph: DeviceGraph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor,
+                      stamp: torch.Tensor, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor, t: int,
+                      hist: tuple, cap: int, beta1: float, beta2: float, eps: float) -> None:
+    """The lazy CF table Adam's forward half (model._LazyTableAdam.reach): stamp[r] = t on the set (rows /
+    count on the device / set_bits) and every column of A's rows in it (kgat_rows_stamp), then every
+    stamped row behind step t - 1 brought up to it, its skipped zero-gradient steps replayed from the
+    device history (kgat_adam_lazy_stamped_f32)."""
     n, d = p.shape
     for x, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
         _req(x, nm, dim=2)
         if tuple(x.shape) != (n, d) or not x.is_contiguous():
             raise ValueError(f"{nm}: contiguous [{n}, {d}] expected")
-    _req(last, "last", dtype=torch.int32, dim=1)
-    if n != graph.n_nodes or last.numel() != n or set_bits.numel() * 32 < n:
-        raise ValueError("lazy_reach_catchup: the table, last[] and set_bits must cover every node")
+    for x, nm in ((last, "last"), (stamp, "stamp"), (rows, "rows"), (count, "count")):
+        _req(x, nm, dtype=torch.int32, dim=1)
+    if n != graph.n_nodes or last.numel() != n or stamp.numel() != n or set_bits.numel() * 32 < n or t < 1:
+        raise ValueError("lazy_mark_catchup: the table, last[], stamp[] and set_bits must cover every node")
     hs, hb, hk = hist
     if min(h.numel() for h in (hs, hb, hk)) < cap:
-        raise ValueError("lazy_reach_catchup: the history holds cap entries")
-    desc = graph.AT.descriptor()
+        raise ValueError("lazy_mark_catchup: the history holds cap entries")
     ev = SPMM_EVENTS
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("kgat_lazy_reach_catchup_f32", ctypes.byref(desc), set_bits.data_ptr(), p.data_ptr(), m.data_ptr(),
-              v.data_ptr(), d, d, last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap), beta1,
-              beta2, eps, stream_ptr(p.device))
+    st = stream_ptr(p.device)
+    desc = graph.A.descriptor()
+    _lib.call("kgat_rows_stamp", ctypes.byref(desc), rows.data_ptr(), count.data_ptr(), rows.numel(),
+              set_bits.data_ptr(), stamp.data_ptr(), int(t), st)
+    _lib.call("kgat_adam_lazy_stamped_f32", stamp.data_ptr(), n, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d,
+              last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap), beta1, beta2, eps, st)
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "reach"))

@@ -270,7 +270,8 @@ class _TableUpdate:
             if lazy is not None:
                 lazy.dirty = True
                 lazy.steps += 1
-                lz = (lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
+                lazy.marked = None
+                lz = (lazy.stamp, lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
                                      lazy=lz)
         return run
@@ -391,6 +392,8 @@ class _LazyTableAdam:
         self.flushed_at = 0
         self.dirty = False  # rows behind the current step (a lazy step since the last flush)
         self.steps = 0  # lazy steps launched (tests, bench)
+        self.stamp = None  # CF: stamp[r] = the step whose forward read row r (reach)
+        self.marked = None  # CF: the step the last reach stamped for
 
     def _t(self, opt) -> int:
         st = opt.state.get(id(self.param))
@@ -441,14 +444,21 @@ class _LazyTableAdam:
             kernels.frontier_reset(rows, row_map)
         return run
 
-    def reach(self, opt, graph, set_bits: torch.Tensor) -> None:
-        """The frontier CF forward's catch-up: the rows its first restricted layer reads (the set and every
-        row with an edge into it, kgat_lazy_reach_catchup_f32) brought up to the optimiser's step."""
+    def reach(self, opt, graph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor) -> None:
+        """The frontier CF forward's catch-up: the set its first restricted layer computes (rows / count /
+        set_bits) and every column of A's rows in it -- the rows the layer reads, and the rows where the
+        step's table gradient can be nonzero -- stamped with the coming step t and brought up to step t - 1
+        (kernels.lazy_mark_catchup); the update then steps the stamped rows only."""
+        t = self._t(opt) + 1
+        if self.stamp is None or self.stamp.numel() != self.last.numel() or self.stamp.device != self.last.device:
+            self.stamp = torch.zeros_like(self.last)  # step numbers start at 1: a zero stamp marks nothing
+        p = self.param.data
         st = opt.state.get(id(self.param))
-        if self.last is None or st is None:
-            return
-        kernels.lazy_reach_catchup(graph, set_bits, self.param.data, st["exp_avg"], st["exp_avg_sq"], self.last,
-                                   int(st["step"]), self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps)
+        if st is None:  # the first step: every row is at step 0, nothing to replay -- the stamps only
+            st = {"exp_avg": p, "exp_avg_sq": p}
+        kernels.lazy_mark_catchup(graph, rows, count, set_bits, self.stamp, p, st["exp_avg"], st["exp_avg_sq"],
+                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps)
+        self.marked = t
 
     def dense_step_done(self, opt) -> None:
         """A dense step t was just applied to every row (each caught up before it): every row is current at
@@ -794,7 +804,7 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=
         if sets[0] is None:
             lz.catch_up(opt)  # layer 0 runs whole: every row
         else:
-            lz.reach(opt, graph, sets[0][2])
+            lz.reach(opt, graph, *sets[0])
     tables, sides, states = [X0], [], []
     x = X0
     for l in range(L):
@@ -1409,7 +1419,8 @@ class KGAT(nn.Module):
             # gradient is summed with the deferred product first (materialize adds into .grad)
             if (row_ranges and id(tu.param) in row_ranges) or tu.param.grad is not None:
                 tu.materialize()
-            elif lazy.enabled and lazy.last is not None:
+            elif lazy.enabled and lazy.last is not None and lazy.marked == lazy._t(opt) + 1:
+                # this step's forward stamped the rows it read and the gradient's rows (reach)
                 if lazy._t(opt) + 1 - lazy.flushed_at >= lazy.CAP:
                     lazy.catch_up(opt)  # no row may fall a whole history behind
                 fused = {id(tu.param): tu.launch(lazy, opt)}
@@ -1421,6 +1432,7 @@ class KGAT(nn.Module):
         if dense_lazy:
             lazy.catch_up(opt)
         opt.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
+        lazy.marked = None
         if dense_lazy:
             lazy.dense_step_done(opt)
         opt.zero_grad()
