@@ -108,33 +108,63 @@ __device__ __forceinline__ void nfm_layer(const NfmNet& N, const NfmLds& plan, c
   const bool w4 = !WLDS && (din & 3) == 0 && (reinterpret_cast<uintptr_t>(N.W[l]) & 15) == 0;
   const float* wlds = WLDS ? smem + plan.w_off[l] + cl * wp + 4 * g : nullptr;
   const float* a_row = tile + cl * P + 4 * g;
-  for (int k0 = 0; k0 < kpad; k0 += 16) {  // one A fragment feeds NB interleaved MFMA chains
-    const float4 a4 = *reinterpret_cast<const float4*>(a_row + k0);
-    float4 b4[NB];
+  if (!WLDS && w4 && (din & 15) == 0 && (dout & 15) == 0) {
+    // global weights whose 16-wide blocks are whole: every fragment is one unconditional 16-byte load
+    // (no per-fragment branches), and the next k-step's fragments are in flight while this step's
+    // MFMAs run -- an L2 round trip per k-step otherwise stalls the wave (8 k-steps per 128-wide layer)
+    // one per-lane base; the blocks' offsets are wave-uniform
+    const float* wb = N.W[l] + static_cast<int64_t>(cl) * din + 4 * g;
+    const int64_t bstride = static_cast<int64_t>(16) * din;
+    float4 bn[NB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {  // every B fragment of the step read before the first MFMA
-      const int nbc = nb < nblk ? nb : nblk - 1;
-      if (WLDS) {
-        b4[nb] = *reinterpret_cast<const float4*>(wlds + nbc * 16 * wp + k0);
-      } else {
-        const int n = nbc * 16 + cl, kk = k0 + 4 * g;
-        const float* wr = N.W[l] + static_cast<int64_t>(n < dout ? n : 0) * din;
-        if (w4 && n < dout && kk + 3 < din) {
-          b4[nb] = *reinterpret_cast<const float4*>(wr + kk);  // one 16-byte load (L1 / L2 resident weights)
-        } else {
-          b4[nb].x = (n < dout && kk < din) ? wr[kk] : 0.f;
-          b4[nb].y = (n < dout && kk + 1 < din) ? wr[kk + 1] : 0.f;
-          b4[nb].z = (n < dout && kk + 2 < din) ? wr[kk + 2] : 0.f;
-          b4[nb].w = (n < dout && kk + 3 < din) ? wr[kk + 3] : 0.f;
-        }
+    for (int nb = 0; nb < NB; ++nb) bn[nb] = *reinterpret_cast<const float4*>(wb + (nb < nblk ? nb : nblk - 1) * bstride);
+    for (int k0 = 0; k0 < kpad; k0 += 16) {
+      const float4 a4 = *reinterpret_cast<const float4*>(a_row + k0);
+      float4 b4[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) b4[nb] = bn[nb];
+      if (k0 + 16 < kpad) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          bn[nb] = *reinterpret_cast<const float4*>(wb + (nb < nblk ? nb : nblk - 1) * bstride + k0 + 16);
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        acc[nb] = mfma16x4(a4.x, b4[nb].x, acc[nb]);
+        acc[nb] = mfma16x4(a4.y, b4[nb].y, acc[nb]);
+        acc[nb] = mfma16x4(a4.z, b4[nb].z, acc[nb]);
+        acc[nb] = mfma16x4(a4.w, b4[nb].w, acc[nb]);
       }
     }
+  } else {
+    for (int k0 = 0; k0 < kpad; k0 += 16) {  // one A fragment feeds NB interleaved MFMA chains
+      const float4 a4 = *reinterpret_cast<const float4*>(a_row + k0);
+      float4 b4[NB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      acc[nb] = mfma16x4(a4.x, b4[nb].x, acc[nb]);
-      acc[nb] = mfma16x4(a4.y, b4[nb].y, acc[nb]);
-      acc[nb] = mfma16x4(a4.z, b4[nb].z, acc[nb]);
-      acc[nb] = mfma16x4(a4.w, b4[nb].w, acc[nb]);
+      for (int nb = 0; nb < NB; ++nb) {  // every B fragment of the step read before the first MFMA
+        const int nbc = nb < nblk ? nb : nblk - 1;
+        if (WLDS) {
+          b4[nb] = *reinterpret_cast<const float4*>(wlds + nbc * 16 * wp + k0);
+        } else {
+          const int n = nbc * 16 + cl, kk = k0 + 4 * g;
+          const float* wr = N.W[l] + static_cast<int64_t>(n < dout ? n : 0) * din;
+          if (w4 && n < dout && kk + 3 < din) {
+            b4[nb] = *reinterpret_cast<const float4*>(wr + kk);  // one 16-byte load (L1 / L2 resident weights)
+          } else {
+            b4[nb].x = (n < dout && kk < din) ? wr[kk] : 0.f;
+            b4[nb].y = (n < dout && kk + 1 < din) ? wr[kk + 1] : 0.f;
+            b4[nb].z = (n < dout && kk + 2 < din) ? wr[kk + 2] : 0.f;
+            b4[nb].w = (n < dout && kk + 3 < din) ? wr[kk + 3] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        acc[nb] = mfma16x4(a4.x, b4[nb].x, acc[nb]);
+        acc[nb] = mfma16x4(a4.y, b4[nb].y, acc[nb]);
+        acc[nb] = mfma16x4(a4.z, b4[nb].z, acc[nb]);
+        acc[nb] = mfma16x4(a4.w, b4[nb].w, acc[nb]);
+      }
     }
   }
   wave_lds_sync();  // every lane has read the layer input

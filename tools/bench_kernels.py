@@ -177,7 +177,7 @@ def graph_section(args, K, g, U, E, n, dev, rec):
             4 * n * (2 * din + dout))
         rec(f"biinter_bwd_{din}x{dout}",
             timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5), args.reps),
-            4 * n * (2 * din + dout + 2 * din), w_lds=os.environ.get("KGAT_BWD_W_LDS", "1"))
+            4 * n * (2 * din + dout + 2 * din), w_lds="1")
         st = K.BiState(n, dev, din, dout)
         rec(f"biinter_fwd_saved_{din}x{dout}",
             timeit(lambda: K.biinter_fwd(X, S, W1, b1, W2, b2, 0.1, 5, out=H, state=st), args.reps),
