@@ -188,6 +188,23 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     return;
   }
 
+  if (MODE == kMaskedAdam && io.adam.rows != nullptr) {
+    // ---- the lazy update's stamped short rows, one group per list entry (as kRows below)
+    const int64_t cnt = *io.adam.count;
+    const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * S::kGroups;
+    for (int64_t k = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kGroups + g; k < cnt;
+         k += stride) {
+      const int64_t r = io.adam.rows[k];
+      const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+      if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      bool any = false;
+      gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
+      store_row<MODE>(io, r, r, gl, acc, any);
+    }
+    return;
+  }
+
   if (MODE == kMaskedRows || MODE == kRows) {
     // ---- short rows of the output set: one group per row, groups stride over the list one row
     // at a time (a set of ~10^4 rows keeps every group of the grid busy instead of a few waves
@@ -259,7 +276,8 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
   int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
-  if ((MODE == kMaskedRows || MODE == kRows) && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
+  if ((MODE == kMaskedRows || MODE == kRows || (MODE == kMaskedAdam && io.adam.rows != nullptr)) && row_blocks > 2048)
+    row_blocks = 2048;  // waves stride over the set (size on device)
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
@@ -589,7 +607,8 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}, nullptr};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}, nullptr,
+                     nullptr, nullptr};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -598,13 +617,15 @@ extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32
                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
                                                   int32_t d, float step_size, float beta1, float beta2,
                                                   float bc2_sqrt, float eps, const int32_t* skip,
-                                                  const int32_t* stamp, int32_t* last, int32_t t, float* hist_sz,
+                                                  const int32_t* stamp, const int32_t* rows, const int32_t* count,
+                                                  int32_t* last, int32_t t, float* hist_sz,
                                                   float* hist_bc, int32_t* hist_skip, int32_t cap, float* workspace,
                                                   int64_t workspace_floats, void* stream) {
   using namespace kgat;
   if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
     return KGAT_ERR_INVALID;
-  if (!stamp || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1) return KGAT_ERR_INVALID;
+  if (!stamp || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || ((rows == nullptr) != (count == nullptr)))
+    return KGAT_ERR_INVALID;
   if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
       (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
     return KGAT_ERR_INVALID;
@@ -614,7 +635,7 @@ extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
   io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, last, t,
-                     LazyHist{hist_sz, hist_bc, hist_skip, cap}, stamp};
+                     LazyHist{hist_sz, hist_bc, hist_skip, cap}, stamp, rows, count};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -629,8 +650,10 @@ namespace kgat {
 __global__ __launch_bounds__(256) void rows_stamp_kernel(kgat_csr A, const int32_t* __restrict__ rows,
                                                          const int32_t* __restrict__ count,
                                                          const uint32_t* __restrict__ set_bits,
-                                                         int32_t* __restrict__ stamp, int32_t s, int seg_blocks) {
+                                                         int32_t* __restrict__ stamp, int32_t s,
+                                                         int32_t* __restrict__ list_count, int seg_blocks) {
   const int lane = threadIdx.x & 63;
+  if (list_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *list_count = 0;  // filled by the next kernel
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (sg >= A.n_seg) return;
@@ -664,7 +687,8 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
                                                            float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, int64_t ld,
                                                            int32_t* __restrict__ last, int32_t t, LazyHist h,
-                                                           float b1, float b2, float eps) {
+                                                           float b1, float b2, float eps, int32_t* __restrict__ list,
+                                                           int32_t* __restrict__ list_count) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
   const int lane = threadIdx.x & 63;
@@ -674,7 +698,20 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
   const int64_t r_end = r_begin + S::kRowsPerWave < n_rows ? r_begin + S::kRowsPerWave : n_rows;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
-    if (stamp[r] != t) continue;
+    const bool stamped = stamp[r] == t;
+    if (list != nullptr) {
+      // the stamped rows appended to the update's list: one atomic per wave (the order is free -- every
+      // row's update is independent of the others)
+      const uint64_t bal = __ballot(stamped && gl == 0);
+      if (bal != 0) {
+        const int leader = __ffsll(static_cast<unsigned long long>(bal)) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(list_count, __popcll(bal));
+        base = __shfl(base, leader);
+        if (stamped && gl == 0) list[base + __popcll(bal & ((uint64_t{1} << lane) - 1))] = static_cast<int32_t>(r);
+      }
+    }
+    if (!stamped) continue;
     const int32_t from = last[r];
     if (from >= t - 1) continue;
     float4* P = reinterpret_cast<float4*>(p + r * ld) + gl;
@@ -694,11 +731,12 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
 
 template <int D>
 static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v, int64_t ld,
-                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, hipStream_t st) {
+                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, int32_t* list,
+                          int32_t* list_count, hipStream_t st) {
   const int64_t blocks = (n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
   if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(lazy_stamped_kernel<D>, dim3(blocks), dim3(256), 0, st, stamp, n_rows, p, m, v, ld, last, t, h,
-                     b1, b2, eps);
+                     b1, b2, eps, list, list_count);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -706,13 +744,15 @@ static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float*
 }  // namespace kgat
 
 extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int32_t* count, int64_t max_rows,
-                               const uint32_t* set_bits, int32_t* stamp, int32_t s, void* stream) {
+                               const uint32_t* set_bits, int32_t* stamp, int32_t s, int32_t* list_count,
+                               void* stream) {
   using namespace kgat;
   if (!A || !rows || !count || !set_bits || !stamp || max_rows < 0 || A->n_rows < 0) return KGAT_ERR_INVALID;
   const int seg_blocks = (A->n_seg + 3) / 4;
   const int64_t list_blocks = std::min<int64_t>(std::max<int64_t>((max_rows + 15) / 16, 1), 2048);
   hipLaunchKernelGGL(rows_stamp_kernel, dim3(seg_blocks + list_blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, seg_blocks);
+                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, list_count,
+                     seg_blocks);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -720,20 +760,20 @@ extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int
 extern "C" int kgat_adam_lazy_stamped_f32(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v,
                                           int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
                                           float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
-                                          float eps, void* stream) {
+                                          float eps, int32_t* list, int32_t* list_count, void* stream) {
   using namespace kgat;
   if (!stamp || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || n_rows < 0 ||
-      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
+      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v) || ((list == nullptr) != (list_count == nullptr)))
     return KGAT_ERR_INVALID;
   if (n_rows == 0) return KGAT_OK;
   const LazyHist h{hist_sz, hist_bc, hist_skip, cap};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (d) {
-    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
-    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, st);
+    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
+    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
+    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
+    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
+    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
     default: return KGAT_ERR_UNSUPPORTED_DIM;
   }
 }

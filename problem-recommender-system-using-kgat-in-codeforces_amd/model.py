@@ -271,7 +271,7 @@ class _TableUpdate:
                 lazy.dirty = True
                 lazy.steps += 1
                 lazy.marked = None
-                lz = (lazy.stamp, lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
+                lz = (lazy.stamp, *lazy._list(), lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
                                      lazy=lz)
         return run
@@ -393,6 +393,7 @@ class _LazyTableAdam:
         self.dirty = False  # rows behind the current step (a lazy step since the last flush)
         self.steps = 0  # lazy steps launched (tests, bench)
         self.stamp = None  # CF: stamp[r] = the step whose forward read row r (reach)
+        self.rows = self.count = None  # CF: the rows stamped by the last reach, listed (any order)
         self.marked = None  # CF: the step the last reach stamped for
 
     def _t(self, opt) -> int:
@@ -452,13 +453,19 @@ class _LazyTableAdam:
         t = self._t(opt) + 1
         if self.stamp is None or self.stamp.numel() != self.last.numel() or self.stamp.device != self.last.device:
             self.stamp = torch.zeros_like(self.last)  # step numbers start at 1: a zero stamp marks nothing
+            self.rows = torch.empty_like(self.last)  # the stamped rows, listed for the update
+            self.count = torch.zeros(1, dtype=torch.int32, device=self.last.device)
         p = self.param.data
         st = opt.state.get(id(self.param))
         if st is None:  # the first step: every row is at step 0, nothing to replay -- the stamps only
             st = {"exp_avg": p, "exp_avg_sq": p}
         kernels.lazy_mark_catchup(graph, rows, count, set_bits, self.stamp, p, st["exp_avg"], st["exp_avg_sq"],
-                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps)
+                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, *self._list())
         self.marked = t
+
+    def _list(self):
+        import os  # TEMP A/B: the stamped rows' list walk vs the per-row stamp test
+        return (self.rows, self.count) if os.environ.get("KGAT_LAZY_LIST", "1") == "1" else (None, None)
 
     def dense_step_done(self, opt) -> None:
         """A dense step t was just applied to every row (each caught up before it): every row is current at
