@@ -145,8 +145,8 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
  * steps last[r]+1 .. t-1 from the device history (hist_*[s % cap]: step size, sqrt(1 - beta2^s),
  * skip flag); last[r] = t for them.  Step t's scalars and skip flag are written to the history; the
  * other rows stay behind until replayed (kgat_adam_lazy_stamped_f32, kgat_adam_lazy_catchup_f32).
- * rows / count (nullable, both or neither): the stamped rows as a list (any order, device count) --
- * its short rows are walked one per lane group instead of testing every row's stamp.
+ * rows / count (nullable, both or neither): the stamped rows as a list (device count) -- its short
+ * rows are walked one per lane group instead of testing every row's stamp.
  * Same bits as the dense step. */
 int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
                                        const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
@@ -160,19 +160,18 @@ int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr *A, const int32_t *src_map
 /* stamp[r] = s for every row r = rows[k], k < *count (device; -1 entries skipped), and every column
  * of A's rows in the set (set_bits: the same rows as a bitmap, for the long rows' segments) -- the
  * rows a layer computed on the set reads, and (A^T's view) the rows where A^T . dS over the set can
- * be nonzero.  max_rows: the list's capacity (sizes the grid).  list_count (nullable): zeroed for
- * kgat_adam_lazy_stamped_f32's list. */
+ * be nonzero.  max_rows: the list's capacity (sizes the grid). */
 int kgat_rows_stamp(const kgat_csr *A, const int32_t *rows, const int32_t *count, int64_t max_rows,
-                    const uint32_t *set_bits, int32_t *stamp, int32_t s, int32_t *list_count, void *stream);
+                    const uint32_t *set_bits, int32_t *stamp, int32_t s, void *stream);
 
 /* The lazy CF table Adam's forward half: every row stamped t that is behind step t - 1 brought up to
  * it (skipped steps replayed from the history, last[r] = t - 1) -- the rows the frontier forward reads
- * are current before it reads them.  list / list_count (nullable, both or neither; the count zeroed
- * by kgat_rows_stamp): every stamped row appended, in no particular order. */
+ * are current before it reads them.  hit (nullable, int32 [n_rows]): 1 on the stamped rows, 0
+ * elsewhere -- kgat_hop_compact lists them for kgat_spmm_csr_masked_adam_lazy_f32. */
 int kgat_adam_lazy_stamped_f32(const int32_t *stamp, int64_t n_rows, float *p, float *m, float *v, int64_t ldp,
                                int32_t d, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
-                               int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, int32_t *list,
-                               int32_t *list_count, void *stream);
+                               int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, int32_t *hit,
+                               void *stream);
 
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);

@@ -112,6 +112,55 @@ __device__ __forceinline__ void lazy_replay(float& p, float& m, float& v, int32_
   }
 }
 
+// The history of the last kHistLds steps staged in LDS by a block before its replays: a replay of k
+// steps then costs k LDS reads instead of k dependent global-load round trips (a stale row's replay
+// loop was latency-bound); older steps still come from the global ring.
+constexpr int kHistLds = 256;
+struct LazyHistLds {
+  float sz[kHistLds];
+  float bc[kHistLds];
+  int32_t skip[kHistLds];
+};
+
+// Stage steps [lo, to] (lo = max(1, to - kHistLds + 1)) of the ring into L; every thread of the block
+// calls it (it ends with a barrier).  Returns lo.
+__device__ __forceinline__ int32_t stage_hist(LazyHistLds& L, const LazyHist& h, int32_t to) {
+  const int32_t lo = to - kHistLds + 1 > 1 ? to - kHistLds + 1 : 1;
+  for (int i = threadIdx.x; i < kHistLds; i += blockDim.x) {
+    const int32_t s = lo + i;
+    if (s <= to) {
+      const int32_t j = s % h.cap;
+      L.sz[i] = h.sz[j];
+      L.bc[i] = h.bc[j];
+      L.skip[i] = h.skip[j];
+    }
+  }
+  __syncthreads();
+  return lo;
+}
+
+// lazy_replay with steps >= lo read from the staged copy (same values, same order: same bits).
+__device__ __forceinline__ void lazy_replay_lds(float& p, float& m, float& v, int32_t from, int32_t to,
+                                                const LazyHist& h, const LazyHistLds& L, int32_t lo, float w1,
+                                                float b2, float w2, float eps) {
+  for (int32_t s = from + 1; s <= to; ++s) {
+    float sz, bc;
+    int32_t sk;
+    if (s >= lo) {
+      sz = L.sz[s - lo];
+      bc = L.bc[s - lo];
+      sk = L.skip[s - lo];
+    } else {
+      const int32_t j = s % h.cap;
+      sz = h.sz[j];
+      bc = h.bc[j];
+      sk = h.skip[j];
+    }
+    if (sk != 0) continue;
+    adam_elem(p, 0.f, m, v, w1, b2, w2, sz, bc, eps);
+  }
+}
+
 inline int blocks_for(int64_t work, int per_block, int cap) {
   int64_t b = (work + per_block - 1) / per_block;
   if (b < 1) b = 1;

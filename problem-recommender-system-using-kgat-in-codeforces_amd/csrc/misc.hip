@@ -346,6 +346,8 @@ __global__ __launch_bounds__(256) void adam_lazy_catchup_kernel(float* __restric
                                                                 int32_t* __restrict__ last, int32_t t, LazyHist h,
                                                                 float b1, float b2, float eps, StepSched sched) {
   if (sched.t != nullptr) t = *sched.t;
+  __shared__ LazyHistLds hl;
+  const int32_t lo = stage_hist(hl, h, t);
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const int64_t k = i / d;
   const int c = static_cast<int>(i % d);
@@ -354,7 +356,7 @@ __global__ __launch_bounds__(256) void adam_lazy_catchup_kernel(float* __restric
   if (from < t) {
     const int64_t o = r * d + c;
     float pp = p[o], mm = m[o], vv = v[o];
-    lazy_replay(pp, mm, vv, from, t, h, 1.f - b1, b2, 1.f - b2, eps);
+    lazy_replay_lds(pp, mm, vv, from, t, h, hl, lo, 1.f - b1, b2, 1.f - b2, eps);
     p[o] = pp;
     m[o] = mm;
     v[o] = vv;

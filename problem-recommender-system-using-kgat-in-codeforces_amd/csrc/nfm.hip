@@ -16,8 +16,6 @@
 
 #include "common.hpp"
 
-#include <cstdlib>
-
 namespace kgat {
 
 constexpr int kNfmMaxLayers = 4;
@@ -767,7 +765,6 @@ extern "C" int kgat_nfm_fwd_f32(const kgat_nfm* net, const int64_t* rowptr, cons
     o += (N.dims[l + 1] + 15) & ~15;
   }
   plan.wlds = o <= 12288;  // <= 48 KB of weights: 2-3 blocks per CU beside the tiles
-  if (getenv("KGAT_NFM_WLDS_BIG") && o + 4 * 16 * plan.P <= 40960) plan.wlds = true;  // TEMP A/B
   plan.tile_off = plan.wlds ? o : 0;
   plan.total = plan.tile_off + 4 * 16 * plan.P;
   const size_t lds = sizeof(float) * static_cast<size_t>(plan.total);

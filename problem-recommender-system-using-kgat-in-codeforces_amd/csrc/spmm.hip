@@ -650,10 +650,8 @@ namespace kgat {
 __global__ __launch_bounds__(256) void rows_stamp_kernel(kgat_csr A, const int32_t* __restrict__ rows,
                                                          const int32_t* __restrict__ count,
                                                          const uint32_t* __restrict__ set_bits,
-                                                         int32_t* __restrict__ stamp, int32_t s,
-                                                         int32_t* __restrict__ list_count, int seg_blocks) {
+                                                         int32_t* __restrict__ stamp, int32_t s, int seg_blocks) {
   const int lane = threadIdx.x & 63;
-  if (list_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *list_count = 0;  // filled by the next kernel
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (sg >= A.n_seg) return;
@@ -687,8 +685,7 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
                                                            float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, int64_t ld,
                                                            int32_t* __restrict__ last, int32_t t, LazyHist h,
-                                                           float b1, float b2, float eps, int32_t* __restrict__ list,
-                                                           int32_t* __restrict__ list_count) {
+                                                           float b1, float b2, float eps, int32_t* __restrict__ hit) {
   using S = SpmmShape<D>;
   constexpr int L = S::kLanes;
   const int lane = threadIdx.x & 63;
@@ -697,20 +694,11 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
   const int64_t r_begin = w * S::kRowsPerWave;
   const int64_t r_end = r_begin + S::kRowsPerWave < n_rows ? r_begin + S::kRowsPerWave : n_rows;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
+  __shared__ LazyHistLds hl;
+  const int32_t lo = stage_hist(hl, h, t - 1);
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
     const bool stamped = stamp[r] == t;
-    if (list != nullptr) {
-      // the stamped rows appended to the update's list: one atomic per wave (the order is free -- every
-      // row's update is independent of the others)
-      const uint64_t bal = __ballot(stamped && gl == 0);
-      if (bal != 0) {
-        const int leader = __ffsll(static_cast<unsigned long long>(bal)) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(list_count, __popcll(bal));
-        base = __shfl(base, leader);
-        if (stamped && gl == 0) list[base + __popcll(bal & ((uint64_t{1} << lane) - 1))] = static_cast<int32_t>(r);
-      }
-    }
+    if (hit != nullptr && gl == 0) hit[r] = stamped ? 1 : 0;  // the update's row list (kgat_hop_compact)
     if (!stamped) continue;
     const int32_t from = last[r];
     if (from >= t - 1) continue;
@@ -718,10 +706,10 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
     float4* M = reinterpret_cast<float4*>(m + r * ld) + gl;
     float4* V = reinterpret_cast<float4*>(v + r * ld) + gl;
     float4 pp = *P, mm = *M, vv = *V;
-    lazy_replay(pp.x, mm.x, vv.x, from, t - 1, h, w1, b2, w2, eps);
-    lazy_replay(pp.y, mm.y, vv.y, from, t - 1, h, w1, b2, w2, eps);
-    lazy_replay(pp.z, mm.z, vv.z, from, t - 1, h, w1, b2, w2, eps);
-    lazy_replay(pp.w, mm.w, vv.w, from, t - 1, h, w1, b2, w2, eps);
+    lazy_replay_lds(pp.x, mm.x, vv.x, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+    lazy_replay_lds(pp.y, mm.y, vv.y, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+    lazy_replay_lds(pp.z, mm.z, vv.z, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+    lazy_replay_lds(pp.w, mm.w, vv.w, from, t - 1, h, hl, lo, w1, b2, w2, eps);
     *P = pp;
     *M = mm;
     *V = vv;
@@ -731,12 +719,12 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
 
 template <int D>
 static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v, int64_t ld,
-                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, int32_t* list,
-                          int32_t* list_count, hipStream_t st) {
+                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, int32_t* hit,
+                          hipStream_t st) {
   const int64_t blocks = (n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
   if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(lazy_stamped_kernel<D>, dim3(blocks), dim3(256), 0, st, stamp, n_rows, p, m, v, ld, last, t, h,
-                     b1, b2, eps, list, list_count);
+                     b1, b2, eps, hit);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -744,15 +732,13 @@ static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float*
 }  // namespace kgat
 
 extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int32_t* count, int64_t max_rows,
-                               const uint32_t* set_bits, int32_t* stamp, int32_t s, int32_t* list_count,
-                               void* stream) {
+                               const uint32_t* set_bits, int32_t* stamp, int32_t s, void* stream) {
   using namespace kgat;
   if (!A || !rows || !count || !set_bits || !stamp || max_rows < 0 || A->n_rows < 0) return KGAT_ERR_INVALID;
   const int seg_blocks = (A->n_seg + 3) / 4;
   const int64_t list_blocks = std::min<int64_t>(std::max<int64_t>((max_rows + 15) / 16, 1), 2048);
   hipLaunchKernelGGL(rows_stamp_kernel, dim3(seg_blocks + list_blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, list_count,
-                     seg_blocks);
+                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, seg_blocks);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -760,20 +746,20 @@ extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int
 extern "C" int kgat_adam_lazy_stamped_f32(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v,
                                           int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
                                           float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
-                                          float eps, int32_t* list, int32_t* list_count, void* stream) {
+                                          float eps, int32_t* hit, void* stream) {
   using namespace kgat;
   if (!stamp || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || n_rows < 0 ||
-      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v) || ((list == nullptr) != (list_count == nullptr)))
+      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
     return KGAT_ERR_INVALID;
   if (n_rows == 0) return KGAT_OK;
   const LazyHist h{hist_sz, hist_bc, hist_skip, cap};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (d) {
-    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
-    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
-    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
-    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
-    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, list, list_count, st);
+    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
+    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
+    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
+    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
+    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
     default: return KGAT_ERR_UNSUPPORTED_DIM;
   }
 }

@@ -35,7 +35,7 @@ struct SpmmAdam {
   int32_t t;
   LazyHist hist;
   const int32_t* stamp;
-  // the stamped rows as a list (kgat_adam_lazy_stamped_f32 appends them, any order): its short rows
+  // the stamped rows as a list (kgat_adam_lazy_stamped_f32's flags, compacted by kgat_hop_compact): its short rows
   // are walked one per lane group, the groups striding over the list (the long rows: their segments)
   const int32_t* rows;
   const int32_t* count;

@@ -271,7 +271,9 @@ class _TableUpdate:
                 lazy.dirty = True
                 lazy.steps += 1
                 lazy.marked = None
-                lz = (lazy.stamp, *lazy._list(), lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
+                ls = lazy._lists()
+                lz = (lazy.stamp, *((ls[2], ls[3]) if ls is not None else (None, None)), lazy.last, lazy._t(opt),
+                      lazy.hist, lazy.CAP)
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
                                      lazy=lz)
         return run
@@ -393,7 +395,7 @@ class _LazyTableAdam:
         self.dirty = False  # rows behind the current step (a lazy step since the last flush)
         self.steps = 0  # lazy steps launched (tests, bench)
         self.stamp = None  # CF: stamp[r] = the step whose forward read row r (reach)
-        self.rows = self.count = None  # CF: the rows stamped by the last reach, listed (any order)
+        self.lists = None  # CF: (hit, map, rows, count, work) -- the rows stamped by the last reach, listed
         self.marked = None  # CF: the step the last reach stamped for
 
     def _t(self, opt) -> int:
@@ -453,19 +455,22 @@ class _LazyTableAdam:
         t = self._t(opt) + 1
         if self.stamp is None or self.stamp.numel() != self.last.numel() or self.stamp.device != self.last.device:
             self.stamp = torch.zeros_like(self.last)  # step numbers start at 1: a zero stamp marks nothing
-            self.rows = torch.empty_like(self.last)  # the stamped rows, listed for the update
-            self.count = torch.zeros(1, dtype=torch.int32, device=self.last.device)
+            # the stamped rows listed for the update: flags, their compaction (kgat_hop_compact)
+            n, dev = self.last.numel(), self.last.device
+            self.lists = (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                          torch.empty(n, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
+                          torch.empty(int(_lib.lib().kgat_hop_compact_work_bytes(n)), dtype=torch.uint8, device=dev))
         p = self.param.data
         st = opt.state.get(id(self.param))
         if st is None:  # the first step: every row is at step 0, nothing to replay -- the stamps only
             st = {"exp_avg": p, "exp_avg_sq": p}
         kernels.lazy_mark_catchup(graph, rows, count, set_bits, self.stamp, p, st["exp_avg"], st["exp_avg_sq"],
-                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, *self._list())
+                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, self._lists())
         self.marked = t
 
-    def _list(self):
+    def _lists(self):
         import os  # TEMP A/B: the stamped rows' list walk vs the per-row stamp test
-        return (self.rows, self.count) if os.environ.get("KGAT_LAZY_LIST", "1") == "1" else (None, None)
+        return self.lists if os.environ.get("KGAT_LAZY_LIST", "1") == "1" else None
 
     def dense_step_done(self, opt) -> None:
         """A dense step t was just applied to every row (each caught up before it): every row is current at
