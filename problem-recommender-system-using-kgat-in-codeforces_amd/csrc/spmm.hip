@@ -679,7 +679,9 @@ __global__ __launch_bounds__(256) void rows_stamp_kernel(kgat_csr A, const int32
 }
 
 // The lazy CF table Adam's forward half: every row stamped t (rows_stamp_kernel) that is behind step t
-// brought up to it (its skipped steps replayed, LazyHist).  Groups of D/4 lanes, one row at a time.
+// brought up to it (its skipped steps replayed, LazyHist).  A wave takes 64 consecutive rows at a time:
+// their stamps and step records are read coalesced (one load each, no per-row dependent chain), the
+// stale ones picked by a ballot and brought current D/4 lanes per row, kGroups rows at once.
 template <int D>
 __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __restrict__ stamp, int64_t n_rows,
                                                            float* __restrict__ p, float* __restrict__ m,
@@ -687,33 +689,44 @@ __global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __rest
                                                            int32_t* __restrict__ last, int32_t t, LazyHist h,
                                                            float b1, float b2, float eps, int32_t* __restrict__ hit) {
   using S = SpmmShape<D>;
-  constexpr int L = S::kLanes;
+  constexpr int G = S::kGroups;
   const int lane = threadIdx.x & 63;
-  const int g = lane / L, gl = lane % L;
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  const int64_t r_begin = w * S::kRowsPerWave;
-  const int64_t r_end = r_begin + S::kRowsPerWave < n_rows ? r_begin + S::kRowsPerWave : n_rows;
+  const int g = lane / S::kLanes, gl = lane % S::kLanes;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   __shared__ LazyHistLds hl;
   const int32_t lo = stage_hist(hl, h, t - 1);
-  for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
-    const bool stamped = stamp[r] == t;
-    if (hit != nullptr && gl == 0) hit[r] = stamped ? 1 : 0;  // the update's row list (kgat_hop_compact)
-    if (!stamped) continue;
-    const int32_t from = last[r];
-    if (from >= t - 1) continue;
-    float4* P = reinterpret_cast<float4*>(p + r * ld) + gl;
-    float4* M = reinterpret_cast<float4*>(m + r * ld) + gl;
-    float4* V = reinterpret_cast<float4*>(v + r * ld) + gl;
-    float4 pp = *P, mm = *M, vv = *V;
-    lazy_replay_lds(pp.x, mm.x, vv.x, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-    lazy_replay_lds(pp.y, mm.y, vv.y, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-    lazy_replay_lds(pp.z, mm.z, vv.z, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-    lazy_replay_lds(pp.w, mm.w, vv.w, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-    *P = pp;
-    *M = mm;
-    *V = vv;
-    if (gl == 0) last[r] = t - 1;  // the group's lanes (one wave) all read last[r] above
+  const int64_t nchunk = (n_rows + 63) / 64;
+  for (int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); c < nchunk;
+       c += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t r = c * 64 + lane;
+    const bool in = r < n_rows;
+    const bool stamped = in && stamp[r] == t;
+    if (hit != nullptr && in) hit[r] = stamped ? 1 : 0;  // the update's row list (kgat_hop_compact)
+    const int32_t fr = stamped ? last[r] : t;
+    uint64_t stale = __ballot(stamped && fr < t - 1);
+    while (stale != 0) {  // G stale rows per pass, row k of the pass -> lane group k
+      uint64_t mine = stale;
+      for (int k = 0; k < g; ++k) mine &= mine - 1;
+      const int bit = mine != 0 ? __ffsll(static_cast<unsigned long long>(mine)) - 1 : -1;
+#pragma unroll
+      for (int k = 0; k < G; ++k) stale &= stale - 1;
+      const int32_t from = __shfl(fr, bit < 0 ? 0 : bit);
+      if (bit >= 0) {
+        const int64_t row = c * 64 + bit;
+        float4* P = reinterpret_cast<float4*>(p + row * ld) + gl;
+        float4* M = reinterpret_cast<float4*>(m + row * ld) + gl;
+        float4* V = reinterpret_cast<float4*>(v + row * ld) + gl;
+        float4 pp = *P, mm = *M, vv = *V;
+        lazy_replay_lds(pp.x, mm.x, vv.x, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+        lazy_replay_lds(pp.y, mm.y, vv.y, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+        lazy_replay_lds(pp.z, mm.z, vv.z, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+        lazy_replay_lds(pp.w, mm.w, vv.w, from, t - 1, h, hl, lo, w1, b2, w2, eps);
+        *P = pp;
+        *M = mm;
+        *V = vv;
+        if (gl == 0) last[row] = t - 1;  // last[row] was read by the chunk load above
+      }
+    }
   }
 }
 
@@ -721,8 +734,7 @@ template <int D>
 static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v, int64_t ld,
                           int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, int32_t* hit,
                           hipStream_t st) {
-  const int64_t blocks = (n_rows + SpmmShape<D>::kRowsPerBlock - 1) / SpmmShape<D>::kRowsPerBlock;
-  if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
+  const int blocks = blocks_for((n_rows + 63) / 64, 4, kCUs * 8);  // persistent waves stride over 64-row chunks
   hipLaunchKernelGGL(lazy_stamped_kernel<D>, dim3(blocks), dim3(256), 0, st, stamp, n_rows, p, m, v, ld, last, t, h,
                      b1, b2, eps, hit);
   KGAT_LAUNCH_CHECK();
