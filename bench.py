@@ -529,8 +529,9 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
             result["frontier_forward"]["dp_table_exchange_steps"] = fr_exchange
         else:
             # + KGAT.lazy_cf_adam (the table Adam on the rows the step reads and reaches only, the others'
-            # zero-gradient steps replayed when next read; same bits, tests/test_gpu_parity.py) -- the
-            # training step driver.py runs
+            # zero-gradient steps replayed when next read; same bits, tests/test_gpu_parity.py).  Opt-in:
+            # at C2 the reached rows are a third of the table and the replays are VALU-bound,
+            # so driver.py keeps the dense fused update
             model.frontier_forward = model.lazy_cf_adam = True
             lel, lev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
             torch.cuda.synchronize()
@@ -563,16 +564,8 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                                "between GPUs): its GPU + host overhead per step, not a scaling measurement")
     if world == 1 and not args.no_kg_leg and not args.exchange_at_1:
         fr = result.get("frontier_forward", {})
-        cf_ms = fr.get("lazy_cf_adam", fr).get("ms_per_step", ms)
+        cf_ms = fr.get("ms_per_step", ms)  # driver.py's CF step: frontier forward + the dense fused update
         result["kg_refresh"] = kg_refresh_legs(model, pkg, layout, cfg, args, dev, len(inter), cf_ms)
-        lz_cf = fr.get("lazy_cf_adam")
-        if lz_cf is not None:
-            # the CF phase ends with one flush of the rows still owed steps (measured after the leg's
-            # warm-up + timed steps; rows are reached every few steps, so the epoch's is of that order)
-            ep = result["kg_refresh"]["epoch_estimate"]
-            ep["cf_flush_ms"] = lz_cf["flush_ms"]
-            ep["seconds"] += lz_cf["flush_ms"] / 1e3
-            ep["seconds_eager_lazy_kg"] += lz_cf["flush_ms"] / 1e3
     if ds is not None and cfg.get("nfm") and world == 1:
         result["nfm"] = nfm_legs(ds, cfg, args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

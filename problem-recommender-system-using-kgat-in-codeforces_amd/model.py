@@ -271,9 +271,7 @@ class _TableUpdate:
                 lazy.dirty = True
                 lazy.steps += 1
                 lazy.marked = None
-                ls = lazy._lists()
-                lz = (lazy.stamp, *((ls[2], ls[3]) if ls is not None else (None, None)), lazy.last, lazy._t(opt),
-                      lazy.hist, lazy.CAP)
+                lz = (lazy.stamp, lazy.lists[2], lazy.lists[3], lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
                                      lazy=lz)
         return run
@@ -465,12 +463,8 @@ class _LazyTableAdam:
         if st is None:  # the first step: every row is at step 0, nothing to replay -- the stamps only
             st = {"exp_avg": p, "exp_avg_sq": p}
         kernels.lazy_mark_catchup(graph, rows, count, set_bits, self.stamp, p, st["exp_avg"], st["exp_avg_sq"],
-                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, self._lists())
+                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, self.lists)
         self.marked = t
-
-    def _lists(self):
-        import os  # TEMP A/B: the stamped rows' list walk vs the per-row stamp test
-        return self.lists if os.environ.get("KGAT_LAZY_LIST", "1") == "1" else None
 
     def dense_step_done(self, opt) -> None:
         """A dense step t was just applied to every row (each caught up before it): every row is current at

@@ -1,15 +1,10 @@
 #!/bin/bash
-# Lazy CF Adam: parity tests (list walk and per-row stamp test), then the C2 bench's lazy_cf_adam leg
-# with both, under rocprofv3 --kernel-trace --stats (per-kernel times of every leg's step).
+# Lazy CF Adam: parity tests, then the C2 bench (lazy_cf_adam leg) under rocprofv3 --kernel-trace --stats.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "lazy or captured or frontier or fused" > gpurun_out/r04_lazycf_t.log 2>&1 || { tail -30 gpurun_out/r04_lazycf_t.log; exit 1; }
 tail -1 gpurun_out/r04_lazycf_t.log
-KGAT_LAZY_LIST=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "lazy_cf" > gpurun_out/r04_lazycf_t0.log 2>&1 || { tail -30 gpurun_out/r04_lazycf_t0.log; exit 1; }
-tail -1 gpurun_out/r04_lazycf_t0.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_lazy1 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-kg-leg > gpurun_out/r04_prof_lazy1.log 2>&1 || { tail -30 gpurun_out/r04_prof_lazy1.log; exit 1; }
-echo list ok
-KGAT_LAZY_LIST=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_lazy0 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-kg-leg > gpurun_out/r04_prof_lazy0.log 2>&1 || { tail -30 gpurun_out/r04_prof_lazy0.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_lazy2 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-kg-leg > gpurun_out/r04_prof_lazy2.log 2>&1 || { tail -30 gpurun_out/r04_prof_lazy2.log; exit 1; }
 echo done
