@@ -157,6 +157,24 @@ int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr *A, const int32_t *src_map
                                        float *hist_bc, int32_t *hist_skip, int32_t cap, float *workspace,
                                        int64_t workspace_floats, void *stream);
 
+/* The split CF table update (KGAT.split_table_update; replaces the dense torch.optim.Adam step of
+ * model.py:404-413 over the whole table): kgat_spmm_csr_masked_adam_ex_f32's product + Adam on the rows
+ * stamped s only (stamp[r] == s, kgat_rows_stamp: the source set and every row with an edge into it),
+ * the other rows passed over without a scan -- kgat_adam_unstamped_f32 steps those, with gradient 0,
+ * typically on a second stream at the same time.  Together: the dense step, bit for bit. */
+int kgat_spmm_csr_masked_adam_stamped_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                          const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
+                                          float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
+                                          float beta2, float bc2_sqrt, float eps, const int32_t *skip,
+                                          const int32_t *stamp, int32_t s, float *workspace, int64_t workspace_floats,
+                                          void *stream);
+
+/* Adam step (gradient 0) on every row of p / m / v ([n_rows, d], contiguous) NOT stamped s; nothing
+ * when *skip != 0 (skip nullable). */
+int kgat_adam_unstamped_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *stamp, int32_t s,
+                            float step_size, float beta1, float beta2, float bc2_sqrt, float eps, const int32_t *skip,
+                            void *stream);
+
 /* stamp[r] = s for every row r = rows[k], k < *count (device; -1 entries skipped), and every column
  * of A's rows in the set (set_bits: the same rows as a bitmap, for the long rows' segments) -- the
  * rows a layer computed on the set reads, and (A^T's view) the rows where A^T . dS over the set can

@@ -612,6 +612,31 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
+extern "C" int kgat_spmm_csr_masked_adam_stamped_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                     int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                                     const uint64_t* src_rank, float* p, float* m, float* v,
+                                                     int64_t ldp, int32_t d, float step_size, float beta1, float beta2,
+                                                     float bc2_sqrt, float eps, const int32_t* skip,
+                                                     const int32_t* stamp, int32_t s, float* workspace,
+                                                     int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !p || !m || !v || !stamp || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) ||
+      (ldp & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
+      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
+            nullptr, nullptr, nullptr, nullptr};
+  // stamp without last[]: the stamped rows get the dense step (adam_row_step), the others none here
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, s, LazyHist{}, stamp,
+                     nullptr, nullptr};
+  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+}
+
 extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
                                                   int64_t ldxc, const float* Yc_init, int64_t ldyc,
                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,

@@ -258,14 +258,28 @@ class _TableUpdate:
         """Drop the pending gradient (a step whose update is abandoned: update_cf_weights raised)."""
         self.pending = None
 
-    def launch(self, lazy: "_LazyTableAdam | None" = None, opt=None):
+    def launch(self, lazy: "_LazyTableAdam | None" = None, opt=None, split: "_SplitTableUpdate | None" = None):
         """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...)); with ``lazy`` on
-        the rows the product reaches only (kgat_spmm_csr_masked_adam_lazy_f32, KGAT.lazy_cf_adam)."""
+        the rows the product reaches only (kgat_spmm_csr_masked_adam_lazy_f32, KGAT.lazy_cf_adam); with
+        ``split`` the reached rows and the others as two launches on two streams (KGAT.split_table_update)."""
         graph, src_map, Xc, Yc, rank = self.pending
         self.pending = None
         p = self.param.data
 
         def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
+            if split is not None:
+                stamp, sv = split.stamp, split.marked
+                split.marked = None
+                cur = torch.cuda.current_stream(p.device)
+                side = split.side_stream(p.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):  # the zero-gradient rows: a pure p / m / v stream
+                    kernels.adam_unstamped(p, m, v, stamp, sv, step_size, b1, b2, bc2s, eps, skip)
+                kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
+                                         stamped=(stamp, sv))
+                cur.wait_stream(side)
+                split.steps += 1
+                return
             lz = None
             if lazy is not None:
                 lazy.dirty = True
@@ -275,6 +289,42 @@ class _TableUpdate:
             kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
                                      lazy=lz)
         return run
+
+
+class _SplitTableUpdate:
+    """The CF step's fused table update as two launches over disjoint rows (opt-in:
+    ``KGAT.split_table_update``, with ``frontier_forward`` and ``fuse_table_update``; single process).
+
+    The dense fused kernel (kgat_spmm_csr_masked_adam_f32) walks every row of A^T: for the two thirds of
+    C2's rows the frontier step's gradient A^T . dS_0 + dXd_0 is exactly zero, yet each is scanned (its
+    edges tested against the first hop, a latency-bound chain) before its Adam step streams p / m / v.
+    Here the frontier forward stamps the rows the gradient can reach (kgat_rows_stamp: the first hop and
+    every column of A's rows in it -- the rows its layer-0 product reads anyway), and the update runs
+    the product + Adam on the stamped rows only (kgat_spmm_csr_masked_adam_stamped_f32) while a second
+    stream steps the others with gradient 0 as a plain stream (kgat_adam_unstamped_f32).  Every row gets
+    its one Adam step with the same gradient: the dense update's bits."""
+
+    def __init__(self, param: torch.Tensor):
+        self.param = param
+        self.enabled = False
+        self.stamp = None
+        self.marked = None  # the stamp value of the current step's forward (None: no marks for it)
+        self.count = 0      # stamp values issued (a value never repeats: zero-initialised stamps mark nothing)
+        self.steps = 0      # split updates launched (tests, bench)
+        self._side = None
+
+    def side_stream(self, dev) -> torch.cuda.Stream:
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
+    def mark(self, graph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor) -> None:
+        n, dev = self.param.shape[0], self.param.device
+        if self.stamp is None or self.stamp.numel() != n or self.stamp.device != dev:
+            self.stamp = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.count += 1
+        kernels.rows_stamp(graph, rows, count, set_bits, self.stamp, self.count)
+        self.marked = self.count
 
 
 class _KGTableUpdate:
@@ -769,7 +819,7 @@ def _tile_forward_ok(din: int, dout: int) -> bool:
         kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
 
 
-def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=None):
+def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=None, split=None):
     """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1, 2 or 3, the
     restricted layers with the fused kernels' saved state).  The BPR loss reads the batch rows F of
     every table (model.py:189-191), so the last layer's output is needed on F only, and layer L-2's
@@ -804,6 +854,12 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=
     # layer l's output row set: None = every row (layer 0 of 3), the first hop for layer L-2, the batch
     # rows F for the last layer
     sets = [None] * first + [(hrows, hcount, bits1)] * (L - 1 - first) + [(rows, fcount, fbits)]
+    if split is not None:
+        # the split table update (KGAT.split_table_update): the rows the step's table gradient can reach
+        if sets[0] is None:
+            split.marked = None  # layer 0 runs whole: the update stays the whole-table kernel
+        else:
+            split.mark(graph, *sets[0])
     if lazy is not None:
         # the lazy CF table Adam (KGAT.lazy_cf_adam): the rows this forward reads brought up to the step
         lz, opt = lazy
@@ -864,11 +920,14 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, hook, _tu, frontier, lazy = cfg
+        graph, drops, seeds, reg, hook, _tu, frontier, lazy, split = cfg
         ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook)
-        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, lazy) if frontier else None
+        fw = (_frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, lazy, split) if frontier
+              else None)
         if fw is None and lazy is not None:
             lazy[0].catch_up(lazy[1])  # the full forward reads every row
+        if fw is None and split is not None:
+            split.marked = None
         if fw is not None:
             tables, sides, states, ctx.early = fw
         else:
@@ -890,7 +949,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg, hook, tu, _frontier, _lazy = ctx.cfg
+        graph, drops, seeds, reg, hook, tu, _frontier, _lazy, _split = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -1106,6 +1165,7 @@ class KGAT(nn.Module):
         self._graph_key = None
         self._ids = _IdGuard()
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
+        self._split_update = _SplitTableUpdate(self._user_entity_embedding.weight)
         self._kg_table_update = _KGTableUpdate(self._user_entity_embedding.weight)
         self._lazy_kg = _LazyTableAdam(self._user_entity_embedding.weight)
         self._lazy_cf = _LazyTableAdam(self._user_entity_embedding.weight)
@@ -1131,6 +1191,18 @@ class KGAT(nn.Module):
         """Bring every table row and the KG optimiser's moments up to the current KG step (lazy_kg_adam)."""
         if self._lazy_kg.last is not None and getattr(self, "_kg_optimizer", None) is not None:
             self._lazy_kg.catch_up(self._kg_optimizer)
+
+    @property
+    def split_table_update(self) -> bool:
+        """Opt-in (with ``frontier_forward`` and ``fuse_table_update``; single process): the fused CF table
+        update as two launches on two streams -- product + Adam on the rows the frontier forward stamped,
+        a zero-gradient Adam stream over the rest (_SplitTableUpdate; same bits as the dense update)."""
+        return self._split_update.enabled
+
+    @split_table_update.setter
+    def split_table_update(self, on: bool) -> None:
+        self._split_update.enabled = bool(on)
+        self._split_update.marked = None
 
     @property
     def lazy_cf_adam(self) -> bool:
@@ -1317,7 +1389,11 @@ class KGAT(nn.Module):
             lazy = (lz, opt)
         else:
             self.flush_cf_table()
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier, lazy)
+        split = self._split_update
+        split.marked = None
+        if lazy is not None or not (split.enabled and frontier and hook is None and self._table_update.enabled):
+            split = None
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier, lazy, split)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
@@ -1425,6 +1501,9 @@ class KGAT(nn.Module):
             # gradient is summed with the deferred product first (materialize adds into .grad)
             if (row_ranges and id(tu.param) in row_ranges) or tu.param.grad is not None:
                 tu.materialize()
+            elif self._split_update.enabled and self._split_update.marked is not None and not lazy.enabled:
+                # this step's forward stamped the rows its table gradient can reach
+                fused = {id(tu.param): tu.launch(split=self._split_update)}
             elif lazy.enabled and lazy.last is not None and lazy.marked == lazy._t(opt) + 1:
                 # this step's forward stamped the rows it read and the gradient's rows (reach)
                 if lazy._t(opt) + 1 - lazy.flushed_at >= lazy.CAP:
@@ -1439,6 +1518,7 @@ class KGAT(nn.Module):
             lazy.catch_up(opt)
         opt.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
         lazy.marked = None
+        self._split_update.marked = None
         if dense_lazy:
             lazy.dense_step_done(opt)
         opt.zero_grad()

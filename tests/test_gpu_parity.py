@@ -1909,13 +1909,16 @@ def test_lazy_kg_adam_bit_identical(pkg, dim):
             assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
 
 
+@pytest.mark.parametrize("mode", ["lazy", "split"])
 @pytest.mark.parametrize("dim", [64, 128])
-def test_lazy_cf_adam_bit_identical(pkg, dim):
+def test_lazy_cf_adam_bit_identical(pkg, dim, mode):
     """KGAT.lazy_cf_adam (the frontier CF step's table Adam on the rows the step reads and reaches only, the
-    other rows' zero-gradient steps replayed when next read) vs the dense fused CF update: over CF phases
-    between lazy KG phases -- with a step whose ids are out of range, the skip flag set while a step is in
-    flight, a full-table (non-frontier) step, a no-grad loss evaluation, a PREDICT and a second
-    build_optimizer -- the losses, parameters and both optimisers' states are equal bit for bit."""
+    other rows' zero-gradient steps replayed when next read) and KGAT.split_table_update (the reached rows'
+    product + Adam and the other rows' zero-gradient Adam as two launches on two streams) vs the dense
+    fused CF update: over CF phases between lazy KG phases -- with a step whose ids are out of range, the
+    skip flag set while a step is in flight, a full-table (non-frontier) step, a no-grad loss evaluation, a
+    PREDICT and a second build_optimizer -- the losses, parameters and both optimisers' states are equal
+    bit for bit."""
     graph_mod, _ = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
     lay = graph_mod.build_layout(U, E, inter, trip)
@@ -1931,7 +1934,10 @@ def test_lazy_cf_adam_bit_identical(pkg, dim):
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
         m.fuse_table_update = m.fuse_kg_table_update = m.lazy_kg_adam = True
         m.frontier_forward = True
-        m.lazy_cf_adam = lazy
+        if mode == "lazy":
+            m.lazy_cf_adam = lazy
+        else:
+            m.split_table_update = lazy
         models.append(m)
     rng = np.random.default_rng(8)
     for phase in range(4):
@@ -1972,7 +1978,8 @@ def test_lazy_cf_adam_bit_identical(pkg, dim):
                     m(cfs[0][0], cfs[0][1], mode=pkg.KGATMode.PREDICT)
                 m.build_optimizer(cf_lr=2e-3, kg_lr=1e-4)
         assert torch.equal(losses[0], losses[1]), phase
-    assert models[1]._lazy_cf.steps >= 15 and models[0]._lazy_cf.steps == 0
+    used = (lambda m: m._lazy_cf.steps) if mode == "lazy" else (lambda m: m._split_update.steps)
+    assert used(models[1]) >= 15 and used(models[0]) == 0
     sa, sb = models[0].state_dict(), models[1].state_dict()
     for k in sa:
         if not sa[k].is_sparse:
