@@ -312,8 +312,7 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(acc[1], acc[2], d, a), compulsory_bytes(acc[1], acc[2], d)))
         elif acc is False:
             fwd.append((e0.elapsed_time(e1), d, spmm_bytes(n, nnz, d, False), compulsory_bytes(n, nnz, d)))
-    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events
-           if tr and acc not in ("masked", "fused_adam", "reach", "unstamped_adam")]
+    bwd = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if tr and acc not in ("masked", "fused_adam")]
     masked = [e0.elapsed_time(e1) for e0, e1, d, tr, acc in events if acc in ("masked", "fused_adam")]
     fused = [(e0.elapsed_time(e1), d) for e0, e1, d, tr, acc in events if acc == "fused_adam"]
     # the layer-0 launches (d0 wide; the row-sharded mode's gathered column chunks are narrower)
@@ -527,48 +526,6 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
                     "does not visit every edge)"}
         if world > 1:
             result["frontier_forward"]["dp_table_exchange_steps"] = fr_exchange
-        else:
-            # + KGAT.lazy_cf_adam (the table Adam on the rows the step reads and reaches only, the others'
-            # zero-gradient steps replayed when next read; same bits, tests/test_gpu_parity.py).  Opt-in:
-            # at C2 the reached rows are a third of the table and the replays are VALU-bound,
-            # so driver.py keeps the dense fused update
-            model.frontier_forward = model.lazy_cf_adam = True
-            lel, lev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            model.flush_cf_table()
-            torch.cuda.synchronize()
-            flush_ms = (time.perf_counter() - t1) * 1e3
-            model.frontier_forward = model.lazy_cf_adam = False
-            lms = lel / args.steps * 1e3
-
-            def ev_ms(tag):
-                t = [e0.elapsed_time(e1) for e0, e1, _d, _tr, acc in lev if acc == tag]
-                return float(np.mean(t)) if t else None
-            # + KGAT.split_table_update (the reached rows' product + Adam, and the other rows' zero-gradient
-            # Adam stream on a second stream; the dense update's bits)
-            model.frontier_forward = model.split_table_update = True
-            sel, sev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
-            model.frontier_forward = model.split_table_update = False
-            sms = sel / args.steps * 1e3
-
-            def sev_ms(tag):
-                t = [e0.elapsed_time(e1) for e0, e1, _d, _tr, acc in sev if acc == tag]
-                return float(np.mean(t)) if t else None
-            result["frontier_forward"]["split_table_update"] = {
-                "ms_per_step": sms, "bpr_pairs_per_s": B / (sms * 1e-3), "speedup_vs_dense_update": fms / sms,
-                "stamped_update_avg_ms": sev_ms("fused_adam"), "unstamped_adam_avg_ms": sev_ms("unstamped_adam"),
-                "what": "frontier CF step with the split table update: the forward stamps the rows its table "
-                        "gradient can reach (kgat_rows_stamp), the update runs product + Adam on them "
-                        "(kgat_spmm_csr_masked_adam_stamped_f32) while a second stream steps the rest with gradient "
-                        "0 (kgat_adam_unstamped_f32); the two launches overlap, so their event times do not add"}
-            result["frontier_forward"]["lazy_cf_adam"] = {
-                "ms_per_step": lms, "bpr_pairs_per_s": B / (lms * 1e-3), "speedup_vs_dense_update": fms / lms,
-                "table_update_avg_ms": ev_ms("fused_adam"), "reach_catchup_avg_ms": ev_ms("reach"),
-                "flush_ms": flush_ms, "flush_steps_pending": args.warmup + args.steps,
-                "what": "frontier CF step with the lazy table Adam: the forward brings the rows it reads current "
-                        "(kgat_lazy_reach_catchup_f32), the fused product + Adam steps the rows its product reaches "
-                        "(kgat_spmm_csr_masked_adam_lazy_f32); flush_ms: every row brought current after the leg"}
     result["value_note"] = ("value = n_gpus x nnz x L / t_step: each data-parallel replica runs the reference step's "
                             "full propagation over every edge for its own 256-pair batch (weak scaling; replicas "
                             "repeat the same graph's work); bpr_pairs_per_s (and frontier_forward.bpr_pairs_per_s, "
@@ -580,8 +537,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         result["rehearsal"] = ("the N-rank table exchange forced at world 1 over RCCL (collectives move no data "
                                "between GPUs): its GPU + host overhead per step, not a scaling measurement")
     if world == 1 and not args.no_kg_leg and not args.exchange_at_1:
-        fr = result.get("frontier_forward", {})
-        cf_ms = fr.get("ms_per_step", ms)  # driver.py's CF step: frontier forward + the dense fused update
+        cf_ms = result.get("frontier_forward", {}).get("ms_per_step", ms)
         result["kg_refresh"] = kg_refresh_legs(model, pkg, layout, cfg, args, dev, len(inter), cf_ms)
     if ds is not None and cfg.get("nfm") and world == 1:
         result["nfm"] = nfm_legs(ds, cfg, args, dev)

@@ -138,59 +138,6 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
                                         float eps, const int32_t *skip, float *workspace, int64_t workspace_floats,
                                         void *stream);
 
-/* Lazy form of kgat_spmm_csr_masked_adam_ex_f32 (the CF phase's table Adam on the rows the step
- * touches; replaces the dense torch.optim.Adam step of model.py:404-413 over the whole table): Adam
- * step t (>= 1) on the rows stamped t (stamp[r] == t, kgat_rows_stamp: the source set and every row
- * with an edge into it -- outside them the gradient is exactly 0), each after replaying its skipped
- * steps last[r]+1 .. t-1 from the device history (hist_*[s % cap]: step size, sqrt(1 - beta2^s),
- * skip flag); last[r] = t for them.  Step t's scalars and skip flag are written to the history; the
- * other rows stay behind until replayed (kgat_adam_lazy_stamped_f32, kgat_adam_lazy_catchup_f32).
- * rows / count (nullable, both or neither): the stamped rows as a list (device count) -- its short
- * rows are walked one per lane group instead of testing every row's stamp.
- * Same bits as the dense step. */
-int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
-                                       const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
-                                       float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
-                                       float beta2, float bc2_sqrt, float eps, const int32_t *skip,
-                                       const int32_t *stamp, const int32_t *rows, const int32_t *count,
-                                       int32_t *last, int32_t t, float *hist_sz,
-                                       float *hist_bc, int32_t *hist_skip, int32_t cap, float *workspace,
-                                       int64_t workspace_floats, void *stream);
-
-/* The split CF table update (KGAT.split_table_update; replaces the dense torch.optim.Adam step of
- * model.py:404-413 over the whole table): kgat_spmm_csr_masked_adam_ex_f32's product + Adam on the rows
- * stamped s only (stamp[r] == s, kgat_rows_stamp: the source set and every row with an edge into it),
- * the other rows passed over without a scan -- kgat_adam_unstamped_f32 steps those, with gradient 0,
- * typically on a second stream at the same time.  Together: the dense step, bit for bit. */
-int kgat_spmm_csr_masked_adam_stamped_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
-                                          const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
-                                          float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
-                                          float beta2, float bc2_sqrt, float eps, const int32_t *skip,
-                                          const int32_t *stamp, int32_t s, float *workspace, int64_t workspace_floats,
-                                          void *stream);
-
-/* Adam step (gradient 0) on every row of p / m / v ([n_rows, d], contiguous) NOT stamped s; nothing
- * when *skip != 0 (skip nullable). */
-int kgat_adam_unstamped_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *stamp, int32_t s,
-                            float step_size, float beta1, float beta2, float bc2_sqrt, float eps, const int32_t *skip,
-                            void *stream);
-
-/* stamp[r] = s for every row r = rows[k], k < *count (device; -1 entries skipped), and every column
- * of A's rows in the set (set_bits: the same rows as a bitmap, for the long rows' segments) -- the
- * rows a layer computed on the set reads, and (A^T's view) the rows where A^T . dS over the set can
- * be nonzero.  max_rows: the list's capacity (sizes the grid). */
-int kgat_rows_stamp(const kgat_csr *A, const int32_t *rows, const int32_t *count, int64_t max_rows,
-                    const uint32_t *set_bits, int32_t *stamp, int32_t s, void *stream);
-
-/* The lazy CF table Adam's forward half: every row stamped t that is behind step t - 1 brought up to
- * it (skipped steps replayed from the history, last[r] = t - 1) -- the rows the frontier forward reads
- * are current before it reads them.  hit (nullable, int32 [n_rows]): 1 on the stamped rows, 0
- * elsewhere -- kgat_hop_compact lists them for kgat_spmm_csr_masked_adam_lazy_f32. */
-int kgat_adam_lazy_stamped_f32(const int32_t *stamp, int64_t n_rows, float *p, float *m, float *v, int64_t ldp,
-                               int32_t d, int32_t *last, int32_t t, float *hist_sz, float *hist_bc,
-                               int32_t *hist_skip, int32_t cap, float beta1, float beta2, float eps, int32_t *hit,
-                               void *stream);
-
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 

@@ -194,18 +194,6 @@ _SIGNATURES = {
     "kgat_spmm_csr_masked_adam_block_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_i64,
                                                            c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32,
                                                            c_f32, c_f32, c_vp, c_vp, c_i64, c_vp]),
-    "kgat_spmm_csr_masked_adam_lazy_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
-                                                          c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
-                                                          c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp,
-                                                          c_vp, c_i32, c_vp, c_i64, c_vp]),
-    "kgat_spmm_csr_masked_adam_stamped_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64,
-                                                             c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32,
-                                                             c_f32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp]),
-    "kgat_adam_unstamped_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32,
-                                               c_f32, c_vp, c_vp]),
-    "kgat_rows_stamp": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp]),
-    "kgat_adam_lazy_stamped_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp,
-                                                  c_vp, c_i32, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "kgat_csr_mark_rows": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kgat_biinter_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),
     "kgat_biinter_bwd_gemm_rows_work_floats": (c_i64, [c_i64, c_i32, c_i32]),

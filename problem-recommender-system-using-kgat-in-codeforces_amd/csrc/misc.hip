@@ -277,63 +277,7 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(float* __restrict__ p, f
   }
 }
 
-// The zero-gradient half of the split CF table update: Adam step on every row NOT stamped s (its
-// gradient is exactly 0 -- stamp: kgat_rows_stamp), a pure p / m / v stream at adam_rows' access
-// pattern; the stamped rows are stepped by kgat_spmm_csr_masked_adam_stamped_f32 (on another stream).
-__global__ __launch_bounds__(256) void adam_unstamped_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                             float* __restrict__ v, int64_t n4, int d4,
-                                                             const int32_t* __restrict__ stamp, int32_t s,
-                                                             float step_size, float b1, float b2, float bc2s,
-                                                             float eps, const int32_t* __restrict__ skip) {
-  if (skip != nullptr && *skip != 0) return;
-  const float w1 = 1.f - b1, w2 = 1.f - b2;
-  const int64_t chunks = (n4 + 1023) / 1024;
-  for (int64_t c = blockIdx.x; c < chunks; c += gridDim.x) {
-    float4 pp[4], mm[4], vv[4];
-    bool go[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t e4 = c * 1024 + u * 256 + threadIdx.x;
-      go[u] = e4 < n4 && stamp[e4 / d4] != s;
-      if (go[u]) {
-        pp[u] = ld4<2>(p + 4 * e4);
-        mm[u] = ld4<2>(m + 4 * e4);
-        vv[u] = ld4<2>(v + 4 * e4);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!go[u]) continue;
-      const int64_t e4 = c * 1024 + u * 256 + threadIdx.x;
-      float* P = &pp[u].x;
-      float* Mv = &mm[u].x;
-      float* Vv = &vv[u].x;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) adam_elem(P[k], 0.f, Mv[k], Vv[k], w1, b2, w2, step_size, bc2s, eps);
-      st4<2>(p + 4 * e4, pp[u]);
-      st4<2>(m + 4 * e4, mm[u]);
-      st4<2>(v + 4 * e4, vv[u]);
-    }
-  }
-}
-
 }  // namespace kgat
-
-extern "C" int kgat_adam_unstamped_f32(float* p, float* m, float* v, int64_t n_rows, int32_t d, const int32_t* stamp,
-                                       int32_t s, float step_size, float beta1, float beta2, float bc2_sqrt, float eps,
-                                       const int32_t* skip, void* stream) {
-  if (!p || !m || !v || !stamp || n_rows < 0 || d < 4 || (d & 3)) return KGAT_ERR_INVALID;
-  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15)
-    return KGAT_ERR_INVALID;
-  const int64_t n4 = n_rows * (d / 4);
-  if (n4 == 0) return KGAT_OK;
-  const int64_t chunks = (n4 + 1023) / 1024;
-  const int grid = static_cast<int>(chunks < kgat::kCUs * 8 ? chunks : kgat::kCUs * 8);
-  hipLaunchKernelGGL(kgat::adam_unstamped_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), p,
-                     m, v, n4, d / 4, stamp, s, step_size, beta1, beta2, bc2_sqrt, eps, skip);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
 
 extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
                                    float eps, void* stream) {

@@ -64,29 +64,6 @@ __device__ __forceinline__ void adam_row_step(const SpmmAdam& a, int64_t row, in
   __builtin_nontemporal_store(r.v, reinterpret_cast<floatx4*>(a.v + o));
 }
 
-// Lazy step t on one row segment: its skipped steps replayed first (rows the forward's
-// kgat_lazy_reach_catchup_f32 brought current replay none), then step t with gradient g.
-__device__ __forceinline__ void adam_row_lazy(const SpmmAdam& a, int64_t row, int gl, float4 g) {
-  const int32_t from = a.last[row];
-  AdamRow r = adam_row_load(a, row, gl);
-  const float w1 = 1.f - a.b1, w2 = 1.f - a.b2;
-  const float gg[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float pk = r.p[k], mk = r.m[k], vk = r.v[k];
-    lazy_replay(pk, mk, vk, from, a.t - 1, a.hist, w1, a.b2, w2, a.eps);
-    adam_elem(pk, gg[k], mk, vk, w1, a.b2, w2, a.step_size, a.bc2s, a.eps);
-    r.p[k] = pk;
-    r.m[k] = mk;
-    r.v[k] = vk;
-  }
-  const int64_t o = row * a.ld + 4 * gl;
-  __builtin_nontemporal_store(r.p, reinterpret_cast<floatx4*>(a.p + o));
-  __builtin_nontemporal_store(r.m, reinterpret_cast<floatx4*>(a.m + o));
-  __builtin_nontemporal_store(r.v, reinterpret_cast<floatx4*>(a.v + o));
-  if (gl == 0) a.last[row] = a.t;  // the group's lanes (one wave) all read last[row] above
-}
-
 // Final write of one output row segment (lane gl) in the five modes: row is
 // the (global-id) row of A, out the row of Y it lands in (row, or its position
 // in the output set for kMaskedRows).  kMaskedAdam writes no Y: the row is the
@@ -106,10 +83,6 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
   if (MODE == kMaskedAdam) {
-    if (io.adam.last != nullptr) {
-      adam_row_lazy(io.adam, row, gl, acc);  // a stamped row (the others never get here)
-      return;
-    }
     adam_row_step(io.adam, row, gl, acc, adam_row_load(io.adam, row, gl));
     return;
   }
@@ -119,12 +92,6 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
   }
   *y = acc;
-}
-
-// The lazy table update passes over the rows not stamped with its step (gradient exactly 0).
-template <int MODE>
-__device__ __forceinline__ bool lazy_pass(const SpmmIo& io, int64_t row) {
-  return MODE == kMaskedAdam && io.adam.stamp != nullptr && io.adam.stamp[row] != io.adam.t;
 }
 
 // Source rows in flight per lane group in the row-set forward (kRows); 4, 8 and 16 measured
@@ -140,7 +107,6 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
   if (s >= A.n_seg) return;
   const int row = A.seg_row[s];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
-  if (lazy_pass<MODE>(io, row)) return;
   const int64_t beg = A.seg_beg[s];
   const int64_t row_end = A.rowptr[row + 1];
   const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
@@ -171,37 +137,10 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
-  if (MODE == kMaskedAdam) {
-    const bool skipped = io.adam.skip != nullptr && *io.adam.skip != 0;
-    if (io.adam.last != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
-      // step t's scalars and skip flag, for the rows whose step t is replayed later
-      const int32_t j = io.adam.t % io.adam.hist.cap;
-      io.adam.hist.sz[j] = io.adam.step_size;
-      io.adam.hist.bc[j] = io.adam.bc2s;
-      io.adam.hist.skip[j] = skipped ? 1 : 0;
-    }
-    if (skipped) return;
-  }
+  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
     long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base);
-    return;
-  }
-
-  if (MODE == kMaskedAdam && io.adam.rows != nullptr) {
-    // ---- the lazy update's stamped short rows, one group per list entry (as kRows below)
-    const int64_t cnt = *io.adam.count;
-    const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * S::kGroups;
-    for (int64_t k = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + wave) * S::kGroups + g; k < cnt;
-         k += stride) {
-      const int64_t r = io.adam.rows[k];
-      const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-      if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      bool any = false;
-      gather_edges<D, true>(A, io, beg, end, base, gl, acc, any);
-      store_row<MODE>(io, r, r, gl, acc, any);
-    }
     return;
   }
 
@@ -233,7 +172,6 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
-    if (lazy_pass<MODE>(io, r)) continue;
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -257,7 +195,6 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
   if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
   const int row = A.long_rows[lr];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
-  if (lazy_pass<MODE>(io, row)) return;
   const float4* P = reinterpret_cast<const float4*>(io.part);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int s_end = A.long_seg_off[lr + 1];
@@ -276,8 +213,7 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
   int64_t row_blocks = (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
-  if ((MODE == kMaskedRows || MODE == kRows || (MODE == kMaskedAdam && io.adam.rows != nullptr)) && row_blocks > 2048)
-    row_blocks = 2048;  // waves stride over the set (size on device)
+  if ((MODE == kMaskedRows || MODE == kRows) && row_blocks > 2048) row_blocks = 2048;  // waves stride over the set (size on device)
   const int64_t grid = seg_blocks + row_blocks;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL((spmm_main_kernel<D, MODE>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
@@ -607,198 +543,8 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
     return KGAT_ERR_WORKSPACE;
   SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, yc_row0, nullptr, src_rank,
             nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, 0, LazyHist{}, nullptr,
-                     nullptr, nullptr};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
-extern "C" int kgat_spmm_csr_masked_adam_stamped_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
-                                                     int64_t ldxc, const float* Yc_init, int64_t ldyc,
-                                                     const uint64_t* src_rank, float* p, float* m, float* v,
-                                                     int64_t ldp, int32_t d, float step_size, float beta1, float beta2,
-                                                     float bc2_sqrt, float eps, const int32_t* skip,
-                                                     const int32_t* stamp, int32_t s, float* workspace,
-                                                     int64_t workspace_floats, void* stream) {
-  using namespace kgat;
-  if (!A || !src_map || !Xc || !p || !m || !v || !stamp || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) ||
-      (ldp & 3))
-    return KGAT_ERR_INVALID;
-  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
-      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
-    return KGAT_ERR_INVALID;
-  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
-    return KGAT_ERR_WORKSPACE;
-  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
-            nullptr, nullptr, nullptr, nullptr};
-  // stamp without last[]: the stamped rows get the dense step (adam_row_step), the others none here
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, nullptr, s, LazyHist{}, stamp,
-                     nullptr, nullptr};
-  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
-extern "C" int kgat_spmm_csr_masked_adam_lazy_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
-                                                  int64_t ldxc, const float* Yc_init, int64_t ldyc,
-                                                  const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
-                                                  int32_t d, float step_size, float beta1, float beta2,
-                                                  float bc2_sqrt, float eps, const int32_t* skip,
-                                                  const int32_t* stamp, const int32_t* rows, const int32_t* count,
-                                                  int32_t* last, int32_t t, float* hist_sz,
-                                                  float* hist_bc, int32_t* hist_skip, int32_t cap, float* workspace,
-                                                  int64_t workspace_floats, void* stream) {
-  using namespace kgat;
-  if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows < 1 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
-    return KGAT_ERR_INVALID;
-  if (!stamp || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || ((rows == nullptr) != (count == nullptr)))
-    return KGAT_ERR_INVALID;
-  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
-      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
-    return KGAT_ERR_INVALID;
-  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
-    return KGAT_ERR_WORKSPACE;
-  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
-            nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip, last, t,
-                     LazyHist{hist_sz, hist_bc, hist_skip, cap}, stamp, rows, count};
-  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
-namespace kgat {
-
-// The lazy CF table Adam's marks: stamp[r] = s for every row r of the set (rows[0 .. *count)) and every
-// column of A's rows in the set -- the rows the frontier forward's layer on the set reads, and the rows
-// of A^T with an edge into it, i.e. where the table gradient A^T . dS can be nonzero.  Every writer
-// stores the same value (no atomics, no clearing: a stamp of an older step never equals s).  Blocks
-// [0, seg_blocks): one long-row segment per wave (its row's set bit decides); the rest: 16-lane groups
-// striding over the list's short rows.
-__global__ __launch_bounds__(256) void rows_stamp_kernel(kgat_csr A, const int32_t* __restrict__ rows,
-                                                         const int32_t* __restrict__ count,
-                                                         const uint32_t* __restrict__ set_bits,
-                                                         int32_t* __restrict__ stamp, int32_t s, int seg_blocks) {
-  const int lane = threadIdx.x & 63;
-  if (static_cast<int>(blockIdx.x) < seg_blocks) {
-    const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (sg >= A.n_seg) return;
-    const int row = A.seg_row[sg];
-    if (!bit_of(set_bits, row)) return;
-    const int64_t beg = A.seg_beg[sg];
-    const int64_t row_end = A.rowptr[row + 1];
-    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
-    for (int64_t e = beg + lane; e < end; e += kWave) stamp[A.col[e]] = s;
-    return;
-  }
-  constexpr int L = 16;
-  const int g = lane / L, gl = lane % L;
-  const int64_t cnt = *count;
-  const int64_t stride = static_cast<int64_t>(gridDim.x - seg_blocks) * 4 * (kWave / L);
-  for (int64_t k = (static_cast<int64_t>(blockIdx.x - seg_blocks) * 4 + (threadIdx.x >> 6)) * (kWave / L) + g;
-       k < cnt; k += stride) {
-    const int32_t r = rows[k];
-    if (r < 0) continue;
-    if (gl == 0) stamp[r] = s;
-    const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-    if (end - beg > A.long_threshold) continue;  // its segments' waves
-    for (int64_t e = beg + gl; e < end; e += L) stamp[A.col[e]] = s;
-  }
-}
-
-// The lazy CF table Adam's forward half: every row stamped t (rows_stamp_kernel) that is behind step t
-// brought up to it (its skipped steps replayed, LazyHist).  A wave takes 64 consecutive rows at a time:
-// their stamps and step records are read coalesced (one load each, no per-row dependent chain), the
-// stale ones picked by a ballot and brought current D/4 lanes per row, kGroups rows at once.
-template <int D>
-__global__ __launch_bounds__(256) void lazy_stamped_kernel(const int32_t* __restrict__ stamp, int64_t n_rows,
-                                                           float* __restrict__ p, float* __restrict__ m,
-                                                           float* __restrict__ v, int64_t ld,
-                                                           int32_t* __restrict__ last, int32_t t, LazyHist h,
-                                                           float b1, float b2, float eps, int32_t* __restrict__ hit) {
-  using S = SpmmShape<D>;
-  constexpr int G = S::kGroups;
-  const int lane = threadIdx.x & 63;
-  const int g = lane / S::kLanes, gl = lane % S::kLanes;
-  const float w1 = 1.f - b1, w2 = 1.f - b2;
-  __shared__ LazyHistLds hl;
-  const int32_t lo = stage_hist(hl, h, t - 1);
-  const int64_t nchunk = (n_rows + 63) / 64;
-  for (int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); c < nchunk;
-       c += static_cast<int64_t>(gridDim.x) * 4) {
-    const int64_t r = c * 64 + lane;
-    const bool in = r < n_rows;
-    const bool stamped = in && stamp[r] == t;
-    if (hit != nullptr && in) hit[r] = stamped ? 1 : 0;  // the update's row list (kgat_hop_compact)
-    const int32_t fr = stamped ? last[r] : t;
-    uint64_t stale = __ballot(stamped && fr < t - 1);
-    while (stale != 0) {  // G stale rows per pass, row k of the pass -> lane group k
-      uint64_t mine = stale;
-      for (int k = 0; k < g; ++k) mine &= mine - 1;
-      const int bit = mine != 0 ? __ffsll(static_cast<unsigned long long>(mine)) - 1 : -1;
-#pragma unroll
-      for (int k = 0; k < G; ++k) stale &= stale - 1;
-      const int32_t from = __shfl(fr, bit < 0 ? 0 : bit);
-      if (bit >= 0) {
-        const int64_t row = c * 64 + bit;
-        float4* P = reinterpret_cast<float4*>(p + row * ld) + gl;
-        float4* M = reinterpret_cast<float4*>(m + row * ld) + gl;
-        float4* V = reinterpret_cast<float4*>(v + row * ld) + gl;
-        float4 pp = *P, mm = *M, vv = *V;
-        lazy_replay_lds(pp.x, mm.x, vv.x, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-        lazy_replay_lds(pp.y, mm.y, vv.y, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-        lazy_replay_lds(pp.z, mm.z, vv.z, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-        lazy_replay_lds(pp.w, mm.w, vv.w, from, t - 1, h, hl, lo, w1, b2, w2, eps);
-        *P = pp;
-        *M = mm;
-        *V = vv;
-        if (gl == 0) last[row] = t - 1;  // last[row] was read by the chunk load above
-      }
-    }
-  }
-}
-
-template <int D>
-static int launch_stamped(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v, int64_t ld,
-                          int32_t* last, int32_t t, LazyHist h, float b1, float b2, float eps, int32_t* hit,
-                          hipStream_t st) {
-  const int blocks = blocks_for((n_rows + 63) / 64, 4, kCUs * 8);  // persistent waves stride over 64-row chunks
-  hipLaunchKernelGGL(lazy_stamped_kernel<D>, dim3(blocks), dim3(256), 0, st, stamp, n_rows, p, m, v, ld, last, t, h,
-                     b1, b2, eps, hit);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
-}  // namespace kgat
-
-extern "C" int kgat_rows_stamp(const kgat_csr* A, const int32_t* rows, const int32_t* count, int64_t max_rows,
-                               const uint32_t* set_bits, int32_t* stamp, int32_t s, void* stream) {
-  using namespace kgat;
-  if (!A || !rows || !count || !set_bits || !stamp || max_rows < 0 || A->n_rows < 0) return KGAT_ERR_INVALID;
-  const int seg_blocks = (A->n_seg + 3) / 4;
-  const int64_t list_blocks = std::min<int64_t>(std::max<int64_t>((max_rows + 15) / 16, 1), 2048);
-  hipLaunchKernelGGL(rows_stamp_kernel, dim3(seg_blocks + list_blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), *A, rows, count, set_bits, stamp, s, seg_blocks);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
-extern "C" int kgat_adam_lazy_stamped_f32(const int32_t* stamp, int64_t n_rows, float* p, float* m, float* v,
-                                          int64_t ldp, int32_t d, int32_t* last, int32_t t, float* hist_sz,
-                                          float* hist_bc, int32_t* hist_skip, int32_t cap, float beta1, float beta2,
-                                          float eps, int32_t* hit, void* stream) {
-  using namespace kgat;
-  if (!stamp || !p || !m || !v || !last || !hist_sz || !hist_bc || !hist_skip || cap < 1 || t < 1 || n_rows < 0 ||
-      ldp < d || (ldp & 3) || misaligned(p) || misaligned(m) || misaligned(v))
-    return KGAT_ERR_INVALID;
-  if (n_rows == 0) return KGAT_OK;
-  const LazyHist h{hist_sz, hist_bc, hist_skip, cap};
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  switch (d) {
-    case 16: return launch_stamped<16>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
-    case 32: return launch_stamped<32>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
-    case 64: return launch_stamped<64>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
-    case 128: return launch_stamped<128>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
-    case 256: return launch_stamped<256>(stamp, n_rows, p, m, v, ldp, last, t, h, beta1, beta2, eps, hit, st);
-    default: return KGAT_ERR_UNSUPPORTED_DIM;
-  }
 }
 
 extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {

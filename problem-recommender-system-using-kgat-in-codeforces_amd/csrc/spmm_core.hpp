@@ -27,18 +27,6 @@ struct SpmmAdam {
   int64_t ld;  // row stride of p, m, v (floats)
   float step_size, b1, b2, bc2s, eps;
   const int32_t* skip;  // nullable: *skip != 0 -> the launch leaves p / m / v untouched (bad step ids)
-  // lazy (last != nullptr; kgat_spmm_csr_masked_adam_lazy_f32): step t on the rows stamped t
-  // (stamp[r] == t: the source set's rows and every row with an edge into it, kgat_rows_stamp), each
-  // after replaying its skipped steps; the other rows' gradient is an exact 0 -- they are passed over
-  // without a scan and their step t is left to a later replay (LazyHist)
-  int32_t* last;
-  int32_t t;
-  LazyHist hist;
-  const int32_t* stamp;
-  // the stamped rows as a list (kgat_adam_lazy_stamped_f32's flags, compacted by kgat_hop_compact): its short rows
-  // are walked one per lane group, the groups striding over the list (the long rows: their segments)
-  const int32_t* rows;
-  const int32_t* count;
 };
 
 struct SpmmIo {

@@ -308,10 +308,6 @@ def spmm_masked_adam_block(csr, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init
         ev.append((e0, e1, d, True, "fused_adam"))
 
 
-def _ptr(t: torch.Tensor | None):
-    return t.data_ptr() if t is not None else None
-
-
 def _skip_ptr(skip: torch.Tensor | None):
     """The optimiser skip flag (device int32 [1], kgat_ids_check_ex's bad_dev) or None."""
     if skip is None:
@@ -323,16 +319,10 @@ def _skip_ptr(skip: torch.Tensor | None):
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None, lazy: tuple | None = None,
-                     stamped: tuple | None = None) -> None:
+                     skip: torch.Tensor | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).  ``lazy``
-    = (stamp int32 [N], rows int32 [N], count int32 [1], last int32 [N], t, (hist_sz, hist_bc, hist_skip), cap):
-    step t on the rows stamped t only, the short ones walked from the list rows[:count]
-    (kgat_spmm_csr_masked_adam_lazy_f32, model._LazyTableAdam).  ``stamped`` = (stamp int32 [N], s): the
-    dense step on the rows stamped s only (kgat_spmm_csr_masked_adam_stamped_f32; adam_unstamped steps
-    the others)."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -356,109 +346,12 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
     rank = _rank_ptr(src_rank, src_map)
 
-    if stamped is not None:
-        stamp, sv = stamped
-        _req(stamp, "stamp", dtype=torch.int32, dim=1)
-        if stamp.numel() != n:
-            raise ValueError("stamped: stamp must cover every row")
-        _lib.call("kgat_spmm_csr_masked_adam_stamped_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
-                  _ld(Xc), yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
-                  bc2_sqrt, eps, _skip_ptr(skip), stamp.data_ptr(), int(sv), ws.data_ptr(), ws.numel(),
-                  stream_ptr(Xc.device))
-    elif lazy is not None:
-        stamp, lrows, lcount, last, t, (hs, hb, hk), cap = lazy
-        _req(last, "last", dtype=torch.int32, dim=1)
-        _req(stamp, "stamp", dtype=torch.int32, dim=1)
-        if last.numel() != n or stamp.numel() != n or min(h.numel() for h in (hs, hb, hk)) < cap:
-            raise ValueError("lazy: last / stamp must cover every row, the history cap entries")
-        _lib.call("kgat_spmm_csr_masked_adam_lazy_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-                  yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
-                  eps, _skip_ptr(skip), stamp.data_ptr(), _ptr(lrows), _ptr(lcount), last.data_ptr(), int(t),
-                  hs.data_ptr(), hb.data_ptr(),
-                  hk.data_ptr(), int(cap), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
-    else:
-        _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
-                  _ld(Xc), yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
-                  beta2, bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
+              eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
-
-
-def lazy_mark_catchup(graph: DeviceGraph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor,
-                      stamp: torch.Tensor, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, last: torch.Tensor, t: int,
-                      hist: tuple, cap: int, beta1: float, beta2: float, eps: float, lists: tuple | None = None) -> None:
-    """The lazy CF table Adam's forward half (model._LazyTableAdam.reach): stamp[r] = t on the set (rows /
-    count on the device / set_bits) and every column of A's rows in it (kgat_rows_stamp), then every
-    stamped row behind step t - 1 brought up to it, its skipped zero-gradient steps replayed from the
-    device history (kgat_adam_lazy_stamped_f32).  ``lists`` = (hit, node_map, out_rows, out_count, work):
-    the stamped rows also listed ascending in out_rows[:out_count] (kgat_hop_compact) for the update."""
-    n, d = p.shape
-    for x, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
-        _req(x, nm, dim=2)
-        if tuple(x.shape) != (n, d) or not x.is_contiguous():
-            raise ValueError(f"{nm}: contiguous [{n}, {d}] expected")
-    for x, nm in ((last, "last"), (stamp, "stamp"), (rows, "rows"), (count, "count")):
-        _req(x, nm, dtype=torch.int32, dim=1)
-    if n != graph.n_nodes or last.numel() != n or stamp.numel() != n or set_bits.numel() * 32 < n or t < 1:
-        raise ValueError("lazy_mark_catchup: the table, last[], stamp[] and set_bits must cover every node")
-    hs, hb, hk = hist
-    if min(h.numel() for h in (hs, hb, hk)) < cap:
-        raise ValueError("lazy_mark_catchup: the history holds cap entries")
-    hit = lists[0] if lists is not None else None
-    if hit is not None and (hit.dtype != torch.int32 or hit.numel() != n):
-        raise ValueError("lazy_mark_catchup: hit must be int32 [N]")
-    ev = SPMM_EVENTS
-    if ev is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-    st = stream_ptr(p.device)
-    desc = graph.A.descriptor()
-    _lib.call("kgat_rows_stamp", ctypes.byref(desc), rows.data_ptr(), count.data_ptr(), rows.numel(),
-              set_bits.data_ptr(), stamp.data_ptr(), int(t), st)
-    _lib.call("kgat_adam_lazy_stamped_f32", stamp.data_ptr(), n, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d,
-              last.data_ptr(), int(t), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), int(cap), beta1, beta2, eps,
-              _ptr(hit), st)
-    if lists is not None:
-        hop_list(*lists)
-    if ev is not None:
-        e1.record()
-        ev.append((e0, e1, d, True, "reach"))
-
-
-def rows_stamp(graph: DeviceGraph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor,
-               stamp: torch.Tensor, s: int) -> None:
-    """stamp[r] = s on the set (rows / count on the device / set_bits) and every column of A's rows in it
-    (kgat_rows_stamp): the rows a layer on the set reads, and where A^T . dS over the set can be nonzero."""
-    for x, nm in ((stamp, "stamp"), (rows, "rows"), (count, "count")):
-        _req(x, nm, dtype=torch.int32, dim=1)
-    if stamp.numel() != graph.n_nodes or set_bits.numel() * 32 < graph.n_nodes or s < 1:
-        raise ValueError("rows_stamp: stamp / set_bits must cover every node, s >= 1")
-    desc = graph.A.descriptor()
-    _lib.call("kgat_rows_stamp", ctypes.byref(desc), rows.data_ptr(), count.data_ptr(), rows.numel(),
-              set_bits.data_ptr(), stamp.data_ptr(), int(s), stream_ptr(stamp.device))
-
-
-def adam_unstamped(p: torch.Tensor, m: torch.Tensor, v: torch.Tensor, stamp: torch.Tensor, s: int, step_size: float,
-                   beta1: float, beta2: float, bc2_sqrt: float, eps: float, skip: torch.Tensor | None = None) -> None:
-    """Adam step with gradient 0 on every row not stamped s (kgat_adam_unstamped_f32), on the current stream."""
-    n, d = p.shape
-    for x, nm in ((p, "param"), (m, "exp_avg"), (v, "exp_avg_sq")):
-        _req(x, nm, dim=2)
-        if tuple(x.shape) != (n, d) or not x.is_contiguous():
-            raise ValueError(f"{nm}: contiguous [{n}, {d}] expected")
-    _req(stamp, "stamp", dtype=torch.int32, dim=1)
-    if stamp.numel() != n:
-        raise ValueError("adam_unstamped: stamp must cover every row")
-    ev = SPMM_EVENTS
-    if ev is not None:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-    _lib.call("kgat_adam_unstamped_f32", p.data_ptr(), m.data_ptr(), v.data_ptr(), n, d, stamp.data_ptr(), int(s),
-              step_size, beta1, beta2, bc2_sqrt, eps, _skip_ptr(skip), stream_ptr(p.device))
-    if ev is not None:
-        e1.record()
-        ev.append((e0, e1, d, True, "unstamped_adam"))
 
 
 def _host_ptr(t: torch.Tensor | None):

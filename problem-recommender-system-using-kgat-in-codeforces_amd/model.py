@@ -258,73 +258,15 @@ class _TableUpdate:
         """Drop the pending gradient (a step whose update is abandoned: update_cf_weights raised)."""
         self.pending = None
 
-    def launch(self, lazy: "_LazyTableAdam | None" = None, opt=None, split: "_SplitTableUpdate | None" = None):
-        """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...)); with ``lazy`` on
-        the rows the product reaches only (kgat_spmm_csr_masked_adam_lazy_f32, KGAT.lazy_cf_adam); with
-        ``split`` the reached rows and the others as two launches on two streams (KGAT.split_table_update)."""
+    def launch(self):
+        """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...))."""
         graph, src_map, Xc, Yc, rank = self.pending
         self.pending = None
         p = self.param.data
 
         def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
-            if split is not None:
-                stamp, sv = split.stamp, split.marked
-                split.marked = None
-                cur = torch.cuda.current_stream(p.device)
-                side = split.side_stream(p.device)
-                side.wait_stream(cur)
-                with torch.cuda.stream(side):  # the zero-gradient rows: a pure p / m / v stream
-                    kernels.adam_unstamped(p, m, v, stamp, sv, step_size, b1, b2, bc2s, eps, skip)
-                kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
-                                         stamped=(stamp, sv))
-                cur.wait_stream(side)
-                split.steps += 1
-                return
-            lz = None
-            if lazy is not None:
-                lazy.dirty = True
-                lazy.steps += 1
-                lazy.marked = None
-                lz = (lazy.stamp, lazy.lists[2], lazy.lists[3], lazy.last, lazy._t(opt), lazy.hist, lazy.CAP)
-            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
-                                     lazy=lz)
+            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip)
         return run
-
-
-class _SplitTableUpdate:
-    """The CF step's fused table update as two launches over disjoint rows (opt-in:
-    ``KGAT.split_table_update``, with ``frontier_forward`` and ``fuse_table_update``; single process).
-
-    The dense fused kernel (kgat_spmm_csr_masked_adam_f32) walks every row of A^T: for the two thirds of
-    C2's rows the frontier step's gradient A^T . dS_0 + dXd_0 is exactly zero, yet each is scanned (its
-    edges tested against the first hop, a latency-bound chain) before its Adam step streams p / m / v.
-    Here the frontier forward stamps the rows the gradient can reach (kgat_rows_stamp: the first hop and
-    every column of A's rows in it -- the rows its layer-0 product reads anyway), and the update runs
-    the product + Adam on the stamped rows only (kgat_spmm_csr_masked_adam_stamped_f32) while a second
-    stream steps the others with gradient 0 as a plain stream (kgat_adam_unstamped_f32).  Every row gets
-    its one Adam step with the same gradient: the dense update's bits."""
-
-    def __init__(self, param: torch.Tensor):
-        self.param = param
-        self.enabled = False
-        self.stamp = None
-        self.marked = None  # the stamp value of the current step's forward (None: no marks for it)
-        self.count = 0      # stamp values issued (a value never repeats: zero-initialised stamps mark nothing)
-        self.steps = 0      # split updates launched (tests, bench)
-        self._side = None
-
-    def side_stream(self, dev) -> torch.cuda.Stream:
-        if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev)
-        return self._side
-
-    def mark(self, graph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor) -> None:
-        n, dev = self.param.shape[0], self.param.device
-        if self.stamp is None or self.stamp.numel() != n or self.stamp.device != dev:
-            self.stamp = torch.zeros(n, dtype=torch.int32, device=dev)
-        self.count += 1
-        kernels.rows_stamp(graph, rows, count, set_bits, self.stamp, self.count)
-        self.marked = self.count
 
 
 class _KGTableUpdate:
@@ -397,9 +339,9 @@ class _KGTableUpdate:
         self.pending = None
         kernels.frontier_reset(rows, self._map)
 
-    def launch(self, lazy: "_LazyTableAdam | None" = None, opt=None):
+    def launch(self, lazy: "_LazyKGAdam | None" = None, opt=None):
         """The table's Adam step on the compact gradient (FusedAdam.step(fused=...)); with ``lazy`` on the
-        batch rows only (_LazyTableAdam)."""
+        batch rows only (_LazyKGAdam)."""
         rows, Gc = self.pending
         self.pending = None
         p, row_map = self.param.data, self._map
@@ -412,25 +354,22 @@ class _KGTableUpdate:
         return run
 
 
-class _LazyTableAdam:
-    """A table's Adam on the rows a step touches only: the KG phase's (opt-in ``KGAT.lazy_kg_adam``, on the
-    fused KG table update's compact batch rows) and the CF phase's (opt-in ``KGAT.lazy_cf_adam``, on the
-    rows the frontier CF step reads and whose gradient can be nonzero; see KGAT.lazy_cf_adam).
+class _LazyKGAdam:
+    """The KG phase's table Adam on the batch rows only (opt-in: ``KGAT.lazy_kg_adam``; needs the fused KG
+    table update's compact rows).
 
-    The reference runs Adam over the whole table every step (model.py:404-419): rows with a zero gradient
-    still move (their moments decay and p takes the step m / (sqrt(v) + eps)).  The KG step's gradient
-    is zero outside its <= 3B batch rows (at C4 a 24 B-per-parameter pass, 5 ms, for 1,536 touched rows);
-    the frontier CF step's outside the first hop's neighbours (a third of C2's rows).  Here each row
-    records the last step of this optimiser applied to it and its skipped zero-gradient steps are
-    replayed, in order and with each step's own step size, bias correction and skip flag (a device
-    history), when the row is next read or updated (kgat_adam_lazy_catchup_f32 / kgat_adam_lazy_rows_f32
-    / kgat_lazy_reach_catchup_f32 / kgat_spmm_csr_masked_adam_lazy_f32) -- the dense step's exact sequence
-    of adam_elem operations per element, so the same bits.  Anything else that reads the table (the
-    other phase's step, a PREDICT or UPDATE_ATTENTION forward, a full-table CF forward, a dense update,
-    state_dict, propagate) flushes first: every row is brought up to the current step.  Between a lazy
-    step and a flush the rows outside recent steps and the optimiser's moments are behind: call
-    ``KGAT.flush_tables()`` before reading ``_user_entity_embedding.weight`` or an optimiser's state
-    directly."""
+    The reference's KG step (main.py:334-342, model.py:414-419) runs Adam over the whole table every
+    step: nn.Embedding's dense gradient is zero outside the <= 3B batch rows, yet those rows still move
+    (their moments decay and p takes the step m / (sqrt(v) + eps)).  At C4 that is 24 B of HBM per
+    parameter per step (5 ms) for 1,536 touched rows.  Here each row records the last KG step applied to
+    it and its skipped zero-gradient steps are replayed, in order and with each step's own step size,
+    bias correction and skip flag (a device history), when the row is next read or updated
+    (kgat_adam_lazy_catchup_f32 / kgat_adam_lazy_rows_f32) -- the dense step's exact sequence of
+    adam_elem operations per element, so the same bits.  Anything that reads the whole table (a CF,
+    PREDICT or UPDATE_ATTENTION forward, the CF update, state_dict, propagate) flushes first: every row
+    is brought up to the current step.  Between a KG step and a flush the table's rows outside recent
+    batches and the KG optimiser's moments are behind: call ``KGAT.flush_kg_table()`` before reading
+    ``_user_entity_embedding.weight`` or the KG optimiser's state directly."""
 
     CAP = 1 << 20  # history entries (steps); a flush is forced before any row falls this far behind
 
@@ -441,10 +380,6 @@ class _LazyTableAdam:
         self.hist = None
         self.flushed_at = 0
         self.dirty = False  # rows behind the current step (a lazy step since the last flush)
-        self.steps = 0  # lazy steps launched (tests, bench)
-        self.stamp = None  # CF: stamp[r] = the step whose forward read row r (reach)
-        self.lists = None  # CF: (hit, map, rows, count, work) -- the rows stamped by the last reach, listed
-        self.marked = None  # CF: the step the last reach stamped for
 
     def _t(self, opt) -> int:
         st = opt.state.get(id(self.param))
@@ -494,27 +429,6 @@ class _LazyTableAdam:
                       skip.data_ptr() if skip is not None else None, stream_ptr(p.device))
             kernels.frontier_reset(rows, row_map)
         return run
-
-    def reach(self, opt, graph, rows: torch.Tensor, count: torch.Tensor, set_bits: torch.Tensor) -> None:
-        """The frontier CF forward's catch-up: the set its first restricted layer computes (rows / count /
-        set_bits) and every column of A's rows in it -- the rows the layer reads, and the rows where the
-        step's table gradient can be nonzero -- stamped with the coming step t and brought up to step t - 1
-        (kernels.lazy_mark_catchup); the update then steps the stamped rows only."""
-        t = self._t(opt) + 1
-        if self.stamp is None or self.stamp.numel() != self.last.numel() or self.stamp.device != self.last.device:
-            self.stamp = torch.zeros_like(self.last)  # step numbers start at 1: a zero stamp marks nothing
-            # the stamped rows listed for the update: flags, their compaction (kgat_hop_compact)
-            n, dev = self.last.numel(), self.last.device
-            self.lists = (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
-                          torch.empty(n, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
-                          torch.empty(int(_lib.lib().kgat_hop_compact_work_bytes(n)), dtype=torch.uint8, device=dev))
-        p = self.param.data
-        st = opt.state.get(id(self.param))
-        if st is None:  # the first step: every row is at step 0, nothing to replay -- the stamps only
-            st = {"exp_avg": p, "exp_avg_sq": p}
-        kernels.lazy_mark_catchup(graph, rows, count, set_bits, self.stamp, p, st["exp_avg"], st["exp_avg_sq"],
-                                  self.last, t, self.hist, self.CAP, opt.beta1, opt.beta2, opt.eps, self.lists)
-        self.marked = t
 
     def dense_step_done(self, opt) -> None:
         """A dense step t was just applied to every row (each caught up before it): every row is current at
@@ -819,7 +733,7 @@ def _tile_forward_ok(din: int, dout: int) -> bool:
         kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
 
 
-def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=None, split=None):
+def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
     """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1, 2 or 3, the
     restricted layers with the fused kernels' saved state).  The BPR loss reads the batch rows F of
     every table (model.py:189-191), so the last layer's output is needed on F only, and layer L-2's
@@ -854,19 +768,6 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, lazy=
     # layer l's output row set: None = every row (layer 0 of 3), the first hop for layer L-2, the batch
     # rows F for the last layer
     sets = [None] * first + [(hrows, hcount, bits1)] * (L - 1 - first) + [(rows, fcount, fbits)]
-    if split is not None:
-        # the split table update (KGAT.split_table_update): the rows the step's table gradient can reach
-        if sets[0] is None:
-            split.marked = None  # layer 0 runs whole: the update stays the whole-table kernel
-        else:
-            split.mark(graph, *sets[0])
-    if lazy is not None:
-        # the lazy CF table Adam (KGAT.lazy_cf_adam): the rows this forward reads brought up to the step
-        lz, opt = lazy
-        if sets[0] is None:
-            lz.catch_up(opt)  # layer 0 runs whole: every row
-        else:
-            lz.reach(opt, graph, *sets[0])
     tables, sides, states = [X0], [], []
     x = X0
     for l in range(L):
@@ -920,14 +821,9 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, hook, _tu, frontier, lazy, split = cfg
+        graph, drops, seeds, reg, hook, _tu, frontier = cfg
         ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook)
-        fw = (_frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, lazy, split) if frontier
-              else None)
-        if fw is None and lazy is not None:
-            lazy[0].catch_up(lazy[1])  # the full forward reads every row
-        if fw is None and split is not None:
-            split.marked = None
+        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early) if frontier else None
         if fw is not None:
             tables, sides, states, ctx.early = fw
         else:
@@ -949,7 +845,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg, hook, tu, _frontier, _lazy, _split = ctx.cfg
+        graph, drops, seeds, reg, hook, tu, _frontier = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -1165,10 +1061,8 @@ class KGAT(nn.Module):
         self._graph_key = None
         self._ids = _IdGuard()
         self._table_update = _TableUpdate(self._user_entity_embedding.weight)
-        self._split_update = _SplitTableUpdate(self._user_entity_embedding.weight)
         self._kg_table_update = _KGTableUpdate(self._user_entity_embedding.weight)
-        self._lazy_kg = _LazyTableAdam(self._user_entity_embedding.weight)
-        self._lazy_cf = _LazyTableAdam(self._user_entity_embedding.weight)
+        self._lazy_kg = _LazyKGAdam(self._user_entity_embedding.weight)
         self._kg_graph = _KGStepGraph(self)
         # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
         # (_frontier_forward) -- same loss, gradients and updates, bit for bit
@@ -1177,7 +1071,7 @@ class KGAT(nn.Module):
     @property
     def lazy_kg_adam(self) -> bool:
         """Opt-in (with ``fuse_kg_table_update``): the KG step's table Adam on the batch rows only, the
-        other rows' zero-gradient steps replayed when they are next read (_LazyTableAdam; same bits)."""
+        other rows' zero-gradient steps replayed when they are next read (_LazyKGAdam; same bits)."""
         return self._lazy_kg.enabled
 
     @lazy_kg_adam.setter
@@ -1192,60 +1086,14 @@ class KGAT(nn.Module):
         if self._lazy_kg.last is not None and getattr(self, "_kg_optimizer", None) is not None:
             self._lazy_kg.catch_up(self._kg_optimizer)
 
-    @property
-    def split_table_update(self) -> bool:
-        """Opt-in (with ``frontier_forward`` and ``fuse_table_update``; single process): the fused CF table
-        update as two launches on two streams -- product + Adam on the rows the frontier forward stamped,
-        a zero-gradient Adam stream over the rest (_SplitTableUpdate; same bits as the dense update)."""
-        return self._split_update.enabled
-
-    @split_table_update.setter
-    def split_table_update(self, on: bool) -> None:
-        self._split_update.enabled = bool(on)
-        self._split_update.marked = None
-
-    @property
-    def lazy_cf_adam(self) -> bool:
-        """Opt-in (with ``frontier_forward`` and ``fuse_table_update``; single process -- a data-parallel
-        exchange runs the dense update): the CF step's table Adam on the rows the step touches only.
-
-        The frontier CF step (2 layers) reads the table on the first hop F + N(F) of the batch rows and on
-        every row with an edge into it, and its table gradient, A^T . dS_0 + dXd_0 over the same first hop,
-        is exactly zero on every other row -- two thirds of C2's rows, which the reference's Adam still
-        moves each step (model.py:404-413).  Here the forward brings the rows it reads up to the current
-        step (kgat_lazy_reach_catchup_f32: their skipped zero-gradient steps replayed) and the fused
-        product + Adam steps only the rows its product reaches (kgat_spmm_csr_masked_adam_lazy_f32); the
-        others' steps are replayed when they are next read (_LazyTableAdam).  Same bits as the dense step;
-        the whole table is brought current before anything else reads it (``flush_tables``)."""
-        return self._lazy_cf.enabled
-
-    @lazy_cf_adam.setter
-    def lazy_cf_adam(self, on: bool) -> None:
-        if not on:
-            self.flush_cf_table()
-            self._lazy_cf.last = None
-        self._lazy_cf.enabled = bool(on)
-
-    def flush_cf_table(self) -> None:
-        """Bring every table row and the CF optimiser's moments up to the current CF step (lazy_cf_adam)."""
-        if self._lazy_cf.last is not None and getattr(self, "_cf_optimizer", None) is not None:
-            self._lazy_cf.catch_up(self._cf_optimizer)
-
-    def flush_tables(self) -> None:
-        """Every table row current under both optimisers (lazy_kg_adam / lazy_cf_adam; at most one of
-        them has steps owed: each phase's step flushes the other's first)."""
-        self.flush_kg_table()
-        self.flush_cf_table()
-
     def state_dict(self, *args, **kwargs):
-        self.flush_tables()
+        self.flush_kg_table()
         return super().state_dict(*args, **kwargs)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
-        self.flush_tables()
+        self.flush_kg_table()
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
-        # every row is current: restart the lazy states at the next step
-        self._lazy_kg.last = self._lazy_cf.last = None
+        self._lazy_kg.last = None  # every row is current: restart the lazy state at the next KG step
         return out
 
     @property
@@ -1367,7 +1215,7 @@ class KGAT(nn.Module):
     def propagate(self) -> list[torch.Tensor]:
         """The propagated tables [X0, H1, ..., HL] (no autograd state): PREDICT's first half,
         computed once per evaluation by evaluation.evaluate / recommend_topk."""
-        self.flush_tables()
+        self.flush_kg_table()
         return self._propagate()
 
     def _build_cf_embeddings(self) -> torch.Tensor:
@@ -1383,17 +1231,7 @@ class KGAT(nn.Module):
         hook = getattr(self, "_table_grad_hook", None) if torch.is_grad_enabled() else None
         # the frontier forward only where a backward follows: its batch-row map is released by the backward
         frontier = self.frontier_forward and torch.is_grad_enabled()
-        lazy, lz, opt = None, self._lazy_cf, getattr(self, "_cf_optimizer", None)
-        if lz.enabled and frontier and hook is None and self._table_update.enabled and opt is not None:
-            lz.ensure(opt)
-            lazy = (lz, opt)
-        else:
-            self.flush_cf_table()
-        split = self._split_update
-        split.marked = None
-        if lazy is not None or not (split.enabled and frontier and hook is None and self._table_update.enabled):
-            split = None
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier, lazy, split)
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
@@ -1462,10 +1300,9 @@ class KGAT(nn.Module):
     def build_optimizer(self, cf_lr: float, kg_lr: float) -> None:
         # lazy KG Adam: the replays still owed are the old optimiser's steps -- apply them, then restart
         # the per-row step record at the new optimiser's t = 0 (a stale last[r] would skip its steps)
-        self.flush_tables()
-        for lz in (self._lazy_kg, self._lazy_cf):
-            lz.last = None
-            lz.dirty = False
+        self.flush_kg_table()
+        self._lazy_kg.last = None
+        self._lazy_kg.dirty = False
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 
@@ -1493,41 +1330,23 @@ class KGAT(nn.Module):
         # device: its optimiser kernels read the check's flag and leave every parameter as it is
         self._raise_or_abandon(self._cf_optimizer)
         self.flush_kg_table()
-        tu, lazy, opt = self._table_update, self._lazy_cf, self._cf_optimizer
-        fused, lazy_step = None, False
+        tu = self._table_update
+        fused = None
         if tu.pending is not None:
             # another term of the loss may have written the table's .grad after the deferral (autograd
             # order, an extra regulariser on the table): the fused launch never reads .grad, so such a
             # gradient is summed with the deferred product first (materialize adds into .grad)
             if (row_ranges and id(tu.param) in row_ranges) or tu.param.grad is not None:
                 tu.materialize()
-            elif self._split_update.enabled and self._split_update.marked is not None and not lazy.enabled:
-                # this step's forward stamped the rows its table gradient can reach
-                fused = {id(tu.param): tu.launch(split=self._split_update)}
-            elif lazy.enabled and lazy.last is not None and lazy.marked == lazy._t(opt) + 1:
-                # this step's forward stamped the rows it read and the gradient's rows (reach)
-                if lazy._t(opt) + 1 - lazy.flushed_at >= lazy.CAP:
-                    lazy.catch_up(opt)  # no row may fall a whole history behind
-                fused = {id(tu.param): tu.launch(lazy, opt)}
-                lazy_step = True
             else:
                 fused = {id(tu.param): tu.launch()}
-        # a dense table step (the whole-table fused launch or a .grad) moves every row: each current first
-        dense_lazy = lazy.last is not None and not lazy_step and (fused is not None or tu.param.grad is not None)
-        if dense_lazy:
-            lazy.catch_up(opt)
-        opt.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
-        lazy.marked = None
-        self._split_update.marked = None
-        if dense_lazy:
-            lazy.dense_step_done(opt)
-        opt.zero_grad()
+        self._cf_optimizer.step(row_ranges, fused=fused, skip=self._ids.skip_flag())
+        self._cf_optimizer.zero_grad()
 
     def update_kg_weights(self, row_ranges: dict | None = None) -> None:
         """A compact KG table gradient (fuse_kg_table_update) is stepped by kgat_adam_rows_f32."""
         self._raise_or_abandon(self._kg_optimizer)
         self._table_update.materialize()
-        self.flush_cf_table()
         step = self._kg_graph
         if step.pending == "bwd":
             ps, _ = step._states(self._kg_optimizer)
@@ -1561,8 +1380,6 @@ class KGAT(nn.Module):
     def forward(self, *args: Any, mode: KGATMode) -> torch.Tensor | None:
         if mode != KGATMode.TRAIN_KG:
             self.flush_kg_table()  # lazy KG Adam: these modes read the whole table
-        if mode != KGATMode.TRAIN_CF:
-            self.flush_cf_table()  # lazy CF Adam: likewise (a TRAIN_CF step decides in _calc_cf_loss)
         if mode != KGATMode.PREDICT:
             # a deferred table gradient refers to this step's hop buffers and A's values (CF) or
             # holds the batch-row map (KG): a new backward or an attention refresh would change them

@@ -1909,92 +1909,6 @@ def test_lazy_kg_adam_bit_identical(pkg, dim):
             assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
 
 
-@pytest.mark.parametrize("mode", ["lazy", "split"])
-@pytest.mark.parametrize("dim", [64, 128])
-def test_lazy_cf_adam_bit_identical(pkg, dim, mode):
-    """KGAT.lazy_cf_adam (the frontier CF step's table Adam on the rows the step reads and reaches only, the
-    other rows' zero-gradient steps replayed when next read) and KGAT.split_table_update (the reached rows'
-    product + Adam and the other rows' zero-gradient Adam as two launches on two streams) vs the dense
-    fused CF update: over CF phases between lazy KG phases -- with a step whose ids are out of range, the
-    skip flag set while a step is in flight, a full-table (non-frontier) step, a no-grad loss evaluation, a
-    PREDICT and a second build_optimizer -- the losses, parameters and both optimisers' states are equal
-    bit for bit."""
-    graph_mod, _ = _mods(pkg)
-    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=5)
-    lay = graph_mod.build_layout(U, E, inter, trip)
-    n = U + E
-    R = len(lay.rel_order)
-    models = []
-    for lazy in (False, True):
-        torch.manual_seed(3)
-        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=R, layer_size=[dim, 32],
-                                  cf_embedding_dim=dim, kg_embedding_dim=dim))
-        m.attach_graph(lay, DEV)
-        m.train()
-        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-        m.fuse_table_update = m.fuse_kg_table_update = m.lazy_kg_adam = True
-        m.frontier_forward = True
-        if mode == "lazy":
-            m.lazy_cf_adam = lazy
-        else:
-            m.split_table_update = lazy
-        models.append(m)
-    rng = np.random.default_rng(8)
-    for phase in range(4):
-        cfs = [[torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
-               for _ in range(7)]
-        kgs = [[torch.from_numpy(rng.integers(0, hi, 48)).to(DEV) for hi in (n, R, n, n)] for _ in range(3)]
-        losses = []
-        for m in models:
-            out = []
-            for j, ids in enumerate(cfs):
-                torch.manual_seed(100 * phase + j)
-                if phase == 1 and j == 2:  # a device-side bad id: the update raises, the step is abandoned
-                    bad = ids[2].clone()
-                    bad[0] = n + 5
-                    m(ids[0], ids[1], bad, mode=pkg.KGATMode.TRAIN_CF).backward()
-                    torch.cuda.synchronize()
-                    with pytest.raises(IndexError):
-                        m.update_cf_weights()
-                    continue
-                if phase == 3 and j == 4:
-                    with torch.no_grad():  # a loss evaluation: no backward, no update
-                        out.append(m(*ids, mode=pkg.KGATMode.TRAIN_CF).detach().clone())
-                m.frontier_forward = not (phase == 2 and j == 1)  # one full-table step
-                loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF)
-                loss.backward()
-                if phase >= 2 and j == 3:
-                    m._ids.skip_flag().fill_(1)  # set on the device while the step is in flight
-                m.update_cf_weights()
-                m._ids.skip_flag().zero_()
-                m.frontier_forward = True
-                out.append(loss.detach().clone())
-            for kg in kgs:
-                m(*kg, mode=pkg.KGATMode.TRAIN_KG).backward()
-                m.update_kg_weights()
-            losses.append(torch.stack(out))
-            if phase == 2:
-                with torch.no_grad():
-                    m(cfs[0][0], cfs[0][1], mode=pkg.KGATMode.PREDICT)
-                m.build_optimizer(cf_lr=2e-3, kg_lr=1e-4)
-        assert torch.equal(losses[0], losses[1]), phase
-    used = (lambda m: m._lazy_cf.steps) if mode == "lazy" else (lambda m: m._split_update.steps)
-    assert used(models[1]) >= 15 and used(models[0]) == 0
-    sa, sb = models[0].state_dict(), models[1].state_dict()
-    for k in sa:
-        if not sa[k].is_sparse:
-            assert torch.equal(sa[k], sb[k]), k
-    for opt in ("_cf_optimizer", "_kg_optimizer"):
-        oa, ob = getattr(models[0], opt), getattr(models[1], opt)
-        for pa, pb in zip(oa.params, ob.params):
-            sa_, sb_ = oa.state.get(id(pa)), ob.state.get(id(pb))
-            assert (sa_ is None) == (sb_ is None), opt
-            if sa_ is None:
-                continue
-            assert sa_["step"] == sb_["step"], opt
-            assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
-
-
 @pytest.mark.parametrize("dim", [64, 128])
 def test_captured_kg_step_bit_identical(pkg, dim):
     """KGAT.capture_kg_step (TRAIN_KG forward, backward and update_kg_weights each one replayed HIP graph,

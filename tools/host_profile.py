@@ -1,5 +1,5 @@
-"""Host-side profile of the CF training step (python tools/host_profile.py [--full | --lazy-cf] [--kg [--unfused |
---lazy | --captured]]: the KG step instead): cProfile over
+"""Host-side profile of the CF training step (python tools/host_profile.py [--full] [--kg [--unfused | --lazy |
+--captured]]: the KG step instead): cProfile over
 200 steps of a small synthetic graph (host launch cost does not depend on the graph size), printing
 the functions with the most own time.  Used to find Python / ctypes overhead in the step's launches."""
 import cProfile
@@ -30,7 +30,6 @@ def main():
     m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
     m.fuse_table_update = True
     m.frontier_forward = not full
-    m.lazy_cf_adam = "--lazy-cf" in sys.argv
     rng = np.random.default_rng(1)
     batches = [[torch.from_numpy(rng.integers(0, hi, 256)).to(dev) for hi in (U, int(E * 0.1), int(E * 0.1))]
                for _ in range(16)]
