@@ -101,7 +101,8 @@ constexpr int kRowsUnroll = 4;
 // One long-row segment s (the whole wave; groups take interleaved sub-chunks) -> its partial sum in
 // io.part, reduced by the fix-up pass.
 template <int D, int MODE>
-__device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io, int s, int g, int gl, int base) {
+__device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io, int s, int g, int gl, int base,
+                                             int2* hb) {
   constexpr int L = SpmmShape<D>::kLanes;
   constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
   if (s >= A.n_seg) return;
@@ -115,7 +116,7 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
   // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
   for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
     const int64_t ce = cb + L < end ? cb + L : end;
-    gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any);
+    gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any, hb);
   }
   // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
   if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
@@ -138,9 +139,11 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   const int wave = threadIdx.x >> 6;
   const int g = lane / L, gl = lane % L, base = g * L;
   if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  __shared__ int2 hitbuf[4][kWave];  // masked modes: each lane group's compacted hits (gather_edges)
+  int2* hb = hitbuf[wave] + base;
 
   if (static_cast<int>(blockIdx.x) < seg_blocks) {
-    long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base);
+    long_segment<D, MODE>(A, io, blockIdx.x * 4 + wave, g, gl, base, hb);
     return;
   }
 
@@ -159,7 +162,8 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
         if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         bool any = false;
-        gather_edges<D, MODE == kMaskedRows, MODE == kRows ? kRowsUnroll : 4>(A, io, beg, end, base, gl, acc, any);
+        gather_edges<D, MODE == kMaskedRows, MODE == kRows ? kRowsUnroll : 4>(A, io, beg, end, base, gl, acc, any,
+                                                                              hb);
         store_row<MODE>(io, r, MODE == kRows ? r : k, gl, acc, any);
       }
     }
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     bool any = false;
-    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any);
+    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any, hb);
     store_row<MODE>(io, r, r, gl, acc, any);
   }
 }

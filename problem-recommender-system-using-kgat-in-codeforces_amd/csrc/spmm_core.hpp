@@ -84,11 +84,19 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.w += b.w;
 }
 
+// Wave-scope LDS ordering: this wave's LDS writes land before its later reads of other lanes' slots.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Accumulate edges [beg, end) of one row into acc.  All lanes of the group
 // (base .. base+kLanes-1) run this with identical bounds (group-uniform).
+// MASKED: hb is the group's kLanes-entry LDS slot array (the chunk's hits compacted there).
 template <int D, bool MASKED, int U = 4, int UM = 4>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
-                                             int gl, float4& acc, bool& any) {
+                                             int gl, float4& acc, bool& any, int2* hb = nullptr) {
   constexpr int L = SpmmShape<D>::kLanes;
   const float4* X4 = reinterpret_cast<const float4*>(io.X);
   const uint32_t ldx4u = static_cast<uint32_t>(io.ldx / 4);
@@ -113,40 +121,40 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
           in = io.src_bits != nullptr ? ((io.src_bits[mc >> 5] >> (mc & 31)) & 1u) != 0 : io.src_map[mc] >= 0;
         }
       }
-      // the group's hit bits in a 32-bit word where they fit (the group's lanes are L <= 32 bits of
-      // the ballot): one v_ffbl per pick instead of the 64-bit scan
+      // the group's hit bits in a 32-bit word where they fit (the group's lanes are L <= 32 bits of the ballot)
       using HitT = typename std::conditional<(L <= 32), uint32_t, uint64_t>::type;
       constexpr HitT kMask = L >= 32 ? static_cast<HitT>(~HitT{0}) : static_cast<HitT>((HitT{1} << L) - 1);
-      HitT hit = static_cast<HitT>(__ballot(in) >> base) & kMask;
+      const HitT hit = static_cast<HitT>(__ballot(in) >> base) & kMask;
       if (hit == 0) continue;
       any = true;
       if (in && io.src_rank == nullptr) mc = io.src_map[mc];
-      // up to UM gathers in flight, summed in edge order.  A pick past the last hit adds
-      // fma(0, 0, acc) = acc + 0 = acc exactly (acc starts at +0 and an exact-zero sum rounds to
-      // +0, so acc is never -0): the same bits as skipping it, without per-pick selects of acc.
-      while (hit) {
-        int jj[UM];
-#pragma unroll
-        for (int k = 0; k < UM; ++k) {
-          if constexpr (L <= 32) jj[k] = __ffs(hit) - 1;
-          else jj[k] = __ffsll(static_cast<unsigned long long>(hit)) - 1;
-          hit &= hit - 1;  // 0 stays 0
-        }
+      // the hits compacted into the group's LDS slots in edge order (slot = hits on lower lanes), then
+      // read back UM at a time with a broadcast read each -- no per-pick lane search and shuffles.  A
+      // pick past the last hit adds fma(0, 0, acc) = acc + 0 = acc exactly (acc starts at +0 and an
+      // exact-zero sum rounds to +0, so acc is never -0): the same bits as skipping it.
+      int nh;
+      if constexpr (L <= 32) {
+        nh = __popc(hit);
+        if (in) hb[__popc(hit & ((1u << gl) - 1u))] = make_int2(mc, __float_as_int(mv));
+      } else {
+        nh = __popcll(hit);
+        if (in) hb[__popcll(hit & ((uint64_t{1} << gl) - 1))] = make_int2(mc, __float_as_int(mv));
+      }
+      wave_lds_order();
+      for (int k0 = 0; k0 < nh; k0 += UM) {
         float4 xs[UM];
         float vs[UM];
 #pragma unroll
         for (int k = 0; k < UM; ++k) {
-          const bool ok = jj[k] >= 0;
-          const int src = base + (jj[k] & (L - 1));  // a lane of the group either way
-          const int c = __shfl(mc, src);
-          const float v = __shfl(mv, src);
-          vs[k] = ok ? v : 0.f;
-          xs[k] = ok ? X4[row_off(c, ldx4u) + gl]
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+          const bool ok = k0 + k < nh;
+          const int2 e = hb[ok ? k0 + k : 0];
+          vs[k] = ok ? __int_as_float(e.y) : 0.f;
+          xs[k] = ok ? X4[row_off(e.x, ldx4u) + gl] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int k = 0; k < UM; ++k) fma4(vs[k], xs[k], acc);
       }
+      wave_lds_order();  // every lane of the group has read the slots before the next chunk writes them
       continue;
     }
     if (gl < n) {
