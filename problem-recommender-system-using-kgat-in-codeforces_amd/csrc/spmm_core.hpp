@@ -16,10 +16,10 @@ enum SpmmMode { kOverwrite = 0, kAccumulate = 1, kMasked = 2, kMaskedRows = 3, k
 
 // kMaskedAdam: the masked product's row is the gradient of a table row and is
 // consumed on the spot by its Adam step (p, m, v rows of the same index), so
-// the dense gradient is never written nor read back.  The row's p / m / v
-// loads go out after its gather: issued before it they keep 12 more VGPRs
-// live across the gather (76 VGPRs, 6 waves/SIMD instead of 64 / 8) and the
-// C2 step is no faster (2.139 vs 2.134 ms, C4 67.47 vs 67.34 ms).
+// the dense gradient is never written nor read back.  A short row's p / m / v
+// loads go out before its gather (76 VGPRs, 6 waves/SIMD): with the hits
+// compacted in LDS that measured ~2 % faster (round 4; in round 2, with the
+// per-pick lane search, it was not).
 struct SpmmAdam {
   float* p;
   float* m;
