@@ -12,7 +12,7 @@ V, rep = sys.argv[1], sys.argv[2]
 line = [l for l in open(f"gpurun_out/r04_ab_{V}_{rep}.log") if l.startswith('{"metric"')][-1]
 d = json.loads(line)
 print(V, rep, "full %.4f" % d["ms_per_step"], "frontier %.4f" % d["frontier_forward"]["ms_per_step"],
-      "tu %.4f" % d["spmm"]["table_update"]["avg_launch_ms"])
+      "tu %.4f" % d["spmm"]["table_update"]["avg_launch_ms"], "fwd %.4f" % d["spmm"]["fwd_avg_ms"])
 PY
 done
 done
