@@ -13,8 +13,9 @@ real RCCL library (forced at world 1) and its results are compared with the gloo
     a model without any exchange -- bit-identical parameters;
 (3) RowShardedKGAT: one CF step with its collectives on RCCL against the same step on a gloo group
     (host-staged transport) -- loss and every gradient bit-identical;
-(4) the library's own RCCL communicator (kgat_comm_*, comm.RcclComm): every call, and the same
-    RowShardedKGAT step with RcclComm as its transport -- bit-identical to (3).
+(4) the library's own RCCL communicator (kgat_comm_*, comm.RcclComm): every call (gather_at on the
+    torch.distributed transports too), and the same RowShardedKGAT step with RcclComm as its transport --
+    bit-identical to (3).
 """
 from __future__ import annotations
 
@@ -128,6 +129,17 @@ def main() -> None:
     recv = torch.empty_like(x)
     rc.exchange(x, recv).wait()
     got["ring_exchange"] = recv
+    # the pipelined row-sharded forward's block post (kgat_comm_gather_at): rows [5, 21) of a 4096 x 1
+    # view land at rows [7, 23) of the output, the rest of it untouched
+    for tag, tp in (("kgat_comm gather_at", rc), ("torch gather_at", sh.Comm(None, force=True)),
+                    ("gloo gather_at", sh.Comm(gloo, force=True))):
+        src = x.view(-1, 16)[5:21].contiguous()
+        dst = torch.full((40, 16), -1.0, device=dev)
+        tp.gather_at(src, dst, [7], [16]).wait()
+        want = torch.full((40, 16), -1.0, device=dev)
+        want[7:23] = src
+        if not torch.equal(dst, want):
+            failures.append(f"(4) {tag} placed the rows wrong")
     for name, t in got.items():
         if not torch.equal(t, x):
             failures.append(f"(4) {name} changed the data")

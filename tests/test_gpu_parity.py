@@ -1984,3 +1984,81 @@ def test_captured_kg_step_bit_identical(pkg, dim):
                 continue
             assert sa_["step"] == sb_["step"], opt
             assert torch.equal(sa_["exp_avg"], sb_["exp_avg"]) and torch.equal(sa_["exp_avg_sq"], sb_["exp_avg_sq"]), opt
+
+
+def test_ids_check_multi_per_array_bounds(pkg):
+    """kgat_ids_check_multi (the captured KG step's id check): four arrays, each against its own bound,
+    copied concatenated into one int64 buffer; an id outside its array's bound is zeroed and raises both
+    flags (pinned host + device skip flag), ids inside are copied exactly."""
+    import ctypes
+    import importlib
+    lib = importlib.import_module(pkg.__name__ + "._lib")
+    graph_mod = importlib.import_module(pkg.__name__ + ".graph")
+    rng = np.random.default_rng(3)
+    sizes, bounds = (100, 37, 1, 64), (50, 7, 1000, 3)
+    arrs = [torch.from_numpy(rng.integers(0, b, n)).to(DEV) for n, b in zip(sizes, bounds)]
+
+    def run(ts):
+        d = lib.Ids()
+        for k, t in enumerate(ts):
+            d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
+        d.count = len(ts)
+        bd = (ctypes.c_int64 * lib.KGAT_IDS_MAX)(*bounds)
+        out = torch.full((sum(sizes),), -5, dtype=torch.int64, device=DEV)
+        host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        dev_flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+        lib.call("kgat_ids_check_multi", ctypes.byref(d), bd, out.data_ptr(), host.data_ptr(), dev_flag.data_ptr(),
+                 graph_mod.stream_ptr(torch.device(DEV)))
+        torch.cuda.synchronize()
+        return out, int(host[0]), int(dev_flag[0])
+
+    out, h, dv = run(arrs)
+    assert torch.equal(out, torch.cat(arrs)) and h == 0 and dv == 0
+    bad = [a.clone() for a in arrs]
+    bad[1][4] = 7   # == its bound
+    bad[3][0] = -1
+    out, h, dv = run(bad)
+    want = torch.cat(bad)
+    want[100 + 4] = 0
+    want[100 + 37 + 1] = 0
+    assert torch.equal(out, want) and h == 1 and dv == 1
+
+
+def test_sched_adam_matches_eager(pkg):
+    """The captured KG step's device-scheduled Adam (kgat_step_advance + kgat_adam_multi_sched_f32: the step
+    number on the device, step size and sqrt(1 - beta2^t) read from host-filled tables) against the eager
+    kgat_adam_multi_ex_f32 with FusedAdam's scalars: parameters and moments equal bit for bit over six steps,
+    one of them with the skip flag set."""
+    import importlib
+    import math
+    lib = importlib.import_module(pkg.__name__ + "._lib")
+    kernels = importlib.import_module(pkg.__name__ + ".kernels")
+    graph_mod = importlib.import_module(pkg.__name__ + ".graph")
+    torch.manual_seed(7)
+    lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+    shapes = [(3000, 64), (17, 64, 64)]
+    ps = [torch.randn(s, device=DEV) for s in shapes]
+    a_state = [(p.clone(), torch.zeros_like(p), torch.zeros_like(p)) for p in ps]
+    b_state = [(p.clone(), torch.zeros_like(p), torch.zeros_like(p)) for p in ps]
+    sz = torch.tensor([0.0] + [lr / (1.0 - b1 ** t) for t in range(1, 16)], dtype=torch.float32, device=DEV)
+    bc = torch.tensor([0.0] + [math.sqrt(1.0 - b2 ** t) for t in range(1, 16)], dtype=torch.float32, device=DEV)
+    t_dev = torch.zeros(1, dtype=torch.int32, device=DEV)
+    skip = torch.zeros(1, dtype=torch.int32, device=DEV)
+    st = graph_mod.stream_ptr(torch.device(DEV))
+    for t in range(1, 7):
+        grads = [torch.randn(s, device=DEV) for s in shapes]
+        skip.fill_(1 if t == 4 else 0)
+        kernels.adam_multi([(p, g, m, v, lr / (1.0 - b1 ** t), math.sqrt(1.0 - b2 ** t))
+                            for (p, m, v), g in zip(a_state, grads)], b1, b2, eps, skip)
+        arr = (lib.AdamTensor * len(shapes))()
+        for a, (p, m, v), g in zip(arr, b_state, grads):
+            a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+            a.n, a.step_size, a.bc2_sqrt = p.numel(), 0.0, 0.0
+        lib.call("kgat_step_advance", t_dev.data_ptr(), st)
+        lib.call("kgat_adam_multi_sched_f32", arr, len(shapes), b1, b2, eps, skip.data_ptr(), t_dev.data_ptr(),
+                 sz.data_ptr(), bc.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert int(t_dev[0]) == 6
+    for x, y in zip(a_state, b_state):
+        for u, w in zip(x, y):
+            assert torch.equal(u, w)
