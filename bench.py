@@ -920,6 +920,21 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
 
     elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
+    if args.timeline:
+        # one more step with the pipelined forward's block marks (sharded.TIMELINE): per rank, GPU time of
+        # each block's compute, host time of its post and of each post's landing, relative to the first mark
+        sh.TIMELINE = []
+        step(batches[0])
+        torch.cuda.synchronize()
+        marks, sh.TIMELINE = sh.TIMELINE, None
+        if marks:
+            e0, h0 = marks[0][1], marks[0][2]
+            lines = [f"# rank {rank} of {world}: gpu ms (event) | host ms | mark -- one CF step, pipelined forward "
+                     f"({getattr(model, 'pipeline_blocks', '?')} row blocks per layer)"]
+            lines += [f"{e0.elapsed_time(e):9.3f} {1e3 * (h - h0):9.3f}  {what}" for what, e, h in marks]
+            out = ROOT / "gpurun_out"
+            out.mkdir(exist_ok=True)
+            (out / f"c5_timeline_rank{rank}.txt").write_text("\n".join(lines) + "\n")
     d0 = cfg["dim"]
     chunked = comm.active and d0 > sh.GATHER_CHUNK > 0
     roof, spmm = roofline(events, args.config, ckg.n_nodes if world == 1 else shard.n, nnz if world == 1 else 0,
@@ -1037,6 +1052,9 @@ def main() -> int:
                     help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
     ap.add_argument("--no-frontier-leg", action="store_true",
                     help="skip the second timed run with KGAT.frontier_forward (training-step speed)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="row-sharded configs: record one step's pipelined-forward block marks per rank "
+                         "(gpurun_out/c5_timeline_rank*.txt)")
     ap.add_argument("--no-kg-leg", action="store_true",
                     help="skip the KG-step / attention-refresh legs and the epoch estimate (c2/c4, N = 1)")
     ap.add_argument("--no-fused-update", action="store_true",

@@ -47,6 +47,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 
 import numpy as np
 import torch
@@ -400,13 +401,28 @@ class _RowBlocks:
         self.sizes = [[cuts[r][b + 1] - cuts[r][b] for r in range(shard.world)] for b in range(K)]
 
 
+# Optional record of one step's pipelined forward (bench.py --timeline): when set to a list, the
+# pipelined layers append (what, GPU event, host seconds) at each block's compute start / end, its post
+# to the peers and each post's landing -- a rehearsal's evidence that block b travels while block b+1
+# computes.
+TIMELINE: list | None = None
+
+
+def _mark(what: str) -> None:
+    if TIMELINE is not None:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        TIMELINE.append((what, e, time.perf_counter()))
+
+
 def _gathered(shard: RowShard, comm, X: torch.Tensor, pre) -> torch.Tensor:
     """[N, d] every rank's rows of X: the blocks a pipelined layer already posted (``pre`` = (buffer,
     pending posts)), else one whole-width all-peer gather."""
     if pre is not None:
         buf, pends = pre
-        for pd in pends:
+        for i, pd in enumerate(pends):
             pd.wait()
+            _mark(f"width {buf.shape[1]}: block {i} post landed")
         return buf
     return gather_table(shard, comm, X)
 
@@ -424,13 +440,16 @@ def _layer_pipelined(shard: RowShard, comm, blocks: _RowBlocks, Xg: torch.Tensor
     pends = []
     for b in range(blocks.K):
         a0, a1 = blocks.mine[b], blocks.mine[b + 1]
+        _mark(f"width {dout}: block {b} compute start")
         if a1 > a0:
             kernels.spmm_block(blocks.views[b], Xg, s[a0:a1])
             if st.kind == "gemm":
                 kernels.biinter_fwd_gemm_rows(x, s, blocks.rows[b], a1 - a0, W1, b1, W2, b2, drop, seed, h, st)
             else:
                 kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drop, seed, h, blocks.bits[b], state=st)
+        _mark(f"width {dout}: block {b} computed")
         pends.append(comm.gather_at(h[a0:a1], nxt, blocks.starts[b], blocks.sizes[b]))
+        _mark(f"width {dout}: block {b} posted")
     return h, (nxt, pends)
 
 
