@@ -16,5 +16,5 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $ctr rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/$ctr.log; exit $rc; fi
 done
-case $cfg in c4) d0=128;; c5) d0=256;; *) d0=64;; esac
+case $cfg in c3|c4) d0=128;; c5) d0=256;; *) d0=64;; esac
 python3 tools/pmc_parse.py $OUT profiles/pmc_$cfg.json "bench.py --config $cfg --steps 5 --warmup 1 $*" $d0 $OUT/FETCH_SIZE.log && cp profiles/pmc_$cfg.json $OUT/
