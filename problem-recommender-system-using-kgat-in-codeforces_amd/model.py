@@ -919,8 +919,15 @@ class _CFLoss(torch.autograd.Function):
                     hrows, hmap, hcount, _ = kernels.hop_compact(graph, count_host=_hop_host(graph, l))
                     _hop_record(graph, l)
             elif sparse:
-                hrows, hmap, hcount, n_hop = kernels.hop_compact(graph, sync=True)
-                sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
+                # the wide kinds size their compact problem on the host (one synchronisation) -- taken only
+                # when the layer's hop set was small at the previous step; a large one goes dense at once
+                # (both paths give the same bits; C3's 3-layer step: its ~80 us stall gone)
+                sparse = _hop_small(graph, l, n_nodes)
+                if sparse:
+                    hrows, hmap, hcount, n_hop = kernels.hop_compact(graph, sync=True,
+                                                                     count_host=_hop_host(graph, l))
+                    _hop_record(graph, l)
+                    sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
             if sparse:
                 # dX is zero outside the hop set: the bi-interaction backward runs on its rows
                 # only and the A^T product gathers from them only (kgat_spmm_csr_masked_ex_f32);
