@@ -292,17 +292,10 @@ inline int64_t wslab_count(int64_t n) { return (n + gemm_chunk(n) - 1) / gemm_ch
     if (int e_ = (call)) return e_;    \
   } while (0)
 
-// The two products of each direction in one dual-GEMM launch (gemm.hip's dual_gemm_kernel: the
-// (X+S, X*S) operands formed at load, dXd / dS formed in the du / dm epilogue -- no U / M arrays,
-// no um / dxs passes; each product the single GEMM's bits).  KGAT_DUAL_GEMM=0: the separate
-// launches (A/B switch).
-inline bool dual_gemm_on() {
-  static const bool on = [] {
-    const char* e = getenv("KGAT_DUAL_GEMM");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return on;
-}
+// The two products of each direction run in one dual-GEMM launch (gemm.hip's dual_gemm_kernel: the
+// (X+S, X*S) operands formed at load, dXd / dS formed in the du / dm epilogue -- no U / M arrays, no
+// um / dxs passes; each product the single GEMM's bits).  The separate launches remain only for row
+// strides that are not a multiple of 4 floats (the dual kernel's float4 operand loads).
 
 }  // namespace kgat
 
@@ -330,7 +323,7 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
   float* slab1 = work + 2 * n * ldu;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
-  const bool dual = (dual_gemm_on() || rows != nullptr) && (ldx & 3) == 0 && (lds & 3) == 0;
+  const bool dual = (ldx & 3) == 0 && (lds & 3) == 0;
   if (rows != nullptr && !dual) return KGAT_ERR_INVALID;
   if (phases != 3 && !dual) return KGAT_ERR_INVALID;
   if (dual && (phases & 1)) {
@@ -447,7 +440,7 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   float* P1 = state;
   float* P2 = state + n * d_out;
   float* norm = state + 2 * n * d_out;
-  if (kgat::dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0) {
+  if ((ldx & 3) == 0 && (lds & 3) == 0) {
     // P1 = (X+S) W1^T, P2 = (X*S) W2^T in one launch, the operands formed at load
     kgat::DualGemm g;
     g.tb = true, g.a_um = true;
@@ -492,7 +485,7 @@ extern "C" int kgat_biinter_fwd_gemm_rows_f32(const float* X, int64_t ldx, const
   float* M = work + m * ldu;
   float* P1 = work + kgat_biinter_gemm_work_floats(m, d_in, d_out);
   float* P2 = P1 + m * d_out;
-  if (kgat::dual_gemm_on() && (ldx & 3) == 0 && (lds & 3) == 0) {
+  if ((ldx & 3) == 0 && (lds & 3) == 0) {
     // P1 = (X+S) W1^T, P2 = (X*S) W2^T on the listed rows, X / S read through the list at load
     kgat::DualGemm g;
     g.tb = true, g.a_um = true;

@@ -184,14 +184,14 @@ def graph_section(args, K, g, U, E, n, dev, rec):
             4 * n * (2 * din + dout) + 36 * n)
         rec(f"biinter_bwd_saved_{din}x{dout}",
             timeit(lambda: K.biinter_bwd(X, S, dH, W1, b1, W2, b2, 0.1, 5, H=H, state=st), args.reps),
-            4 * n * (2 * din + 2 * dout + 2 * din) + 36 * n, split=os.environ.get("KGAT_BWD_SPLIT", "auto"))
+            4 * n * (2 * din + 2 * dout + 2 * din) + 36 * n, split="auto")
     p = torch.randn(n * 64, device=dev)
     gg = torch.randn_like(p)
     m = torch.zeros_like(p)
     v = torch.zeros_like(p)
     rec("adam_table", timeit(lambda: K.adam(p, gg, m, v, 1e-3, 0.9, 0.999, 0.03, 1e-8), args.reps), 28 * p.numel())
     rec("adam_multi_table", timeit(lambda: K.adam_multi([(p, gg, m, v, 1e-3, 0.03)], 0.9, 0.999, 1e-8), args.reps),
-        28 * p.numel(), variant=os.environ.get("KGAT_ADAM_VARIANT", "0"))
+        28 * p.numel(), variant="0")
     tables = [torch.randn(n, 64, device=dev), torch.randn(n, 64, device=dev), torch.randn(n, 32, device=dev)]
     rec("bpr_fwd", timeit(lambda: K.bpr_fwd(tables, users, pos, neg, 1e-5), args.reps))
 
