@@ -650,11 +650,13 @@ int kgat_adam_lazy_catchup_sched_f32(float *p, float *m, float *v, int64_t n_row
                                      int64_t n_list, int32_t *last, const int32_t *t_dev, float *hist_sz,
                                      float *hist_bc, int32_t *hist_skip, int32_t cap, float beta1, float beta2,
                                      float eps, void *stream);
+/* row_map (nullable): the batch rows' kgat_frontier_build map entries are reset to -1 by the same launch
+ * (kgat_frontier_reset folded in; a skipped step resets them too). */
 int kgat_adam_lazy_rows_sched_f32(float *p, float *m, float *v, int32_t d, const int32_t *rows, int64_t n_list,
                                   const float *Gc, int64_t ldg, int32_t *last, float *hist_sz, float *hist_bc,
                                   int32_t *hist_skip, int32_t cap, const int32_t *t_dev, const float *sched_sz,
                                   const float *sched_bc, float beta1, float beta2, float eps, const int32_t *skip,
-                                  void *stream);
+                                  int32_t *row_map, void *stream);
 
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);

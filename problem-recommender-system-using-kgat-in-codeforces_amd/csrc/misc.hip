@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
                                                              int32_t* __restrict__ last, int32_t t, LazyHist h,
                                                              float step_size, float b1, float b2, float bc2s,
                                                              float eps, const int32_t* __restrict__ skip,
-                                                             StepSched sched) {
+                                                             StepSched sched, int32_t* __restrict__ row_map) {
   if (sched.t != nullptr) {
     t = *sched.t;
     step_size = sched.sz[t];
@@ -404,6 +404,9 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
   }
   __syncthreads();
   if (c == 0 && r >= 0 && !skipped) last[r] = t;
+  // the batch rows' map entries back to -1 (the captured update's frontier_reset, folded in: nothing
+  // after this kernel reads the map in the step; a skipped step resets it too)
+  if (row_map != nullptr && c == 0 && r >= 0) row_map[r] = -1;
 }
 
 }  // namespace kgat
@@ -450,14 +453,14 @@ extern "C" int kgat_adam_lazy_catchup_sched_f32(float* p, float* m, float* v, in
 static int lazy_rows(float* p, float* m, float* v, int32_t d, const int32_t* rows, int64_t n_list, const float* Gc,
                      int64_t ldg, int32_t* last, int32_t t, float* hist_sz, float* hist_bc, int32_t* hist_skip,
                      int32_t cap, float step_size, float beta1, float beta2, float bc2_sqrt, float eps,
-                     const int32_t* skip, kgat::StepSched sched, void* stream) {
+                     const int32_t* skip, kgat::StepSched sched, void* stream, int32_t* row_map = nullptr) {
   if (!lazy_args_ok(p, m, v, d, last, hist_sz, hist_bc, hist_skip, cap) || !rows || !Gc || n_list < 0 || ldg < d ||
       (sched.t == nullptr && t < 1))
     return KGAT_ERR_INVALID;
   const int64_t blocks = (std::max<int64_t>(n_list, 1) * d + 255) / 256;  // >= 1 block: the history entry
   hipLaunchKernelGGL(kgat::adam_lazy_rows_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      p, m, v, d, rows, n_list, Gc, ldg, last, t, kgat::LazyHist{hist_sz, hist_bc, hist_skip, cap},
-                     step_size, beta1, beta2, bc2_sqrt, eps, skip, sched);
+                     step_size, beta1, beta2, bc2_sqrt, eps, skip, sched, row_map);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -475,10 +478,11 @@ extern "C" int kgat_adam_lazy_rows_sched_f32(float* p, float* m, float* v, int32
                                              int64_t n_list, const float* Gc, int64_t ldg, int32_t* last,
                                              float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
                                              const int32_t* t_dev, const float* sched_sz, const float* sched_bc,
-                                             float beta1, float beta2, float eps, const int32_t* skip, void* stream) {
+                                             float beta1, float beta2, float eps, const int32_t* skip, int32_t* row_map,
+                                             void* stream) {
   if (!t_dev || !sched_sz || !sched_bc) return KGAT_ERR_INVALID;
   return lazy_rows(p, m, v, d, rows, n_list, Gc, ldg, last, 0, hist_sz, hist_bc, hist_skip, cap, 0.f, beta1, beta2,
-                   0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc}, stream);
+                   0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc}, stream, row_map);
 }
 
 extern "C" int kgat_step_advance(int32_t* t, void* stream) {

@@ -450,8 +450,8 @@ class _KGStepGraph:
       forward -- frontier_build (the batch rows' map), the lazy Adam catch-up of those rows, TransR
                  forward (loss + the backward's work buffer);
       update  -- TransR backward (the table gradient's compact rows, d_rel, d_trans), kgat_step_advance
-                 (the device step counter), the lazy table Adam on the batch rows, the Adam of the
-                 relation embeddings and trans matrices, frontier_reset.
+                 (the device step counter), the lazy table Adam on the batch rows (which also resets
+                 their map entries), the Adam of the relation embeddings and trans matrices.
     ``loss.backward()`` only copies its upstream gradient into the graphs' input (the backward kernels
     run in the update graph, so one replay fewer); a third graph -- the TransR backward alone -- serves
     anything that needs the gradients before the update (``materialize``).  Outside the graphs: one id
@@ -557,14 +557,13 @@ class _KGStepGraph:
                       sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
                       Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,
                       b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), opt.beta1, opt.beta2, opt.eps,
-                      skip.data_ptr(), st_)
+                      skip.data_ptr(), row_map.data_ptr(), st_)  # + the batch rows' map reset (frontier_reset)
             arr = (_lib.AdamTensor * 2)()
             for a, (pp, gg, stt) in zip(arr, ((rel, d_rel, sts[1]), (trans, d_trans, sts[2]))):
                 a.p, a.g, a.m, a.v = pp.data_ptr(), gg.data_ptr(), stt["exp_avg"].data_ptr(), stt["exp_avg_sq"].data_ptr()
                 a.n, a.step_size, a.bc2_sqrt = pp.numel(), 0.0, 0.0
             _lib.call("kgat_adam_multi_sched_f32", arr, 2, opt.beta1, opt.beta2, opt.eps, skip.data_ptr(),
                       b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), st_)
-            kernels.frontier_reset(rows, row_map)
 
         try:
             torch.cuda.synchronize(dev)
