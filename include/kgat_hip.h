@@ -645,18 +645,22 @@ int kgat_adam_lazy_rows_f32(float *p, float *m, float *v, int32_t d, const int32
 int kgat_step_advance(int32_t *t_dev, void *stream);
 int kgat_adam_multi_sched_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
                               const int32_t *skip, const int32_t *t_dev, const float *sched_sz, const float *sched_bc,
-                              void *stream);
+                              int32_t t_add, int32_t *t_out, void *stream);
 int kgat_adam_lazy_catchup_sched_f32(float *p, float *m, float *v, int64_t n_rows, int32_t d, const int32_t *rows,
                                      int64_t n_list, int32_t *last, const int32_t *t_dev, float *hist_sz,
                                      float *hist_bc, int32_t *hist_skip, int32_t cap, float beta1, float beta2,
                                      float eps, void *stream);
 /* row_map (nullable): the batch rows' kgat_frontier_build map entries are reset to -1 by the same launch
- * (kgat_frontier_reset folded in; a skipped step resets them too). */
+ * (kgat_frontier_reset folded in; a skipped step resets them too).  t_add / t_out (kgat_adam_multi_sched_f32
+ * and kgat_adam_lazy_rows_sched_f32): the step applied is *t_dev + t_add, and its number is written to
+ * t_out (nullable) -- the captured KG update applies step *t + 1 in the lazy rows' launch, hands it on
+ * through a second cell, and the relation / trans Adam writes it back to t: kgat_step_advance's launch
+ * folded into the two. */
 int kgat_adam_lazy_rows_sched_f32(float *p, float *m, float *v, int32_t d, const int32_t *rows, int64_t n_list,
                                   const float *Gc, int64_t ldg, int32_t *last, float *hist_sz, float *hist_bc,
                                   int32_t *hist_skip, int32_t cap, const int32_t *t_dev, const float *sched_sz,
                                   const float *sched_bc, float beta1, float beta2, float eps, const int32_t *skip,
-                                  int32_t *row_map, void *stream);
+                                  int32_t *row_map, int32_t t_add, int32_t *t_out, void *stream);
 
 /* dst[i] = src[idx[i]] (int32 idx) -- used to refresh transposed CSR values. */
 int kgat_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);

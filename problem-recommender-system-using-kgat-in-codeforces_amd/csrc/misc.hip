@@ -117,14 +117,24 @@ extern "C" int kgat_version(void) { return 1; }
 namespace kgat {
 
 // A captured optimiser step's scalars on the device (a HIP graph replays the same kernel arguments every
-// step): t = *t (advanced by kgat_step_advance inside the graph), step size and sqrt(1 - beta2^t) =
+// step): t = *t + add (the captured update's first Adam launch applies *t + 1 and hands the number on
+// through out; the second reads it there and writes it back to t), step size and sqrt(1 - beta2^t) =
 // sz[t] / bc[t] -- tables the host filled with FusedAdam's own expressions, so the same floats the
 // by-value launches get.  t == nullptr: the by-value arguments.
 struct StepSched {
   const int32_t* t;
   const float* sz;
   const float* bc;
+  int32_t add = 0;         // the step applied is *t + add
+  int32_t* out = nullptr;  // nullable: block 0 / thread 0 writes that step number there (the next launch's t)
 };
+
+// The step a scheduled launch applies; its number handed on to the next launch of the captured update.
+__device__ __forceinline__ int32_t sched_step(const StepSched& s) {
+  const int32_t t = *s.t + s.add;
+  if (s.out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *s.out = t;
+  return t;
+}
 
 __global__ void step_advance_kernel(int32_t* __restrict__ t) {
   if (threadIdx.x == 0) t[0] = t[0] + 1;
@@ -161,11 +171,11 @@ __device__ __forceinline__ void st4(float* p, float4 v) {
 template <int V>
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, float b2, float eps,
                                                          const int32_t* __restrict__ skip, StepSched sched) {
+  // a captured step (kgat_adam_multi_sched_f32): every tensor's step size and bias correction are step t's
+  // entries of the host-computed schedule, t read on the device (and handed on before a skip returns)
+  const int32_t ts = sched.t != nullptr ? sched_step(sched) : 0;
   if (skip != nullptr && *skip != 0) return;  // the step's ids were out of range: no parameter moves
   const float w1 = 1.f - b1, w2 = 1.f - b2;
-  // a captured step (kgat_adam_multi_sched_f32): every tensor's step size and bias correction are step t's
-  // entries of the host-computed schedule, t read on the device
-  const int32_t ts = sched.t != nullptr ? *sched.t : 0;
   const int64_t total = T.chunk_off[T.count];
   for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
     int i = 0;
@@ -286,15 +296,16 @@ extern "C" int kgat_adam_multi_f32(const kgat_adam_tensor* tensors, int32_t coun
 
 extern "C" int kgat_adam_multi_ex_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
                                       float eps, const int32_t* skip, void* stream) {
-  return kgat_adam_multi_sched_f32(tensors, count, beta1, beta2, eps, skip, nullptr, nullptr, nullptr, stream);
+  return kgat_adam_multi_sched_f32(tensors, count, beta1, beta2, eps, skip, nullptr, nullptr, nullptr, 0, nullptr,
+                                   stream);
 }
 
 extern "C" int kgat_adam_multi_sched_f32(const kgat_adam_tensor* tensors, int32_t count, float beta1, float beta2,
                                          float eps, const int32_t* skip, const int32_t* t_dev, const float* sched_sz,
-                                         const float* sched_bc, void* stream) {
+                                         const float* sched_bc, int32_t t_add, int32_t* t_out, void* stream) {
   if (!tensors || count < 1 || count > KGAT_ADAM_MAX_TENSORS) return KGAT_ERR_INVALID;
   if (t_dev != nullptr && (!sched_sz || !sched_bc)) return KGAT_ERR_INVALID;
-  const kgat::StepSched sched{t_dev, sched_sz, sched_bc};
+  const kgat::StepSched sched{t_dev, sched_sz, sched_bc, t_add, t_out};
   kgat::AdamTable T{};
   T.count = count;
   int64_t off = 0;
@@ -376,7 +387,7 @@ __global__ __launch_bounds__(256) void adam_lazy_rows_kernel(float* __restrict__
                                                              float eps, const int32_t* __restrict__ skip,
                                                              StepSched sched, int32_t* __restrict__ row_map) {
   if (sched.t != nullptr) {
-    t = *sched.t;
+    t = sched_step(sched);
     step_size = sched.sz[t];
     bc2s = sched.bc[t];
   }
@@ -479,10 +490,10 @@ extern "C" int kgat_adam_lazy_rows_sched_f32(float* p, float* m, float* v, int32
                                              float* hist_sz, float* hist_bc, int32_t* hist_skip, int32_t cap,
                                              const int32_t* t_dev, const float* sched_sz, const float* sched_bc,
                                              float beta1, float beta2, float eps, const int32_t* skip, int32_t* row_map,
-                                             void* stream) {
+                                             int32_t t_add, int32_t* t_out, void* stream) {
   if (!t_dev || !sched_sz || !sched_bc) return KGAT_ERR_INVALID;
   return lazy_rows(p, m, v, d, rows, n_list, Gc, ldg, last, 0, hist_sz, hist_bc, hist_skip, cap, 0.f, beta1, beta2,
-                   0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc}, stream, row_map);
+                   0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc, t_add, t_out}, stream, row_map);
 }
 
 extern "C" int kgat_step_advance(int32_t* t, void* stream) {

@@ -449,9 +449,9 @@ class _KGStepGraph:
     Here the forward and the update each replay one graph captured once per shape:
       forward -- frontier_build (the batch rows' map), the lazy Adam catch-up of those rows, TransR
                  forward (loss + the backward's work buffer);
-      update  -- TransR backward (the table gradient's compact rows, d_rel, d_trans), kgat_step_advance
-                 (the device step counter), the lazy table Adam on the batch rows (which also resets
-                 their map entries), the Adam of the relation embeddings and trans matrices.
+      update  -- TransR backward (the table gradient's compact rows, d_rel, d_trans), the lazy table Adam
+                 on the batch rows (which also resets their map entries), the Adam of the relation
+                 embeddings and trans matrices (the two advance the device step counter between them).
     ``loss.backward()`` only copies its upstream gradient into the graphs' input (the backward kernels
     run in the update graph, so one replay fewer); a third graph -- the TransR backward alone -- serves
     anything that needs the gradients before the update (``materialize``).  Outside the graphs: one id
@@ -543,7 +543,8 @@ class _KGStepGraph:
         reg = float(m._regularization_params[1])
         b = {"ids": torch.zeros(4 * B, dtype=torch.int64, device=dev),  # heads | pos | neg | relations
              "gout": torch.ones(1, dtype=torch.float32, device=dev),
-             "t": torch.zeros(1, dtype=torch.int32, device=dev)}
+             "t": torch.zeros(1, dtype=torch.int32, device=dev),
+             "t_next": torch.zeros(1, dtype=torch.int32, device=dev)}
         h, p, q, r = b["ids"].split(B)
         ev = (kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS)
         kernels.KERNEL_EVENTS = kernels.SPMM_EVENTS = None  # no event records inside a capture
@@ -552,18 +553,19 @@ class _KGStepGraph:
 
         def update_kernels(Gc, d_rel, d_trans):
             st_ = stream_ptr(dev)
-            _lib.call("kgat_step_advance", b["t"].data_ptr(), st_)
+            # step t + 1 applied by the lazy rows' launch, its number passed on in t_next; the relation /
+            # trans Adam reads it there and writes it back to t (kgat_step_advance folded into the two)
             _lib.call("kgat_adam_lazy_rows_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
                       sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
                       Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,
                       b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), opt.beta1, opt.beta2, opt.eps,
-                      skip.data_ptr(), row_map.data_ptr(), st_)  # + the batch rows' map reset (frontier_reset)
+                      skip.data_ptr(), row_map.data_ptr(), 1, b["t_next"].data_ptr(), st_)  # + the map reset
             arr = (_lib.AdamTensor * 2)()
             for a, (pp, gg, stt) in zip(arr, ((rel, d_rel, sts[1]), (trans, d_trans, sts[2]))):
                 a.p, a.g, a.m, a.v = pp.data_ptr(), gg.data_ptr(), stt["exp_avg"].data_ptr(), stt["exp_avg_sq"].data_ptr()
                 a.n, a.step_size, a.bc2_sqrt = pp.numel(), 0.0, 0.0
             _lib.call("kgat_adam_multi_sched_f32", arr, 2, opt.beta1, opt.beta2, opt.eps, skip.data_ptr(),
-                      b["t"].data_ptr(), sz.data_ptr(), bc.data_ptr(), st_)
+                      b["t_next"].data_ptr(), sz.data_ptr(), bc.data_ptr(), 0, b["t"].data_ptr(), st_)
 
         try:
             torch.cuda.synchronize(dev)

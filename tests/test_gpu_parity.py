@@ -2043,6 +2043,7 @@ def test_sched_adam_matches_eager(pkg):
     sz = torch.tensor([0.0] + [lr / (1.0 - b1 ** t) for t in range(1, 16)], dtype=torch.float32, device=DEV)
     bc = torch.tensor([0.0] + [math.sqrt(1.0 - b2 ** t) for t in range(1, 16)], dtype=torch.float32, device=DEV)
     t_dev = torch.zeros(1, dtype=torch.int32, device=DEV)
+    t_next = torch.zeros(1, dtype=torch.int32, device=DEV)
     skip = torch.zeros(1, dtype=torch.int32, device=DEV)
     st = graph_mod.stream_ptr(torch.device(DEV))
     for t in range(1, 7):
@@ -2054,9 +2055,15 @@ def test_sched_adam_matches_eager(pkg):
         for a, (p, m, v), g in zip(arr, b_state, grads):
             a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
             a.n, a.step_size, a.bc2_sqrt = p.numel(), 0.0, 0.0
-        lib.call("kgat_step_advance", t_dev.data_ptr(), st)
-        lib.call("kgat_adam_multi_sched_f32", arr, len(shapes), b1, b2, eps, skip.data_ptr(), t_dev.data_ptr(),
-                 sz.data_ptr(), bc.data_ptr(), st)
+        if t % 2:
+            lib.call("kgat_step_advance", t_dev.data_ptr(), st)
+            lib.call("kgat_adam_multi_sched_f32", arr, len(shapes), b1, b2, eps, skip.data_ptr(), t_dev.data_ptr(),
+                     sz.data_ptr(), bc.data_ptr(), 0, None, st)
+        else:  # the captured update's form: step *t + 1 applied, its number handed on in a second cell
+            # (the kernel reads one cell and writes the other), then copied back for the next step
+            lib.call("kgat_adam_multi_sched_f32", arr, len(shapes), b1, b2, eps, skip.data_ptr(), t_dev.data_ptr(),
+                     sz.data_ptr(), bc.data_ptr(), 1, t_next.data_ptr(), st)
+            t_dev.copy_(t_next)
     torch.cuda.synchronize()
     assert int(t_dev[0]) == 6
     for x, y in zip(a_state, b_state):
