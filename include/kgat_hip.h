@@ -636,13 +636,12 @@ int kgat_adam_lazy_rows_f32(float *p, float *m, float *v, int32_t d, const int32
 
 /* The KG step captured as a HIP graph (KGAT.capture_kg_step; main.py:324-345, model.py:204-261,
  * 414-419): a graph replays the kernel arguments it was captured with, so a step's scalars live on
- * the device.  t_dev (int32 [1]) holds the optimiser's step number: kgat_step_advance adds 1 (the
- * graph's first update node); the _sched variants read t = *t_dev and the step's size and
+ * the device.  t_dev (int32 [1]) holds the optimiser's step number; the _sched variants read t = *t_dev
+ * (+ t_add, below) and the step's size and
  * sqrt(1 - beta2^t) from the schedule tables sched_sz[t] / sched_bc[t] (float, > t entries, filled by
  * the host with the by-value launches' own float values: lr / (1 - beta1^t), sqrt(1 - beta2^t)).
  * Otherwise each is kgat_adam_multi_ex_f32 (every tensor at step t), kgat_adam_lazy_catchup_f32 and
  * kgat_adam_lazy_rows_f32, bit for bit. */
-int kgat_step_advance(int32_t *t_dev, void *stream);
 int kgat_adam_multi_sched_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
                               const int32_t *skip, const int32_t *t_dev, const float *sched_sz, const float *sched_bc,
                               int32_t t_add, int32_t *t_out, void *stream);
@@ -654,8 +653,9 @@ int kgat_adam_lazy_catchup_sched_f32(float *p, float *m, float *v, int64_t n_row
  * (kgat_frontier_reset folded in; a skipped step resets them too).  t_add / t_out (kgat_adam_multi_sched_f32
  * and kgat_adam_lazy_rows_sched_f32): the step applied is *t_dev + t_add, and its number is written to
  * t_out (nullable) -- the captured KG update applies step *t + 1 in the lazy rows' launch, hands it on
- * through a second cell, and the relation / trans Adam writes it back to t: kgat_step_advance's launch
- * folded into the two. */
+ * through a second cell, and the relation / trans Adam writes it back to t (no separate counter launch).
+ * Both write t_out before a set skip flag returns, so a skipped step advances the counter as
+ * FusedAdam's step count does. */
 int kgat_adam_lazy_rows_sched_f32(float *p, float *m, float *v, int32_t d, const int32_t *rows, int64_t n_list,
                                   const float *Gc, int64_t ldg, int32_t *last, float *hist_sz, float *hist_bc,
                                   int32_t *hist_skip, int32_t cap, const int32_t *t_dev, const float *sched_sz,

@@ -183,7 +183,6 @@ _SIGNATURES = {
                                                   c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_adam_lazy_rows_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
                                                c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp]),
-    "kgat_step_advance": (ctypes.c_int, [c_vp, c_vp]),
     "kgat_adam_multi_sched_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp, c_vp,
                                                  c_vp, c_vp, c_i32, c_vp, c_vp]),
     "kgat_adam_lazy_catchup_sched_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,

@@ -136,10 +136,6 @@ __device__ __forceinline__ int32_t sched_step(const StepSched& s) {
   return t;
 }
 
-__global__ void step_advance_kernel(int32_t* __restrict__ t) {
-  if (threadIdx.x == 0) t[0] = t[0] + 1;
-}
-
 // Every tensor of one optimiser step in ONE launch: the tensor table travels in
 // the kernel arguments; block b works on chunk b of the concatenated float4
 // index space (tensor chosen by a scan of <= 16 chunk offsets).
@@ -496,12 +492,6 @@ extern "C" int kgat_adam_lazy_rows_sched_f32(float* p, float* m, float* v, int32
                    0.f, eps, skip, kgat::StepSched{t_dev, sched_sz, sched_bc, t_add, t_out}, stream, row_map);
 }
 
-extern "C" int kgat_step_advance(int32_t* t, void* stream) {
-  if (!t) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::step_advance_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), t);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
 
 extern "C" int kgat_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float step_size, float beta1,
                              float beta2, float bc2_sqrt, float eps, void* stream) {

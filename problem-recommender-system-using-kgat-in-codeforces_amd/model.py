@@ -554,7 +554,7 @@ class _KGStepGraph:
         def update_kernels(Gc, d_rel, d_trans):
             st_ = stream_ptr(dev)
             # step t + 1 applied by the lazy rows' launch, its number passed on in t_next; the relation /
-            # trans Adam reads it there and writes it back to t (kgat_step_advance folded into the two)
+            # trans Adam reads it there and writes it back to t (no separate counter launch)
             _lib.call("kgat_adam_lazy_rows_sched_f32", emb.data_ptr(), sts[0]["exp_avg"].data_ptr(),
                       sts[0]["exp_avg_sq"].data_ptr(), d, rows.data_ptr(), rows.numel(), Gc.data_ptr(),
                       Gc.stride(0), lz.last.data_ptr(), hs.data_ptr(), hb.data_ptr(), hk.data_ptr(), lz.CAP,

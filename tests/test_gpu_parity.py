@@ -2025,7 +2025,7 @@ def test_ids_check_multi_per_array_bounds(pkg):
 
 
 def test_sched_adam_matches_eager(pkg):
-    """The captured KG step's device-scheduled Adam (kgat_step_advance + kgat_adam_multi_sched_f32: the step
+    """The captured KG step's device-scheduled Adam (kgat_adam_multi_sched_f32: the step
     number on the device, step size and sqrt(1 - beta2^t) read from host-filled tables) against the eager
     kgat_adam_multi_ex_f32 with FusedAdam's scalars: parameters and moments equal bit for bit over six steps,
     one of them with the skip flag set."""
@@ -2055,8 +2055,8 @@ def test_sched_adam_matches_eager(pkg):
         for a, (p, m, v), g in zip(arr, b_state, grads):
             a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
             a.n, a.step_size, a.bc2_sqrt = p.numel(), 0.0, 0.0
-        if t % 2:
-            lib.call("kgat_step_advance", t_dev.data_ptr(), st)
+        if t % 2:  # t advanced beforehand, applied as read (t_add 0, no hand-on)
+            t_dev.add_(1)
             lib.call("kgat_adam_multi_sched_f32", arr, len(shapes), b1, b2, eps, skip.data_ptr(), t_dev.data_ptr(),
                      sz.data_ptr(), bc.data_ptr(), 0, None, st)
         else:  # the captured update's form: step *t + 1 applied, its number handed on in a second cell
