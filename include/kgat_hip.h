@@ -163,11 +163,19 @@ int kgat_hop_compact(const int32_t *hit, int64_t n, int32_t *node_map, int32_t *
  * order (node_map fully written, -1 outside); hop_count_host (nullable) as kgat_hop_compact's
  * count_host; hop_rank (nullable, uint64
  * [ceil(n/32)]) gets the set's rank words (kgat_map_rank's layout).  work:
- * kgat_frontier_hop_work_bytes(n) bytes. */
+ * kgat_frontier_hop_work_bytes(n) bytes (8-byte aligned), zero-filled before
+ * its first use; every call leaves it reusable (it holds the single-pass
+ * scan's state: one call at a time per work buffer, stream-ordered). */
 int64_t kgat_frontier_hop_work_bytes(int64_t n);
 int kgat_frontier_hop(const kgat_csr *A, const int32_t *rows0, int32_t n0, uint32_t *bits0, uint32_t *bits1,
                       int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, int32_t *hop_count_host,
                       uint64_t *hop_rank, void *work, int64_t work_bytes, void *stream);
+/* flags: KGAT_HOP_PRECLEARED -- bits0 / bits1 are already zero (kgat_cf_begin cleared them): the
+ * clearing launch is skipped. */
+#define KGAT_HOP_PRECLEARED 1
+int kgat_frontier_hop_ex(const kgat_csr *A, const int32_t *rows0, int32_t n0, uint32_t *bits0, uint32_t *bits1,
+                         int32_t *node_map, int32_t *hop_rows, int32_t *hop_count, int32_t *hop_count_host,
+                         uint64_t *hop_rank, void *work, int64_t work_bytes, int32_t flags, void *stream);
 
 /* kgat_spmm_csr_masked_f32 restricted to an output row set (A = A^T of the
  * graph; out_bits / out_map / out_rows / out_count from kgat_frontier_hop):
@@ -180,6 +188,17 @@ int kgat_spmm_csr_masked_rows_f32(const kgat_csr *A, const int32_t *src_map, con
                                   const uint32_t *out_bits, const int32_t *out_map, const int32_t *out_rows,
                                   const int32_t *out_count, float *Y, int64_t ldy, int32_t d, float *workspace,
                                   int64_t workspace_floats, void *stream);
+/* ... plus Gc (nullable, ldgc): compact rows added to Y[k] after the Yc_init term through the same
+ * src_map row -- the BPR loss's direct gradient of the batch rows (kgat_bpr_bwd_multi_f32), i.e.
+ * kgat_bpr_bwd_f32 into Y with row_map = out_map folded into this launch (same bits); out_src
+ * (nullable, int32 [n_rows]): out_src[k] = src_map[out_rows[k]] for k < *out_count (the compact source
+ * row of output row k, -1 = none: kgat_biinter_bwd_hop_ex_f32's gidx). */
+int kgat_spmm_csr_masked_rows_ex_f32(const kgat_csr *A, const int32_t *src_map, const uint32_t *src_bits,
+                                     const float *Xc, int64_t ldxc, const float *Yc_init, int64_t ldyc,
+                                     const float *Gc, int64_t ldgc, const uint32_t *out_bits, const int32_t *out_map,
+                                     const int32_t *out_rows, const int32_t *out_count, float *Y, int64_t ldy,
+                                     int32_t *out_src, int32_t d, float *workspace, int64_t workspace_floats,
+                                     void *stream);
 
 /* Rows of A that are in a node set or have an edge into it: hit[r] = 1 iff bit (row0 + r) of
  * bits or bit col of one of row r's edges is set, else 0 (n_bits: the bitmap's size in nodes,
@@ -291,6 +310,20 @@ int kgat_biinter_bwd_hop_f32(const float *X, int64_t ldx, const float *S, int64_
                              const int32_t *count, int64_t n_max, int64_t src_rows, int32_t dh_compact,
                              int32_t d_in, int32_t d_out, float dropout_p, float *workspace,
                              int64_t workspace_floats, void *stream);
+/* ... plus the BPR term of the batch rows: G (nullable, ldg >= d_in) holds compact rows and gidx (int32,
+ * with G; by hop position, e.g. kgat_spmm_csr_masked_rows_ex_f32's out_src) names the G row of hop row i
+ * or -1.  Hop row i with gidx[i] >= 0 gets dXd += G[gidx[i]] after its bi-interaction term
+ * (kgat_bpr_bwd_f32 into dXd with row_map = the hop map, folded in: same bits).  gmap (nullable): the
+ * batch-row node map that numbers G; its entries of those rows are reset to -1 by the same launch
+ * (kgat_frontier_reset folded in: rows must hold every node gmap numbers). */
+int kgat_biinter_bwd_hop_ex_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *H, int64_t ldh,
+                                const float *norm, const uint64_t *mask, const float *dH, int64_t lddh,
+                                const float *W1, const float *W2, float *dXd, int64_t lddxd, float *dS, int64_t ldds,
+                                float *dW1, float *db1, float *dW2, float *db2, const int32_t *rows,
+                                const int32_t *count, int64_t n_max, int64_t src_rows, int32_t dh_compact,
+                                int32_t d_in, int32_t d_out, float dropout_p, const float *G, int64_t ldg,
+                                const int32_t *gidx, int32_t *gmap, float *workspace, int64_t workspace_floats,
+                                void *stream);
 
 /* The dense fp32 contractions of the wide layers (a2 / a6 at d = 128 / 256: W1, W2,
  * W_r, W_v, W_o products and the split-K weight-gradient slabs), hand-written MFMA
@@ -425,6 +458,11 @@ typedef struct kgat_tables {
  * half keeps the per-sample loss terms, summed in index order). */
 int kgat_bpr_fwd_f32(const kgat_tables *T, const int64_t *users, const int64_t *pos, const int64_t *neg,
                      int32_t batch, float reg, float *loss, float *coef, void *stream);
+/* ... in one launch: ticket (nullable; device uint32, 0 on entry, left 0) -- the block that finishes
+ * last sums the loss terms (same order, same bits as the second kernel of kgat_bpr_fwd_f32).  Calls
+ * sharing a ticket must be stream-ordered. */
+int kgat_bpr_fwd_ex_f32(const kgat_tables *T, const int64_t *users, const int64_t *pos, const int64_t *neg,
+                        int32_t batch, float reg, float *loss, float *coef, uint32_t *ticket, void *stream);
 
 /* a3/a4 backward: for table t, dst[id] += d loss / d table_t[id] for every
  * gathered id, duplicates summed in slot order (deterministic).  grad_out
@@ -434,6 +472,15 @@ int kgat_bpr_fwd_f32(const kgat_tables *T, const int64_t *users, const int64_t *
 int kgat_bpr_bwd_f32(const kgat_tables *T, int32_t table, const int64_t *users, const int64_t *pos,
                      const int64_t *neg, int32_t batch, float reg, const float *coef,
                      const float *grad_out, float *dst, int64_t lddst, const int32_t *row_map, void *stream);
+/* kgat_bpr_bwd_f32 for tables t0 .. T->count - 1 in one launch, each WRITTEN (not added) into its
+ * own compact buffer D->ptr[t] (ld D->ld[t]; null = skip that table) at the row's frontier position
+ * (rows / *count: kgat_frontier_build's list of the batch's distinct ids): the summed gradient with
+ * kgat_bpr_bwd_f32's arithmetic into zeros (same bits); rows [*count, 3 * batch) of every buffer are
+ * zeroed.  The backward's batch-row terms of every layer at once, consumed as the last layer's dH, by
+ * kgat_spmm_csr_masked_rows_ex_f32 (Gc) and by kgat_biinter_bwd_hop_ex_f32 (G). */
+int kgat_bpr_bwd_multi_f32(const kgat_tables *T, int32_t t0, const int64_t *users, const int64_t *pos,
+                           const int64_t *neg, int32_t batch, float reg, const float *coef, const float *grad_out,
+                           const kgat_tables *D, const int32_t *rows, const int32_t *count, void *stream);
 
 /* The BPR batch's distinct rows (the backward frontier of the last layer,
  * model.py:189-191 gathers only these): rows[0..count) = ids in
@@ -443,6 +490,16 @@ int kgat_bpr_bwd_f32(const kgat_tables *T, int32_t table, const int64_t *users, 
 int kgat_frontier_build(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch,
                         int32_t *node_map, int32_t *rows, int32_t *count, void *stream);
 int kgat_frontier_reset(const int32_t *rows, int32_t n, int32_t *node_map, void *stream);
+
+/* The prologue of a TRAIN_CF step (model.py:165-202 on device ids) in one launch: kgat_ids_check_ex on
+ * users | pos | neg (int64 [batch] each) against [0, bound) -- ids_out (int64 [3 * batch]) gets the
+ * checked copies in that order, an id out of range becomes 0 and sets *bad (and *bad_dev when given) --,
+ * kgat_frontier_build on the checked ids (node_map / rows / count), and, when clear0 / clear1 are given
+ * (16-byte aligned, clear_words uint32 each), the zeroing of kgat_frontier_hop's two bitmaps
+ * (then call it with KGAT_HOP_PRECLEARED).  3 * batch <= 4096. */
+int kgat_cf_begin(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch, int64_t bound,
+                  int64_t *ids_out, int32_t *bad, int32_t *bad_dev, int32_t *node_map, int32_t *rows, int32_t *count,
+                  uint32_t *clear0, uint32_t *clear1, int64_t clear_words, void *stream);
 
 /* a5 -- TransR KG loss (model.py:204-261): h' = e_h W_r etc., scalar loss
  * written to *loss.  work (kgat_transr_work_floats) keeps per-sample terms and

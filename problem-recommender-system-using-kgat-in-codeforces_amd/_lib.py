@@ -48,6 +48,7 @@ class Tables(ctypes.Structure):
 
 
 KGAT_IDS_MAX = 4
+KGAT_HOP_PRECLEARED = 1
 
 
 class Ids(ctypes.Structure):
@@ -96,7 +97,13 @@ _SIGNATURES = {
     "kgat_biinter_bwd_hop_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp,
                                                 c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_i64, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp]),
+    "kgat_biinter_bwd_hop_ex_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                                   c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                   c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp,
+                                                   c_vp, c_vp, c_i64, c_vp]),
     "kgat_frontier_hop_work_bytes": (c_i64, [c_i64]),
+    "kgat_frontier_hop_ex": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_i64, c_i32, c_vp]),
     "kgat_frontier_hop": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_vp, c_i64, c_vp]),
     "kgat_rows_union": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
@@ -105,6 +112,9 @@ _SIGNATURES = {
                                            c_i64, c_f32, c_vp]),
     "kgat_spmm_csr_masked_rows_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
                                                      c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "kgat_spmm_csr_masked_rows_ex_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                                        c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
+                                                        c_vp, c_i64, c_vp]),
     "kgat_spmm_csr_rows_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                               c_vp, c_i64, c_vp]),
     "kgat_biinter_fwd_tiles_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
@@ -116,6 +126,12 @@ _SIGNATURES = {
     "kgat_bpr_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp]),
     "kgat_bpr_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_i32, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp,
                                         c_vp, c_i64, c_vp, c_vp]),
+    "kgat_bpr_fwd_ex_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp,
+                                           c_vp]),
+    "kgat_bpr_bwd_multi_f32": (ctypes.c_int, [ctypes.POINTER(Tables), c_i32, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp,
+                                              c_vp, ctypes.POINTER(Tables), c_vp, c_vp, c_vp]),
+    "kgat_cf_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_i64, c_vp]),
     "kgat_frontier_build": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "kgat_frontier_reset": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp]),
     "kgat_transr_work_floats": (c_i64, [c_i32, c_i32, c_i32]),

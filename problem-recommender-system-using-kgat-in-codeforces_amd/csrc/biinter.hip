@@ -601,7 +601,8 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     int64_t ldh, const float* __restrict__ norm, const uint64_t* __restrict__ mask, const float* __restrict__ dH,
     int64_t lddh, const float* __restrict__ W1, const float* __restrict__ W2, float* __restrict__ dXd,
     int64_t lddxd, float* __restrict__ dS, int64_t ldds, float* __restrict__ slab, int64_t n, float p,
-    const int32_t* __restrict__ rows, int64_t n_src, const int32_t* __restrict__ n_dev, int dh_by_node) {
+    const int32_t* __restrict__ rows, int64_t n_src, const int32_t* __restrict__ n_dev, int dh_by_node,
+    const float* __restrict__ G, int64_t ldg, const int32_t* __restrict__ gidx, int32_t* __restrict__ gmap) {
   using B = BiShape<DIN, DOUT>;
   using F = SavedBwd<DIN, DOUT>;
   // hop mode: the row count is produced on the device (kgat_hop_compact); n is its bound
@@ -647,15 +648,29 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
   int64_t st = static_cast<int64_t>(blockIdx.x) * 4 + wave;
 
+  // frontier mode with G: the G row of each of this lane's 4 rows (gidx, by row position: -1 = none), loaded
+  // with the sub-tile's DMA; the G rows themselves are loaded once it has landed, under the tile's math
+  int32_t gnext[4] = {-1, -1, -1, -1};
+  int32_t ndnext = -1;  // frontier mode: the node of row (lane & 15) of the sub-tile in flight
   // issue the DMA of sub-tile t into this wave's image
   auto issue = [&](int64_t t) {
     const int64_t r0 = t * 16;
+    if constexpr (FRONTIER) {
+      if (gidx != nullptr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t cr = r0 + q * 4 + i;
+          gnext[i] = cr < n ? gidx[cr] : -1;
+        }
+      }
+    }
     const int64_t lim = n - r0;  // rows of this sub-tile that exist
     int32_t nd = -1;             // frontier mode: node of row (lane & 15)
     if constexpr (FRONTIER) {
       const int64_t r = r0 + (lane & 15);
       nd = r < n ? rows[r] : -1;
       if (nd >= n_src) nd = -1;
+      ndnext = nd;
     }
     auto node_of = [&](int row) -> int64_t {
       if constexpr (FRONTIER) return __shfl(nd, row);
@@ -685,7 +700,20 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
   if (st < nsub) issue(st);
   for (; st < nsub; st += stride) {
     const int64_t r0 = st * 16;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sub-tile's DMA has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sub-tile's DMA (and its G row indices) has landed
+    const int32_t ndcur = ndnext;
+    int32_t grow[4] = {-1, -1, -1, -1};
+    float gv[NIB][4];
+    if constexpr (FRONTIER) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        grow[i] = gnext[i];
+#pragma unroll
+        for (int ib = 0; ib < NIB; ++ib)
+          gv[ib][i] = grow[i] >= 0 ? G[static_cast<int64_t>(grow[i]) * ldg + ib * 16 + c] : 0.f;
+      }
+    }
+    int32_t gnode[4] = {0, 0, 0, 0};
     float x[NIB][4], sv[NIB][4], da[NCB][4], db[NCB][4];
     {
       float h[NCB][4], dh[NCB][4], nrm[4];
@@ -698,9 +726,13 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
         const int64_t cr = r0 + row;
         inr[i] = cr < n;
         int64_t nn = cr;
-        if constexpr (FRONTIER) nn = inr[i] ? rows[cr] : -1;
+        if constexpr (FRONTIER) {
+          const int32_t v = __shfl(ndcur, row);  // issue()'s load of rows[cr] (-1 past n or n_src)
+          nn = inr[i] ? v : -1;
+        }
         okr[i] = inr[i] && nn >= 0 && nn < n_src;
         node[i] = okr[i] ? static_cast<int32_t>(nn) : 0;
+        gnode[i] = node[i];
 #pragma unroll
         for (int ib = 0; ib < NIB; ++ib) {
           x[ib][i] = img_at<DIN>(ix, row, ib * 16 + c);
@@ -794,10 +826,19 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (full || q * 4 + i < n - r0) {
-            pxd[i][ib * 16] = fmaf(dm[i], sv[ib][i], du[i]);
+            float vx = fmaf(dm[i], sv[ib][i], du[i]);
+            if (FRONTIER && grow[i] >= 0) vx = vx + gv[ib][i];  // kgat_bpr_bwd_f32's dst += g, folded
+            pxd[i][ib * 16] = vx;
             psd[i][ib * 16] = fmaf(dm[i], x[ib][i], du[i]);
           }
         }
+      }
+      if constexpr (FRONTIER) {
+        // the batch-row map entries this tile consumed go back to -1 (kgat_frontier_reset folded in): each
+        // node is in one tile only, and the store depends on the loaded entry
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (c == 0 && grow[i] >= 0 && gmap != nullptr) gmap[gnode[i]] = -1;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -955,7 +996,9 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
                         const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
                         const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, int64_t n, float p,
                         const int32_t* rows, int64_t n_src, float* ws, int64_t ws_floats, int* nslab,
-                        hipStream_t st, const int32_t* n_dev = nullptr, int dh_by_node = 0) {
+                        hipStream_t st, const int32_t* n_dev = nullptr, int dh_by_node = 0,
+                        const float* G = nullptr, int64_t ldg = 0, const int32_t* gidx = nullptr,
+                        int32_t* gmap = nullptr) {
   using F = SavedBwd<DIN, DOUT>;
   const int width = 2 * DOUT * DIN + 2 * DOUT;
   const int grid = saved_grid<DIN, DOUT>(n);
@@ -974,11 +1017,11 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
   if (rows != nullptr)
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, true>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
                        lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src,
-                       n_dev, dh_by_node);
+                       n_dev, dh_by_node, G, ldg, gidx, gmap);
   else
     hipLaunchKernelGGL((biinter_bwd_saved_kernel<DIN, DOUT, false>), dim3(grid), dim3(256), lds_bytes, st, X, ldx, S,
                        lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, ws, n, p, rows, n_src,
-                       nullptr, 0);
+                       nullptr, 0, nullptr, 0, nullptr, nullptr);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -990,14 +1033,17 @@ static int launch_hop(const float* X, int64_t ldx, const float* S, int64_t lds, 
                       const float* norm, const uint64_t* mask, const float* dH, int64_t lddh, const float* W1,
                       const float* W2, float* dXd, int64_t lddxd, float* dS, int64_t ldds, float* dW1, float* db1,
                       float* dW2, float* db2, int64_t n_max, float p, const int32_t* rows, const int32_t* n_dev,
-                      int64_t src_rows, int dh_by_node, float* ws, int64_t ws_floats, hipStream_t st) {
+                      int64_t src_rows, int dh_by_node, float* ws, int64_t ws_floats, hipStream_t st,
+                      const float* G = nullptr, int64_t ldg = 0, const int32_t* gidx = nullptr,
+                      int32_t* gmap = nullptr) {
   if constexpr (!SavedBwd<DIN, DOUT>::kOk) {
     return KGAT_ERR_UNSUPPORTED_DIM;
   } else {
     const int width = 2 * DOUT * DIN + 2 * DOUT;
     int nslab = 0;
     if (int e = launch_saved<DIN, DOUT>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds,
-                                        n_max, p, rows, src_rows, ws, ws_floats, &nslab, st, n_dev, dh_by_node))
+                                        n_max, p, rows, src_rows, ws, ws_floats, &nslab, st, n_dev, dh_by_node, G,
+                                        ldg, gidx, gmap))
       return e;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, st, ws, nslab, width, dW1, dW2,
                        db1, db2, DIN, DOUT);
@@ -1148,13 +1194,15 @@ extern "C" int kgat_biinter_bwd_f32(const float* X, int64_t ldx, const float* S,
 #undef KGAT_BWD_CALL
 }
 
-extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
-                                        int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
-                                        int64_t lddh, const float* W1, const float* W2, float* dXd, int64_t lddxd,
-                                        float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2,
-                                        const int32_t* rows, const int32_t* count, int64_t n_max, int64_t src_rows,
-                                        int32_t dh_compact, int32_t d_in, int32_t d_out, float dropout_p,
-                                        float* workspace, int64_t workspace_floats, void* stream) {
+extern "C" int kgat_biinter_bwd_hop_ex_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                           int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
+                                           int64_t lddh, const float* W1, const float* W2, float* dXd, int64_t lddxd,
+                                           float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2,
+                                           const int32_t* rows, const int32_t* count, int64_t n_max, int64_t src_rows,
+                                           int32_t dh_compact, int32_t d_in, int32_t d_out, float dropout_p,
+                                           const float* G, int64_t ldg, const int32_t* gidx, int32_t* gmap,
+                                           float* workspace,
+                                           int64_t workspace_floats, void* stream) {
   if (!X || !S || !H || !norm || !mask || !dH || !W1 || !W2 || !dXd || !dS || !dW1 || !db1 || !dW2 || !db2 ||
       !rows || !count || n_max < 0 || src_rows < 0)
     return KGAT_ERR_INVALID;
@@ -1162,10 +1210,24 @@ extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float
     return KGAT_ERR_INVALID;
   if (ldx < d_in || lds < d_in || lddh < d_out || lddxd < d_in || ldds < d_in || ldh < d_out) return KGAT_ERR_INVALID;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if ((G == nullptr) != (gidx == nullptr) || (G != nullptr && ldg < d_in)) return KGAT_ERR_INVALID;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define KGAT_HOP_CALL(a, b)                                                                                       \
   kgat::launch_hop<a, b>(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, dW1, db1, dW2, \
-                         db2, n_max, dropout_p, rows, count, src_rows, dh_compact ? 0 : 1, workspace, workspace_floats, st)
+                         db2, n_max, dropout_p, rows, count, src_rows, dh_compact ? 0 : 1, workspace, workspace_floats, \
+                         st, G, ldg, gidx, gmap)
   KGAT_BI_DISPATCH(KGAT_HOP_CALL)
 #undef KGAT_HOP_CALL
+}
+
+extern "C" int kgat_biinter_bwd_hop_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* H,
+                                        int64_t ldh, const float* norm, const uint64_t* mask, const float* dH,
+                                        int64_t lddh, const float* W1, const float* W2, float* dXd, int64_t lddxd,
+                                        float* dS, int64_t ldds, float* dW1, float* db1, float* dW2, float* db2,
+                                        const int32_t* rows, const int32_t* count, int64_t n_max, int64_t src_rows,
+                                        int32_t dh_compact, int32_t d_in, int32_t d_out, float dropout_p,
+                                        float* workspace, int64_t workspace_floats, void* stream) {
+  return kgat_biinter_bwd_hop_ex_f32(X, ldx, S, lds, H, ldh, norm, mask, dH, lddh, W1, W2, dXd, lddxd, dS, ldds, dW1,
+                                     db1, dW2, db2, rows, count, n_max, src_rows, dh_compact, d_in, d_out, dropout_p,
+                                     nullptr, 0, nullptr, nullptr, workspace, workspace_floats, stream);
 }

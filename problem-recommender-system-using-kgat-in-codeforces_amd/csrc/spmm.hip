@@ -72,13 +72,20 @@ template <int MODE>
 __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t out, int gl, float4 acc,
                                           bool any = false) {
   if (MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam) {
-    if (io.Yc != nullptr) {
+    if (io.Yc != nullptr || io.Gc != nullptr || (MODE == kMaskedRows && io.out_src != nullptr)) {
       const int m = io.src_map[io.row0 + row];
       if (m >= 0) {
-        const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
-        acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+        if (io.Yc != nullptr) {
+          const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(m) * io.ldyc)[gl];
+          acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+        }
+        if (MODE != kMaskedAdam && io.Gc != nullptr) {
+          const float4 o = reinterpret_cast<const float4*>(io.Gc + static_cast<int64_t>(m) * io.ldgc)[gl];
+          acc = make_float4(acc.x + o.x, acc.y + o.y, acc.z + o.z, acc.w + o.w);
+        }
         any = true;
       }
+      if (MODE == kMaskedRows && io.out_src != nullptr && gl == 0) io.out_src[out] = m;
     }
     if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
   }
@@ -337,31 +344,135 @@ __global__ __launch_bounds__(256) void csr_mark_rows_kernel(kgat_csr A, const ui
     }
 }
 
-struct Popc {
-  __device__ int32_t operator()(uint32_t w) const { return __popc(w); }
-};
+// The set in a bitmap listed in one launch: node_map[i] = position of i among the members (ascending
+// node order) or -1, rows[pos] = i, *count (and *count_host), rank words (kgat_map_rank's layout).
+// Positions come from a single-pass scan of the word popcounts: each block takes kListWords words and a
+// ticket (launch order, so every block it waits for is already running), publishes its popcount total
+// as an 8-byte {tag | status | value} granule (one write-through agent-scope store, polled with
+// agent-scope loads: self-contained, no fence), and looks back over its predecessors' granules for its
+// prefix (decoupled look-back).  The tag is the launch's epoch + 1, so the granules of earlier launches
+// never match and nothing is reset between launches; the last block to finish zeroes the ticket and
+// advances the epoch.  state: uint32 [4] {ticket, done, epoch, -} + uint64 [blocks] granules, zero
+// before the first launch (kgat_frontier_hop_work_bytes), never shared by concurrent launches.
+constexpr int kListWords = 256;  // bitmap words (8192 nodes) per block
 
-// node_map / rows / count of the set in bits from the exclusive scan of the
-// word popcounts (woff): thread i alone writes node_map[i].
-__global__ __launch_bounds__(256) void bits_finish_kernel(const uint32_t* __restrict__ bits,
-                                                          const int32_t* __restrict__ woff, int64_t n,
-                                                          int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
-                                                          int32_t* __restrict__ count, uint64_t* __restrict__ rank,
-                                                          int32_t* __restrict__ count_host) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t w = bits[i >> 5];
-  const uint32_t b = static_cast<uint32_t>(i & 31);
-  const int32_t pos = woff[i >> 5] + __popc(w & ((1u << b) - 1u));
-  const bool in = ((w >> b) & 1u) != 0;
-  node_map[i] = in ? pos : -1;
-  if (in) rows[pos] = static_cast<int32_t>(i);
-  if (i == n - 1) {
-    *count = pos + (in ? 1 : 0);
-    if (count_host != nullptr) *count_host = pos + (in ? 1 : 0);  // pinned host mirror: no copy launch
+__device__ __forceinline__ uint64_t lb_granule(uint32_t tag, uint32_t status, int32_t v) {
+  return (static_cast<uint64_t>(tag) << 34) | (static_cast<uint64_t>(status) << 32) | static_cast<uint32_t>(v);
+}
+
+__global__ __launch_bounds__(256) void bits_list_kernel(const uint32_t* __restrict__ bits, int64_t n, int64_t words,
+                                                        int32_t* __restrict__ node_map, int32_t* __restrict__ rows,
+                                                        int32_t* __restrict__ count, int32_t* __restrict__ count_host,
+                                                        uint64_t* __restrict__ rank, uint32_t* __restrict__ state) {
+  __shared__ uint32_t s_w[kListWords];
+  __shared__ int32_t s_off[kListWords];
+  __shared__ int32_t s_wsum[4];
+  __shared__ int32_t s_blk, s_prefix;
+  __shared__ uint32_t s_tag;
+  uint64_t* granule = reinterpret_cast<uint64_t*>(state + 4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    s_blk = static_cast<int32_t>(__hip_atomic_fetch_add(&state[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    s_tag = (__hip_atomic_load(&state[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x3FFFFFFFu) + 1u;
   }
-  // the set's rank words (kgat_map_rank's layout): members before the word << 32 | its bits
-  if (rank != nullptr && b == 0) rank[i >> 5] = (static_cast<uint64_t>(static_cast<uint32_t>(woff[i >> 5])) << 32) | w;
+  __syncthreads();
+  const int blk = s_blk;
+  const uint32_t tag = s_tag;
+  const int64_t w = static_cast<int64_t>(blk) * kListWords + tid;
+  const uint32_t bw = w < words ? bits[w] : 0u;
+  const int c = __popc(bw);
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  s_w[tid] = bw;
+  __syncthreads();
+  int base = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < wave) base += s_wsum[k];
+    agg += s_wsum[k];
+  }
+  if (wave == 0) {
+    // look-back by the whole wave: lane i reads predecessor p_hi - i, 64 granules per round
+    int32_t prefix = 0;
+    if (lane == 0)
+      __hip_atomic_store(&granule[blk], lb_granule(tag, blk == 0 ? 2u : 1u, agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    for (int p_hi = blk - 1; p_hi >= 0; p_hi -= 64) {
+      const int p = p_hi - lane;
+      uint64_t g = p >= 0 ? __hip_atomic_load(&granule[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : lb_granule(tag, 2u, 0);
+      while (__any(static_cast<uint32_t>(g >> 34) != tag)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (static_cast<uint32_t>(g >> 34) != tag)
+          g = __hip_atomic_load(&granule[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint64_t incl_lanes = __ballot(((g >> 32) & 3u) == 2u);
+      const int lim = incl_lanes ? __ffsll(static_cast<long long>(incl_lanes)) - 1 : 63;
+      int32_t v = lane <= lim ? static_cast<int32_t>(static_cast<uint32_t>(g)) : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      prefix += v;
+      if (incl_lanes) break;
+    }
+    if (lane == 0) {
+      if (blk > 0)
+        __hip_atomic_store(&granule[blk], lb_granule(tag, 2u, prefix + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+      if (blk == static_cast<int>(gridDim.x) - 1) {
+        *count = prefix + agg;
+        if (count_host != nullptr) *count_host = prefix + agg;  // pinned host mirror: no copy launch
+      }
+    }
+  }
+  __syncthreads();
+  const int32_t off = s_prefix + base + incl - c;
+  s_off[tid] = off;
+  if (rank != nullptr && w < words) rank[w] = (static_cast<uint64_t>(static_cast<uint32_t>(off)) << 32) | bw;
+  __syncthreads();
+  const int64_t node0 = static_cast<int64_t>(blk) * kListWords * 32;
+  for (int q = tid; q < kListWords * 8; q += 256) {
+    const int64_t nd = node0 + 4LL * q;
+    if (nd >= n) break;
+    const int wl = q >> 3, sh = (q & 7) * 4;
+    const uint32_t wv = s_w[wl];
+    int32_t pos = s_off[wl] + __popc(wv & ((1u << sh) - 1u));
+    int32_t m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool in = ((wv >> (sh + j)) & 1u) != 0;
+      m[j] = in ? pos : -1;
+      if (in) rows[pos++] = static_cast<int32_t>(nd + j);
+    }
+    if (nd + 4 <= n) {
+      *reinterpret_cast<int4*>(node_map + nd) = make_int4(m[0], m[1], m[2], m[3]);
+    } else {
+      for (int j = 0; j < 4 && nd + j < n; ++j) node_map[nd + j] = m[j];
+    }
+  }
+  __syncthreads();
+  if (tid == 0 &&
+      __hip_atomic_fetch_add(&state[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    __hip_atomic_store(&state[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&state[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&state[2], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+static int launch_bits_list(const uint32_t* bits, int64_t n, int32_t* node_map, int32_t* rows, int32_t* count,
+                            int32_t* count_host, uint64_t* rank, void* work, hipStream_t st) {
+  const int64_t words = (n + 31) / 32;
+  const int64_t blocks = (words + kListWords - 1) / kListWords;
+  if (blocks > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(bits_list_kernel, dim3(blocks), dim3(256), 0, st, bits, n, words, node_map, rows, count,
+                     count_host, rank, static_cast<uint32_t*>(work));
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
 }
 
 __global__ __launch_bounds__(256) void clear2_kernel(uint32_t* __restrict__ a, uint32_t* __restrict__ b, int64_t words) {
@@ -603,47 +714,69 @@ extern "C" int kgat_map_bits(const int32_t* node_map, int64_t n, uint32_t* bits,
   return KGAT_OK;
 }
 
-// Scratch of kgat_frontier_hop: word offsets + the scan's temporary storage.
+// Scratch of kgat_frontier_hop / kgat_rows_union: bits_list_kernel's scan state (zero before the
+// first call, left reusable by every call).
 extern "C" int64_t kgat_frontier_hop_work_bytes(int64_t n) {
   if (n < 0 || n > INT32_MAX) return -1;
   const int64_t words = (n + 31) / 32;
-  size_t bytes = 0;
-  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(nullptr, kgat::Popc{});
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, static_cast<int32_t*>(nullptr),
-                                       static_cast<int>(words)) != hipSuccess)
-    return -1;
-  return 4 * (words + 64) + static_cast<int64_t>(bytes);
+  return 16 + 8 * ((words + kgat::kListWords - 1) / kgat::kListWords + 1);
+}
+
+extern "C" int kgat_frontier_hop_ex(const kgat_csr* A, const int32_t* rows0, int32_t n0, uint32_t* bits0,
+                                    uint32_t* bits1, int32_t* node_map, int32_t* hop_rows, int32_t* hop_count,
+                                    int32_t* hop_count_host, uint64_t* hop_rank, void* work, int64_t work_bytes,
+                                    int32_t flags, void* stream) {
+  if (!A || !rows0 || !bits0 || !bits1 || !node_map || !hop_rows || !hop_count || n0 < 0 || A->n_rows < 0 ||
+      (flags & ~KGAT_HOP_PRECLEARED))
+    return KGAT_ERR_INVALID;
+  const int64_t n = A->n_rows;
+  const int64_t need = kgat_frontier_hop_work_bytes(n);
+  if (need < 0 || !work || work_bytes < need || (reinterpret_cast<uintptr_t>(work) & 7)) return KGAT_ERR_WORKSPACE;
+  if (hop_rank != nullptr && (reinterpret_cast<uintptr_t>(hop_rank) & 7)) return KGAT_ERR_INVALID;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t words = (n + 31) / 32;
+  if (n == 0) return hipMemsetAsync(hop_count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
+  if (!(flags & KGAT_HOP_PRECLEARED)) {
+    hipLaunchKernelGGL(kgat::clear2_kernel, dim3((words + 255) / 256), dim3(256), 0, st, bits0, bits1, words);
+    KGAT_LAUNCH_CHECK();
+  }
+  if (n0 > 0) {
+    hipLaunchKernelGGL(kgat::frontier_mark_kernel, dim3(n0), dim3(256), 0, st, *A, rows0, bits0, bits1);
+    KGAT_LAUNCH_CHECK();
+  }
+  return kgat::launch_bits_list(bits1, n, node_map, hop_rows, hop_count, hop_count_host, hop_rank, work, st);
 }
 
 extern "C" int kgat_frontier_hop(const kgat_csr* A, const int32_t* rows0, int32_t n0, uint32_t* bits0,
                                  uint32_t* bits1, int32_t* node_map, int32_t* hop_rows, int32_t* hop_count,
                                  int32_t* hop_count_host, uint64_t* hop_rank, void* work, int64_t work_bytes,
                                  void* stream) {
-  if (!A || !rows0 || !bits0 || !bits1 || !node_map || !hop_rows || !hop_count || n0 < 0 || A->n_rows < 0)
+  return kgat_frontier_hop_ex(A, rows0, n0, bits0, bits1, node_map, hop_rows, hop_count, hop_count_host, hop_rank,
+                              work, work_bytes, 0, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_rows_ex_f32(const kgat_csr* A, const int32_t* src_map, const uint32_t* src_bits,
+                                                const float* Xc, int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                                const float* Gc, int64_t ldgc, const uint32_t* out_bits,
+                                                const int32_t* out_map, const int32_t* out_rows,
+                                                const int32_t* out_count, float* Y, int64_t ldy, int32_t* out_src,
+                                                int32_t d, float* workspace, int64_t workspace_floats, void* stream) {
+  using namespace kgat;
+  if (!A || !src_map || !Xc || !Y || !out_bits || !out_map || !out_rows || !out_count || A->n_rows < 0 || ldxc < d ||
+      ldy < d || (ldxc & 3) || (ldy & 3))
     return KGAT_ERR_INVALID;
-  const int64_t n = A->n_rows;
-  const int64_t need = kgat_frontier_hop_work_bytes(n);
-  if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t words = (n + 31) / 32;
-  if (n == 0) return hipMemsetAsync(hop_count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::clear2_kernel, dim3((words + 255) / 256), dim3(256), 0, st, bits0, bits1, words);
-  KGAT_LAUNCH_CHECK();
-  if (n0 > 0) {
-    hipLaunchKernelGGL(kgat::frontier_mark_kernel, dim3(n0), dim3(256), 0, st, *A, rows0, bits0, bits1);
-    KGAT_LAUNCH_CHECK();
-  }
-  int32_t* woff = static_cast<int32_t*>(work);
-  void* temp = static_cast<char*>(work) + 4 * (words + 64);
-  size_t bytes = static_cast<size_t>(need - 4 * (words + 64));
-  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(bits1, kgat::Popc{});
-  const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
-  if (e != hipSuccess) return static_cast<int>(e);
-  if (hop_rank != nullptr && (reinterpret_cast<uintptr_t>(hop_rank) & 7)) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits1, woff, n, node_map,
-                     hop_rows, hop_count, hop_rank, hop_count_host);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
+  if (misaligned(Xc) || misaligned(Y) || (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))) ||
+      (Gc && (misaligned(Gc) || ldgc < d || (ldgc & 3))))
+    return KGAT_ERR_INVALID;
+  if (A->n_rows == 0) return KGAT_OK;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits, nullptr,
+            out_bits, out_map, out_rows, out_count};
+  io.Gc = Gc;
+  io.ldgc = ldgc;
+  io.out_src = out_src;
+  return dispatch<kMaskedRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* src_map, const uint32_t* src_bits,
@@ -651,18 +784,8 @@ extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* s
                                              const uint32_t* out_bits, const int32_t* out_map, const int32_t* out_rows,
                                              const int32_t* out_count, float* Y, int64_t ldy, int32_t d,
                                              float* workspace, int64_t workspace_floats, void* stream) {
-  using namespace kgat;
-  if (!A || !src_map || !Xc || !Y || !out_bits || !out_map || !out_rows || !out_count || A->n_rows < 0 || ldxc < d ||
-      ldy < d || (ldxc & 3) || (ldy & 3))
-    return KGAT_ERR_INVALID;
-  if (misaligned(Xc) || misaligned(Y) || (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
-    return KGAT_ERR_INVALID;
-  if (A->n_rows == 0) return KGAT_OK;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
-    return KGAT_ERR_WORKSPACE;
-  const SpmmIo io{Xc, ldxc, Y, ldy, workspace, src_map, Yc_init, ldyc, nullptr, 0, src_bits, nullptr,
-                  out_bits, out_map, out_rows, out_count};
-  return dispatch<kMaskedRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
+  return kgat_spmm_csr_masked_rows_ex_f32(A, src_map, src_bits, Xc, ldxc, Yc_init, ldyc, nullptr, 0, out_bits, out_map,
+                                          out_rows, out_count, Y, ldy, nullptr, d, workspace, workspace_floats, stream);
 }
 
 extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t ldx, const uint32_t* out_bits,
@@ -717,7 +840,7 @@ extern "C" int kgat_rows_union(const int32_t* lists, const int32_t* counts, int3
   if (cap > 0 && !lists) return KGAT_ERR_INVALID;
   if (rank != nullptr && (reinterpret_cast<uintptr_t>(rank) & 7)) return KGAT_ERR_INVALID;
   const int64_t need = kgat_frontier_hop_work_bytes(n);
-  if (need < 0 || !work || work_bytes < need) return KGAT_ERR_WORKSPACE;
+  if (need < 0 || !work || work_bytes < need || (reinterpret_cast<uintptr_t>(work) & 7)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n == 0) return hipMemsetAsync(count, 0, 4, st) == hipSuccess ? KGAT_OK : KGAT_ERR_INVALID;
   const int64_t words = (n + 31) / 32;
@@ -728,16 +851,7 @@ extern "C" int kgat_rows_union(const int32_t* lists, const int32_t* counts, int3
                        total, n, bits);
     KGAT_LAUNCH_CHECK();
   }
-  int32_t* woff = static_cast<int32_t*>(work);
-  void* temp = static_cast<char*>(work) + 4 * (words + 64);
-  size_t bytes = static_cast<size_t>(need - 4 * (words + 64));
-  hipcub::TransformInputIterator<int32_t, kgat::Popc, const uint32_t*> it(bits, kgat::Popc{});
-  const hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, bytes, it, woff, static_cast<int>(words), st);
-  if (e != hipSuccess) return static_cast<int>(e);
-  hipLaunchKernelGGL(kgat::bits_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, bits, woff, n, node_map, rows,
-                     count, rank, nullptr);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
+  return kgat::launch_bits_list(bits, n, node_map, rows, count, nullptr, rank, work, st);
 }
 
 extern "C" int kgat_rows_merge_f32(const int32_t* lists, const int32_t* counts, int32_t G, int32_t cap,

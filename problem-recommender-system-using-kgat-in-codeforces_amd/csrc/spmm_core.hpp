@@ -49,6 +49,13 @@ struct SpmmIo {
   const int32_t* out_rows;   // k -> r, ascending
   const int32_t* out_count;  // device: the set's size
   SpmmAdam adam;             // kMaskedAdam only
+  // masked modes (not kMaskedAdam): compact rows added after the Yc term through the same src_map row --
+  // the BPR loss's direct gradient of the batch rows (kgat_bpr_bwd_multi_f32), folded into the product's
+  // store instead of a kgat_bpr_bwd_f32 launch after it (same bits: (Yc + sum) + g either way)
+  const float* Gc = nullptr;
+  int64_t ldgc = 0;
+  int32_t* out_src = nullptr;  // kMaskedRows (nullable): out_src[k] = src_map[out_rows[k]] -- which output rows
+                               // have a compact source row (the batch rows' BPR terms, kgat_biinter_bwd_hop_ex_f32)
 };
 
 __device__ __forceinline__ bool bit_of(const uint32_t* bits, int64_t i) {

@@ -255,7 +255,9 @@ class DeviceGraph:
                   torch.zeros(1, dtype=torch.int32, pin_memory=True),
                   torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
                   torch.zeros(2 * ((n + 63) // 64) + 2, dtype=torch.int32, device=self.device),
-                  torch.empty(max(int(_lib.lib().kgat_frontier_hop_work_bytes(n)), 1), dtype=torch.uint8,
+                  # the single-pass scan's state: zero before the first kgat_frontier_hop / kgat_rows_union,
+                  # left reusable by every call
+                  torch.zeros(max(int(_lib.lib().kgat_frontier_hop_work_bytes(n)), 8), dtype=torch.uint8,
                               device=self.device),
                   torch.zeros((n + 31) // 32 + 1, dtype=torch.int64, device=self.device))
             self._hop = hb

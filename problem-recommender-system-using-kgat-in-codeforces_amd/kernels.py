@@ -398,18 +398,27 @@ def hop_list(hit: torch.Tensor, node_map: torch.Tensor, rows: torch.Tensor, coun
               _host_ptr(count_host), work.data_ptr(), work.numel(), stream_ptr(hit.device))
 
 
-def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor, count_host: torch.Tensor | None = None):
+def hop_bitmaps(graph: DeviceGraph):
+    """(bits0, bits1, words): the two bitmaps kgat_frontier_hop marks (frontier, hop set) and their size in
+    uint32 words -- what kgat_cf_begin zeroes for a following frontier_hop(precleared=True)."""
+    hb = graph.hop_buffers()
+    return hb[7], hb[6], (graph.n_nodes + 31) // 32
+
+
+def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor, count_host: torch.Tensor | None = None,
+                 precleared: bool = False):
     """The first hop set of the backward chain from the batch frontier rows0 (frontier_build's
     rows, -1 padded): (hop rows int32 [N] ascending -- first count valid --, node_map, count int32 [1]
     on the device, hop-set bitmap, frontier bitmap).  No graph scan: the frontier rows' A edges are
-    marked (kgat_frontier_hop)."""
+    marked (kgat_frontier_hop_ex); ``precleared``: kgat_cf_begin zeroed the bitmaps already."""
     _req(rows0, "rows0", dtype=torch.int32, dim=1)
     hb = graph.hop_buffers()
     _, node_map, rows, count, _, _, bits1, bits0, work = hb[:9]
     desc = graph.A.descriptor()
-    _lib.call("kgat_frontier_hop", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
+    _lib.call("kgat_frontier_hop_ex", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
               bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), _host_ptr(count_host),
-              hb[9].data_ptr(), work.data_ptr(), work.numel(), stream_ptr(rows0.device))
+              hb[9].data_ptr(), work.data_ptr(), work.numel(), _lib.KGAT_HOP_PRECLEARED if precleared else 0,
+              stream_ptr(rows0.device))
     return rows, node_map, count, bits1, bits0
 
 
@@ -450,10 +459,13 @@ def rows_merge(lists: torch.Tensor, counts: torch.Tensor, cap: int, vals: torch.
 
 
 def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_rows, out_map, out_count, out_bits,
-                     transpose: bool = True) -> torch.Tensor:
+                     transpose: bool = True, Gc: torch.Tensor | None = None,
+                     out_src: torch.Tensor | None = None) -> torch.Tensor:
     """The masked product (see spmm_masked) on the output rows of a hop set only, written compactly:
-    Y[k] = row out_rows[k] for k < out_count (kgat_spmm_csr_masked_rows_f32); returns Y [N, d]
-    (capacity; the first count rows are valid)."""
+    Y[k] = row out_rows[k] for k < out_count (kgat_spmm_csr_masked_rows_ex_f32); returns Y [N, d]
+    (capacity; the first count rows are valid).  ``Gc``: compact rows (src_map's numbering) added after
+    the Yc_init term -- the BPR loss's batch-row gradient of this table (bpr_bwd_multi).  ``out_src`` (int32
+    [N]): gets src_map[out_rows[k]] for the valid k (biinter_bwd_hop's gidx)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     d = Xc.shape[1]
@@ -475,10 +487,20 @@ def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_row
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("kgat_spmm_csr_masked_rows_f32", ctypes.byref(desc), src_map.data_ptr(), _bits_ptr(src_bits, src_map),
-              Xc.data_ptr(), _ld(Xc), Yc_init.data_ptr() if Yc_init is not None else None,
-              _ld(Yc_init) if Yc_init is not None else 0, out_bits.data_ptr(), out_map.data_ptr(),
-              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(),
+    if Gc is not None:
+        _req(Gc, "Gc", dim=2)
+        if Gc.shape[1] != d:
+            raise ValueError("Gc width mismatch")
+    if out_src is not None:
+        _req(out_src, "out_src", dtype=torch.int32, dim=1)
+        if out_src.numel() < n:
+            raise ValueError("out_src must cover every node")
+    _lib.call("kgat_spmm_csr_masked_rows_ex_f32", ctypes.byref(desc), src_map.data_ptr(),
+              _bits_ptr(src_bits, src_map), Xc.data_ptr(), _ld(Xc), Yc_init.data_ptr() if Yc_init is not None else None,
+              _ld(Yc_init) if Yc_init is not None else 0, Gc.data_ptr() if Gc is not None else None,
+              _ld(Gc) if Gc is not None else 0, out_bits.data_ptr(), out_map.data_ptr(),
+              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out),
+              out_src.data_ptr() if out_src is not None else None, d, ws.data_ptr(), ws.numel(),
               stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
@@ -612,13 +634,17 @@ def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: to
 
 
 def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int,
-                    dh_compact: bool = False, out=None):
+                    dh_compact: bool = False, out=None, G: torch.Tensor | None = None,
+                    gidx: torch.Tensor | None = None, gmap: torch.Tensor | None = None):
     """Saved-state bi-interaction backward on a hop set whose size is only known on the device:
     rows / count from hop_compact or frontier_hop, dH indexed by node ([N, d_out], the previous
     masked product's output) or, with ``dh_compact``, by hop position (spmm_masked_rows' output).
     Returns compact (dXd, dS) with ``out_rows`` rows allocated (the first count are valid) and
     (dW1, db1, dW2, db2).  ``out`` = (dXd, dS): caller-owned [>= out_rows, d_in] views to write
-    (e.g. the two halves of one [cap, 2*d_in] exchange buffer)."""
+    (e.g. the two halves of one [cap, 2*d_in] exchange buffer).  ``G`` / ``gidx``: the BPR loss's
+    batch-row gradient of this table (compact, bpr_bwd_multi) and, per hop position, its G row or -1
+    (spmm_masked_rows' out_src) -- added to dXd in the same launch; ``gmap`` (optional): the batch-row
+    node map numbering G, its entries of those rows reset to -1 (kgat_biinter_bwd_hop_ex_f32)."""
     src_rows, din = X.shape
     dout = W1.shape[0]
     for t, nm in ((X, "X"), (S, "S"), (dH, "dH"), (H, "H")):
@@ -645,11 +671,24 @@ def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: B
     db2 = torch.empty(dout, dtype=torch.float32, device=dev)
     ws_n = int(_lib.lib().kgat_biinter_bwd_workspace(out_rows, din, dout))
     ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=dev)
-    _lib.call("kgat_biinter_bwd_hop_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
+    if (G is None) != (gidx is None):
+        raise ValueError("G and gidx go together")
+    if G is not None:
+        _req(G, "G", dim=2)
+        _req(gidx, "gidx", dtype=torch.int32, dim=1)
+        if G.shape[1] != din or gidx.numel() < out_rows:
+            raise ValueError("G / gidx shape mismatch")
+    if gmap is not None:
+        _req(gmap, "gmap", dtype=torch.int32, dim=1)
+        if gmap.numel() < src_rows:
+            raise ValueError("gmap must cover every node")
+    _lib.call("kgat_biinter_bwd_hop_ex_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), H.data_ptr(), _ld(H),
               state.norm.data_ptr(), state.mask.data_ptr(), dH.data_ptr(), _ld(dH), W1.data_ptr(), W2.data_ptr(),
               dXd.data_ptr(), _ld(dXd), dS.data_ptr(), _ld(dS), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(),
               db2.data_ptr(), rows.data_ptr(), count.data_ptr(), out_rows, src_rows, int(dh_compact), din, dout,
-              float(dropout_p), ws.data_ptr(), ws.numel(), stream_ptr(dev))
+              float(dropout_p), G.data_ptr() if G is not None else None, _ld(G) if G is not None else 0,
+              gidx.data_ptr() if gidx is not None else None, gmap.data_ptr() if gmap is not None else None,
+              ws.data_ptr(), ws.numel(), stream_ptr(dev))
     return dXd, dS, dW1, db1, dW2, db2
 
 
@@ -970,8 +1009,25 @@ def make_tables(tables: list[torch.Tensor]) -> _lib.Tables:
     return T
 
 
+_TICKETS: dict = {}
+
+
+def ticket_word(device: torch.device, slot: int) -> torch.Tensor:
+    """A device uint32 word that is 0 between launches (the in-launch reductions' arrival counters,
+    e.g. kgat_bpr_fwd_ex_f32's): per device, one slot per kernel kind; launches sharing one are
+    stream-ordered (every caller in this package issues them on the device's current stream)."""
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    buf = _TICKETS.get(key)
+    if buf is None:
+        buf = _TICKETS[key] = torch.zeros(64, dtype=torch.int32, device=device)
+    return buf[slot:slot + 1]
+
+
+TICKET_BPR_FWD = 0
+
+
 def bpr_fwd(tables: list[torch.Tensor], users, pos, neg, reg: float):
-    """(loss [1], coef [B])."""
+    """(loss [1], coef [B]); one launch (kgat_bpr_fwd_ex_f32: the loss summed by the last block)."""
     for t, nm in ((users, "users"), (pos, "pos"), (neg, "neg")):
         _req(t, nm, dtype=torch.int64, dim=1)
     B = users.numel()
@@ -981,9 +1037,57 @@ def bpr_fwd(tables: list[torch.Tensor], users, pos, neg, reg: float):
     loss = torch.empty(1, dtype=torch.float32, device=dev)
     coef = torch.empty(2 * B, dtype=torch.float32, device=dev)  # [coef | per-sample terms]
     T = make_tables(tables)
-    _lib.call("kgat_bpr_fwd_f32", ctypes.byref(T), users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg),
-              loss.data_ptr(), coef.data_ptr(), stream_ptr(dev))
+    _lib.call("kgat_bpr_fwd_ex_f32", ctypes.byref(T), users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, float(reg),
+              loss.data_ptr(), coef.data_ptr(), ticket_word(dev, TICKET_BPR_FWD).data_ptr(), stream_ptr(dev))
     return loss, coef
+
+
+def bpr_bwd_multi(tables: list[torch.Tensor], t0: int, users, pos, neg, reg: float, coef, grad_out,
+                  dsts: list, rows: torch.Tensor, count: torch.Tensor) -> None:
+    """kgat_bpr_bwd_multi_f32: for t >= t0 with dsts[t] given, dsts[t][p] = dL/d tables[t][rows[p]] for the
+    frontier rows p < count (frontier_build's list; written, rows [count, 3B) zeroed) -- every layer's
+    batch-row term in one launch."""
+    _req(grad_out, "grad_out")
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    _req(count, "count", dtype=torch.int32, dim=1)
+    T = make_tables(tables)
+    D = _lib.Tables()
+    B = users.numel()
+    for i, t in enumerate(tables):
+        d = dsts[i] if i < len(dsts) else None
+        if i >= t0 and d is not None:
+            _req(d, f"dst{i}", dim=2)
+            if d.shape[1] != t.shape[1] or d.shape[0] < 3 * B:
+                raise ValueError(f"bpr_bwd_multi: dst{i} must be [>= 3B, {t.shape[1]}]")
+            D.ptr[i], D.ld[i], D.width[i] = d.data_ptr(), _ld(d), t.shape[1]
+    D.count = T.count
+    _lib.call("kgat_bpr_bwd_multi_f32", ctypes.byref(T), int(t0), users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B,
+              float(reg), coef.data_ptr(), grad_out.data_ptr(), ctypes.byref(D), rows.data_ptr(), count.data_ptr(),
+              stream_ptr(users.device))
+
+
+def cf_begin(users, pos, neg, bound: int, bad_host: torch.Tensor, bad_dev: torch.Tensor | None,
+             node_map: torch.Tensor, clear: tuple | None = None):
+    """kgat_cf_begin: (checked int64 ids [3B] = users | pos | neg, frontier rows int32 [3B], count int32 [1]).
+    ``clear`` = (bits0, bits1, words): kgat_frontier_hop's bitmaps, zeroed by the same launch."""
+    for t, nm in ((users, "users"), (pos, "pos"), (neg, "neg")):
+        _req(t, nm, dtype=torch.int64, dim=1)
+    B = users.numel()
+    if pos.numel() != B or neg.numel() != B or B == 0 or 3 * B > 4096:
+        raise ValueError("cf_begin: three id arrays of one batch size, 3B <= 4096")
+    dev = users.device
+    ids = torch.empty(3 * B, dtype=torch.int64, device=dev)
+    rows = torch.empty(3 * B, dtype=torch.int32, device=dev)
+    count = torch.empty(1, dtype=torch.int32, device=dev)
+    c0 = c1 = None
+    words = 0
+    if clear is not None:
+        b0, b1, words = clear
+        c0, c1 = b0.data_ptr(), b1.data_ptr()
+    _lib.call("kgat_cf_begin", users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, int(bound), ids.data_ptr(),
+              bad_host.data_ptr(), bad_dev.data_ptr() if bad_dev is not None else None, node_map.data_ptr(),
+              rows.data_ptr(), count.data_ptr(), c0, c1, int(words), stream_ptr(dev))
+    return ids, rows, count
 
 
 def bpr_bwd(tables: list[torch.Tensor], t: int, users, pos, neg, reg: float, coef, grad_out, dst,

@@ -198,6 +198,30 @@ class _IdGuard:
         self._pending = what
         return outs
 
+    def check_cf(self, what: str, ids, bound: int, device, node_map: torch.Tensor, clear=None):
+        """TRAIN_CF's ids checked (the rules of ``check``) and numbered as the batch frontier in one launch
+        (kgat_cf_begin: kgat_ids_check_ex + kgat_frontier_build, and the hop bitmaps zeroed when ``clear``
+        = kernels.hop_bitmaps(graph)).  Returns ((users, pos, neg), rows, count) or None when the ids do not
+        take this path (sizes differ, 3B > 4096, an id array is empty)."""
+        ts = [torch.as_tensor(t) for t in ids]
+        B = ts[0].numel()
+        if B == 0 or 3 * B > 4096 or any(t.numel() != B for t in ts):
+            return None
+        self.raise_pending()
+        if all(t.device.type == "cpu" for t in ts):
+            for t in ts:
+                if int(t.min()) < 0 or int(t.max()) >= bound:
+                    raise IndexError(f"{what}: id out of range [0, {bound}) (min {int(t.min())}, max {int(t.max())})")
+        if self._host is None:
+            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._event = torch.cuda.Event()
+            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+        src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
+        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear)
+        self._event.record()
+        self._pending = what
+        return tuple(out.split(B)), rows, count
+
     def check_multi(self, what: str, ts, bounds, out: torch.Tensor, device) -> None:
         """The captured KG step's check: ``ts`` (<= KGAT_IDS_MAX int64 contiguous 1-D device tensors) checked
         against their own bounds (a ctypes int64 array) and copied, concatenated, into the preallocated ``out``
@@ -685,9 +709,15 @@ class _MarkedBatch:
     """The batch rows a forward marked in ``graph.node_map`` (and, with 2 layers, the first hop it left
     in the graph's hop buffers) for its own backward -- at most one outstanding per graph."""
 
-    def __init__(self, rows: torch.Tensor):
+    def __init__(self, rows: torch.Tensor, count: torch.Tensor | None = None, cleared: bool = False):
         self.rows = rows
+        self.count = count
         self.stale = False
+        self.cleared = cleared  # kgat_cf_begin zeroed the hop bitmaps, and no kgat_frontier_hop has run since
+
+    def take_cleared(self) -> bool:
+        c, self.cleared = self.cleared, False
+        return c
 
 
 def _release_marks(graph) -> None:
@@ -696,19 +726,23 @@ def _release_marks(graph) -> None:
     tok = getattr(graph, "_marked", None)
     if tok is not None:
         tok.stale = True
+        tok.cleared = False  # the next step's kgat_cf_begin / kgat_frontier_hop own the bitmaps now
         kernels.frontier_reset(tok.rows, graph.node_map)
         graph._marked = None
 
 
-def _mark_batch(graph, users, pos, neg):
-    """frontier_build for a forward that hands its marks to its backward: (rows, count, token)."""
+def _mark_batch(graph, users, pos, neg, marks=None):
+    """frontier_build for a forward that hands its marks to its backward: (rows, count, token); ``marks``:
+    the (rows, count, token) kgat_cf_begin already made for this step."""
+    if marks is not None:
+        return marks
     _release_marks(graph)
     rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
-    graph._marked = tok = _MarkedBatch(rows)
+    graph._marked = tok = _MarkedBatch(rows, fcount)
     return rows, fcount, tok
 
 
-def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
+def _early_first_hop(graph, users, pos, neg, ws, L: int, hook, marks=None):
     """Data-parallel replicas exchanging the layer-0 hop-set terms (replicas.ShardedGradSync,
     replicated) with 2 layers: the layer-0 hop set is the first hop F + N(F) of the batch rows F,
     fixed by the batch and the graph alone.  It is marked here, before the propagation, and its
@@ -720,8 +754,8 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook):
     W1 = ws[0]
     if not kernels.saved_state_supported(W1.shape[1], W1.shape[0]) or not _hop_small(graph, 0, graph.n_nodes):
         return None
-    rows, fcount, tok = _mark_batch(graph, users, pos, neg)
-    hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0))
+    rows, fcount, tok = _mark_batch(graph, users, pos, neg, marks)
+    hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0), precleared=tok.take_cleared())
     _hop_record(graph, 0)
     hook.announce(True, hop[2])
     return rows, hop, fcount, tok
@@ -734,7 +768,7 @@ def _tile_forward_ok(din: int, dout: int) -> bool:
         kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
 
 
-def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
+def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks=None):
     """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1, 2 or 3, the
     restricted layers with the fused kernels' saved state).  The BPR loss reads the batch rows F of
     every table (model.py:189-191), so the last layer's output is needed on F only, and layer L-2's
@@ -759,8 +793,9 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early):
         return None
     n = graph.n_nodes
     if early is None:
-        rows, fcount, tok = _mark_batch(graph, users, pos, neg)
-        hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, L - 2) if L >= 2 else None)
+        rows, fcount, tok = _mark_batch(graph, users, pos, neg, marks)
+        hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, L - 2) if L >= 2 else None,
+                                   precleared=tok.take_cleared())
         if L >= 2:
             _hop_record(graph, L - 2)
         early = (rows, hop, fcount, tok)
@@ -822,9 +857,10 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, hook, _tu, frontier = cfg
-        ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook)
-        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early) if frontier else None
+        graph, drops, seeds, reg, hook, _tu, frontier, marks = cfg
+        ctx.marks = marks
+        ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook, marks)
+        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, marks) if frontier else None
         if fw is not None:
             tables, sides, states, ctx.early = fw
         else:
@@ -846,7 +882,7 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        graph, drops, seeds, reg, hook, tu, _frontier = ctx.cfg
+        graph, drops, seeds, reg, hook, tu, _frontier, _marks = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -856,41 +892,68 @@ class _CFLoss(torch.autograd.Function):
         hit = graph.hop_buffers()[0] if L > 1 else None
         # ---- last layer on the batch frontier
         early, ctx.early = ctx.early, None
-        if early is not None:
-            if early[3].stale:
+        marks, ctx.marks = ctx.marks, None
+        tok = early[3] if early is not None else (marks[2] if marks is not None else None)
+        if tok is not None and tok.stale and early is None:
+            tok = None  # a later forward released this step's marks (two losses, one backward): number them again
+        if tok is not None:
+            if tok.stale:
                 raise RuntimeError("TRAIN_CF backward: a later TRAIN_CF forward on this graph reused the batch-row "
-                                   "marks and hop buffers this step's forward left for it (frontier_forward / the "
-                                   "replicated DP exchange need each forward's backward before the next forward)")
+                                   "marks and hop buffers this step's forward left for it (each TRAIN_CF forward "
+                                   "needs its backward before the next forward)")
             graph._marked = None  # consumed: this backward resets the marks itself
-            rows = early[0]
+            rows, fcount = (early[0], early[2]) if early is not None else (marks[0], marks[1])
         else:
             _release_marks(graph)  # a dropped forward's marks would collide with this batch's
-            rows = kernels.frontier_build(users, pos, neg, graph.node_map)[0]
+            rows, fcount = kernels.frontier_build(users, pos, neg, graph.node_map)
+            tok = _MarkedBatch(rows, fcount)
         if early is not None and early[1] is None:
             early = None  # 1-layer frontier forward: the batch rows only
-        dHc = kernels.zeros((rows.numel(), tables[L].shape[1]), users.device)
-        kernels.bpr_bwd(tables, L, users, pos, neg, reg, ctx.coef, gout, dHc, row_map=graph.node_map)
+        # a rank that announced its layer-0 hop set to the replicas (forward) is committed to the hop path
+        sparse = early is not None or (hit is not None and HOP_DENSE_FRACTION > 0)
+        nxt = L - 2
+        first_hop = early is not None or (sparse and states[nxt] is not None and states[nxt].kind == "fused"
+                                          and _hop_small(graph, nxt, n_nodes))
+        # The BPR loss's direct gradients of the batch rows (model.py:189-191 gathers every layer's table) in
+        # one launch (kgat_bpr_bwd_multi_f32), each folded into the kernel that produces that table's
+        # gradient rows: the last layer's is dH itself, layer L-1's is added by the first-hop A^T product
+        # (Gc), layer L-2's by its hop-set bi-interaction backward (G), which also resets the batch-row map
+        # -- instead of a zero fill, three kgat_bpr_bwd_f32 launches and a kgat_frontier_reset (same bits)
+        B = users.numel()
+        fold2 = first_hop and L >= 2 and states[nxt] is not None and states[nxt].kind == "fused"
+        dsts: list = [None] * (L + 1)
+        dsts[L] = dHc = torch.empty(rows.numel(), tables[L].shape[1], dtype=torch.float32, device=users.device)
+        if first_hop:
+            dsts[L - 1] = torch.empty(3 * B, tables[L - 1].shape[1], dtype=torch.float32, device=users.device)
+        if fold2:
+            dsts[nxt] = torch.empty(3 * B, tables[nxt].shape[1], dtype=torch.float32, device=users.device)
+        t0 = min(k for k, d in enumerate(dsts) if d is not None)
+        kernels.bpr_bwd_multi(tables, t0, users, pos, neg, reg, ctx.coef, gout, dsts, rows, fcount)
         l = L - 1
         dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dHc, *ws[4 * l: 4 * l + 4],
                                                             drops[l], seeds[l], rows=rows, **_saved(tables, states, l))
         bits = graph.hop_buffers()[6]
         rank = graph.hop_buffers()[9]  # rank words of the current hop set (frontier_hop / hop_compact)
-        # a rank that announced its layer-0 hop set to the replicas (forward) is committed to the hop path
-        sparse = early is not None or (hit is not None and HOP_DENSE_FRACTION > 0)
         pending = None
-        nxt = L - 2
-        if early is not None or (sparse and states[nxt] is not None and states[nxt].kind == "fused"
-                                 and _hop_small(graph, nxt, n_nodes)):
+        if first_hop:
             # first hop marked from the frontier rows' A edges (no graph scan); the A^T product is
-            # computed on those rows only, compactly (kgat_spmm_csr_masked_rows_f32)
+            # computed on those rows only, compactly (kgat_spmm_csr_masked_rows_ex_f32)
             if early is not None:
                 hrows, hmap, hcount, bits, fbits = early[1]
             else:
-                hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, nxt))
+                hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, nxt),
+                                                                        precleared=tok.take_cleared())
                 _hop_record(graph, nxt)
-            dX = kernels.spmm_masked_rows(graph, graph.node_map, fbits, dSc, dXdc, hrows, hmap, hcount, bits)
-            kernels.frontier_reset(rows, graph.node_map)
-            kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dX, row_map=hmap)
+            # hop position -> frontier position of the batch rows (the G rows layer L-2's backward adds)
+            gidx = None
+            if fold2:
+                gidx = getattr(graph, "_hop_src", None)
+                if gidx is None or gidx.numel() != n_nodes:
+                    gidx = graph._hop_src = torch.empty(n_nodes, dtype=torch.int32, device=users.device)
+            dX = kernels.spmm_masked_rows(graph, graph.node_map, fbits, dSc, dXdc, hrows, hmap, hcount, bits,
+                                          Gc=dsts[L - 1], out_src=gidx)
+            if not fold2:
+                kernels.frontier_reset(rows, graph.node_map)
             pending = (hrows, hmap, hcount)
         else:
             kernels.map_bits(graph.node_map, bits)
@@ -942,9 +1005,11 @@ class _CFLoss(torch.autograd.Function):
                         din = W1.shape[1]
                         packed = torch.empty(cap, 2 * din, dtype=torch.float32, device=dX.device)
                         out_rows, out = cap, (packed[:, din:], packed[:, :din])
+                    gfold = fold2 and l == nxt
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd_hop(
                         tables[l], sides[l], dX, W1, W2, drops[l], hrows, hcount, tables[l + 1], states[l], out_rows,
-                        dh_compact=compact_dh, out=out)
+                        dh_compact=compact_dh, out=out, G=dsts[l] if gfold else None,
+                        gidx=gidx if gfold else None, gmap=graph.node_map if gfold else None)
                 elif compact_dh:
                     # wide kinds after the first-hop product: dX holds the hop rows compactly
                     hr = hrows[:n_hop]
@@ -957,7 +1022,8 @@ class _CFLoss(torch.autograd.Function):
                     dXdc, dSc, dW1, db1, dW2, db2 = kernels.biinter_bwd(tables[l], sides[l], dX, W1, b1, W2, b2,
                                                                         drops[l], seeds[l], rows=hrows,
                                                                         dh_full=True, **_saved(tables, states, l))
-                kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
+                if not (fold2 and l == nxt):
+                    kernels.bpr_bwd(tables, l, users, pos, neg, reg, ctx.coef, gout, dXdc, row_map=hmap)
                 if l == 0 and hook is not None and hook.replicated:
                     # data-parallel replicas exchange the compact hop-set terms and each computes the
                     # mean table gradient A^T . mean(dS) + mean(dXd) itself (replicas.ShardedGradSync)
@@ -1232,14 +1298,27 @@ class KGAT(nn.Module):
     # ------------------------------------------------------------------ modes
     def _calc_cf_loss(self, user_ids, positive_item_ids, negative_item_ids) -> torch.Tensor:
         g = self.graph()
-        ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes, g.device)
         drops, seeds = self._dropouts()
         # the data-parallel hook only where a backward follows (a no_grad loss evaluation has none: it must
         # not open the replicas' exchange of a step)
         hook = getattr(self, "_table_grad_hook", None) if torch.is_grad_enabled() else None
         # the frontier forward only where a backward follows: its batch-row map is released by the backward
         frontier = self.frontier_forward and torch.is_grad_enabled()
-        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier)
+        marks = None
+        if torch.is_grad_enabled():
+            # ids checked and numbered as the batch frontier, and the hop bitmaps zeroed, in one launch
+            # (kgat_cf_begin); the marks go to this step's backward (and frontier forward / DP hop exchange)
+            _release_marks(g)
+            r = self._ids.check_cf("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
+                                   g.device, g.node_map, kernels.hop_bitmaps(g))
+            if r is not None:
+                ids, rows, fcount = r
+                g._marked = tok = _MarkedBatch(rows, fcount, cleared=True)
+                marks = (rows, fcount, tok)
+        if marks is None:
+            ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
+                                  g.device)
+        cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier, marks)
         return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round 5 iteration on one GPU: the GPU suite, a short C2 bench line (no CPU baseline / parity / KG legs),
+# and a rocprof kernel trace of the same run with one full and one frontier step's timelines.
+# usage: tools/gpu_r05_iter.sh TAG [tests] [bench] [prof]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=$1
+shift
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+        > gpurun_out/${TAG}_tests.log 2>&1 || { grep -E "^E |FAILED|Error" gpurun_out/${TAG}_tests.log | head -30; tail -3 gpurun_out/${TAG}_tests.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+      tail -2 gpurun_out/${TAG}_smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity --no-kg-leg \
+        > gpurun_out/${TAG}_c2_bench.log 2>&1 || { tail -30 gpurun_out/${TAG}_c2_bench.log; exit 1; }
+      python3 - gpurun_out/${TAG}_c2_bench.log <<'EOF'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+fr = d.get("frontier_forward", {})
+print("full ms", round(d["ms_per_step"], 4), "frontier ms", round(fr.get("ms_per_step", 0), 4),
+      "bit_identical", fr.get("bit_identical_to_full", {}).get("pass"), "roofline", round(d["roofline"]["frac"], 3))
+EOF
+      ;;
+    prof)
+      rm -rf gpurun_out/${TAG}_prof
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
+        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-parity --no-kg-leg \
+        > gpurun_out/${TAG}_prof.log 2>&1 || { tail -20 gpurun_out/${TAG}_prof.log; exit 1; }
+      T=$(find gpurun_out/${TAG}_prof -name "*kernel_trace.csv" | head -1)
+      python3 tools/step_timeline.py "$T" bpr_fwd_kernel 5 > gpurun_out/${TAG}_full_step.txt
+      python3 tools/step_timeline.py "$T" bpr_fwd_kernel -6 > gpurun_out/${TAG}_frontier_step.txt
+      tail -1 gpurun_out/${TAG}_full_step.txt
+      tail -1 gpurun_out/${TAG}_frontier_step.txt ;;
+    hostprof)
+      timeout -k 10 300 python3 tools/host_profile.py > gpurun_out/${TAG}_host.txt 2>&1 || { tail -20 gpurun_out/${TAG}_host.txt; exit 1; }
+      timeout -k 10 300 python3 tools/host_profile.py --full > gpurun_out/${TAG}_host_full.txt 2>&1 || { tail -20 gpurun_out/${TAG}_host_full.txt; exit 1; }
+      grep "ms/step" gpurun_out/${TAG}_host.txt gpurun_out/${TAG}_host_full.txt ;;
+  esac
+done
+echo done
