@@ -250,32 +250,6 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   return KGAT_OK;
 }
 
-// Only the long rows: segment partials + fix-up, writing Y's long rows (the
-// fused propagation + bi-interaction forward reads them back).
-template <int D>
-static int launch_long(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
-  if (A.n_long == 0) return KGAT_OK;
-  const int seg_blocks = (A.n_seg + 3) / 4;
-  hipLaunchKernelGGL((spmm_main_kernel<D, kOverwrite>), dim3(seg_blocks), dim3(256), 0, st, A, io, seg_blocks);
-  KGAT_LAUNCH_CHECK();
-  hipLaunchKernelGGL((spmm_fixup_kernel<D, kOverwrite>), dim3(A.n_long), dim3(256), 0, st, A, io);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
-int spmm_long_rows(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) {
-  switch (d) {
-    case 16: return launch_long<16>(A, io, st);
-    case 32: return launch_long<32>(A, io, st);
-    case 64: return launch_long<64>(A, io, st);
-    case 128: return launch_long<128>(A, io, st);
-    case 256: return launch_long<256>(A, io, st);
-    default: return KGAT_ERR_UNSUPPORTED_DIM;
-  }
-}
-
-
-
 template <int MODE>
 static int dispatch(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st) {
   switch (d) {

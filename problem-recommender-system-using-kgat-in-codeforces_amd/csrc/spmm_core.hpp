@@ -216,7 +216,4 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
   }
 }
 
-// Long rows only (segments + fix-up) of Y = A . X, kOverwrite; defined in spmm.hip.
-int spmm_long_rows(const kgat_csr& A, const SpmmIo& io, int d, hipStream_t st);
-
 }  // namespace kgat

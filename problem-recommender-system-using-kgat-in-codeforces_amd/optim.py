@@ -22,6 +22,7 @@ class FusedAdam:
         self.beta1, self.beta2 = float(betas[0]), float(betas[1])
         self.eps = float(eps)
         self.state: dict[int, dict] = {}
+        self._side: dict = {}  # device -> side stream of step()
 
     def _advance(self, key, like: torch.Tensor) -> tuple[dict, float, float]:
         """Count one more step for state ``key`` (created zeroed like ``like``): (state, step_size, bc2_sqrt)."""
@@ -51,6 +52,7 @@ class FusedAdam:
         ``skip``: a device int32 flag (the model's device-side id check); when it is set as the
         kernels run, no parameter or moment moves (the step counters still advance)."""
         items = []
+        runs = []
         for p in self.params:
             launch = fused.get(id(p)) if fused else None
             if launch is not None:
@@ -60,7 +62,7 @@ class FusedAdam:
                     raise RuntimeError("FusedAdam: a parameter stepped by a fused launch also has a .grad "
                                        "(materialise the deferred gradient into it first)")
                 st, step_size, bc2s = self._advance(id(p), p.data)
-                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
+                runs.append((launch, st, step_size, bc2s))
                 continue
             g = p.grad
             if g is None:
@@ -74,7 +76,25 @@ class FusedAdam:
             for key, pv, gv in views:
                 st, step_size, bc2s = self._advance(key, pv)
                 items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
-        if items:
+        ready = None
+        if items and runs and items[0][0].is_cuda:
+            ready = torch.cuda.Event()
+            ready.record()  # every gradient of this step is in place (current stream)
+        for launch, st, step_size, bc2s in runs:
+            launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
+        if ready is not None:
+            # the small tensors' Adam (one short launch) runs on a side stream beside the fused launch(es),
+            # which hold every CU for hundreds of microseconds (issued first, so the host work of the fork
+            # overlaps them); the current stream waits for it at the end
+            dev = items[0][0].device
+            side = self._side.get(dev)
+            if side is None:
+                side = self._side[dev] = torch.cuda.Stream(device=dev)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
+            torch.cuda.current_stream(dev).wait_stream(side)
+        elif items:
             kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
