@@ -138,26 +138,6 @@ int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr *A, const int32_t *src_ma
                                         float eps, const int32_t *skip, float *workspace, int64_t workspace_floats,
                                         void *stream);
 
-/* The table update with reach marks: reach (uint8 [n_rows]) holds a superset of the rows whose gradient
- * (the masked product's row, plus its Yc_init row) can be nonzero -- kgat_spmm_csr_mark_f32 /
- * kgat_spmm_csr_rows_mark_f32 set it in the forward.  A short row with reach[r] == 0 takes its Adam step
- * with g = +0 (the bits the scan would give) without reading its edges, rank words or map entry; the
- * marks of the rows scanned are reset to 0 (a stale mark only costs a scan).  Otherwise as
- * kgat_spmm_csr_masked_adam_ex_f32. */
-int kgat_spmm_csr_masked_adam_reach_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
-                                        const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
-                                        float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
-                                        float beta2, float bc2_sqrt, float eps, const int32_t *skip, uint8_t *reach,
-                                        float *workspace, int64_t workspace_floats, void *stream);
-
-/* kgat_spmm_csr_f32 (overwrite) that also marks, for every row r in mark_rows (uint32 bitmap), reach[c] = 1
- * for each column c it gathers from and reach[r] = 1: with mark_rows = the layer-0 hop set of the
- * backward (kgat_frontier_hop's bits1), the rows of A^T whose table gradient can be nonzero
- * (A^T[c, r] != 0 <=> A[r, c] != 0) -- kgat_spmm_csr_masked_adam_reach_f32's reach. */
-int kgat_spmm_csr_mark_f32(const kgat_csr *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int32_t d,
-                           const uint32_t *mark_rows, uint8_t *reach, float *workspace, int64_t workspace_floats,
-                           void *stream);
-
 /* bits (uint32 [2 * ceil(n / 64)], 8-byte aligned): bit i set <=> node_map[i] >= 0. */
 int kgat_map_bits(const int32_t *node_map, int64_t n, uint32_t *bits, void *stream);
 
@@ -239,10 +219,6 @@ int kgat_csr_mark_rows(const kgat_csr *A, const uint32_t *bits, int64_t n_bits, 
 int kgat_spmm_csr_rows_f32(const kgat_csr *A, const float *X, int64_t ldx, const uint32_t *out_bits,
                            const int32_t *out_rows, const int32_t *out_count, float *Y, int64_t ldy, int32_t d,
                            float *workspace, int64_t workspace_floats, void *stream);
-/* ... marking reach (nullable, uint8 [n_rows]) as kgat_spmm_csr_mark_f32 does, for every row of the set. */
-int kgat_spmm_csr_rows_mark_f32(const kgat_csr *A, const float *X, int64_t ldx, const uint32_t *out_bits,
-                                const int32_t *out_rows, const int32_t *out_count, float *Y, int64_t ldy, int32_t d,
-                                uint8_t *reach, float *workspace, int64_t workspace_floats, void *stream);
 
 /* Data-parallel exchange of the compact table gradient (replicas.ShardedGradSync,
  * replicate_table mode; no reference counterpart -- the reference is one

@@ -115,13 +115,6 @@ _SIGNATURES = {
     "kgat_spmm_csr_masked_rows_ex_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                                         c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                                                         c_vp, c_i64, c_vp]),
-    "kgat_spmm_csr_rows_mark_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
-                                                   c_i32, c_vp, c_vp, c_i64, c_vp]),
-    "kgat_spmm_csr_mark_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp,
-                                              c_i64, c_vp]),
-    "kgat_spmm_csr_masked_adam_reach_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
-                                                           c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
-                                                           c_f32, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_spmm_csr_rows_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32,
                                               c_vp, c_i64, c_vp]),
     "kgat_biinter_fwd_tiles_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,

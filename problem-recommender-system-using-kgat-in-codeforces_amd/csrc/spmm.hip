@@ -120,14 +120,10 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
   const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   bool any = false;
-  uint8_t* mark = nullptr;
-  if ((MODE == kRows || MODE == kOverwrite) && io.reach_mark != nullptr &&
-      (MODE == kRows || bit_of(io.out_bits, row)))
-    mark = io.reach_mark;
   // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
   for (int64_t cb = beg + g * L; cb < end; cb += kWave) {
     const int64_t ce = cb + L < end ? cb + L : end;
-    gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any, hb, mark);
+    gather_edges<D, MASKED>(A, io, cb, ce, base, gl, acc, any, hb);
   }
   // a long row is flagged by any of its segments that gathered (row_hit was zeroed)
   if (MODE == kMasked && io.row_hit != nullptr && any && gl == 0) io.row_hit[row] = 1;
@@ -173,10 +169,8 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
         if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         bool any = false;
-        uint8_t* mark = MODE == kRows ? io.reach_mark : nullptr;
         gather_edges<D, MODE == kMaskedRows, MODE == kRows ? kRowsUnroll : 4>(A, io, beg, end, base, gl, acc, any,
-                                                                              hb, mark);
-        if (mark != nullptr && gl == 0) mark[r] = 1;
+                                                                              hb);
         store_row<MODE>(io, r, MODE == kRows ? r : k, gl, acc, any);
       }
     }
@@ -189,27 +183,6 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
   int64_t r_end = r_begin + S::kRowsPerWave;
   if (r_end > A.n_rows) r_end = A.n_rows;
   for (int64_t r = r_begin + g; r < r_end; r += S::kGroups) {
-    if (MODE == kMaskedAdam && io.reach != nullptr) {
-      // reach marks: an unmarked row's gradient is exactly zero -- its p / m / v stream through the Adam
-      // step with g = +0 (what the scan below would give: no hit, no Yc row), no edge, rank or map traffic
-      const AdamRow pre = adam_row_load(io.adam, r, gl);
-      const uint8_t rc = io.reach[io.row0 + r];
-      const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
-      if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rc != 0) {
-        bool any = false;
-        const int ym = io.Yc != nullptr ? io.src_map[io.row0 + r] : -1;
-        gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any, hb);
-        if (ym >= 0) {
-          const float4 o = reinterpret_cast<const float4*>(io.Yc + static_cast<int64_t>(ym) * io.ldyc)[gl];
-          acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
-        }
-        if (gl == 0) io.reach[io.row0 + r] = 0;
-      }
-      adam_row_step(io.adam, r, gl, acc, pre);
-      continue;
-    }
     const int64_t beg = A.rowptr[r], end = A.rowptr[r + 1];
     if (end - beg > A.long_threshold) continue;  // produced by the fix-up pass
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -228,10 +201,7 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
       adam_row_step(io.adam, r, gl, acc, pre);
       continue;
     }
-    uint8_t* mark = nullptr;
-    if (MODE == kOverwrite && io.reach_mark != nullptr && bit_of(io.out_bits, r)) mark = io.reach_mark;
-    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any, hb, mark);
-    if (mark != nullptr && gl == 0) mark[r] = 1;
+    gather_edges<D, MASKED>(A, io, beg, end, base, gl, acc, any, hb);
     store_row<MODE>(io, r, r, gl, acc, any);
   }
 }
@@ -680,46 +650,6 @@ extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int3
   return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
 }
 
-extern "C" int kgat_spmm_csr_mark_f32(const kgat_csr* A, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
-                                      const uint32_t* mark_rows, uint8_t* reach, float* workspace,
-                                      int64_t workspace_floats, void* stream) {
-  using namespace kgat;
-  if (!A || !X || !Y || !mark_rows || !reach || A->n_rows < 0 || ldx < d || ldy < d || (ldx & 3) || (ldy & 3))
-    return KGAT_ERR_INVALID;
-  if (misaligned(X) || misaligned(Y)) return KGAT_ERR_INVALID;
-  if (A->n_rows == 0) return KGAT_OK;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
-    return KGAT_ERR_WORKSPACE;
-  SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr,
-            mark_rows, nullptr, nullptr, nullptr};
-  io.reach_mark = reach;
-  return dispatch<kOverwrite>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
-extern "C" int kgat_spmm_csr_masked_adam_reach_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
-                                                   int64_t ldxc, const float* Yc_init, int64_t ldyc,
-                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
-                                                   int32_t d, float step_size, float beta1, float beta2,
-                                                   float bc2_sqrt, float eps, const int32_t* skip, uint8_t* reach,
-                                                   float* workspace, int64_t workspace_floats, void* stream) {
-  using namespace kgat;
-  if (!A || !src_map || !Xc || !p || !m || !v || !reach || A->n_rows < 0 || ldxc < d || ldp < d || (ldxc & 3) ||
-      (ldp & 3))
-    return KGAT_ERR_INVALID;
-  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
-      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
-    return KGAT_ERR_INVALID;
-  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
-  if (A->n_rows == 0) return KGAT_OK;
-  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
-    return KGAT_ERR_WORKSPACE;
-  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
-            nullptr, nullptr, nullptr, nullptr};
-  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
-  io.reach = reach;
-  return dispatch<kMaskedAdam>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
 extern "C" int64_t kgat_hop_compact_work_bytes(int64_t n) {
   if (n < 0 || n > INT32_MAX) return -1;
   size_t bytes = 0;
@@ -832,10 +762,9 @@ extern "C" int kgat_spmm_csr_masked_rows_f32(const kgat_csr* A, const int32_t* s
                                           out_rows, out_count, Y, ldy, nullptr, d, workspace, workspace_floats, stream);
 }
 
-extern "C" int kgat_spmm_csr_rows_mark_f32(const kgat_csr* A, const float* X, int64_t ldx, const uint32_t* out_bits,
-                                           const int32_t* out_rows, const int32_t* out_count, float* Y, int64_t ldy,
-                                           int32_t d, uint8_t* reach, float* workspace, int64_t workspace_floats,
-                                           void* stream) {
+extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t ldx, const uint32_t* out_bits,
+                                      const int32_t* out_rows, const int32_t* out_count, float* Y, int64_t ldy,
+                                      int32_t d, float* workspace, int64_t workspace_floats, void* stream) {
   using namespace kgat;
   if (!A || !X || !Y || !out_bits || !out_rows || !out_count || A->n_rows < 0 || ldx < d || ldy < d || (ldx & 3) ||
       (ldy & 3))
@@ -844,17 +773,9 @@ extern "C" int kgat_spmm_csr_rows_mark_f32(const kgat_csr* A, const float* X, in
   if (A->n_rows == 0) return KGAT_OK;
   if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
     return KGAT_ERR_WORKSPACE;
-  SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr,
-            out_bits, nullptr, out_rows, out_count};
-  io.reach_mark = reach;
+  const SpmmIo io{X, ldx, Y, ldy, workspace, nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr,
+                  out_bits, nullptr, out_rows, out_count};
   return dispatch<kRows>(*A, io, d, reinterpret_cast<hipStream_t>(stream));
-}
-
-extern "C" int kgat_spmm_csr_rows_f32(const kgat_csr* A, const float* X, int64_t ldx, const uint32_t* out_bits,
-                                      const int32_t* out_rows, const int32_t* out_count, float* Y, int64_t ldy,
-                                      int32_t d, float* workspace, int64_t workspace_floats, void* stream) {
-  return kgat_spmm_csr_rows_mark_f32(A, X, ldx, out_bits, out_rows, out_count, Y, ldy, d, nullptr, workspace,
-                                     workspace_floats, stream);
 }
 
 extern "C" int kgat_csr_mark_rows(const kgat_csr* A, const uint32_t* bits, int64_t n_bits, int64_t row0,

@@ -54,13 +54,6 @@ struct SpmmIo {
   // store instead of a kgat_bpr_bwd_f32 launch after it (same bits: (Yc + sum) + g either way)
   const float* Gc = nullptr;
   int64_t ldgc = 0;
-  // Table-update reach marks (one byte per node): kRows / kOverwrite (nullable reach_mark): every column a
-  // marked row gathers from, and the row itself, get reach_mark[.] = 1 -- kRows marks every row of its
-  // set, kOverwrite the rows of out_bits; kMaskedAdam (nullable reach): a short row with reach[row] == 0
-  // has a zero gradient (no edge into the source set, no Yc row) and takes the Adam step with g = +0
-  // without scanning its edges; the bytes it read are reset to 0.
-  uint8_t* reach_mark = nullptr;
-  uint8_t* reach = nullptr;
   int32_t* out_src = nullptr;  // kMaskedRows (nullable): out_src[k] = src_map[out_rows[k]] -- which output rows
                                // have a compact source row (the batch rows' BPR terms, kgat_biinter_bwd_hop_ex_f32)
 };
@@ -110,8 +103,7 @@ __device__ __forceinline__ void wave_lds_order() {
 // MASKED: hb is the group's kLanes-entry LDS slot array (the chunk's hits compacted there).
 template <int D, bool MASKED, int U = 4, int UM = 4>
 __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io, int64_t beg, int64_t end, int base,
-                                             int gl, float4& acc, bool& any, int2* hb = nullptr,
-                                             uint8_t* mark = nullptr) {
+                                             int gl, float4& acc, bool& any, int2* hb = nullptr) {
   constexpr int L = SpmmShape<D>::kLanes;
   const float4* X4 = reinterpret_cast<const float4*>(io.X);
   const uint32_t ldx4u = static_cast<uint32_t>(io.ldx / 4);
@@ -175,7 +167,6 @@ __device__ __forceinline__ void gather_edges(const kgat_csr& A, const SpmmIo& io
     if (gl < n) {
       mc = A.col[cb + gl];
       mv = A.val[cb + gl];
-      if (mark != nullptr) mark[mc] = 1;  // the row's gradient reaches column mc's table row (SpmmIo::reach_mark)
     }
     int j = 0;
     for (; j + U <= n; j += U) {

@@ -263,14 +263,6 @@ class DeviceGraph:
             self._hop = hb
         return hb
 
-    def reach_marks(self) -> torch.Tensor:
-        """uint8 [N]: the table update's reach marks (kgat_spmm_csr_masked_adam_reach_f32), zero between
-        uses except for stale marks, which only cost a scan."""
-        r = getattr(self, "_reach", None)
-        if r is None:
-            r = self._reach = torch.zeros(self.n_nodes + 16, dtype=torch.uint8, device=self.device)
-        return r
-
     def row_blocks(self, k: int) -> list[_CSRRowView]:
         """k row-block views of A with (about) equal edge counts, boundaries on multiples of 16
         rows (the bi-interaction's sub-tiles), cached per k."""

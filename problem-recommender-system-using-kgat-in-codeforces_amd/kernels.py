@@ -65,13 +65,8 @@ EDGE_GEMM_CHUNK = 1 << 20
 
 
 def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, transpose: bool = False,
-         accumulate: bool = False, mark_rows: torch.Tensor | None = None,
-         reach: torch.Tensor | None = None) -> torch.Tensor:
-    """Y = A . X (or A^T . X); with accumulate, Y += ...  ``mark_rows`` (int32 bitmap) / ``reach`` (uint8
-    [N]): every column a marked row gathers from, and the row, get reach[.] = 1 (kgat_spmm_csr_mark_f32:
-    the table update's reach marks, spmm_masked_adam)."""
-    if (mark_rows is None) != (reach is None) or (reach is not None and (transpose or accumulate)):
-        raise ValueError("spmm: mark_rows and reach go together, with the plain A . X only")
+         accumulate: bool = False) -> torch.Tensor:
+    """Y = A . X (or A^T . X); with accumulate, Y += ..."""
     _req(X, "X", dim=2)
     n, d = X.shape
     if n != graph.n_nodes:
@@ -90,24 +85,12 @@ def spmm(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor | None = None, t
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    if reach is not None:
-        _check_reach(reach, graph.n_nodes)
-        if mark_rows.dtype != torch.int32 or mark_rows.numel() * 32 < n:
-            raise ValueError("mark_rows must be an int32 bitmap covering every row")
-        _lib.call("kgat_spmm_csr_mark_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
-                  mark_rows.data_ptr(), reach.data_ptr(), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
-    else:
-        _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
-                  int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    _lib.call("kgat_spmm_csr_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out.data_ptr(), _ld(out), d,
+              int(accumulate), ws.data_ptr(), ws.numel(), stream_ptr(X.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, transpose, accumulate))
     return out
-
-
-def _check_reach(reach: torch.Tensor, n: int) -> None:
-    if reach.dtype != torch.uint8 or reach.dim() != 1 or reach.numel() < n or not reach.is_cuda:
-        raise ValueError("reach: a uint8 device array covering every node")
 
 
 def spmm_block(csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
@@ -336,13 +319,10 @@ def _skip_ptr(skip: torch.Tensor | None):
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None, reach: torch.Tensor | None = None) -> None:
+                     skip: torch.Tensor | None = None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).  ``reach``
-    (uint8 [N], a superset of the rows with a nonzero gradient, spmm / spmm_rows marks): an unmarked row
-    takes the step with g = +0 without scanning its edges; the marks read are cleared
-    (kgat_spmm_csr_masked_adam_reach_f32)."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -366,15 +346,9 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
     rank = _rank_ptr(src_rank, src_map)
 
-    if reach is not None:
-        _check_reach(reach, n)
-        _lib.call("kgat_spmm_csr_masked_adam_reach_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
-                  _ld(Xc), yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2,
-                  bc2_sqrt, eps, _skip_ptr(skip), reach.data_ptr(), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
-    else:
-        _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
-                  _ld(Xc), yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
-                  beta2, bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
+              yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
+              eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
@@ -535,10 +509,9 @@ def spmm_masked_rows(graph: DeviceGraph, src_map, src_bits, Xc, Yc_init, out_row
 
 
 def spmm_rows(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor, out_rows: torch.Tensor,
-              out_count: torch.Tensor, out_bits: torch.Tensor, reach: torch.Tensor | None = None) -> torch.Tensor:
+              out_count: torch.Tensor, out_bits: torch.Tensor) -> torch.Tensor:
     """out[r] = (A . X)[r] for the rows r = out_rows[k], k < out_count (device), only; the other
-    rows of ``out`` are left as they are (kgat_spmm_csr_rows_f32: same bits per row as spmm).  ``reach``
-    (uint8 [N]): the rows' columns and the rows themselves get reach[.] = 1 (kgat_spmm_csr_rows_mark_f32)."""
+    rows of ``out`` are left as they are (kgat_spmm_csr_rows_f32: same bits per row as spmm)."""
     _req(X, "X", dim=2)
     _req(out, "out", dim=2)
     n, d = X.shape
@@ -555,11 +528,9 @@ def spmm_rows(graph: DeviceGraph, X: torch.Tensor, out: torch.Tensor, out_rows: 
     if ev is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-    if reach is not None:
-        _check_reach(reach, n)
-    _lib.call("kgat_spmm_csr_rows_mark_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out_bits.data_ptr(),
-              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d,
-              reach.data_ptr() if reach is not None else None, ws.data_ptr(), ws.numel(), stream_ptr(X.device))
+    _lib.call("kgat_spmm_csr_rows_f32", ctypes.byref(desc), X.data_ptr(), _ld(X), out_bits.data_ptr(),
+              out_rows.data_ptr(), out_count.data_ptr(), out.data_ptr(), _ld(out), d, ws.data_ptr(), ws.numel(),
+              stream_ptr(X.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, False, "rows"))
@@ -842,12 +813,11 @@ def biinter_fwd(X, S, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0, out
 
 
 def propagate_layer(graph: DeviceGraph, X, W1, b1, W2, b2, dropout_p: float = 0.0, seed: int = 0,
-                    state: BiState | None = None, mark_rows: torch.Tensor | None = None,
-                    reach: torch.Tensor | None = None):
+                    state: BiState | None = None):
     """One KGAT layer forward (aggregator.py:54-65): S = A . X, H = biinter(X, S); returns (S, H).
     (Row-block pipelining of the two launches on two streams and a one-pass propagation +
-    bi-interaction kernel both measured slower)  ``mark_rows`` / ``reach``: see spmm."""
-    S = spmm(graph, X, mark_rows=mark_rows, reach=reach)
+    bi-interaction kernel both measured slower)"""
+    S = spmm(graph, X)
     return S, biinter_fwd(X, S, W1, b1, W2, b2, dropout_p, seed, state=state)
 
 

@@ -260,17 +260,17 @@ class _TableUpdate:
         self.enabled = False
         self.pending = None
 
-    def defer(self, graph, src_map, Xc, Yc, rank, reach=None) -> bool:
+    def defer(self, graph, src_map, Xc, Yc, rank) -> bool:
         if not self.enabled or self.param.grad is not None or self.pending is not None:
             return False
-        self.pending = (graph, src_map, Xc, Yc, rank, reach)
+        self.pending = (graph, src_map, Xc, Yc, rank)
         return True
 
     @torch.no_grad()
     def materialize(self) -> None:
         if self.pending is None:
             return
-        graph, src_map, Xc, Yc, rank, _reach = self.pending  # (stale reach marks only cost a later scan)
+        graph, src_map, Xc, Yc, rank = self.pending
         self.pending = None
         g = kernels.spmm_masked(graph, src_map, Xc, Yc_init=Yc, transpose=True, src_rank=rank)
         if self.param.grad is None:
@@ -284,13 +284,12 @@ class _TableUpdate:
 
     def launch(self):
         """The fused product + Adam of the pending gradient (FusedAdam.step(fused=...))."""
-        graph, src_map, Xc, Yc, rank, reach = self.pending
+        graph, src_map, Xc, Yc, rank = self.pending
         self.pending = None
         p = self.param.data
 
         def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
-            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
-                                     reach=reach)
+            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip)
         return run
 
 
@@ -762,23 +761,6 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook, marks=None):
     return rows, hop, fcount, tok
 
 
-def _early_reach_hop(graph, ws, L: int, hook, tu, marks):
-    """The fused table update's reach marks (kgat_spmm_csr_masked_adam_reach_f32): with 2 layers the
-    backward's layer-0 hop set is the first hop F + N(F) of the batch rows, fixed by the batch and the
-    graph, so it is listed before the propagation and the layer-0 product marks every table row its
-    gradient can reach (the columns of the hop rows, and the rows themselves) while it gathers them; the
-    update then streams the unmarked rows (68 % at C2) through Adam with g = +0 instead of scanning their
-    edges.  Returns (early hop as _early_first_hop's, reach marks) or (None, None)."""
-    if (hook is not None or marks is None or tu is None or not tu.enabled or L != 2 or HOP_DENSE_FRACTION <= 0
-            or not kernels.saved_state_supported(ws[0].shape[1], ws[0].shape[0])
-            or not _hop_small(graph, 0, graph.n_nodes)):
-        return None, None
-    rows, fcount, tok = marks
-    hop = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, 0), precleared=tok.take_cleared())
-    _hop_record(graph, 0)
-    return (rows, hop, fcount, tok), graph.reach_marks()
-
-
 def _tile_forward_ok(din: int, dout: int) -> bool:
     """Shapes whose forward can run on a row set's 16-row tiles (kgat_biinter_fwd_tiles_f32: the fused
     kernels with their saved state -- norm + sign/keep words)."""
@@ -786,7 +768,7 @@ def _tile_forward_ok(din: int, dout: int) -> bool:
         kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
 
 
-def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks=None, reach=None):
+def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks=None):
     """The forward on the rows the loss can reach only (KGAT.frontier_forward; L = 1, 2 or 3, the
     restricted layers with the fused kernels' saved state).  The BPR loss reads the batch rows F of
     every table (model.py:189-191), so the last layer's output is needed on F only, and layer L-2's
@@ -832,7 +814,7 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks
         else:
             out_rows, out_count, out_bits = sets[l]
             s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
-                                  out_count, out_bits, reach=reach if l == 0 else None)
+                                  out_count, out_bits)
             x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
                                           torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device),
                                           out_bits, state=st)
@@ -875,14 +857,10 @@ class _CFLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, users, pos, neg, cfg, X0, *ws):
-        graph, drops, seeds, reg, hook, tu, frontier, marks = cfg
+        graph, drops, seeds, reg, hook, _tu, frontier, marks = cfg
         ctx.marks = marks
         ctx.early = _early_first_hop(graph, users, pos, neg, ws, len(drops), hook, marks)
-        ctx.reach = None
-        if ctx.early is None:
-            ctx.early, ctx.reach = _early_reach_hop(graph, ws, len(drops), hook, tu, marks)
-        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, marks,
-                               ctx.reach) if frontier else None
+        fw = _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, ctx.early, marks) if frontier else None
         if fw is not None:
             tables, sides, states, ctx.early = fw
         else:
@@ -891,9 +869,7 @@ class _CFLoss(torch.autograd.Function):
             for l in range(len(drops)):
                 W1, b1, W2, b2 = ws[4 * l: 4 * l + 4]
                 st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
-                mark = ctx.early[1][3] if l == 0 and ctx.reach is not None else None
-                s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st, mark_rows=mark,
-                                               reach=ctx.reach if mark is not None else None)
+                s, x = kernels.propagate_layer(graph, x, W1, b1, W2, b2, drops[l], seeds[l], state=st)
                 sides.append(s)
                 states.append(st)
                 tables.append(x)
@@ -1061,7 +1037,7 @@ class _CFLoss(torch.autograd.Function):
                     # the exchange owns the table gradient now (its blocks are in flight): autograd gets
                     # none (it would copy the whole [N, d] tensor), ShardedGradSync.reduce hands it over
                     dX = None
-                elif l == 0 and tu is not None and tu.defer(graph, hmap, dSc, dXdc, rank, reach=ctx.reach):
+                elif l == 0 and tu is not None and tu.defer(graph, hmap, dSc, dXdc, rank):
                     dX = None  # computed fused with the table's Adam step by update_cf_weights
                 else:
                     dX = kernels.spmm_masked(graph, hmap, dSc, Yc_init=dXdc, transpose=True,
@@ -1084,7 +1060,7 @@ class _CFLoss(torch.autograd.Function):
                 kernels.spmm(graph, dS, out=dXd, transpose=True, accumulate=True)
             wgrads[4 * l: 4 * l + 4] = [dW1, db1, dW2, db2]
             dX = dXd
-        ctx.tables = ctx.sides = ctx.states = ctx.reach = None
+        ctx.tables = ctx.sides = ctx.states = None
         return (None, None, None, None, dX, *wgrads)
 
 

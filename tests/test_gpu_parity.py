@@ -1439,61 +1439,6 @@ def test_fused_table_update_bit_identical(pkg, layers):
     assert torch.equal(grads[0], grads[1])
 
 
-@pytest.mark.parametrize("frontier", [False, True])
-def test_fused_table_update_reach_marks(pkg, frontier):
-    """The fused table update with reach marks (kgat_spmm_csr_masked_adam_reach_f32): the layer-0 product of
-    the forward marks every table row the step's gradient can reach (kgat_spmm_csr_mark_f32 on the full
-    path, kgat_spmm_csr_rows_mark_f32 on the frontier forward) and the update streams the unmarked rows
-    through Adam with g = +0.  Parameters and Adam moments bit for bit against the unfused step over CF + KG
-    steps -- also with stale marks (random rows marked before every step, and a step whose deferred
-    gradient is materialised instead, leaving its marks): a stale mark only costs a scan."""
-    graph_mod, _ = _mods(pkg)
-    U, E, inter, trip = graph_mod.synthetic_ckg(20000, 200000, seed=11)
-    lay = graph_mod.build_layout(U, E, inter, trip)
-    models = []
-    for fused, stale in ((False, False), (True, False), (True, True)):
-        torch.manual_seed(77)
-        m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
-                                  message_dropout=[0.1, 0.1]))
-        m.attach_graph(lay, DEV)
-        m.train()
-        m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
-        m.fuse_table_update = fused
-        m.frontier_forward = frontier
-        models.append((m, stale))
-    rng = np.random.default_rng(12)
-    R, n = len(lay.rel_order), U + E
-    for step in range(4):
-        ids = [torch.from_numpy(rng.integers(0, hi, 64)).to(DEV) for hi in (U, int(E * 0.1), int(E * 0.1))]
-        kg = [torch.from_numpy(rng.integers(0, hi, 32)).to(DEV) for hi in (U + E, R, U + E, U + E)]
-        junk = torch.from_numpy(rng.integers(0, n, 5000)).to(DEV)
-        for m, stale in models:
-            if stale:
-                m.graph().reach_marks()[junk] = 1
-            torch.manual_seed(300 + step)
-            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
-            if m.fuse_table_update:
-                assert m._table_update.pending is not None and m._table_update.pending[5] is not None
-                if stale and step == 2:
-                    m.materialize_table_grad()  # the marks of this step stay behind
-            m.update_cf_weights()
-            m(kg[0], kg[1], kg[2], kg[3], mode=pkg.KGATMode.TRAIN_KG).backward()
-            m.update_kg_weights()
-    base = models[0][0]
-    tb = base._cf_optimizer.state[id(base._user_entity_embedding.weight)]
-    for m, _ in models[1:]:
-        for (k, pa), (_, pb) in zip(base.named_parameters(), m.named_parameters()):
-            if not pa.is_sparse:
-                assert torch.equal(pa, pb), k
-        ta = m._cf_optimizer.state[id(m._user_entity_embedding.weight)]
-        assert torch.equal(ta["exp_avg"], tb["exp_avg"]) and torch.equal(ta["exp_avg_sq"], tb["exp_avg_sq"])
-    # the clean fused model's marks were consumed: only long rows (never scanned) may keep one
-    m = models[1][0]
-    marks = m.graph().reach_marks()[:n].nonzero().flatten().cpu().numpy()
-    long_rows = m.graph().AT.long_rows.cpu().numpy()
-    assert np.isin(marks, long_rows).all()
-
-
 def test_fused_table_update_keeps_extra_table_gradient(pkg):
     """with fuse_table_update the CF backward defers the table's gradient, but
     another term of the loss (here an L2 penalty on the whole table) still writes .grad through
