@@ -561,6 +561,14 @@ int kgat_row_softmax_f32(const int64_t *rowptr, int64_t n_rows, const float *slo
  * long_rows == NULL: the long rows are found by a scan of all rows. */
 int kgat_row_softmax_ex_f32(const int64_t *rowptr, int64_t n_rows, const int32_t *long_rows, int32_t n_long,
                             const float *slot_logits, float *val, void *stream);
+/* a7 with the CSR's long-row plan (seg_len 512, long_threshold 256, as kgat_csr_plan's defaults): rows of
+ * <= 256 entries take a 16-lane group each; a longer row is cut into its plan segments -- pass 1 keeps
+ * each segment's max and sum of exp (work: kgat_row_softmax_work_floats(A) floats), pass 2 combines the
+ * row's segments in segment order (max, then the rescaled sums) and every segment writes its entries.
+ * A hub row runs on all its segments' waves at once instead of one block. */
+int64_t kgat_row_softmax_work_floats(const kgat_csr *A);
+int kgat_row_softmax_plan_f32(const kgat_csr *A, const float *slot_logits, float *val, float *work,
+                              int64_t work_floats, void *stream);
 
 /* a6 for wide embeddings (d > 128, multiple of 16, <= 1024; C5's 256): the edge scorer
  * of kgat_edge_logits_f32 as kgat_gemm_f32 products over chunks of the relation-sorted edge

@@ -231,44 +231,134 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(const int64_t* __restrict
   slog[s] = v;
 }
 
-// val[slot] = softmax over the stored entries of each row; one wave per row.
-// Row softmax over the stored entries (model.py:355-366, torch.sparse.softmax):
-// rows of <= 256 entries (all but the hubs) take a 16-lane group each, every
-// lane keeping its <= 16 logits in registers -- one read and one write of the
-// row; the lane partials reduce in a fixed butterfly order (deterministic).
+// val[slot] = softmax over the stored entries of each row (model.py:355-366, torch.sparse.softmax).
+// Rows of <= 256 entries (all but the hubs) take a 4-lane group each, 16 rows per wave in flight: a row of
+// <= 32 entries is read once into 8 registers per lane (max, exp-sum, write from registers), a longer one
+// in max / exp-sum / write passes of 32-entry chunks (the later passes re-read it from L1/L2).  Lane j of
+// the group holds entries j, j + 4, ...; the lane partials reduce in a fixed butterfly (deterministic, and
+// the same bits wherever the row sits).  Longer rows: the segment plan below.
 constexpr int kSoftmaxShort = 256;
+
+__device__ __forceinline__ void short_row_softmax(const int64_t* __restrict__ rowptr, int64_t row, int j,
+                                                  const float* __restrict__ logit, float* __restrict__ val) {
+  const int64_t beg = rowptr[row], end = rowptr[row + 1];
+  const int64_t len = end - beg;
+  if (len == 0 || len > kSoftmaxShort) return;  // (group-uniform) long rows: the segment kernels
+  if (len <= 32) {
+    float x[8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = beg + j + 4 * k;
+      x[k] = e < end ? logit[e] : -INFINITY;
+      m = fmaxf(m, x[k]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 1));
+    m = fmaxf(m, __shfl_xor(m, 2));
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      x[k] = beg + j + 4 * k < end ? expf(x[k] - m) : 0.f;
+      s += x[k];
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = beg + j + 4 * k;
+      if (e < end) val[e] = x[k] * inv;
+    }
+    return;
+  }
+  float m = -INFINITY;
+  for (int64_t e = beg + j; e < end; e += 4) m = fmaxf(m, logit[e]);
+  m = fmaxf(m, __shfl_xor(m, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  float s = 0.f;
+  for (int64_t e = beg + j; e < end; e += 4) s += expf(logit[e] - m);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float inv = 1.f / s;
+  for (int64_t e = beg + j; e < end; e += 4) val[e] = expf(logit[e] - m) * inv;
+}
 
 __global__ __launch_bounds__(256) void row_softmax_kernel(const int64_t* __restrict__ rowptr, int64_t n_rows,
                                                           const float* __restrict__ logit, float* __restrict__ val) {
-  const int64_t row = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4;
-  const int gl = threadIdx.x & 15;
-  if (row >= n_rows) return;  // whole 16-lane groups leave together
-  const int64_t beg = rowptr[row], end = rowptr[row + 1];
-  const int64_t len = end - beg;
-  if (len == 0 || len > kSoftmaxShort) return;  // long rows: row_softmax_long_kernel
-  float x[kSoftmaxShort / 16];
+  const int64_t row = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2;
+  if (row >= n_rows) return;  // whole 4-lane groups leave together
+  short_row_softmax(rowptr, row, threadIdx.x & 3, logit, val);
+}
+
+// Long rows, cut into the CSR's long-row plan segments (one wave each, <= kSoftmaxSeg entries, 8 per lane
+// in registers).  Pass 1 (with the short rows, segment waves first): each segment's max m_s and
+// s_s = sum exp(x - m_s) -> stat[2s], stat[2s + 1].  Pass 2: every segment wave of a row combines the
+// row's segment stats in segment order -- M = max m_s, S = sum_s s_s exp(m_s - M), lane-strided partials
+// then a fixed butterfly, the same bits in every wave of the row -- and writes its own entries
+// exp(x - M) / S.  A hub row of 10^5 entries runs on ~200 waves instead of one block's three serial passes.
+constexpr int kSoftmaxSeg = 512;
+
+__global__ __launch_bounds__(256) void row_softmax_stats_kernel(kgat_csr A, const float* __restrict__ logit,
+                                                                float* __restrict__ val, float* __restrict__ stat,
+                                                                int seg_blocks) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // short rows (row_softmax_kernel's body)
+    const int64_t row = (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + threadIdx.x) >> 2;
+    if (row < A.n_rows) short_row_softmax(A.rowptr, row, threadIdx.x & 3, logit, val);
+    return;
+  }
+  const int sg = blockIdx.x * 4 + wave;
+  if (sg >= A.n_seg) return;
+  const int64_t row = A.seg_row[sg];
+  const int64_t beg = A.seg_beg[sg], row_end = A.rowptr[row + 1];
+  const int64_t end = beg + kSoftmaxSeg < row_end ? beg + kSoftmaxSeg : row_end;
+  float x[kSoftmaxSeg / 64];
   float m = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
-    const int64_t e = beg + gl + 16 * k;
+  for (int k = 0; k < kSoftmaxSeg / 64; ++k) {
+    const int64_t e = beg + lane + 64 * k;
     x[k] = e < end ? logit[e] : -INFINITY;
     m = fmaxf(m, x[k]);
   }
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
-    x[k] = beg + gl + 16 * k < end ? expf(x[k] - m) : 0.f;
-    s += x[k];
+  for (int k = 0; k < kSoftmaxSeg / 64; ++k) s += beg + lane + 64 * k < end ? expf(x[k] - m) : 0.f;
+  s = wave_sum(s);
+  if (lane == 0) {
+    stat[2 * static_cast<int64_t>(sg)] = m;
+    stat[2 * static_cast<int64_t>(sg) + 1] = s;
   }
+}
+
+__global__ __launch_bounds__(256) void row_softmax_seg_write_kernel(kgat_csr A, const float* __restrict__ logit,
+                                                                    const float* __restrict__ stat,
+                                                                    float* __restrict__ val) {
+  const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sg >= A.n_seg) return;
+  const int64_t row = A.seg_row[sg];
+  const int64_t rbeg = A.rowptr[row], rend = A.rowptr[row + 1];
+  const int64_t beg = A.seg_beg[sg];
+  const int s0 = sg - static_cast<int>((beg - rbeg) / kSoftmaxSeg);  // the row's first segment
+  const int ns = static_cast<int>((rend - rbeg + kSoftmaxSeg - 1) / kSoftmaxSeg);
+  float M = -INFINITY;
+  for (int i = lane; i < ns; i += 64) M = fmaxf(M, stat[2 * static_cast<int64_t>(s0 + i)]);
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float inv = 1.f / s;
+  for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+  float S = 0.f;
+  for (int i = lane; i < ns; i += 64) {
+    const int64_t k = 2 * static_cast<int64_t>(s0 + i);
+    S += stat[k + 1] * expf(stat[k] - M);
+  }
+  S = wave_sum(S);
+  const float inv = 1.f / S;
+  const int64_t end = beg + kSoftmaxSeg < rend ? beg + kSoftmaxSeg : rend;
 #pragma unroll
-  for (int k = 0; k < kSoftmaxShort / 16; ++k) {
-    const int64_t e = beg + gl + 16 * k;
-    if (e < end) val[e] = x[k] * inv;
+  for (int k = 0; k < kSoftmaxSeg / 64; ++k) {
+    const int64_t e = beg + lane + 64 * k;
+    if (e < end) val[e] = expf(logit[e] - M) * inv;
   }
 }
 
@@ -330,13 +420,37 @@ static int launch_scores(const EdgeScoreArgs& a, hipStream_t st) {
 
 }  // namespace kgat
 
+extern "C" int64_t kgat_row_softmax_work_floats(const kgat_csr* A) { return A ? 2 * static_cast<int64_t>(A->n_seg) + 2 : -1; }
+
+extern "C" int kgat_row_softmax_plan_f32(const kgat_csr* A, const float* slot_logits, float* val, float* work,
+                                         int64_t work_floats, void* stream) {
+  if (!A || !slot_logits || !val || A->n_rows < 0) return KGAT_ERR_INVALID;
+  if (A->n_seg > 0 && (A->seg_len != kgat::kSoftmaxSeg || A->long_threshold != kgat::kSoftmaxShort))
+    return KGAT_ERR_INVALID;  // the plan's cut must be the softmax's
+  if (A->n_rows == 0) return KGAT_OK;
+  if (!work || work_floats < kgat_row_softmax_work_floats(A)) return KGAT_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int seg_blocks = (A->n_seg + 3) / 4;
+  const int64_t grid = seg_blocks + (A->n_rows * 4 + 255) / 256;
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL(kgat::row_softmax_stats_kernel, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
+                     seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  if (A->n_seg > 0) {
+    hipLaunchKernelGGL(kgat::row_softmax_seg_write_kernel, dim3(seg_blocks), dim3(256), 0, st, *A, slot_logits, work,
+                       val);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
+
 extern "C" int kgat_row_softmax_ex_f32(const int64_t* rowptr, int64_t n_rows, const int32_t* long_rows,
                                        int32_t n_long, const float* slot_logits, float* val, void* stream) {
   if (!rowptr || !slot_logits || !val || n_rows < 0 || n_long < 0 || (n_long > 0 && !long_rows))
     return KGAT_ERR_INVALID;
   if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows * 16 + 255) / 256), dim3(256), 0, st, rowptr, n_rows,
+  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows * 4 + 255) / 256), dim3(256), 0, st, rowptr, n_rows,
                      slot_logits, val);
   KGAT_LAUNCH_CHECK();
   if (long_rows == nullptr) {

@@ -35,33 +35,6 @@ __device__ __forceinline__ uint32_t gemm_threshold(float p) {
   return t >= 65536.f ? 65536u : static_cast<uint32_t>(t);
 }
 
-// U = X+S, M = X*S with row pitch d+4 (16-byte aligned rows; the 4 pad columns are written 1, 0, 0, 0
-// and never read).  rows (nullable): row r of U / M comes from row rows[r] of X / S (-1: zeros).
-__global__ __launch_bounds__(256) void um_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ S,
-                                                 int64_t lds, float* __restrict__ U, float* __restrict__ M, int64_t n,
-                                                 int d, const int32_t* __restrict__ rows = nullptr) {
-  const int q = d / 4 + 1;  // float4 groups per padded row
-  const int64_t total = n * q;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  const int64_t ldu = d + 4;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int64_t r = i / q;
-    const int c = static_cast<int>(i % q) * 4;
-    if (c == d) {
-      const float4 e = make_float4(1.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(U + r * ldu + c) = e;
-      *reinterpret_cast<float4*>(M + r * ldu + c) = e;
-      continue;
-    }
-    const int64_t src = rows != nullptr ? static_cast<int64_t>(rows[r]) : r;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 x = src >= 0 ? *reinterpret_cast<const float4*>(X + src * ldx + c) : z;
-    const float4 s = src >= 0 ? *reinterpret_cast<const float4*>(S + src * lds + c) : z;
-    *reinterpret_cast<float4*>(U + r * ldu + c) = make_float4(x.x + s.x, x.y + s.y, x.z + s.z, x.w + s.w);
-    *reinterpret_cast<float4*>(M + r * ldu + c) = make_float4(x.x * s.x, x.y * s.y, x.z * s.z, x.w * s.w);
-  }
-}
-
 // [dW | db] = sum over row chunks of the slabs [nb][dout][d_in + 4], in chunk order, in two
 // levels: pass 1 (blockIdx.y = group g of kSlabGroups) sums the slabs of group g's contiguous
 // range in order into part[g]; pass 2 sums the groups in order.  (One thread per output
@@ -260,21 +233,6 @@ __global__ __launch_bounds__(256) void epi_bwd_bits_kernel(float* __restrict__ d
   }
 }
 
-// in place: (du, dm) in (dXd, dS) -> dXd = du + dm*S, dS = du + dm*X
-__global__ __launch_bounds__(256) void dxs_kernel(float* __restrict__ dXd, int64_t lda, float* __restrict__ dS,
-                                                  int64_t ldb, const float* __restrict__ X, int64_t ldx,
-                                                  const float* __restrict__ S, int64_t lds, int64_t n, int d) {
-  const int64_t total = n * d;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int64_t r = i / d;
-    const int c = static_cast<int>(i % d);
-    const float du = dXd[r * lda + c], dm = dS[r * ldb + c];
-    dXd[r * lda + c] = fmaf(dm, S[r * lds + c], du);
-    dS[r * ldb + c] = fmaf(dm, X[r * ldx + c], du);
-  }
-}
-
 // Rows per split-K chunk of the weight-gradient GEMMs.  dW is one or two 128 x 128 output tiles,
 // so the chunks are the GEMM's only parallelism: about 1k chunks (>= 4 blocks per CU, so two
 // stay resident per CU and hide each other's barriers), 512 .. 65536 rows each, a multiple of
@@ -294,8 +252,8 @@ inline int64_t wslab_count(int64_t n) { return (n + gemm_chunk(n) - 1) / gemm_ch
 
 // The two products of each direction run in one dual-GEMM launch (gemm.hip's dual_gemm_kernel: the
 // (X+S, X*S) operands formed at load, dXd / dS formed in the du / dm epilogue -- no U / M arrays, no
-// um / dxs passes; each product the single GEMM's bits).  The separate launches remain only for row
-// strides that are not a multiple of 4 floats (the dual kernel's float4 operand loads).
+// um / dxs passes).  Every entry point requires row strides that are multiples of 4 floats (the dual
+// kernel's float4 operand loads), so there is no separate-launch path.
 
 }  // namespace kgat
 
@@ -308,25 +266,20 @@ static int zero_wgrads(float* dW1, float* db1, float* dW2, float* db2, int32_t d
   return KGAT_OK;
 }
 
-// du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, dW = dA^T U, db = colsum dA
-// (split-K over row chunks, slabs summed in chunk order); U, M and the slabs live in work.
+// du = dA W1, dm = dB W2 (into dXd / dS), dXd = du + dm*S, dS = du + dm*X, dW1 = dA^T (X+S), dW2 = dB^T (X*S),
+// db = colsum dA / dB (split-K over row chunks, slabs summed in chunk order); the slabs live in work.
 static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1, const float* W2,
                          const float* dA, const float* dB, float* dXd, int64_t lddxd, float* dS, int64_t ldds,
                          float* dW1, float* db1, float* dW2, float* db2, int64_t n, int32_t d_in, int32_t d_out,
                          float* work, hipStream_t st, const int32_t* rows = nullptr, int phases = 3) {
-  // rows (dual GEMM only): row r of dA / dB / dXd / dS is row rows[r] of X / S (-1: zero).
+  // rows: row r of dA / dB / dXd / dS is row rows[r] of X / S (-1: zero).
   // phases: bit 1 the dXd / dS GEMM, bit 2 the weight gradients (work keeps what the second needs)
   const int ldu = d_in + 4;
-  float* U = work;
-  float* M = work + n * ldu;
   const int64_t nb = wslab_count(n);
-  float* slab1 = work + 2 * n * ldu;
+  float* slab1 = work;
   float* slab2 = slab1 + nb * d_out * static_cast<int64_t>(ldu);
   float* part = slab2 + nb * d_out * static_cast<int64_t>(ldu);  // [kSlabGroups][d_out][d_in + 1]
-  const bool dual = (ldx & 3) == 0 && (lds & 3) == 0;
-  if (rows != nullptr && !dual) return KGAT_ERR_INVALID;
-  if (phases != 3 && !dual) return KGAT_ERR_INVALID;
-  if (dual && (phases & 1)) {
+  if (phases & 1) {
     // du = dA W1, dm = dB W2, then dXd = du + dm*S, dS = du + dm*X in the epilogue: one launch
     DualGemm g;
     g.dxs = true;
@@ -337,62 +290,40 @@ static int bwd_gemm_tail(const float* X, int64_t ldx, const float* S, int64_t ld
     g.X = X, g.S = S, g.ldx = ldx, g.lds = lds;
     g.erows = rows;
     KGAT_GEMM(dual_gemm_f32(g, st));
-  } else if (!dual) {
-    // du = dA W1 -> dXd, dm = dB W2 -> dS   (row-major [n, o] x [o, k])
-    KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dA, d_out, 0, W1, d_in, 0, dXd, lddxd, 0, 1, false, st));
-    KGAT_GEMM(gemm_f32(false, false, n, d_in, d_out, dB, d_out, 0, W2, d_in, 0, dS, ldds, 0, 1, false, st));
-    hipLaunchKernelGGL(um_kernel, dim3(blocks_for(n * (d_in / 4 + 1), 256, kCUs * 8)), dim3(256), 0,
-                       st, X, ldx, S, lds, U, M, n, d_in, nullptr);
-    KGAT_LAUNCH_CHECK();
-    hipLaunchKernelGGL(dxs_kernel, dim3(blocks_for(n * d_in, 256, kCUs * 8)), dim3(256), 0, st, dXd,
-                       lddxd, dS, ldds, X, ldx, S, lds, n, d_in);
-    KGAT_LAUNCH_CHECK();
   }
   if (!(phases & 2)) return KGAT_OK;
   // [dW | db] = [dA^T U | colsum dA], split over row chunks (deterministic: chunk slabs summed in
   // order): slab_b[d_out, 0:d_in] = dA_b[chunk, d_out]^T . U_b[chunk, d_in], slab_b[:, d_in] = the
-  // chunk's column sums of dA, produced by the same GEMM from its A tiles (a [U | 1] operand
-  // would add a whole 128-wide output tile for its one column)
+  // chunk's column sums of dA, produced by the same GEMM from its A tiles.  [dW1 | db1], [dW2 | db2]
+  // chunk slabs in one launch per batch shape: dA^T (X+S), dB^T (X*S), the operands formed from X and S
+  // at load, the column sums from the dA / dB tiles
   const int64_t chunk = gemm_chunk(n);
   const int64_t full = n / chunk, rest = n - full * chunk;
   const int64_t sl_stride = static_cast<int64_t>(ldu) * d_out;
-  if (dual) {
-    // [dW1 | db1], [dW2 | db2] chunk slabs in one launch per batch shape: dA^T (X+S), dB^T (X*S), the
-    // operands formed from X and S at load, the column sums from the dA / dB tiles
-    DualGemm g;
-    g.ta = true, g.b_um = true;
-    g.M = d_out, g.N = d_in;
-    g.lda1 = g.lda2 = d_out, g.ldb1 = ldx, g.ldb2 = lds;
-    g.ldc1 = g.ldc2 = ldu, g.ldcs = ldu;
-    for (int part = 0; part < 2; ++part) {
-      const int64_t nbat = part == 0 ? full : (rest > 0 ? 1 : 0);
-      if (nbat == 0) continue;
-      const int64_t r0 = part == 0 ? 0 : full * chunk;
-      g.K = part == 0 ? chunk : rest, g.batch = nbat;
-      g.A1 = dA + r0 * d_out, g.A2 = dB + r0 * d_out, g.sA1 = g.sA2 = chunk * d_out;
-      if (rows != nullptr) {  // X / S rows through the list: the chunk offsets move the list
-        g.B1 = X, g.B2 = S, g.sB1 = g.sB2 = 0;
-        g.brows = rows + r0, g.sBrows = chunk;
-      } else {
-        g.B1 = X + r0 * ldx, g.B2 = S + r0 * lds, g.sB1 = chunk * ldx, g.sB2 = chunk * lds;
-      }
-      g.C1 = slab1 + (part == 0 ? 0 : full) * sl_stride, g.C2 = slab2 + (part == 0 ? 0 : full) * sl_stride;
-      g.sC1 = g.sC2 = sl_stride;
-      g.cs1 = g.C1 + d_in, g.cs2 = g.C2 + d_in, g.sCS1 = g.sCS2 = sl_stride;
-      KGAT_GEMM(dual_gemm_f32(g, st));
+  DualGemm g;
+  g.ta = true, g.b_um = true;
+  g.M = d_out, g.N = d_in;
+  g.lda1 = g.lda2 = d_out, g.ldb1 = ldx, g.ldb2 = lds;
+  g.ldc1 = g.ldc2 = ldu, g.ldcs = ldu;
+  for (int pt = 0; pt < 2; ++pt) {
+    const int64_t nbat = pt == 0 ? full : (rest > 0 ? 1 : 0);
+    if (nbat == 0) continue;
+    const int64_t r0 = pt == 0 ? 0 : full * chunk;
+    g.K = pt == 0 ? chunk : rest, g.batch = nbat;
+    g.A1 = dA + r0 * d_out, g.A2 = dB + r0 * d_out, g.sA1 = g.sA2 = chunk * d_out;
+    if (rows != nullptr) {  // X / S rows through the list: the chunk offsets move the list
+      g.B1 = X, g.B2 = S, g.sB1 = g.sB2 = 0;
+      g.brows = rows + r0, g.sBrows = chunk;
+    } else {
+      g.B1 = X + r0 * ldx, g.B2 = S + r0 * lds, g.sB1 = chunk * ldx, g.sB2 = chunk * lds;
     }
+    g.C1 = slab1 + (pt == 0 ? 0 : full) * sl_stride, g.C2 = slab2 + (pt == 0 ? 0 : full) * sl_stride;
+    g.sC1 = g.sC2 = sl_stride;
+    g.cs1 = g.C1 + d_in, g.cs2 = g.C2 + d_in, g.sCS1 = g.sCS2 = sl_stride;
+    KGAT_GEMM(dual_gemm_f32(g, st));
   }
   for (int mat = 0; mat < 2; ++mat) {
-    const float* Um = mat == 0 ? U : M;
-    const float* G = mat == 0 ? dA : dB;
     float* sl = mat == 0 ? slab1 : slab2;
-    if (!dual && full > 0)
-      KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, chunk, G, d_out, chunk * d_out, Um, ldu, chunk * ldu, sl, ldu,
-                                   sl_stride, sl + d_in, ldu, sl_stride, full, st));
-    if (!dual && rest > 0)
-      KGAT_GEMM(gemm_f32_tn_colsum(d_out, d_in, rest, G + full * chunk * d_out, d_out, 0, Um + full * chunk * ldu,
-                                   ldu, 0, sl + full * sl_stride, ldu, 0, sl + full * sl_stride + d_in, ldu, 0, 1,
-                                   st));
     const int eblocks = (d_out * (d_in + 1) + 255) / 256;
     hipLaunchKernelGGL(wslab_part_kernel, dim3(eblocks, kSlabGroups), dim3(256), 0, st, sl, static_cast<int>(nb), d_in,
                        d_out, part);
@@ -417,9 +348,8 @@ extern "C" int64_t kgat_biinter_gemm_state_floats(int64_t n_rows, int32_t d_in, 
 
 extern "C" int64_t kgat_biinter_gemm_work_floats(int64_t n_rows, int32_t d_in, int32_t d_out) {
   if (n_rows < 0 || !gemm_dims_ok(d_in, d_out)) return -1;
-  // U', M' [n, d_in + 4] + two sets of split-K slabs [chunks][d_out][d_in + 4]
-  return n_rows * 2 * static_cast<int64_t>(d_in + 4) +
-         2 * kgat::wslab_count(n_rows) * d_out * static_cast<int64_t>(d_in + 4) +
+  // two sets of split-K slabs [chunks][d_out][d_in + 4] + the two-level reduction's group sums
+  return 2 * kgat::wslab_count(n_rows) * d_out * static_cast<int64_t>(d_in + 4) +
          kgat::kSlabGroups * static_cast<int64_t>(d_out) * (d_in + 1) + 4;
 }
 
@@ -434,29 +364,17 @@ extern "C" int kgat_biinter_fwd_gemm_f32(const float* X, int64_t ldx, const floa
   if (n == 0) return KGAT_OK;
   if (!work || work_floats < kgat_biinter_gemm_work_floats(n, d_in, d_out)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int ldu = d_in + 4;
-  float* U = work;
-  float* M = work + n * ldu;
   float* P1 = state;
   float* P2 = state + n * d_out;
   float* norm = state + 2 * n * d_out;
-  if ((ldx & 3) == 0 && (lds & 3) == 0) {
-    // P1 = (X+S) W1^T, P2 = (X*S) W2^T in one launch, the operands formed at load
-    kgat::DualGemm g;
-    g.tb = true, g.a_um = true;
-    g.M = n, g.N = d_out, g.K = d_in;
-    g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds;
-    g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
-    g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
-    KGAT_GEMM(kgat::dual_gemm_f32(g, st));
-  } else {
-    hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(n * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256),
-                       0, st, X, ldx, S, lds, U, M, n, d_in, nullptr);
-    KGAT_LAUNCH_CHECK();
-    // P[n, o] = U[n, k] . W[o, k]^T
-    KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
-    KGAT_GEMM(kgat::gemm_f32(false, true, n, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
-  }
+  // P1 = (X+S) W1^T, P2 = (X*S) W2^T in one launch, the operands formed at load
+  kgat::DualGemm g;
+  g.tb = true, g.a_um = true;
+  g.M = n, g.N = d_out, g.K = d_in;
+  g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds;
+  g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
+  g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
+  KGAT_GEMM(kgat::dual_gemm_f32(g, st));
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh, norm, n, d_out,
                      dropout_p, seed);
   KGAT_LAUNCH_CHECK();
@@ -480,27 +398,16 @@ extern "C" int kgat_biinter_fwd_gemm_rows_f32(const float* X, int64_t ldx, const
   if (m == 0) return KGAT_OK;
   if (!work || work_floats < kgat_biinter_gemm_rows_work_floats(m, d_in, d_out)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int ldu = d_in + 4;
-  float* U = work;
-  float* M = work + m * ldu;
   float* P1 = work + kgat_biinter_gemm_work_floats(m, d_in, d_out);
   float* P2 = P1 + m * d_out;
-  if ((ldx & 3) == 0 && (lds & 3) == 0) {
-    // P1 = (X+S) W1^T, P2 = (X*S) W2^T on the listed rows, X / S read through the list at load
-    kgat::DualGemm g;
-    g.tb = true, g.a_um = true;
-    g.M = m, g.N = d_out, g.K = d_in;
-    g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds, g.arows = rows;
-    g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
-    g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
-    KGAT_GEMM(kgat::dual_gemm_f32(g, st));
-  } else {
-    hipLaunchKernelGGL(kgat::um_kernel, dim3(kgat::blocks_for(m * (d_in / 4 + 1), 256, kgat::kCUs * 8)), dim3(256),
-                       0, st, X, ldx, S, lds, U, M, m, d_in, rows);
-    KGAT_LAUNCH_CHECK();
-    KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, U, ldu, 0, W1, d_in, 0, P1, d_out, 0, 1, false, st));
-    KGAT_GEMM(kgat::gemm_f32(false, true, m, d_out, d_in, M, ldu, 0, W2, d_in, 0, P2, d_out, 0, 1, false, st));
-  }
+  // P1 = (X+S) W1^T, P2 = (X*S) W2^T on the listed rows, X / S read through the list at load
+  kgat::DualGemm g;
+  g.tb = true, g.a_um = true;
+  g.M = m, g.N = d_out, g.K = d_in;
+  g.A1 = X, g.A2 = S, g.lda1 = ldx, g.lda2 = lds, g.arows = rows;
+  g.B1 = W1, g.B2 = W2, g.ldb1 = g.ldb2 = d_in;
+  g.C1 = P1, g.C2 = P2, g.ldc1 = g.ldc2 = d_out;
+  KGAT_GEMM(kgat::dual_gemm_f32(g, st));
   hipLaunchKernelGGL(kgat::epi_fwd_kernel, dim3((m + 3) / 4), dim3(256), 0, st, P1, P2, b1, b2, H, ldh,
                      state + 2 * n * d_out, m, d_out, dropout_p, seed, rows, state, state + n * d_out);
   KGAT_LAUNCH_CHECK();

@@ -508,22 +508,6 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
   return KGAT_OK;
 }
 
-int gemm_f32_tn_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int64_t sA, const float* B,
-                       int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, float* cs, int64_t ldcs,
-                       int64_t sCS, int64_t batch, hipStream_t st) {
-  if (cs == nullptr) return gemm_f32(true, false, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, false, st);
-  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return KGAT_ERR_INVALID;
-  if ((lda | ldb | sA | sB) & 3 || !aligned16(A) || !aligned16(B) || (M & 3) || (N & 3)) return KGAT_ERR_INVALID;
-  if (lda < M || ldb < N || ldc < N) return KGAT_ERR_INVALID;
-  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
-  if (tiles > 0x7fffffff || batch > 65535) return KGAT_ERR_INVALID;
-  GemmArgs g{A, B, C, lda, ldb, ldc, sA, sB, sC, M, N, K, 0, cs, ldcs, sCS};
-  const dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(batch));
-  KGAT_GEMM_LAUNCH(true, false);
-  KGAT_LAUNCH_CHECK();
-  return KGAT_OK;
-}
-
 }  // namespace kgat
 
 extern "C" int kgat_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t m, int64_t n, int64_t k, const float* A,

@@ -12,13 +12,6 @@ int gemm_f32(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, 
              const float* B, int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, int64_t batch,
              bool accumulate, hipStream_t st);
 
-// The same with ta = true, plus the column sums of op(A) over k: cs[z*sCS + m*ldcs] =
-// sum_k A_z[k][m] (written by the blocks of output tile column 0; per-thread partial sums
-// over fixed k residues combined in a fixed order -- deterministic).  cs may be null.
-int gemm_f32_tn_colsum(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int64_t sA, const float* B,
-                       int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC, float* cs, int64_t ldcs,
-                       int64_t sCS, int64_t batch, hipStream_t st);
-
 // Two products on the same tile coordinates in one launch (gemm.hip's dual_gemm_kernel):
 // C1 = op(A1) op(B1), C2 = op(A2) op(B2), each with gemm_f32's bits.  a_um: (A1, A2) = (X, S)
 // and the products take (X + S, X * S) (not transposed A only); b_um: the same for (B1, B2)

@@ -1254,11 +1254,20 @@ def row_softmax(graph: DeviceGraph, slot_logits: torch.Tensor) -> None:
     A = graph.A
     if LONG_THRESHOLD_SOFTMAX != graph_long_threshold():
         raise RuntimeError("row softmax long-row split must match the CSR plan")
-    tok = _ev_begin("row_softmax")
-    _lib.call("kgat_row_softmax_ex_f32", A.rowptr.data_ptr(), graph.n_nodes, A.long_rows.data_ptr(), A.n_long,
-              slot_logits.data_ptr(), A.val.data_ptr(), stream_ptr(slot_logits.device))
-    _ev_end(tok)
+    row_softmax_csr(A, slot_logits, A.val)
     graph.refresh_transpose()
+
+
+def row_softmax_csr(A, slot_logits: torch.Tensor, val: torch.Tensor) -> None:
+    """val <- softmax over each row's stored entries of a device CSR (graph._DeviceCSR or a shard's),
+    hub rows by their long-row plan segments (kgat_row_softmax_plan_f32)."""
+    desc = A.descriptor()
+    work = torch.empty(max(int(_lib.lib().kgat_row_softmax_work_floats(ctypes.byref(desc))), 1),
+                       dtype=torch.float32, device=slot_logits.device)
+    tok = _ev_begin("row_softmax")
+    _lib.call("kgat_row_softmax_plan_f32", ctypes.byref(desc), slot_logits.data_ptr(), val.data_ptr(),
+              work.data_ptr(), work.numel(), stream_ptr(slot_logits.device))
+    _ev_end(tok)
 
 
 def scores(tables: list[torch.Tensor], users, items) -> torch.Tensor:

@@ -119,6 +119,22 @@ def _hop_record(graph, l: int) -> None:
     graph._hop_est[l][1].record()
 
 
+# A layer that went dense on its last-known hop-set size re-measures the set every this many dense steps.
+HOP_REPROBE_STEPS = 8
+
+
+def _hop_reprobe(graph, l: int) -> None:
+    """Layer l runs densely because its hop set was large at a previous step; no hop listing refreshes the
+    estimate then, so every HOP_REPROBE_STEPS-th such step lists the set anyway from the row flags the
+    previous product left (kgat_hop_compact: the count lands in the pinned mirror, no host sync; the dense
+    path reads none of its outputs) -- a set that shrank takes the layer back to the hop chain."""
+    cnt = graph.__dict__.setdefault("_hop_dense_steps", {})
+    cnt[l] = cnt.get(l, 0) + 1
+    if cnt[l] % HOP_REPROBE_STEPS == 0:
+        kernels.hop_compact(graph, count_host=_hop_host(graph, l))
+        _hop_record(graph, l)
+
+
 class _IdGuard:
     """Ids are range-checked before any kernel indexes a table with them (the reference's
     nn.Embedding gathers raise IndexError, model.py:188-191, 219-222, 389-391).
@@ -982,6 +998,8 @@ class _CFLoss(torch.autograd.Function):
                 if sparse:
                     hrows, hmap, hcount, _ = kernels.hop_compact(graph, count_host=_hop_host(graph, l))
                     _hop_record(graph, l)
+                else:
+                    _hop_reprobe(graph, l)
             elif sparse:
                 # the wide kinds size their compact problem on the host (one synchronisation) -- taken only
                 # when the layer's hop set was small at the previous step; a large one goes dense at once
@@ -992,6 +1010,8 @@ class _CFLoss(torch.autograd.Function):
                                                                      count_host=_hop_host(graph, l))
                     _hop_record(graph, l)
                     sparse = n_hop <= HOP_DENSE_FRACTION * n_nodes
+                else:
+                    _hop_reprobe(graph, l)
             if sparse:
                 # dX is zero outside the hop set: the bi-interaction backward runs on its rows
                 # only and the A^T product gathers from them only (kgat_spmm_csr_masked_ex_f32);
@@ -1407,6 +1427,9 @@ class KGAT(nn.Module):
             self._table_update.discard()
             self._kg_table_update.discard()
             self._kg_graph.release()
+            hook = getattr(self, "_table_grad_hook", None)
+            if hook is not None and opt is getattr(self, "_cf_optimizer", None):
+                hook.abandon_step()  # a pipelined owner step's counter goes back (replicas.ShardedGradSync)
             opt.zero_grad()
             raise
 

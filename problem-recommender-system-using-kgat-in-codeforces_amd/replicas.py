@@ -284,6 +284,7 @@ class ShardedGradSync:
         if self._early is None or self._early[0] is not grad:
             self._early = (grad, [])
             self._bcast, self._stepped = [], set()
+            self._advanced = []  # this step's owner-block optimiser counters advanced by _owner_step
         r0, r1 = self.bounds[k]
         view = grad[r0:r1]
         if k < n and _is_nccl():
@@ -323,12 +324,24 @@ class ShardedGradSync:
                 gv.div_(n)
                 from . import kernels
                 st, step_size, bc2s = opt._advance((id(p), r0, r1), p.data[r0:r1])
+                self._advanced.append((opt, (id(p), r0, r1)))
                 kernels.adam_multi([(p.data[r0:r1], gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s)],
                                    opt.beta1, opt.beta2, opt.eps, model._ids.skip_flag())
                 self._bcast.append(dist.broadcast(p.data[r0:r1], src=j, async_op=True))
             grad.record_stream(side)
         else:
             self._bcast.append(dist.broadcast(p.data[r0:r1], src=j, async_op=True))
+
+    def abandon_step(self) -> None:
+        """The step was abandoned before its update (KGAT._raise_or_abandon: an earlier step's device-side
+        id error surfaced).  The pipelined owner step already took its block's Adam step inside the backward
+        -- a no-op on p / m / v under the device skip flag, but its step counter advanced; it is taken back,
+        so every block's bias correction stays the eager path's (which advances nothing)."""
+        for opt, key in getattr(self, "_advanced", []):
+            st = opt.state.get(key)
+            if st is not None and st["step"] > 0:
+                st["step"] -= 1
+        self._advanced = []
 
     def reduce(self) -> dict | None:
         n = world()

@@ -974,8 +974,7 @@ class RowShardedKGAT(nn.Module):
         _lib.call("kgat_slot_sum_f32", slot_ptr.data_ptr(), slot_order.data_ptr(), nnz, logits.data_ptr(),
                   slot_logits.data_ptr(), st)
         A = sh.A
-        _lib.call("kgat_row_softmax_ex_f32", A.rowptr.data_ptr(), sh.n, A.long_rows.data_ptr(), A.n_long,
-                  slot_logits.data_ptr(), A.val.data_ptr(), st)
+        kernels.row_softmax_csr(A, slot_logits, A.val)
         # A^T's rows live with the owners of A's columns: move the refreshed values there
         send_pos, send_off, recv_inv, recv_off = sh.value_plan()
         send = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)

@@ -89,12 +89,45 @@ def main() -> None:
             if step == 0:
                 with torch.no_grad():  # a loss evaluation without backward opens no exchange
                     m(*b, mode=pkg.KGATMode.TRAIN_CF)
+    # a step abandoned at its update (an out-of-range id, reported by update_cf_weights) takes no
+    # optimiser step on any path -- the pipelined owner step (I) already ran its block's Adam inside the
+    # backward under the device skip flag and takes its step counter back -- and the next good step keeps
+    # every path's bits (I still equal to C below)
+    for bad in (True, False):
+        b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
+                                                  rng.integers(0, E // 10, 64))]
+        if bad:
+            b[0][5] = U + E + 7
+        for k, m in enumerate(models):
+            torch.manual_seed(5000 + int(bad) + rank)
+            frac = model_mod.HOP_DENSE_FRACTION
+            if k == 4 and rank == 1:
+                model_mod.HOP_DENSE_FRACTION = 0.0
+            try:
+                m(*b, mode=pkg.KGATMode.TRAIN_CF).backward()
+            finally:
+                model_mod.HOP_DENSE_FRACTION = frac
+            torch.cuda.synchronize()  # the id check's flag is in: update_cf_weights reports it
+            params = [p for p in m.parameters() if not p.is_sparse and p.requires_grad]
+            try:
+                if k == 0:
+                    rep.allreduce_gradients(params)
+                    m.update_cf_weights()
+                else:
+                    m.update_cf_weights(row_ranges=syncs[k].reduce())
+                raised = False
+            except IndexError:
+                raised = True
+            if k:
+                syncs[k].gather()
+            if raised != bad:
+                failures.append(f"{'ABCDEFGHI'[k]}: bad-id step raised={raised}")
     for tag, want in (("D", "hop"), ("E", "dense"), ("F", "hop"), ("G", "hop")):
         got = syncs["ABCDEFGHI".index(tag)].stats
         # 2 layers: the layer-0 hop set is the first hop (small); 3 layers: the second hop, which may
         # cross HOP_DENSE_FRACTION -- then every rank agrees on the dense exchange
-        if (got.get(want, 0) != 3) if len(layer_size) == 2 else (sum(got.values()) != 3):
-            failures.append(f"{tag}: table exchange paths {got}, expected 3 x {want}")
+        if (got.get(want, 0) != 5) if len(layer_size) == 2 else (sum(got.values()) != 5):
+            failures.append(f"{tag}: table exchange paths {got}, expected 5 x {want}")
     for named in zip(*(m.named_parameters() for m in models)):
         na, pa = named[0]
         if pa.is_sparse:

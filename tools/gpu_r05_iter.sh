@@ -28,6 +28,20 @@ print("full ms", round(d["ms_per_step"], 4), "frontier ms", round(fr.get("ms_per
       "bit_identical", fr.get("bit_identical_to_full", {}).get("pass"), "roofline", round(d["roofline"]["frac"], 3))
 EOF
       ;;
+    benchkg)
+      timeout -k 10 900 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity \
+        > gpurun_out/${TAG}_c2_benchkg.log 2>&1 || { tail -30 gpurun_out/${TAG}_c2_benchkg.log; exit 1; }
+      python3 - gpurun_out/${TAG}_c2_benchkg.log <<'EOF2'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+kg = d.get("kg_refresh", {})
+r = kg.get("refresh", {})
+print("full ms", round(d["ms_per_step"], 4), "frontier ms", round(d.get("frontier_forward", {}).get("ms_per_step", 0), 4))
+print("refresh ms", r.get("ms_per_call"), "edge_scores ms", r.get("edge_scores_avg_ms"), "frac", r.get("roofline", {}).get("frac"),
+      "softmax ms", r.get("row_softmax_avg_ms"), "GB/s", r.get("row_softmax_GBps"))
+print("kg captured ms", kg.get("captured", {}).get("ms_per_step"), "epoch s", kg.get("epoch_estimate", {}).get("seconds"))
+EOF2
+      ;;
     prof)
       rm -rf gpurun_out/${TAG}_prof
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
