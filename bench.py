@@ -885,8 +885,9 @@ class ShareComm:
     force = False
     active = True
 
-    def __init__(self, world: int):
+    def __init__(self, world: int, bounds):
         self.rank, self.world = 0, int(world)
+        self.bounds = [int(x) for x in bounds]
         self.peer_ids = None
 
     def gather_at(self, send, out, starts, sizes):
@@ -895,6 +896,16 @@ class ShareComm:
         own = out[lo:lo + n_own]
         if n_own and send.data_ptr() != own.data_ptr():
             own.copy_(send)
+        if out.dtype == torch.int32 and out.dim() == 1:
+            # a gathered id list (the hop layer's global hop rows): the peers' blocks must be ids their rows
+            # hold -- evenly spaced distinct rows of each peer's range (ascending, as the real gather's)
+            for k in range(1, self.world):
+                s0, n = int(starts[k]), int(sizes[k])
+                if n:
+                    b0, b1 = self.bounds[k], self.bounds[k + 1]
+                    stride = max(1, (b1 - b0) // n)
+                    ids = torch.arange(n, dtype=torch.int64, device=out.device) * stride + b0
+                    out[s0:s0 + n].copy_(ids.clamp_(max=b1 - 1))
         return sh._Pending([])
 
     def gather_v(self, send, out, bounds):
@@ -940,7 +951,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     shard = sh.RowShard(rowptr, col, val, bounds, rank, dev, local=True, transpose=ckg.shard(lo, hi, transpose=True))
     whole = (rowptr, col, val) if parts == 1 and not args.no_parity else None  # the oracle's graph (parity leg)
     del rowptr, col, val
-    comm = ShareComm(share) if share else sh.Comm()
+    comm = ShareComm(share, bounds) if share else sh.Comm()
     nnz_t = torch.tensor([shard.nnz], dtype=torch.int64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(nnz_t)

@@ -557,15 +557,16 @@ int kgat_row_softmax_f32(const int64_t *rowptr, int64_t n_rows, const float *slo
                          void *stream);
 /* kgat_row_softmax_f32 with the rows of more than 256 entries listed
  * (long_rows[0..n_long), e.g. the CSR's long-row plan at threshold 256): those
- * take a block each, the others a 16-lane group with the row in registers.
+ * take a block each, the others 4- or 16-lane groups with the row in registers.
  * long_rows == NULL: the long rows are found by a scan of all rows. */
 int kgat_row_softmax_ex_f32(const int64_t *rowptr, int64_t n_rows, const int32_t *long_rows, int32_t n_long,
                             const float *slot_logits, float *val, void *stream);
 /* a7 with the CSR's long-row plan (seg_len 512, long_threshold 256, as kgat_csr_plan's defaults): rows of
- * <= 256 entries take a 16-lane group each; a longer row is cut into its plan segments -- pass 1 keeps
+ * <= 256 entries 16 per wave, by length class (<= 8 and <= 32 entries: a 4-lane group, 2 / 8 entries per
+ * lane; 33..256: a 16-lane group, 16 per lane); a longer row is cut into its plan segments -- pass 1 keeps
  * each segment's max and sum of exp (work: kgat_row_softmax_work_floats(A) floats), pass 2 combines the
  * row's segments in segment order (max, then the rescaled sums) and every segment writes its entries.
- * A hub row runs on all its segments' waves at once instead of one block. */
+ * A row's values depend on its entries only (the same bits in a row view or a shard). */
 int64_t kgat_row_softmax_work_floats(const kgat_csr *A);
 int kgat_row_softmax_plan_f32(const kgat_csr *A, const float *slot_logits, float *val, float *work,
                               int64_t work_floats, void *stream);

@@ -10,12 +10,13 @@
 //   logit_e = sum_j tanh(o_j) / (log1p(deg_h) + log1p(deg_t))   (per-relation degrees)
 // Edges are processed in 16-edge tiles of ONE relation (a relation-sorted
 // permutation built once per graph), one tile per wave: the three d x d
-// contractions are fp32 MFMA (v_mfma_f32_16x16x4_f32) chains, the tile is
-// re-laid from accumulator layout to operand layout through a per-wave LDS
-// scratch, and LayerNorm / tanh / sum are fused epilogues.
+// contractions are fp32 MFMA (v_mfma_f32_16x16x4_f32) chains computed
+// transposed, so each product's accumulators are the next one's operand (no
+// relayout); dropout, LayerNorm, tanh and the sum are fused epilogues.
 //
 // Neighbour softmax: A[h, :] = softmax over the stored entries of row h
-// (torch.sparse.softmax(dim=1), model.py:364), one wave per CSR row.
+// (torch.sparse.softmax(dim=1), model.py:364): rows by length class (4-lane
+// groups, 16-lane groups, 512-entry segments of hub rows).
 #include <cmath>
 
 #include "common.hpp"
@@ -67,61 +68,30 @@ __device__ __forceinline__ void load_a(const float* __restrict__ P, int64_t ld, 
   }
 }
 
-// C-layout accumulators -> LDS tile [16][D+4] -> A-operand layout registers.
-template <int D>
-__device__ __forceinline__ void relayout(float* tile, const floatx4 (&acc)[D / 16], int q, int c,
-                                         float (&out)[D / 4]) {
-  constexpr int TLD = D + 4, KQ = D / 4;
-#pragma unroll
-  for (int cb = 0; cb < D / 16; ++cb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) tile[(q * 4 + i) * TLD + cb * 16 + c] = acc[cb][i];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const float* src = tile + c * TLD + q * KQ;
-#pragma unroll
-  for (int t = 0; t < KQ; t += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(src + t);
-    out[t] = v.x;
-    out[t + 1] = v.y;
-    out[t + 2] = v.z;
-    out[t + 3] = v.w;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+// tanh from one v_exp_f32 and one v_rcp_f32, branch-free: tanh|x| = (1 - e^{-2|x|}) / (1 + e^{-2|x|}),
+// absolute error ~3e-7 (the logit sums 64 of them).  libm's tanhf is ~25 VALU with branches, 64 per lane
+// per tile -- as much issue time as the tile's MFMA chain.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float t = __expf(-2.f * fabsf(x));
+  return copysignf(__fdividef(1.f - t, 1.f + t), x);
 }
 
-// acc[cb] = A . W^T for nn.Linear weight W [D out][D in] (row stride wld),
-// A in operand layout (k = q*KQ + step).
-template <int D>
-__device__ __forceinline__ void linear_t(const float (&a)[D / 4], const float* W, int wld, int q, int c,
-                                         floatx4 (&acc)[D / 16]) {
-  constexpr int KQ = D / 4;
-#pragma unroll
-  for (int cb = 0; cb < D / 16; ++cb) {
-    __builtin_amdgcn_sched_barrier(0);
-    floatx4 s = {0.f, 0.f, 0.f, 0.f};
-    const float* w = W + (cb * 16 + c) * wld + q * KQ;
-#pragma unroll
-    for (int t = 0; t < KQ; t += 4) {
-      const float4 x = *reinterpret_cast<const float4*>(w + t);
-      s = mfma16x4(a[t], x.x, s);
-      s = mfma16x4(a[t + 1], x.y, s);
-      s = mfma16x4(a[t + 2], x.z, s);
-      s = mfma16x4(a[t + 3], x.w, s);
-    }
-    acc[cb] = s;
-  }
-}
-
+// The scorer computes every contraction transposed (features x edges): out^T = W . in^T, the weights
+// the MFMA A operand and the tile's edges its B operand.  The accumulator layout of one product
+// (lane (q, c): features mb*16 + q*4 + i of edge c) is then the B-operand layout of the next with the
+// contraction index taken in the permuted order k = kb*16 + q*4 + i -- the chain needs no LDS relayout,
+// and each lane's A operand for 4 consecutive MFMAs is one float4 of a weight row.  Per lane: one edge,
+// 16 of its features; LayerNorm and the tanh sum reduce over the 4 lanes c + 16 q.
+//   t'^T = W_r^T e_t^T : A[m][kk] = W_r[q*KQ + t][mb*16 + c], B = e_t[c][q*KQ + t] (load_a's layout)
+//   v^T  = W_v t'^T     : A = W_v[mb*16 + c][kb*16 + q*4 + i], B = t'^T from the accumulators
+//   o^T  = W_o v^T
 template <int D, bool WLDS>
-__global__ __launch_bounds__(256) void edge_score_kernel(EdgeScoreArgs a) {
-  constexpr int KQ = D / 4, NCB = D / 16, WLD = D + 4, TLD = D + 4;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4 : 1))) void edge_score_t_kernel(EdgeScoreArgs a) {
+  constexpr int KQ = D / 4, NB = D / 16, WLD = D + 4;
   constexpr int kDepth = D / 8;  // 8 heads (multi_head_attention.py:6)
   constexpr int kWFloats = WLDS ? 2 * D * WLD : 0;
-  __shared__ __attribute__((aligned(16))) float smem[kWFloats + 4 * 16 * TLD];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  __shared__ __attribute__((aligned(16))) float smem[kWFloats + 4 * D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
   const float* wv = a.Wv;
   const float* wo = a.Wo;
   int wld = D;
@@ -131,90 +101,119 @@ __global__ __launch_bounds__(256) void edge_score_kernel(EdgeScoreArgs a) {
       *reinterpret_cast<float4*>(smem + j * WLD + k) = reinterpret_cast<const float4*>(a.Wv)[i];
       *reinterpret_cast<float4*>(smem + D * WLD + j * WLD + k) = reinterpret_cast<const float4*>(a.Wo)[i];
     }
-    __syncthreads();
     wv = smem;
     wo = smem + D * WLD;
     wld = WLD;
   }
-  float* tile = smem + kWFloats + wave * 16 * TLD;
-  float bv[NCB], bo[NCB], lw[NCB], lb[NCB];
-#pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) {
-    bv[cb] = a.bv[cb * 16 + c];
-    bo[cb] = a.bo[cb * 16 + c];
-    lw[cb] = a.ln_w[cb * 16 + c];
-    lb[cb] = a.ln_b[cb * 16 + c];
+  float* cst = smem + kWFloats;  // b_v, b_o, LayerNorm weight, bias
+  for (int i = threadIdx.x; i < D; i += 256) {
+    cst[i] = a.bv[i];
+    cst[D + i] = a.bo[i];
+    cst[2 * D + i] = a.ln_w[i];
+    cst[3 * D + i] = a.ln_b[i];
   }
+  __syncthreads();
   const float scale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
   for (int tl = blockIdx.x * 4 + wave; tl < a.n_tiles; tl += gridDim.x * 4) {
     const int beg = a.tile_beg[tl], cnt = a.tile_beg[tl + 1] - beg;
     const int64_t r = a.tile_rel[tl];
-    const int ea = c < cnt ? a.rel_perm[beg + c] : -1;  // A-operand row edge
+    const int ec = c < cnt ? a.rel_perm[beg + c] : -1;  // this lane's edge
     float x[KQ];
-    load_a<D>(a.emb, a.ld_emb, ea >= 0 ? static_cast<int64_t>(a.tails[ea]) : -1, q, x);
-    // t' = e_t W_r : B[k][j] = W_r[k][j], k = q*KQ + step
-    floatx4 acc[NCB];
+    load_a<D>(a.emb, a.ld_emb, ec >= 0 ? static_cast<int64_t>(a.tails[ec]) : -1, q, x);
+    uint64_t keep_lo = ~0ull, keep_hi = ~0ull;  // train-mode dropout bits, pair = edge * 8 + head
+    if (a.p > 0.f) {
+      const int er = lane >> 3, head = lane & 7;
+      const int64_t e0 = er < cnt ? a.rel_perm[beg + er] : 0;
+      const int64_t e1 = er + 8 < cnt ? a.rel_perm[beg + er + 8] : 0;
+      keep_lo = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e0) * 8 + head, a.p));
+      keep_hi = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e1) * 8 + head, a.p));
+    }
+    const uint64_t keep = (c < 8 ? keep_lo : keep_hi) >> ((c & 7) * 8);  // this edge's 8 head bits
+    floatx4 acc[NB];
     const float* Wr = a.trans + r * D * D;
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) {
+    for (int mb = 0; mb < NB; ++mb) {
       __builtin_amdgcn_sched_barrier(0);
       floatx4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) s = mfma16x4(x[t], Wr[(q * KQ + t) * D + cb * 16 + c], s);
-      acc[cb] = s;
+      for (int t = 0; t < KQ; ++t) s = mfma16x4(Wr[(q * KQ + t) * D + mb * 16 + c], x[t], s);
+      acc[mb] = s;
     }
-    relayout<D>(tile, acc, q, c, x);
-    // v = W_v t' + b_v, with the per-(edge, head) attention dropout of train mode
-    linear_t<D>(x, wv, wld, q, c, acc);
+    // v^T = W_v t'^T + b_v, dropped per (edge, head)
+    floatx4 acc2[NB];
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb)
+    for (int mb = 0; mb < NB; ++mb) {
+      __builtin_amdgcn_sched_barrier(0);
+      floatx4 s = {0.f, 0.f, 0.f, 0.f};
+      const float* w = wv + (mb * 16 + c) * wld + q * 4;
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        const float4 wk = *reinterpret_cast<const float4*>(w + kb * 16);
+        s = mfma16x4(wk.x, acc[kb][0], s);
+        s = mfma16x4(wk.y, acc[kb][1], s);
+        s = mfma16x4(wk.z, acc[kb][2], s);
+        s = mfma16x4(wk.w, acc[kb][3], s);
+      }
+      const float4 b = *reinterpret_cast<const float4*>(cst + mb * 16 + q * 4);
+      const float bb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = acc[cb][i] + bv[cb];
-        if (a.p > 0.f) {
-          const int er = q * 4 + i;
-          const int64_t e = er < cnt ? a.rel_perm[beg + er] : 0;
-          const int head = (cb * 16 + c) / kDepth;
-          v = dropout_keep(a.seed, static_cast<uint64_t>(e) * 8 + head, a.p) ? v * scale : 0.f;
-        }
-        acc[cb][i] = v;
+        const float v = s[i] + bb[i];
+        const int head = (mb * 16 + q * 4 + i) / kDepth;
+        s[i] = (keep >> head) & 1 ? (a.p > 0.f ? v * scale : v) : 0.f;
       }
-    relayout<D>(tile, acc, q, c, x);
-    // o = W_o v + b_o, then LayerNorm and sum tanh
-    linear_t<D>(x, wo, wld, q, c, acc);
-    float mean[4], var[4], tsum[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float s = 0.f;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        acc[cb][i] += bo[cb];
-        s += acc[cb][i];
-      }
-      mean[i] = sum16(s) / static_cast<float>(D);
-      float v2 = 0.f;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const float dlt = acc[cb][i] - mean[i];
-        v2 = fmaf(dlt, dlt, v2);
-      }
-      var[i] = sum16(v2) / static_cast<float>(D);
-      const float rstd = 1.f / sqrtf(var[i] + kLnEps);
-      float ts = 0.f;
-#pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) ts += tanhf((acc[cb][i] - mean[i]) * rstd * lw[cb] + lb[cb]);
-      tsum[i] = sum16(ts);
+      acc2[mb] = s;
     }
-    if (c == 0) {
+    // o^T = W_o v^T + b_o, then LayerNorm over the features and the tanh sum
+    float sum = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < NB; ++mb) {
+      __builtin_amdgcn_sched_barrier(0);
+      floatx4 s = {0.f, 0.f, 0.f, 0.f};
+      const float* w = wo + (mb * 16 + c) * wld + q * 4;
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        const float4 wk = *reinterpret_cast<const float4*>(w + kb * 16);
+        s = mfma16x4(wk.x, acc2[kb][0], s);
+        s = mfma16x4(wk.y, acc2[kb][1], s);
+        s = mfma16x4(wk.z, acc2[kb][2], s);
+        s = mfma16x4(wk.w, acc2[kb][3], s);
+      }
+      const float4 b = *reinterpret_cast<const float4*>(cst + D + mb * 16 + q * 4);
+      s[0] += b.x;
+      s[1] += b.y;
+      s[2] += b.z;
+      s[3] += b.w;
+      sum += (s[0] + s[1]) + (s[2] + s[3]);
+      acc[mb] = s;
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / static_cast<float>(D);
+    float v2 = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < NB; ++mb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int er = q * 4 + i;
-        if (er < cnt) {
-          const int e = a.rel_perm[beg + er];
-          a.logits[a.out_pos ? a.out_pos[e] : e] = tsum[i] * a.edge_weight[e];
-        }
+        const float dl = acc[mb][i] - mean;
+        v2 = fmaf(dl, dl, v2);
       }
+    v2 += __shfl_xor(v2, 16);
+    v2 += __shfl_xor(v2, 32);
+    const float rstd = 1.f / sqrtf(v2 / static_cast<float>(D) + kLnEps);
+    float ts = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < NB; ++mb) {
+      const float4 lw = *reinterpret_cast<const float4*>(cst + 2 * D + mb * 16 + q * 4);
+      const float4 lb = *reinterpret_cast<const float4*>(cst + 3 * D + mb * 16 + q * 4);
+      ts += tanh_fast((acc[mb][0] - mean) * rstd * lw.x + lb.x);
+      ts += tanh_fast((acc[mb][1] - mean) * rstd * lw.y + lb.y);
+      ts += tanh_fast((acc[mb][2] - mean) * rstd * lw.z + lb.z);
+      ts += tanh_fast((acc[mb][3] - mean) * rstd * lw.w + lb.w);
     }
+    ts += __shfl_xor(ts, 16);
+    ts += __shfl_xor(ts, 32);
+    if (q == 0 && ec >= 0) a.logits[a.out_pos ? a.out_pos[ec] : ec] = ts * a.edge_weight[ec];
   }
 }
 
@@ -232,62 +231,130 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(const int64_t* __restrict
 }
 
 // val[slot] = softmax over the stored entries of each row (model.py:355-366, torch.sparse.softmax).
-// Rows of <= 256 entries (all but the hubs) take a 4-lane group each, 16 rows per wave in flight: a row of
-// <= 32 entries is read once into 8 registers per lane (max, exp-sum, write from registers), a longer one
-// in max / exp-sum / write passes of 32-entry chunks (the later passes re-read it from L1/L2).  Lane j of
-// the group holds entries j, j + 4, ...; the lane partials reduce in a fixed butterfly (deterministic, and
-// the same bits wherever the row sits).  Longer rows: the segment plan below.
+// A wave takes 16 consecutive rows.  Rows of <= 32 entries: a 4-lane group each, read once into 8
+// registers per lane (max, exp-sum, write from registers) -- 16 rows in flight per wave.  Rows of
+// 33..256 entries (half of a power-law CKG's entries): a 16-lane group each, 4 rows per round, 16 entries
+// per lane in registers (one read round instead of a 4-lane group's 8-64 serial ones).  Lane partials reduce in a fixed butterfly relative
+// to the row's first entry: deterministic, and the same bits wherever the row sits.  Longer rows: the
+// segment plan below.
 constexpr int kSoftmaxShort = 256;
 
-__device__ __forceinline__ void short_row_softmax(const int64_t* __restrict__ rowptr, int64_t row, int j,
-                                                  const float* __restrict__ logit, float* __restrict__ val) {
-  const int64_t beg = rowptr[row], end = rowptr[row + 1];
-  const int64_t len = end - beg;
-  if (len == 0 || len > kSoftmaxShort) return;  // (group-uniform) long rows: the segment kernels
-  if (len <= 32) {
-    float x[8];
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t e = beg + j + 4 * k;
-      x[k] = e < end ? logit[e] : -INFINITY;
-      m = fmaxf(m, x[k]);
-    }
-    m = fmaxf(m, __shfl_xor(m, 1));
-    m = fmaxf(m, __shfl_xor(m, 2));
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      x[k] = beg + j + 4 * k < end ? expf(x[k] - m) : 0.f;
-      s += x[k];
-    }
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    const float inv = 1.f / s;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t e = beg + j + 4 * k;
-      if (e < end) val[e] = x[k] * inv;
-    }
-    return;
-  }
+__device__ __forceinline__ void wave_lds_sync() {
+  // orders this wave's LDS writes before its later LDS reads of other lanes' data
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// softmax of one 16-lane group's row held in y[16] (entry gl + 16 k), written to val
+__device__ __forceinline__ void group16_softmax(float (&y)[16], int64_t b, int64_t e1, int gl, float* __restrict__ val) {
   float m = -INFINITY;
-  for (int64_t e = beg + j; e < end; e += 4) m = fmaxf(m, logit[e]);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m = fmaxf(m, y[k]);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    y[k] = b + gl + 16 * k < e1 ? __expf(y[k] - m) : 0.f;
+    s += y[k];
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t e = b + gl + 16 * k;
+    if (e < e1) val[e] = y[k] * inv;
+  }
+}
+
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+  const int lo = __shfl(static_cast<int>(v & 0xffffffff), src);
+  const int hi = __shfl(static_cast<int>(v >> 32), src);
+  return (static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo);
+}
+
+// The k-th (k = this lane's 16-lane group) set bit of med, or -1; med loses its first 4 set bits.
+__device__ __forceinline__ int take_group_row(unsigned long long& med, int g) {
+  int src = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = med ? __ffsll(static_cast<long long>(med)) - 1 : -1;
+    if (k == g) src = f;
+    if (med) med &= med - 1;
+  }
+  return src;
+}
+
+// softmax of one 4-lane group's row held in x[S] (entry j + 4 k), written to val
+template <int S>
+__device__ __forceinline__ void group4_softmax(float (&x)[S], int64_t beg, int64_t end, int j, float* __restrict__ val) {
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < S; ++k) m = fmaxf(m, x[k]);
   m = fmaxf(m, __shfl_xor(m, 1));
   m = fmaxf(m, __shfl_xor(m, 2));
   float s = 0.f;
-  for (int64_t e = beg + j; e < end; e += 4) s += expf(logit[e] - m);
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    x[k] = beg + j + 4 * k < end ? __expf(x[k] - m) : 0.f;
+    s += x[k];
+  }
   s += __shfl_xor(s, 1);
   s += __shfl_xor(s, 2);
   const float inv = 1.f / s;
-  for (int64_t e = beg + j; e < end; e += 4) val[e] = expf(logit[e] - m) * inv;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const int64_t e = beg + j + 4 * k;
+    if (e < end) val[e] = x[k] * inv;
+  }
+}
+
+__device__ __forceinline__ void wave_rows_softmax(const int64_t* __restrict__ rowptr, int64_t n_rows, int64_t row0,
+                                                  int lane, const float* __restrict__ logit, float* __restrict__ val) {
+  const int j = lane & 3, g = lane >> 4, gl = lane & 15;
+  const int64_t row = row0 + (lane >> 2);
+  int64_t beg = 0, end = 0;
+  if (row < n_rows) {
+    beg = rowptr[row];
+    end = rowptr[row + 1];
+  }
+  const int64_t len = end - beg;
+  if (len > 0 && len <= 8) {  // (group-uniform) two entries per lane
+    float x[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) x[k] = beg + j + 4 * k < end ? logit[beg + j + 4 * k] : -INFINITY;
+    group4_softmax<2>(x, beg, end, j, val);
+  } else if (len > 8 && len <= 32) {
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = beg + j + 4 * k < end ? logit[beg + j + 4 * k] : -INFINITY;
+    group4_softmax<8>(x, beg, end, j, val);
+  }
+  unsigned long long med = __ballot(j == 0 && len > 32 && len <= kSoftmaxShort);
+  while (med) {  // rows of 33..256 entries: up to 4 per round, one per 16-lane group
+    const int src = take_group_row(med, g);
+    // (every lane takes part in the shuffles: a source lane may sit in a group with no row this round)
+    const int64_t b2 = shfl64(beg, src < 0 ? 0 : src), e2_src = shfl64(end, src < 0 ? 0 : src);
+    const int64_t e2 = src < 0 ? b2 : e2_src;
+    if (src >= 0) {
+      float y[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int64_t e = b2 + gl + 16 * k;
+        y[k] = e < e2 ? logit[e] : -INFINITY;
+      }
+      group16_softmax(y, b2, e2, gl, val);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void row_softmax_kernel(const int64_t* __restrict__ rowptr, int64_t n_rows,
                                                           const float* __restrict__ logit, float* __restrict__ val) {
-  const int64_t row = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2;
-  if (row >= n_rows) return;  // whole 4-lane groups leave together
-  short_row_softmax(rowptr, row, threadIdx.x & 3, logit, val);
+  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63)) >> 2;
+  if (row0 >= n_rows) return;  // (wave-uniform)
+  wave_rows_softmax(rowptr, n_rows, row0, threadIdx.x & 63, logit, val);
 }
 
 // Long rows, cut into the CSR's long-row plan segments (one wave each, <= kSoftmaxSeg entries, 8 per lane
@@ -302,9 +369,9 @@ __global__ __launch_bounds__(256) void row_softmax_stats_kernel(kgat_csr A, cons
                                                                 float* __restrict__ val, float* __restrict__ stat,
                                                                 int seg_blocks) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // short rows (row_softmax_kernel's body)
-    const int64_t row = (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + threadIdx.x) >> 2;
-    if (row < A.n_rows) short_row_softmax(A.rowptr, row, threadIdx.x & 3, logit, val);
+  if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // rows of <= 256 entries, 16 per wave
+    const int64_t row0 = (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + (threadIdx.x & ~63)) >> 2;
+    if (row0 < A.n_rows) wave_rows_softmax(A.rowptr, A.n_rows, row0, lane, logit, val);
     return;
   }
   const int sg = blockIdx.x * 4 + wave;
@@ -324,7 +391,7 @@ __global__ __launch_bounds__(256) void row_softmax_stats_kernel(kgat_csr A, cons
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < kSoftmaxSeg / 64; ++k) s += beg + lane + 64 * k < end ? expf(x[k] - m) : 0.f;
+  for (int k = 0; k < kSoftmaxSeg / 64; ++k) s += beg + lane + 64 * k < end ? __expf(x[k] - m) : 0.f;
   s = wave_sum(s);
   if (lane == 0) {
     stat[2 * static_cast<int64_t>(sg)] = m;
@@ -339,26 +406,35 @@ __global__ __launch_bounds__(256) void row_softmax_seg_write_kernel(kgat_csr A, 
   const int lane = threadIdx.x & 63;
   if (sg >= A.n_seg) return;
   const int64_t row = A.seg_row[sg];
-  const int64_t rbeg = A.rowptr[row], rend = A.rowptr[row + 1];
   const int64_t beg = A.seg_beg[sg];
+  const int64_t rbeg = A.rowptr[row], rend = A.rowptr[row + 1];
   const int s0 = sg - static_cast<int>((beg - rbeg) / kSoftmaxSeg);  // the row's first segment
   const int ns = static_cast<int>((rend - rbeg + kSoftmaxSeg - 1) / kSoftmaxSeg);
-  float M = -INFINITY;
-  for (int i = lane; i < ns; i += 64) M = fmaxf(M, stat[2 * static_cast<int64_t>(s0 + i)]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
-  float S = 0.f;
-  for (int i = lane; i < ns; i += 64) {
-    const int64_t k = 2 * static_cast<int64_t>(s0 + i);
-    S += stat[k + 1] * expf(stat[k] - M);
-  }
-  S = wave_sum(S);
-  const float inv = 1.f / S;
   const int64_t end = beg + kSoftmaxSeg < rend ? beg + kSoftmaxSeg : rend;
+  // this segment's entries and the row's first 64 segment stats in one round trip
+  float x[kSoftmaxSeg / 64];
 #pragma unroll
   for (int k = 0; k < kSoftmaxSeg / 64; ++k) {
     const int64_t e = beg + lane + 64 * k;
-    if (e < end) val[e] = expf(logit[e] - M) * inv;
+    x[k] = e < end ? logit[e] : 0.f;
+  }
+  const float m0 = lane < ns ? stat[2 * static_cast<int64_t>(s0 + lane)] : -INFINITY;
+  const float z0 = lane < ns ? stat[2 * static_cast<int64_t>(s0 + lane) + 1] : 0.f;
+  float M = m0;
+  for (int i = lane + 64; i < ns; i += 64) M = fmaxf(M, stat[2 * static_cast<int64_t>(s0 + i)]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+  float S = lane < ns ? z0 * __expf(m0 - M) : 0.f;
+  for (int i = lane + 64; i < ns; i += 64) {
+    const int64_t k = 2 * static_cast<int64_t>(s0 + i);
+    S += stat[k + 1] * __expf(stat[k] - M);
+  }
+  S = wave_sum(S);
+  const float inv = 1.f / S;
+#pragma unroll
+  for (int k = 0; k < kSoftmaxSeg / 64; ++k) {
+    const int64_t e = beg + lane + 64 * k;
+    if (e < end) val[e] = __expf(x[k] - M) * inv;
   }
 }
 
@@ -377,9 +453,9 @@ __global__ __launch_bounds__(256) void row_softmax_scan_long_kernel(const int64_
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   float s = 0.f;
-  for (int64_t e = beg + lane; e < end; e += 64) s += expf(logit[e] - m);
+  for (int64_t e = beg + lane; e < end; e += 64) s += __expf(logit[e] - m);
   const float inv = 1.f / wave_sum(s);
-  for (int64_t e = beg + lane; e < end; e += 64) val[e] = expf(logit[e] - m) * inv;
+  for (int64_t e = beg + lane; e < end; e += 64) val[e] = __expf(logit[e] - m) * inv;
 }
 
 // Rows longer than kSoftmaxShort: one 256-thread block per row, block
@@ -401,19 +477,19 @@ __global__ __launch_bounds__(256) void row_softmax_long_kernel(const int64_t* __
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   __syncthreads();
   float s = 0.f;
-  for (int64_t e = beg + threadIdx.x; e < end; e += 256) s += expf(logit[e] - m);
+  for (int64_t e = beg + threadIdx.x; e < end; e += 256) s += __expf(logit[e] - m);
   s = wave_sum(s);
   if (lane == 0) red[wave] = s;
   __syncthreads();
   const float inv = 1.f / (((red[0] + red[1]) + red[2]) + red[3]);
-  for (int64_t e = beg + threadIdx.x; e < end; e += 256) val[e] = expf(logit[e] - m) * inv;
+  for (int64_t e = beg + threadIdx.x; e < end; e += 256) val[e] = __expf(logit[e] - m) * inv;
 }
 
 template <int D>
 static int launch_scores(const EdgeScoreArgs& a, hipStream_t st) {
   constexpr bool wlds = D <= 64;
   const int grid = blocks_for(a.n_tiles, 4, kCUs * 8);
-  hipLaunchKernelGGL((edge_score_kernel<D, wlds>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((edge_score_t_kernel<D, wlds>), dim3(grid), dim3(256), 0, st, a);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -41,15 +41,16 @@ def _mods(pkg):
     return graph, kernels
 
 
-def random_graph(graph_mod, n, avg_deg, hubs=0, hub_deg=0, seed=0):
+def random_graph(graph_mod, n, avg_deg, hubs=0, hub_deg=0, seed=0, mids=0, mid_deg=0):
     rng = np.random.default_rng(seed)
     e = n * avg_deg
     rows = rng.integers(0, n, e)
     cols = rng.integers(0, n, e)
-    if hubs:
-        hr = rng.integers(0, n, hubs)
-        rows = np.concatenate([rows, np.repeat(hr, hub_deg)])
-        cols = np.concatenate([cols, rng.integers(0, n, hubs * hub_deg)])
+    for k, deg in ((hubs, hub_deg), (mids, mid_deg)):
+        if k:
+            hr = rng.integers(0, n, k)
+            rows = np.concatenate([rows, np.repeat(hr, deg)])
+            cols = np.concatenate([cols, rng.integers(0, n, k * deg)])
     vals = rng.standard_normal(rows.size).astype(np.float32)
     rowptr, col, val = graph_mod.csr_from_coo(n, rows, cols, vals)
     lay = graph_mod.GraphLayout(n_nodes=n, rel_order=[], heads=np.zeros(0, np.int64), rels=np.zeros(0, np.int64),
@@ -602,13 +603,16 @@ def test_biinter_fwd_row_blocks_bit_identical(pkg, din, dout):
 
 
 def test_row_softmax_short_and_long_rows(pkg):
-    """a7: the 16-lane short-row softmax + the hub rows by their long-row plan segments (model.py:355-366)
+    """a7: the windowed short-row softmax + the hub rows by their long-row plan segments (model.py:355-366)
     against torch.sparse.softmax on the same CSR; the scan fallback (no long-row list: a block per hub
-    row) agrees to fp32 rounding (the segmented sum associates the hub rows' terms differently)."""
+    row) agrees to fp32 rounding.  A row's bits do not depend on where the entry windows cut: a row view
+    starting mid-window (as a shard's rows) reproduces the whole-CSR values bit for bit."""
     graph_mod, kernels = _mods(pkg)
-    lay, A = random_graph(graph_mod, 4000, 9, hubs=4, hub_deg=3000, seed=17)
+    # short rows (~9), 300 rows of 33..256 entries, 4 hubs of ~3000 (several 512-entry segments each)
+    lay, A = random_graph(graph_mod, 4000, 9, hubs=4, hub_deg=3000, seed=17, mids=300, mid_deg=90)
     g = graph_mod.DeviceGraph(lay, DEV)
-    assert g.A.n_long > 0
+    deg = np.diff(lay.rowptr)
+    assert g.A.n_long > 0 and ((deg > 32) & (deg <= 256)).sum() > 200
     logits = torch.randn(lay.nnz) * 3
     kernels.row_softmax(g, logits.to(DEV))
     got = g.A.val.detach().cpu()
@@ -619,8 +623,13 @@ def test_row_softmax_short_and_long_rows(pkg):
     lib.call("kgat_row_softmax_f32", g.A.rowptr.data_ptr(), g.n_nodes, logits.to(DEV).data_ptr(), out.data_ptr(),
              torch.cuda.current_stream().cuda_stream)
     np.testing.assert_allclose(out.cpu().numpy(), got.numpy(), rtol=1e-5, atol=1e-8)
-    short = np.repeat(np.diff(lay.rowptr) <= 256, np.diff(lay.rowptr))
-    assert np.array_equal(out.cpu().numpy()[short], got.numpy()[short])  # short rows: the same kernel body
+    for r0, r1 in ((0, 4000), (7, 3901), (1234, 1300), (2999, 4000)):
+        view = graph_mod._CSRRowView(g.A, r0, r1, DEV)
+        part = torch.full((lay.nnz,), float("nan"), device=DEV)
+        kernels.row_softmax_csr(view, logits.to(DEV), part)
+        e0, e1 = int(lay.rowptr[r0]), int(lay.rowptr[r1])
+        assert torch.equal(part[e0:e1].cpu(), got[e0:e1]), (r0, r1)
+        assert torch.isnan(part[:e0]).all() and torch.isnan(part[e1:]).all()  # nothing written outside
 
 
 def test_biinter_bwd_rows_matches_dense(pkg):

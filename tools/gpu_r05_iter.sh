@@ -52,6 +52,18 @@ EOF2
       python3 tools/step_timeline.py "$T" bpr_fwd_kernel -6 > gpurun_out/${TAG}_frontier_step.txt
       tail -1 gpurun_out/${TAG}_full_step.txt
       tail -1 gpurun_out/${TAG}_frontier_step.txt ;;
+    profkg)
+      rm -rf gpurun_out/${TAG}_profkg
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_profkg -o run --output-format csv -- \
+        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-frontier-leg \
+        > gpurun_out/${TAG}_profkg.log 2>&1 || { tail -20 gpurun_out/${TAG}_profkg.log; exit 1; }
+      S=$(find gpurun_out/${TAG}_profkg -name "*kernel_stats.csv" | head -1)
+      cp "$S" gpurun_out/${TAG}_profkg_stats.csv
+      grep -E "softmax|score|slot_sum" "$S" | cut -c1-200 ;;
+    c5small)
+      timeout -k 10 400 python -u bench.py --config c5 --scale 0.02 --rank-share 8 --steps 3 --warmup 1 --no-cpu-baseline \
+        > gpurun_out/${TAG}_c5small.log 2>&1 || { tail -30 gpurun_out/${TAG}_c5small.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_c5small.log | cut -c1-400 ;;
     hostprof)
       timeout -k 10 300 python3 tools/host_profile.py > gpurun_out/${TAG}_host.txt 2>&1 || { tail -20 gpurun_out/${TAG}_host.txt; exit 1; }
       timeout -k 10 300 python3 tools/host_profile.py --full > gpurun_out/${TAG}_host_full.txt 2>&1 || { tail -20 gpurun_out/${TAG}_host_full.txt; exit 1; }
