@@ -1040,7 +1040,9 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         fms = fel / args.steps * 1e3
         res["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
-            "bit_identical_to_full": sharded_frontier_matches_full(model, pkg, batches[0]),
+            "bit_identical_to_full": sharded_frontier_matches_full(model, pkg, batches[0]) if not share else {
+                "pass": None, "what": "not checked in a rank share: the peers' rows of every gathered buffer are "
+                                      "never computed, so the two forwards read different (uninitialised) rows"},
             "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer L-1 on the batch rows, "
                     "layer L-2 on F + N(F)); not counted in value (it does not visit every edge)"}
     if whole is not None and rank == 0:
