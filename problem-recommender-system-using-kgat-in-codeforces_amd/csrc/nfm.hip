@@ -359,6 +359,132 @@ __global__ __launch_bounds__(256, NC <= 4 ? 3 : NC <= 8 ? 2 : 1) void nfm_fwd_ke
 }
 
 
+// Inference forward (PREDICT / eval: no dropout, no saved activations) for feature widths that are
+// multiples of 16 up to 128: every MLP layer computed transposed, pre^T = W h^T with the weights the MFMA A
+// operand and the tile's 16 rows its B operand, so a layer's accumulators (lane (q, c): features
+// mb*16 + q*4 + i of row c) are the next layer's operand -- no LDS tile between layers -- and each lane's A
+// operand of 4 consecutive MFMAs is one float4 of a weight row (all layers staged in LDS once per block).
+// Pooling produces that layout directly: the four lanes c + 16 q of a row each read a quarter of every entry's
+// feature row (float4 at kb*16 + q*4), 16 rows per wave at once; per feature the entries are summed in entry
+// order (s and sum of squares: the training kernel's z bits).
+constexpr int kNfmTB = 8;  // 16-wide feature blocks (widths <= 128)
+
+struct NfmTPlan {
+  int w_off[kNfmMaxLayers], pitch[kNfmMaxLayers], b_off[kNfmMaxLayers];
+  int wout_off, total;
+};
+
+__global__ __launch_bounds__(1024) void nfm_fwd_t_kernel(NfmNet N, NfmTPlan plan, const int64_t* __restrict__ rowptr,
+                                                         const int64_t* __restrict__ col,
+                                                         const float* __restrict__ val, int64_t rows,
+                                                         float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  for (int l = 0; l < N.n_layers; ++l) {
+    const int din = N.dims[l], dout = N.dims[l + 1];
+    for (int t = threadIdx.x; t < din * dout; t += 1024) {
+      const int n = t / din, k = t - n * din;
+      smem[plan.w_off[l] + n * plan.pitch[l] + k] = N.W[l][t];
+    }
+    for (int t = threadIdx.x; t < dout; t += 1024) smem[plan.b_off[l] + t] = N.b[l][t];
+  }
+  for (int t = threadIdx.x; t < N.dims[N.n_layers]; t += 1024) smem[plan.wout_off + t] = N.W_out[t];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  const int nb0 = N.dims[0] >> 4;
+  const int64_t ntiles = (rows + 15) / 16;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * 16 + wave; t < ntiles; t += static_cast<int64_t>(gridDim.x) * 16) {
+    const int64_t r = t * 16 + c;
+    float h[kNfmTB][4];
+    float wd = 0.f;
+    {
+      float sq[kNfmTB][4];
+#pragma unroll
+      for (int kb = 0; kb < kNfmTB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[kb][i] = sq[kb][i] = 0.f;
+      if (r < rows) {
+        const int64_t beg = rowptr[r], end = rowptr[r + 1];
+        int64_t cn = beg < end ? col[beg] : 0;  // the next entry's id and value load under this one's row
+        float xn = beg < end ? val[beg] : 0.f;
+        for (int64_t e = beg; e < end; ++e) {
+          const int64_t ce = cn;
+          const float xe = xn;
+          if (e + 1 < end) {
+            cn = col[e + 1];
+            xn = val[e + 1];
+          }
+          const float* v = N.V + ce * N.ldv + q * 4;
+#pragma unroll
+          for (int kb = 0; kb < kNfmTB; ++kb) {
+            if (kb < nb0) {
+              const float4 f = *reinterpret_cast<const float4*>(v + kb * 16);
+              const float tv[4] = {xe * f.x, xe * f.y, xe * f.z, xe * f.w};
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                h[kb][i] += tv[i];
+                sq[kb][i] = fmaf(tv[i], tv[i], sq[kb][i]);
+              }
+            }
+          }
+          wd = fmaf(xe, N.w_lin[ce], wd);  // the wide head, entries in order (every lane of the row alike)
+        }
+      }
+#pragma unroll
+      for (int kb = 0; kb < kNfmTB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[kb][i] = 0.5f * (h[kb][i] * h[kb][i] - sq[kb][i]);
+    }
+    for (int l = 0; l < N.n_layers; ++l) {
+      const int nbi = N.dims[l] >> 4, nbo = N.dims[l + 1] >> 4, pitch = plan.pitch[l];
+      const float* W = smem + plan.w_off[l] + c * pitch + q * 4;
+      const float* bs = smem + plan.b_off[l] + q * 4;
+      float o[kNfmTB][4];
+#pragma unroll
+      for (int mb = 0; mb < kNfmTB; ++mb) {
+        o[mb][0] = o[mb][1] = o[mb][2] = o[mb][3] = 0.f;
+        if (mb < nbo) {  // (wave-uniform)
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* w = W + mb * 16 * pitch;
+#pragma unroll
+          for (int kb = 0; kb < kNfmTB; ++kb) {
+            if (kb < nbi) {
+              const float4 wk = *reinterpret_cast<const float4*>(w + kb * 16);
+              acc = mfma16x4(wk.x, h[kb][0], acc);
+              acc = mfma16x4(wk.y, h[kb][1], acc);
+              acc = mfma16x4(wk.z, h[kb][2], acc);
+              acc = mfma16x4(wk.w, h[kb][3], acc);
+            }
+          }
+          const float4 b = *reinterpret_cast<const float4*>(bs + mb * 16);
+          o[mb][0] = fmaxf(acc[0] + b.x, 0.f);
+          o[mb][1] = fmaxf(acc[1] + b.y, 0.f);
+          o[mb][2] = fmaxf(acc[2] + b.z, 0.f);
+          o[mb][3] = fmaxf(acc[3] + b.w, 0.f);
+        }
+      }
+#pragma unroll
+      for (int mb = 0; mb < kNfmTB; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[mb][i] = o[mb][i];
+    }
+    const int nbl = N.dims[N.n_layers] >> 4;
+    float deep = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < kNfmTB; ++mb) {
+      if (mb < nbl) {
+        const float4 wo = *reinterpret_cast<const float4*>(smem + plan.wout_off + mb * 16 + q * 4);
+        deep = fmaf(wo.x, h[mb][0], deep);
+        deep = fmaf(wo.y, h[mb][1], deep);
+        deep = fmaf(wo.z, h[mb][2], deep);
+        deep = fmaf(wo.w, h[mb][3], deep);
+      }
+    }
+    deep += __shfl_xor(deep, 16);
+    deep += __shfl_xor(deep, 32);
+    if (q == 0 && r < rows) y[r] = (wd + N.b_lin[0]) + deep;
+  }
+}
+
 // loss over B pairs (rows b and B+b); dy[row] = dL/dy (before the upstream scale)
 __global__ __launch_bounds__(256) void nfm_loss_kernel(const float* __restrict__ y, int batch, const float* __restrict__ W_out,
                                                        int dl, float lam, float* __restrict__ loss,
@@ -754,6 +880,43 @@ extern "C" int kgat_nfm_fwd_f32(const kgat_nfm* net, const int64_t* rowptr, cons
   if (rows == 0) return KGAT_OK;
   int dmax = 16;
   for (int l = 0; l <= N.n_layers; ++l) dmax = N.dims[l] > dmax ? N.dims[l] : dmax;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // inference (no dropout, nothing saved) at widths that are multiples of 16 up to 128: the transposed-MLP
+  // kernel with every layer's weights in LDS
+  bool t_ok = act == nullptr && N.p == 0.f && N.n_layers >= 1 && (N.ldv & 3) == 0 &&
+              (reinterpret_cast<uintptr_t>(N.V) & 15) == 0;
+  for (int l = 0; l <= N.n_layers && t_ok; ++l) t_ok = N.dims[l] % 16 == 0 && N.dims[l] <= 16 * kgat::kNfmTB;
+  if (t_ok) {
+    kgat::NfmTPlan tp{};
+    int to = 0;
+    for (int l = 0; l < N.n_layers; ++l) {
+      tp.w_off[l] = to;
+      tp.pitch[l] = N.dims[l] + 4;  // rows 4 banks apart for the float4 A-operand reads
+      to += N.dims[l + 1] * tp.pitch[l];
+      tp.b_off[l] = to;
+      to += N.dims[l + 1];
+    }
+    tp.wout_off = to;
+    to += N.dims[N.n_layers];
+    tp.total = to;
+    const size_t tlds = sizeof(float) * static_cast<size_t>(to);
+    if (tlds <= 150 * 1024) {
+      const void* fn = reinterpret_cast<const void*>(kgat::nfm_fwd_t_kernel);
+      if (tlds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(tlds));
+        if (e != hipSuccess) return static_cast<int>(e);
+      }
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 1024, tlds) != hipSuccess || per_cu < 1) per_cu = 1;
+      const int64_t tiles = (rows + 15) / 16;
+      const int64_t cap = static_cast<int64_t>(per_cu) * kgat::kCUs;
+      const int64_t need = (tiles + 15) / 16;
+      hipLaunchKernelGGL(kgat::nfm_fwd_t_kernel, dim3(static_cast<unsigned>(need < cap ? need : cap)), dim3(1024), tlds,
+                         st, N, tp, rowptr, col, val, rows, y);
+      KGAT_LAUNCH_CHECK();
+      return KGAT_OK;
+    }
+  }
   kgat::NfmLds plan{};
   plan.P = ((dmax + 15) & ~15) + 4;  // tile pitch: rows 4 banks apart
   int o = 0;
@@ -768,7 +931,6 @@ extern "C" int kgat_nfm_fwd_f32(const kgat_nfm* net, const int64_t* rowptr, cons
   plan.tile_off = plan.wlds ? o : 0;
   plan.total = plan.tile_off + 4 * 16 * plan.P;
   const size_t lds = sizeof(float) * static_cast<size_t>(plan.total);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nc = dmax <= 64 ? 4 : dmax <= 128 ? 8 : 16;
   // float4 pooling loads where the feature rows allow them (bit-identical: per column the same sums)
   const bool v4 = (N.dims[0] & 3) == 0 && (N.ldv & 3) == 0 && (reinterpret_cast<uintptr_t>(N.V) & 15) == 0;

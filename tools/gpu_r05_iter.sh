@@ -60,6 +60,27 @@ EOF2
       S=$(find gpurun_out/${TAG}_profkg -name "*kernel_stats.csv" | head -1)
       cp "$S" gpurun_out/${TAG}_profkg_stats.csv
       grep -E "softmax|score|slot_sum" "$S" | cut -c1-200 ;;
+    nfm)
+      timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "nfm or NFM" \
+        > gpurun_out/${TAG}_nfm_tests.log 2>&1 || { grep -E "^E |FAILED|Error" gpurun_out/${TAG}_nfm_tests.log | head -30; exit 1; }
+      tail -1 gpurun_out/${TAG}_nfm_tests.log ;;
+    c3prof)
+      rm -rf gpurun_out/${TAG}_c3prof
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_c3prof -o run --output-format csv -- \
+        python3 bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-kg-leg \
+        > gpurun_out/${TAG}_c3prof.log 2>&1 || { tail -20 gpurun_out/${TAG}_c3prof.log; exit 1; }
+      S=$(find gpurun_out/${TAG}_c3prof -name "*kernel_stats.csv" | head -1)
+      grep -E "nfm" "$S" | cut -c1-160
+      python3 - gpurun_out/${TAG}_c3prof.log <<'EOF3'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+nf = d.get("nfm", {})
+print("c3 ms", round(d["ms_per_step"], 3), "nfm keys", list(nf.keys())[:12])
+for k in ("predict", "train"):
+    if k in nf:
+        print(k, {kk: nf[k][kk] for kk in list(nf[k])[:10]})
+EOF3
+      ;;
     c5small)
       timeout -k 10 400 python -u bench.py --config c5 --scale 0.02 --rank-share 8 --steps 3 --warmup 1 --no-cpu-baseline \
         > gpurun_out/${TAG}_c5small.log 2>&1 || { tail -30 gpurun_out/${TAG}_c5small.log; exit 1; }
