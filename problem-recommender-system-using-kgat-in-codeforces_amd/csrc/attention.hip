@@ -311,32 +311,61 @@ __device__ __forceinline__ void group4_softmax(float (&x)[S], int64_t beg, int64
   }
 }
 
+// A wave takes kSoftmaxRG x 16 rows: 4-lane group g4 the rows row0 + g4 + 16 t (t < kSoftmaxRG), all their
+// row pointers, then all their entries, in flight together before the first reduction.
+constexpr int kSoftmaxRG = 2;
+
 __device__ __forceinline__ void wave_rows_softmax(const int64_t* __restrict__ rowptr, int64_t n_rows, int64_t row0,
                                                   int lane, const float* __restrict__ logit, float* __restrict__ val) {
-  const int j = lane & 3, g = lane >> 4, gl = lane & 15;
-  const int64_t row = row0 + (lane >> 2);
-  int64_t beg = 0, end = 0;
-  if (row < n_rows) {
-    beg = rowptr[row];
-    end = rowptr[row + 1];
-  }
-  const int64_t len = end - beg;
-  if (len > 0 && len <= 8) {  // (group-uniform) two entries per lane
-    float x[2];
+  constexpr int R = kSoftmaxRG;
+  const int j = lane & 3, g = lane >> 4, gl = lane & 15, g4 = lane >> 2;
+  int64_t beg[R], end[R];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) x[k] = beg + j + 4 * k < end ? logit[beg + j + 4 * k] : -INFINITY;
-    group4_softmax<2>(x, beg, end, j, val);
-  } else if (len > 8 && len <= 32) {
-    float x[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = beg + j + 4 * k < end ? logit[beg + j + 4 * k] : -INFINITY;
-    group4_softmax<8>(x, beg, end, j, val);
+  for (int t = 0; t < R; ++t) {
+    const int64_t row = row0 + g4 + 16 * t;
+    beg[t] = end[t] = 0;
+    if (row < n_rows) {
+      beg[t] = rowptr[row];
+      end[t] = rowptr[row + 1];
+    }
   }
-  unsigned long long med = __ballot(j == 0 && len > 32 && len <= kSoftmaxShort);
-  while (med) {  // rows of 33..256 entries: up to 4 per round, one per 16-lane group
+  float x[R][8];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    const int64_t len = end[t] - beg[t];
+    const int slots = len <= 8 ? 2 : 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = beg[t] + j + 4 * k;
+      x[t][k] = len <= 32 && k < slots && e < end[t] ? logit[e] : -INFINITY;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    const int64_t len = end[t] - beg[t];
+    if (len > 0 && len <= 8) {  // (group-uniform) two entries per lane
+      float x2[2] = {x[t][0], x[t][1]};
+      group4_softmax<2>(x2, beg[t], end[t], j, val);
+    } else if (len > 8 && len <= 32) {
+      group4_softmax<8>(x[t], beg[t], end[t], j, val);
+    }
+  }
+  // rows of 33..256 entries: up to 4 per round, one per 16-lane group; lane 4 g4 + t reports row t of its group
+  bool is_med = false;
+  int64_t pb = 0, pe = 0;
+#pragma unroll
+  for (int t = 0; t < R; ++t)
+    if (j == t) {
+      const int64_t len = end[t] - beg[t];
+      is_med = len > 32 && len <= kSoftmaxShort;
+      pb = beg[t];
+      pe = end[t];
+    }
+  unsigned long long med = __ballot(is_med);
+  while (med) {
     const int src = take_group_row(med, g);
     // (every lane takes part in the shuffles: a source lane may sit in a group with no row this round)
-    const int64_t b2 = shfl64(beg, src < 0 ? 0 : src), e2_src = shfl64(end, src < 0 ? 0 : src);
+    const int64_t b2 = shfl64(pb, src < 0 ? 0 : src), e2_src = shfl64(pe, src < 0 ? 0 : src);
     const int64_t e2 = src < 0 ? b2 : e2_src;
     if (src >= 0) {
       float y[16];
@@ -352,7 +381,7 @@ __device__ __forceinline__ void wave_rows_softmax(const int64_t* __restrict__ ro
 
 __global__ __launch_bounds__(256) void row_softmax_kernel(const int64_t* __restrict__ rowptr, int64_t n_rows,
                                                           const float* __restrict__ logit, float* __restrict__ val) {
-  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63)) >> 2;
+  const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63)) / 4 * kSoftmaxRG;
   if (row0 >= n_rows) return;  // (wave-uniform)
   wave_rows_softmax(rowptr, n_rows, row0, threadIdx.x & 63, logit, val);
 }
@@ -370,7 +399,8 @@ __global__ __launch_bounds__(256) void row_softmax_stats_kernel(kgat_csr A, cons
                                                                 int seg_blocks) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // rows of <= 256 entries, 16 per wave
-    const int64_t row0 = (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + (threadIdx.x & ~63)) >> 2;
+    const int64_t row0 =
+        (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + (threadIdx.x & ~63)) / 4 * kSoftmaxRG;
     if (row0 < A.n_rows) wave_rows_softmax(A.rowptr, A.n_rows, row0, lane, logit, val);
     return;
   }
@@ -507,7 +537,7 @@ extern "C" int kgat_row_softmax_plan_f32(const kgat_csr* A, const float* slot_lo
   if (!work || work_floats < kgat_row_softmax_work_floats(A)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int seg_blocks = (A->n_seg + 3) / 4;
-  const int64_t grid = seg_blocks + (A->n_rows * 4 + 255) / 256;
+  const int64_t grid = seg_blocks + (A->n_rows * 4 / kgat::kSoftmaxRG + 255) / 256;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(kgat::row_softmax_stats_kernel, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
                      seg_blocks);
@@ -526,7 +556,8 @@ extern "C" int kgat_row_softmax_ex_f32(const int64_t* rowptr, int64_t n_rows, co
     return KGAT_ERR_INVALID;
   if (n_rows == 0) return KGAT_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows * 4 + 255) / 256), dim3(256), 0, st, rowptr, n_rows,
+  hipLaunchKernelGGL(kgat::row_softmax_kernel, dim3((n_rows * 4 / kgat::kSoftmaxRG + 255) / 256), dim3(256), 0, st,
+                     rowptr, n_rows,
                      slot_logits, val);
   KGAT_LAUNCH_CHECK();
   if (long_rows == nullptr) {
