@@ -85,8 +85,8 @@ __device__ __forceinline__ float tanh_fast(float x) {
 //   t'^T = W_r^T e_t^T : A[m][kk] = W_r[q*KQ + t][mb*16 + c], B = e_t[c][q*KQ + t] (load_a's layout)
 //   v^T  = W_v t'^T     : A = W_v[mb*16 + c][kb*16 + q*4 + i], B = t'^T from the accumulators
 //   o^T  = W_o v^T
-template <int D, bool WLDS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4 : 1))) void edge_score_t_kernel(EdgeScoreArgs a) {
+template <int D, bool WLDS, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4 : 1))) void edge_score_t_kernel(EdgeScoreArgs a) {
   constexpr int KQ = D / 4, NB = D / 16, WLD = D + 4;
   constexpr int kDepth = D / 8;  // 8 heads (multi_head_attention.py:6)
   constexpr int kWFloats = WLDS ? 2 * D * WLD : 0;
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
   const float* wo = a.Wo;
   int wld = D;
   if constexpr (WLDS) {
-    for (int i = threadIdx.x; i < D * D / 4; i += 256) {
+    for (int i = threadIdx.x; i < D * D / 4; i += 64 * NW) {
       const int j = (i * 4) / D, k = (i * 4) % D;
       *reinterpret_cast<float4*>(smem + j * WLD + k) = reinterpret_cast<const float4*>(a.Wv)[i];
       *reinterpret_cast<float4*>(smem + D * WLD + j * WLD + k) = reinterpret_cast<const float4*>(a.Wo)[i];
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
     wld = WLD;
   }
   float* cst = smem + kWFloats;  // b_v, b_o, LayerNorm weight, bias
-  for (int i = threadIdx.x; i < D; i += 256) {
+  for (int i = threadIdx.x; i < D; i += 64 * NW) {
     cst[i] = a.bv[i];
     cst[D + i] = a.bo[i];
     cst[2 * D + i] = a.ln_w[i];
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
   }
   __syncthreads();
   const float scale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
-  for (int tl = blockIdx.x * 4 + wave; tl < a.n_tiles; tl += gridDim.x * 4) {
+  for (int tl = blockIdx.x * NW + wave; tl < a.n_tiles; tl += gridDim.x * NW) {
     const int beg = a.tile_beg[tl], cnt = a.tile_beg[tl + 1] - beg;
     const int64_t r = a.tile_rel[tl];
     const int ec = c < cnt ? a.rel_perm[beg + c] : -1;  // this lane's edge
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
     const float* Wr = a.trans + r * D * D;
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) {
-      __builtin_amdgcn_sched_barrier(0);
+      // (product 1: the column blocks' chains interleave)
       floatx4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < KQ; ++t) s = mfma16x4(Wr[(q * KQ + t) * D + mb * 16 + c], x[t], s);
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
     floatx4 acc2[NB];
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) {
-      __builtin_amdgcn_sched_barrier(0);
+      if (mb % 2 == 0) __builtin_amdgcn_sched_barrier(0);  // two column blocks' chains interleave
       floatx4 s = {0.f, 0.f, 0.f, 0.f};
       const float* w = wv + (mb * 16 + c) * wld + q * 4;
 #pragma unroll
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4
     float sum = 0.f;
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) {
-      __builtin_amdgcn_sched_barrier(0);
+      if (mb % 2 == 0) __builtin_amdgcn_sched_barrier(0);  // two column blocks' chains interleave
       floatx4 s = {0.f, 0.f, 0.f, 0.f};
       const float* w = wo + (mb * 16 + c) * wld + q * 4;
 #pragma unroll
@@ -519,7 +519,8 @@ template <int D>
 static int launch_scores(const EdgeScoreArgs& a, hipStream_t st) {
   constexpr bool wlds = D <= 64;
   const int grid = blocks_for(a.n_tiles, 4, kCUs * 8);
-  hipLaunchKernelGGL((edge_score_t_kernel<D, wlds>), dim3(grid), dim3(256), 0, st, a);
+  // (4 waves per block: 8-wave blocks at 6 waves / SIMD measured 6.14 vs 6.05 ms at C2 -- not occupancy-bound)
+  hipLaunchKernelGGL((edge_score_t_kernel<D, wlds, 4>), dim3(grid), dim3(256), 0, st, a);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
