@@ -230,3 +230,28 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus, config, scale):
         assert sum(fr["dp_table_exchange_steps"].values()) == 4
     if config == "c4":
         assert rec["config"]["embed_dim"] == 128 and rec["config"]["layer_size"] == [128, 64, 32]
+
+
+def test_bench_c5_rank_share_small():
+    """bench.py --rank-share K (one process, rank 0 of K alone: its rows of A / A^T, the full gathered layer
+    buffers, the global batch from simulated peers, every collective local) at a tiny C5 scale: one JSON line
+    with the share's shapes and HBM high-water mark, and a finite loss."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "c5", "--scale", "0.002", "--rank-share", "4",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    rs = rec["rank_share"]
+    assert rec["n_gpus"] == 1 and rs["ranks"] == 4 and rs["rank"] == 0
+    assert 0 < rs["shard_rows"] < rec["config"]["nodes"] and rs["shard_nnz_A"] > 0
+    assert 0 < rs["hbm_peak_bytes"] and rec["value"] > 0 and np.isfinite(rec["final_loss"])
+    assert rec["frontier_forward"]["bit_identical_to_full"]["pass"] is None  # not checkable in a share
