@@ -625,6 +625,7 @@ class _KGStepGraph:
             kernels.KERNEL_EVENTS, kernels.SPMM_EVENTS = ev
         b.update(rows=rows, loss=loss, work=work, Gc=grads[0], d_rel=grads[1], d_trans=grads[2])
         self.g, self.buf = g, b
+        self.gout_one = True  # b["gout"] starts as ones
         self.t_dev_value = None
         self.key = self._key(B, opt, ps, sts)
 
@@ -652,12 +653,20 @@ class _KGStepGraph:
         self.replays += 1
         return b["loss"]
 
-    def backward(self, gout: torch.Tensor) -> None:
-        """The upstream gradient into the graphs' input; the TransR backward runs in the update graph."""
+    def backward(self, gout: torch.Tensor | None) -> None:
+        """The upstream gradient into the graphs' input; the TransR backward runs in the update graph.
+        ``gout`` None: the plain ``loss.backward()`` (upstream gradient 1, written only when a scaled one
+        was there before)."""
         if self.pending != "fwd":
             raise RuntimeError("TRAIN_KG backward: the captured step's forward buffers were reused by a later "
                                "TRAIN_KG forward before this backward ran")
-        self.buf["gout"].copy_(gout.reshape(1))
+        if gout is None:
+            if not self.gout_one:
+                self.buf["gout"].fill_(1.0)
+                self.gout_one = True
+        else:
+            self.buf["gout"].copy_(gout.reshape(1))
+            self.gout_one = False
         self.pending = "bwd"
 
     def update(self, opt) -> None:
@@ -705,6 +714,37 @@ class _KGStepGraph:
         self.release()
 
 
+class _StepLoss(torch.Tensor):
+    """A step loss whose plain ``loss.backward()`` -- no gradient argument, no retain_graph / create_graph /
+    inputs, the reference training loops' call (main.py:312, 340) -- runs its step's backward directly
+    (``grad_fn.fast_backward``) instead of through the autograd engine: no ones_like fill launch and no
+    hand-off to the engine's device thread (~30-50 us of host time per call, the bulk of a captured KG
+    step's host cost).  Anything else (a scaled or summed loss, ``torch.autograd.backward``, ``retain_graph``)
+    takes the engine and the node's ordinary backward, the same state transitions either way; a second
+    backward raises as the engine's would.  Every other operation sees a plain tensor."""
+
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
+        node = self.grad_fn
+        fast = getattr(node, "fast_backward", None) if node is not None else None
+        if fast is not None and gradient is None and not retain_graph and not create_graph and inputs is None:
+            node.fast_backward = None
+            try:
+                fast(node)
+                return None
+            except _UseEngine:
+                pass
+        return super().backward(gradient, retain_graph, create_graph, inputs)
+
+
+def _kg_fast_backward(ctx) -> None:
+    step, ctx.step = ctx.step, None
+    if step is None:
+        raise RuntimeError("Trying to backward through the graph a second time")
+    step.backward(None)
+
+
 class _KGGraphLoss(torch.autograd.Function):
     """The captured KG step's loss node: forward replays the forward graph (its loss copied out, so a
     kept loss survives the next step), backward hands the upstream gradient to the update graph."""
@@ -712,12 +752,16 @@ class _KGGraphLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, step, ids, opt, states, emb, rel_emb, trans):
         ctx.step = step
-        return step.forward(ids, opt, *states).clone().view(())
+        ctx.fast_backward = _kg_fast_backward
+        return step.forward(ids, opt, *states).clone().view(()).as_subclass(_StepLoss)
 
     @staticmethod
     def backward(ctx, gout):
-        ctx.step.backward(gout.to(torch.float32))
-        ctx.step = None
+        step, ctx.step = ctx.step, None
+        ctx.fast_backward = None
+        if step is None:
+            raise RuntimeError("Trying to backward through the graph a second time")
+        step.backward(gout.to(torch.float32))
         return None, None, None, None, None, None, None
 
 
@@ -894,10 +938,15 @@ class _CFLoss(torch.autograd.Function):
         ctx.tables, ctx.sides, ctx.states, ctx.ws = tables, sides, states, ws
         ctx.ids = (users, pos, neg)
         ctx.coef = coef
-        return loss.view(())
+        ctx.leaves = (X0, *ws)
+        ctx.fast_backward = _cf_fast_backward
+        return loss.view(()).as_subclass(_StepLoss)
 
     @staticmethod
     def backward(ctx, gout):
+        ctx.fast_backward = None
+        if ctx.tables is None:
+            raise RuntimeError("Trying to backward through the graph a second time")
         graph, drops, seeds, reg, hook, tu, _frontier, _marks = ctx.cfg
         tables, sides, states, ws = ctx.tables, ctx.sides, ctx.states, ctx.ws
         users, pos, neg = ctx.ids
@@ -1082,6 +1131,37 @@ class _CFLoss(torch.autograd.Function):
             dX = dXd
         ctx.tables = ctx.sides = ctx.states = None
         return (None, None, None, None, dX, *wgrads)
+
+
+_ONE: dict = {}  # device -> a resident fp32 1.0 (the plain backward's upstream gradient)
+
+
+def _cf_fast_backward(ctx) -> None:
+    """``loss.backward()`` of a TRAIN_CF loss without the engine (model._StepLoss): the node's backward with
+    upstream gradient 1, its gradients accumulated into the leaves as the engine's AccumulateGrad does (set, or
+    added in place).  A leaf with gradient hooks (DDP and the like) sends the call through the engine."""
+    leaves = ctx.leaves
+    if any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
+           for p in leaves if p is not None):
+        ctx.fast_backward = _cf_fast_backward
+        raise _UseEngine
+    dev = ctx.coef.device
+    one = _ONE.get(dev)
+    if one is None:
+        one = _ONE[dev] = torch.ones((), dtype=torch.float32, device=dev)
+    grads = _CFLoss.backward(ctx, one)[4:]
+    with torch.no_grad():
+        for p, g in zip(leaves, grads):
+            if g is None or p is None or not p.requires_grad:
+                continue
+            if p.grad is None:
+                p.grad = g.detach()
+            else:
+                p.grad.add_(g)
+
+
+class _UseEngine(Exception):
+    """A fast backward declined (model._StepLoss falls back to the autograd engine)."""
 
 
 class _KGLoss(torch.autograd.Function):

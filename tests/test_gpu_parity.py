@@ -1981,7 +1981,13 @@ def test_captured_kg_step_bit_identical(pkg, dim):
                     out.append(m(*kg, mode=pkg.KGATMode.TRAIN_KG).detach().clone())
                     continue
                 loss = m(*kg, mode=pkg.KGATMode.TRAIN_KG)
-                loss.backward()
+                if j == 4:  # a scaled loss takes the autograd engine (upstream gradient 0.5)
+                    (loss * 0.5).backward()
+                else:  # the plain call: the captured step's direct backward (model._StepLoss)
+                    loss.backward()
+                if phase == 0 and j == 0:
+                    with pytest.raises(RuntimeError):
+                        loss.backward()  # a second backward of one loss raises, as the engine does
                 if phase == 3 and j == 5:  # two backwards, one update (gradient accumulation)
                     kg2 = kgs[(j + 1) % len(kgs)]
                     m(*kg2, mode=pkg.KGATMode.TRAIN_KG).backward()

@@ -230,3 +230,54 @@ def test_driver_dataset_split_and_early_stopping():
         assert not (a & b or a & c or b & c) and len(c) == math.ceil(0.2 * n)  # sklearn's sizes
     assert drv.early_stopping([0.1, 0.2] + [0.1] * 9) == (0.2, False)
     assert drv.early_stopping([0.1, 0.2] + [0.1] * 10) == (0.2, True)
+
+
+def test_step_loss_plain_backward_takes_the_direct_path():
+    """model._StepLoss: a plain ``loss.backward()`` calls the node's ``fast_backward`` (no autograd engine);
+    a scaled loss, ``retain_graph`` or a leaf with gradient hooks goes through the engine and the node's
+    ordinary backward; either way a second backward of the same loss raises."""
+    model = __import__(load_pkg().__name__ + ".model", fromlist=["model"])
+    calls = []
+
+    def fast(ctx):
+        if any(getattr(p, "_post_accumulate_grad_hooks", None) for p in ctx.leaves):
+            ctx.fast_backward = fast
+            raise model._UseEngine
+        calls.append("fast")
+        ctx.done = True
+        ctx.leaves[0].grad = torch.full((3,), 2.0)
+
+    class F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            ctx.leaves, ctx.done, ctx.fast_backward = (x,), False, fast
+            return (2 * x).sum().as_subclass(model._StepLoss)
+
+        @staticmethod
+        def backward(ctx, g):
+            ctx.fast_backward = None
+            if ctx.done:
+                raise RuntimeError("Trying to backward through the graph a second time")
+            ctx.done = True
+            calls.append("engine")
+            return g * 2 * torch.ones(3)
+
+    x = torch.ones(3, requires_grad=True)
+    loss = F.apply(x)
+    assert isinstance(loss, model._StepLoss) and float(loss) == 6.0
+    assert type(loss + 1) is torch.Tensor  # every other operation sees a plain tensor
+    loss.backward()
+    assert calls == ["fast"] and torch.equal(x.grad, torch.full((3,), 2.0))
+    with pytest.raises(RuntimeError):
+        loss.backward()
+    x.grad = None
+    (F.apply(x) * 0.5).backward()  # scaled: the engine
+    assert calls[-1] == "engine" and torch.equal(x.grad, torch.ones(3))
+    x.grad = None
+    F.apply(x).backward(retain_graph=True)
+    assert calls[-1] == "engine"
+    x.grad = None
+    h = x.register_post_accumulate_grad_hook(lambda p: calls.append("hook"))
+    F.apply(x).backward()  # a leaf with hooks: the engine (the hook runs)
+    assert calls[-2:] == ["engine", "hook"]
+    h.remove()
