@@ -163,7 +163,7 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
     if (row < n) {
       float* h = H + row * ldh + c;
 #pragma unroll
-      for (int cb = 0; cb < B::NCB; ++cb) h[cb * 16] = g[cb][i] * inv;
+      for (int cb = 0; cb < B::NCB; ++cb) __builtin_nontemporal_store(g[cb][i] * inv, h + cb * 16);
       // saved norm; negative = the clamp was active (F.normalize's eps)
       if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
     }

@@ -98,6 +98,12 @@ __device__ __forceinline__ void store_row(const SpmmIo& io, int64_t row, int64_t
     const float4 o = *y;
     acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
   }
+  if (MODE == kOverwrite) {  // the dense product's output is written once: non-temporal, so the gathered table keeps the
+                    // caches (C2 forward 0.555 -> 0.550 ms, full step 2.040 -> 2.025 ms, two interleaved A/B pairs)
+    const floatx4 v = {acc.x, acc.y, acc.z, acc.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(y));
+    return;
+  }
   *y = acc;
 }
 
