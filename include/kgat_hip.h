@@ -55,6 +55,12 @@ typedef struct kgat_csr {
   int32_t n_seg;
   int32_t seg_len;
   int32_t long_threshold;
+  /* [4 * ceil(n_seg / 4)] or null (= identity): the segment each launch slot of the
+   * SpMM's long-row blocks takes (slot = 4 * block + wave; values >= n_seg are
+   * padding).  A scheduling choice only: partials stay indexed by segment and the
+   * fix-up sums them in row order, so every result is bit-identical for any order.
+   * kgat_csr_seg_order() builds the XCD-grouped column-sorted order. */
+  const int32_t *seg_order;
 } kgat_csr;
 
 const char *kgat_strerror(int status);
@@ -66,6 +72,12 @@ int kgat_version(void);
 int kgat_csr_plan(const int64_t *rowptr_host, int64_t n_rows, int32_t long_threshold, int32_t seg_len,
                   int32_t *n_long, int32_t *n_seg, int32_t *long_rows, int32_t *long_seg_off,
                   int32_t *seg_row, int64_t *seg_beg);
+
+/* Host helper: the launch order of a plan's segments for kgat_csr::seg_order
+ * (host arrays; order holds 4 * ceil(n_seg / 4) entries): segments stable-sorted
+ * by their first column, dealt so the long-row blocks sharing an XCD take one
+ * contiguous run of that list. */
+int kgat_csr_seg_order(const int32_t *col, const int64_t *seg_beg, int32_t n_seg, int32_t *order);
 
 /* a1 -- attentive propagation SpMM, Y = A . X (+ Y when accumulate != 0).
  * Replaces torch.matmul(sparse attentive_matrix, ego_embeddings) at

@@ -28,6 +28,7 @@ class CSR(ctypes.Structure):
         ("rowptr", c_vp), ("col", c_vp), ("val", c_vp), ("n_rows", c_i64), ("nnz", c_i64),
         ("long_rows", c_vp), ("long_seg_off", c_vp), ("seg_row", c_vp), ("seg_beg", c_vp),
         ("n_long", c_i32), ("n_seg", c_i32), ("seg_len", c_i32), ("long_threshold", c_i32),
+        ("seg_order", c_vp),
     ]
 
 
@@ -73,6 +74,7 @@ _SIGNATURES = {
     "kgat_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "kgat_version": (ctypes.c_int, []),
     "kgat_csr_plan": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "kgat_csr_seg_order": (ctypes.c_int, [c_vp, c_vp, c_i32, c_vp]),
     "kgat_spmm_csr_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_i64,
                                          c_vp]),
     "kgat_biinter_fwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,

@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <vector>
 
 #include "common.hpp"
 
@@ -678,5 +679,30 @@ extern "C" int kgat_csr_plan(const int64_t* rowptr, int64_t n_rows, int32_t long
   if (nl > 0x7fffffff || ns > 0x7fffffff) return KGAT_ERR_INVALID;
   *n_long = static_cast<int32_t>(nl);
   *n_seg = static_cast<int32_t>(ns);
+  return KGAT_OK;
+}
+
+// Host: the SpMM's launch order of the long-row segments (kgat_csr::seg_order).  Segments sorted
+// by their first column (stable), then dealt so that the long-row blocks sharing an XCD (blocks
+// b, b + 8, ... -- round-robin dispatch) take one contiguous run of the sorted list: each XCD's
+// L2 then holds the source rows of one eighth of the column range instead of all of it (the hub
+// rows of a user -> item graph all gather the same user table).
+extern "C" int kgat_csr_seg_order(const int32_t* col, const int64_t* seg_beg, int32_t n_seg, int32_t* order) {
+  if (n_seg < 0 || (n_seg > 0 && (!col || !seg_beg || !order))) return KGAT_ERR_INVALID;
+  constexpr int kXcds = 8;
+  std::vector<int32_t> by_col(n_seg);
+  for (int32_t s = 0; s < n_seg; ++s) by_col[s] = s;
+  std::stable_sort(by_col.begin(), by_col.end(),
+                   [&](int32_t a, int32_t b) { return col[seg_beg[a]] < col[seg_beg[b]]; });
+  const int64_t nb = (static_cast<int64_t>(n_seg) + 3) / 4;
+  int64_t start[kXcds + 1] = {0};
+  for (int x = 0; x < kXcds; ++x) start[x + 1] = start[x] + (nb > x ? (nb - x + kXcds - 1) / kXcds : 0);
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t vb = start[b % kXcds] + b / kXcds;
+    for (int w = 0; w < 4; ++w) {
+      const int64_t pos = vb * 4 + w;
+      order[b * 4 + w] = pos < n_seg ? by_col[pos] : n_seg;
+    }
+  }
   return KGAT_OK;
 }

@@ -118,6 +118,7 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
                                              int2* hb) {
   constexpr int L = SpmmShape<D>::kLanes;
   constexpr bool MASKED = MODE == kMasked || MODE == kMaskedRows || MODE == kMaskedAdam;
+  if (A.seg_order != nullptr) s = A.seg_order[s];  // launch slot -> segment (kgat_csr_seg_order)
   if (s >= A.n_seg) return;
   const int row = A.seg_row[s];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row

@@ -144,6 +144,41 @@ def long_row_plan(rowptr: np.ndarray, long_threshold: int = LONG_THRESHOLD, seg_
     return (long_rows.astype(np.int32), off.astype(np.int32), seg_row.astype(np.int32), seg_beg.astype(np.int64))
 
 
+N_XCDS = 8  # blocks b, b + 8, ... share an XCD (round-robin dispatch)
+
+
+def seg_launch_order(col: np.ndarray, seg_beg: np.ndarray) -> np.ndarray:
+    """numpy twin of kgat_csr_seg_order(): the SpMM's launch slot -> segment map.
+
+    Segments stable-sorted by first column, dealt so that the long-row blocks sharing an XCD take
+    one contiguous run of that list (each XCD's L2 then serves one slice of the column range).
+    Scheduling only: results are bit-identical for any order.
+    """
+    n_seg = int(seg_beg.size)
+    by_col = np.argsort(np.asarray(col)[seg_beg], kind="stable").astype(np.int32)
+    nb = (n_seg + 3) // 4
+    cnt = np.array([(nb - x + N_XCDS - 1) // N_XCDS if nb > x else 0 for x in range(N_XCDS)], np.int64)
+    start = np.concatenate([[0], np.cumsum(cnt)])
+    b = np.arange(nb, dtype=np.int64)
+    pos = ((start[b % N_XCDS] + b // N_XCDS)[:, None] * 4 + np.arange(4)).ravel()
+    out = np.full(4 * nb, n_seg, np.int32)
+    ok = pos < n_seg
+    out[ok] = by_col[pos[ok]]
+    return out
+
+
+def _ptr(t) -> int:
+    return t.data_ptr() if t is not None else 0
+
+
+def _seg_order_device(col: np.ndarray, seg_beg: np.ndarray, device):
+    import os
+
+    if seg_beg.size == 0 or os.environ.get("KGAT_SEG_ORDER", "1") == "0":
+        return None
+    return torch.from_numpy(seg_launch_order(col, seg_beg)).to(device)
+
+
 def degree_weights(heads: np.ndarray, tails: np.ndarray, rels: np.ndarray, n: int) -> np.ndarray:
     """1 / (log1p(deg_h) + log1p(deg_t)), degrees counted within each relation (model.py:309-314)."""
     w = np.empty(heads.size, np.float32)
@@ -171,12 +206,14 @@ class _DeviceCSR:
         self.seg_beg = torch.from_numpy(sb).to(device)
         self.n_long, self.n_seg = int(lr.size), int(sr.size)
         self.max_deg = int(np.diff(rowptr).max()) if self.n_rows else 0
+        self.col_host = np.ascontiguousarray(col, np.int32)
+        self.seg_order = _seg_order_device(self.col_host, sb, device)
 
     def descriptor(self) -> _lib.CSR:
         return _lib.CSR(self.rowptr.data_ptr(), self.col.data_ptr(), self.val.data_ptr(), self.n_rows,
                         self.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
                         self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
-                        LONG_THRESHOLD)
+                        LONG_THRESHOLD, _ptr(self.seg_order))
 
 
 class _CSRRowView:
@@ -193,13 +230,14 @@ class _CSRRowView:
         self.seg_row = torch.from_numpy(sr).to(device)
         self.seg_beg = torch.from_numpy(sb).to(device)
         self.n_long, self.n_seg = int(lr.size), int(sr.size)
+        self.seg_order = _seg_order_device(base.col_host, sb, device)
 
     def descriptor(self) -> _lib.CSR:
         b = self.base
         return _lib.CSR(b.rowptr.data_ptr() + 8 * self.r0, b.col.data_ptr(), b.val.data_ptr(), self.n_rows,
                         b.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
                         self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
-                        LONG_THRESHOLD)
+                        LONG_THRESHOLD, _ptr(self.seg_order))
 
 
 class DeviceGraph:

@@ -107,6 +107,30 @@ def test_long_row_plan_matches_c_helper():
         assert begs[0] == rowptr[r] and np.all(np.diff(begs) == 512) and begs[-1] < rowptr[r + 1]
 
 
+@pytest.mark.parametrize("n_seg", [0, 1, 5, 37, 64, 1001])
+def test_seg_launch_order_matches_c_helper(n_seg):
+    """kgat_csr_seg_order == graph.seg_launch_order; a permutation of the segments (padding = n_seg);
+    the slots of blocks sharing an XCD (b % 8) hold one contiguous run of the column-sorted list."""
+    rng = np.random.default_rng(n_seg)
+    col = rng.integers(0, 1 << 20, 4096).astype(np.int32)
+    seg_beg = rng.integers(0, col.size, n_seg).astype(np.int64)
+    order = graph.seg_launch_order(col, seg_beg)
+    nb = (n_seg + 3) // 4
+    assert order.dtype == np.int32 and order.size == 4 * nb
+    c = np.zeros(max(4 * nb, 1), np.int32)
+    assert _lib.lib().kgat_csr_seg_order(col.ctypes.data, seg_beg.ctypes.data, n_seg, c.ctypes.data) == 0
+    np.testing.assert_array_equal(c[:order.size], order)
+    real = order[order < n_seg]
+    np.testing.assert_array_equal(np.sort(real), np.arange(n_seg))
+    assert np.count_nonzero(order == n_seg) == 4 * nb - n_seg
+    by_col = np.argsort(col[seg_beg], kind="stable")
+    run = []
+    for x in range(8):
+        for b in range(x, nb, 8):
+            run.extend(order[4 * b:4 * b + 4].tolist())
+    np.testing.assert_array_equal(np.array([s for s in run if s < n_seg], np.int64), by_col)
+
+
 def test_synthetic_ckg_shape():
     U, E, inter, trip = graph.synthetic_ckg(20000, 200000, seed=1)
     assert U == 2000 and E == 18000
