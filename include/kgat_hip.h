@@ -73,6 +73,17 @@ int kgat_csr_plan(const int64_t *rowptr_host, int64_t n_rows, int32_t long_thres
                   int32_t *n_long, int32_t *n_seg, int32_t *long_rows, int32_t *long_seg_off,
                   int32_t *seg_row, int64_t *seg_beg);
 
+/* Host helper: the SpMM's long-row plan with column-aware cuts (host arrays).  A
+ * row of degree > long_threshold is cut where a segment reaches seg_len entries, or
+ * where its column crosses a multiple of col_block once the segment holds min_piece
+ * entries, so a hub row's segments each gather from one slice of the source table.
+ * Segments still tile each long row in order (the SpMM reads a segment's end from
+ * the next segment's start).  Same outputs and count-only mode as kgat_csr_plan;
+ * col_block = INT32_MAX gives kgat_csr_plan's plan. */
+int kgat_csr_plan_cols(const int64_t *rowptr, const int32_t *col, int64_t n_rows, int32_t long_threshold,
+                       int32_t seg_len, int32_t col_block, int32_t min_piece, int32_t *n_long, int32_t *n_seg,
+                       int32_t *long_rows, int32_t *long_seg_off, int32_t *seg_row, int64_t *seg_beg);
+
 /* Host helper: the launch order of a plan's segments for kgat_csr::seg_order
  * (host arrays; order holds 4 * ceil(n_seg / 4) entries): segments stable-sorted
  * by their first column, dealt so the long-row blocks sharing an XCD take one

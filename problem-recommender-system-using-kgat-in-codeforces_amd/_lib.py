@@ -74,6 +74,8 @@ _SIGNATURES = {
     "kgat_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "kgat_version": (ctypes.c_int, []),
     "kgat_csr_plan": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "kgat_csr_plan_cols": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp, c_vp]),
     "kgat_csr_seg_order": (ctypes.c_int, [c_vp, c_vp, c_i32, c_vp]),
     "kgat_spmm_csr_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_i64,
                                          c_vp]),

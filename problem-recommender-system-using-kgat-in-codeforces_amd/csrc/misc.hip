@@ -682,6 +682,52 @@ extern "C" int kgat_csr_plan(const int64_t* rowptr, int64_t n_rows, int32_t long
   return KGAT_OK;
 }
 
+// Host: the SpMM's long-row plan with column-aware cuts.  A long row (degree > long_threshold) is
+// cut where a segment reaches seg_len entries, or where its column crosses a multiple of col_block
+// once the segment holds min_piece entries: a hub row's segments then each gather from one
+// col_block-row slice of the source table (with kgat_csr_seg_order, one XCD's L2 serves a few
+// slices instead of the whole table).  A pure function of each row's entries, so a row view's plan
+// matches the full matrix's row by row.  Pass null outputs to only count.
+extern "C" int kgat_csr_plan_cols(const int64_t* rowptr, const int32_t* col, int64_t n_rows, int32_t long_threshold,
+                                  int32_t seg_len, int32_t col_block, int32_t min_piece, int32_t* n_long,
+                                  int32_t* n_seg, int32_t* long_rows, int32_t* long_seg_off, int32_t* seg_row,
+                                  int64_t* seg_beg) {
+  if (!rowptr || n_rows < 0 || long_threshold < 1 || seg_len < 1 || col_block < 1 || min_piece < 1 || !n_long ||
+      !n_seg || (n_rows > 0 && !col))
+    return KGAT_ERR_INVALID;
+  int64_t nl = 0, ns = 0;
+  for (int64_t r = 0; r < n_rows; ++r) {
+    const int64_t a = rowptr[r], b = rowptr[r + 1];
+    if (b - a <= long_threshold) continue;
+    if (long_rows) {
+      long_rows[nl] = static_cast<int32_t>(r);
+      long_seg_off[nl] = static_cast<int32_t>(ns);
+    }
+    int64_t s = a;
+    for (int64_t i = a + 1; i < b; ++i) {
+      if (i - s >= seg_len || (col[i] / col_block != col[i - 1] / col_block && i - s >= min_piece)) {
+        if (seg_row) {
+          seg_row[ns] = static_cast<int32_t>(r);
+          seg_beg[ns] = s;
+        }
+        ++ns;
+        s = i;
+      }
+    }
+    if (seg_row) {
+      seg_row[ns] = static_cast<int32_t>(r);
+      seg_beg[ns] = s;
+    }
+    ++ns;
+    ++nl;
+  }
+  if (long_rows) long_seg_off[nl] = static_cast<int32_t>(ns);
+  if (nl > 0x7fffffff || ns > 0x7fffffff) return KGAT_ERR_INVALID;
+  *n_long = static_cast<int32_t>(nl);
+  *n_seg = static_cast<int32_t>(ns);
+  return KGAT_OK;
+}
+
 // Host: the SpMM's launch order of the long-row segments (kgat_csr::seg_order).  Segments sorted
 // by their first column (stable), then dealt so that the long-row blocks sharing an XCD (blocks
 // b, b + 8, ... -- round-robin dispatch) take one contiguous run of the sorted list: each XCD's

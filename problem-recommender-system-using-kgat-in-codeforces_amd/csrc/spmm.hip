@@ -124,7 +124,8 @@ __device__ __forceinline__ void long_segment(const kgat_csr& A, const SpmmIo& io
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // not an output row
   const int64_t beg = A.seg_beg[s];
   const int64_t row_end = A.rowptr[row + 1];
-  const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+  const int64_t nxt = s + 1 < A.n_seg ? A.seg_beg[s + 1] : row_end;  // segments tile each long row in order
+  const int64_t end = nxt < row_end ? nxt : row_end;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   bool any = false;
   // group g handles edges [beg + g*L + k*64, ... + L) for k = 0, 1, ...
@@ -304,7 +305,8 @@ __global__ __launch_bounds__(256) void csr_mark_rows_kernel(kgat_csr A, const ui
     const int row = A.seg_row[s];
     const int64_t beg = A.seg_beg[s];
     const int64_t row_end = A.rowptr[row + 1];
-    const int64_t end = beg + A.seg_len < row_end ? beg + A.seg_len : row_end;
+    const int64_t nxt = s + 1 < A.n_seg ? A.seg_beg[s + 1] : row_end;
+    const int64_t end = nxt < row_end ? nxt : row_end;
     for (int64_t e = beg + (threadIdx.x & 63); e < end; e += 64)
       if (bit_of(bits, A.col[e])) {
         hit[row] = 1;

@@ -167,6 +167,37 @@ def seg_launch_order(col: np.ndarray, seg_beg: np.ndarray) -> np.ndarray:
     return out
 
 
+SEG_COL_BLOCK = 8192   # SpMM plan: hub-row segments also cut at multiples of this column (csrc kgat_csr_plan_cols)
+SEG_MIN_PIECE = 32     # ... once they hold this many entries
+
+
+def long_row_plan_cols(rowptr: np.ndarray, col: np.ndarray, long_threshold: int = LONG_THRESHOLD,
+                       seg_len: int = SEG_LEN, col_block: int | None = None, min_piece: int = SEG_MIN_PIECE):
+    """The SpMM's long-row plan with column-aware cuts (kgat_csr_plan_cols, host C): like
+    :func:`long_row_plan`, but a segment also ends where its column crosses a multiple of
+    ``col_block`` once it holds ``min_piece`` entries.  ``KGAT_SEG_COLBLOCK=0`` (A/B switch) gives
+    the fixed-length plan."""
+    import os
+
+    if col_block is None:
+        col_block = int(os.environ.get("KGAT_SEG_COLBLOCK", SEG_COL_BLOCK))
+    if col_block <= 0:
+        return long_row_plan(rowptr, long_threshold, seg_len)
+    rp = np.ascontiguousarray(rowptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    n = rp.size - 1
+    lib = _lib.lib()
+    nl, ns = ctypes.c_int32(), ctypes.c_int32()
+    args = (rp.ctypes.data, cl.ctypes.data, n, long_threshold, seg_len, col_block, min_piece)
+    _lib.check(lib.kgat_csr_plan_cols(*args, ctypes.byref(nl), ctypes.byref(ns), None, None, None, None),
+               "kgat_csr_plan_cols")
+    lr, off = np.zeros(nl.value, np.int32), np.zeros(nl.value + 1, np.int32)
+    sr, sb = np.zeros(ns.value, np.int32), np.zeros(ns.value, np.int64)
+    _lib.check(lib.kgat_csr_plan_cols(*args, ctypes.byref(nl), ctypes.byref(ns), lr.ctypes.data, off.ctypes.data,
+                                      sr.ctypes.data, sb.ctypes.data), "kgat_csr_plan_cols")
+    return lr, off, sr, sb
+
+
 def _ptr(t) -> int:
     return t.data_ptr() if t is not None else 0
 
@@ -190,33 +221,60 @@ def degree_weights(heads: np.ndarray, tails: np.ndarray, rels: np.ndarray, n: in
     return w
 
 
-class _DeviceCSR:
-    """A CSR resident on the device plus its ctypes descriptor."""
+class _PlanArrays:
+    """The two long-row plans of a CSR (or a row view of one), resident on the device: the SpMM's
+    column-cut plan with its launch order (:meth:`descriptor`), and the fixed-length plan the row
+    softmax's hub-segment arithmetic assumes (:meth:`softmax_descriptor`)."""
 
-    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: torch.Tensor, device):
-        self.n_rows = rowptr.size - 1
-        self.rowptr_host = np.ascontiguousarray(rowptr, np.int64)
-        self.rowptr = torch.from_numpy(self.rowptr_host).to(device)
-        self.col = torch.from_numpy(np.ascontiguousarray(col, np.int32)).to(device)
-        self.val = val
-        lr, off, sr, sb = long_row_plan(rowptr)
+    def __init__(self, rowptr: np.ndarray, col_host: np.ndarray, device, col_cuts: bool = True):
+        self.col_cuts = col_cuts
+        lr, off, sr, sb = long_row_plan_cols(rowptr, col_host) if col_cuts else long_row_plan(rowptr)
         self.long_rows = torch.from_numpy(lr).to(device)
         self.long_seg_off = torch.from_numpy(off).to(device)
         self.seg_row = torch.from_numpy(sr).to(device)
         self.seg_beg = torch.from_numpy(sb).to(device)
         self.n_long, self.n_seg = int(lr.size), int(sr.size)
+        self.seg_order = _seg_order_device(col_host, sb, device)
+        flr, foff, fsr, fsb = long_row_plan(rowptr)
+        self._fixed = [torch.from_numpy(a).to(device) for a in (flr, foff, fsr, fsb)]
+        self._fixed_n = (int(flr.size), int(fsr.size))
+
+    def _desc(self, rowptr_ptr: int, val) -> _lib.CSR:
+        b = getattr(self, "base", self)
+        return _lib.CSR(rowptr_ptr, b.col.data_ptr(), val.data_ptr(), self.n_rows, b.col.numel(),
+                        self.long_rows.data_ptr(), self.long_seg_off.data_ptr(), self.seg_row.data_ptr(),
+                        self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN, LONG_THRESHOLD,
+                        _ptr(self.seg_order))
+
+    def softmax_descriptor(self) -> _lib.CSR:
+        """The descriptor with the fixed-length plan (kgat_row_softmax_plan_f32)."""
+        d = self.descriptor()
+        lr, off, sr, sb = self._fixed
+        d.long_rows, d.long_seg_off, d.seg_row, d.seg_beg = (lr.data_ptr(), off.data_ptr(), sr.data_ptr(),
+                                                            sb.data_ptr())
+        d.n_long, d.n_seg = self._fixed_n
+        d.seg_order = None
+        return d
+
+
+class _DeviceCSR(_PlanArrays):
+    """A CSR resident on the device plus its ctypes descriptor."""
+
+    def __init__(self, rowptr: np.ndarray, col: np.ndarray, val: torch.Tensor, device, col_cuts: bool = True):
+        self.n_rows = rowptr.size - 1
+        self.rowptr_host = np.ascontiguousarray(rowptr, np.int64)
+        self.rowptr = torch.from_numpy(self.rowptr_host).to(device)
+        self.col = torch.from_numpy(np.ascontiguousarray(col, np.int32)).to(device)
+        self.val = val
         self.max_deg = int(np.diff(rowptr).max()) if self.n_rows else 0
         self.col_host = np.ascontiguousarray(col, np.int32)
-        self.seg_order = _seg_order_device(self.col_host, sb, device)
+        _PlanArrays.__init__(self, self.rowptr_host, self.col_host, device, col_cuts)
 
     def descriptor(self) -> _lib.CSR:
-        return _lib.CSR(self.rowptr.data_ptr(), self.col.data_ptr(), self.val.data_ptr(), self.n_rows,
-                        self.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
-                        self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
-                        LONG_THRESHOLD, _ptr(self.seg_order))
+        return self._desc(self.rowptr.data_ptr(), self.val)
 
 
-class _CSRRowView:
+class _CSRRowView(_PlanArrays):
     """Rows [r0, r1) of a _DeviceCSR, sharing its device arrays (values stay live across
     refreshes): the descriptor points at rowptr + r0 -- row pointers are absolute
     offsets into col / val -- with a long-row plan of its own rows."""
@@ -224,20 +282,10 @@ class _CSRRowView:
     def __init__(self, base: _DeviceCSR, r0: int, r1: int, device):
         self.base, self.r0, self.n_rows = base, int(r0), int(r1) - int(r0)
         self.nnz = int(base.rowptr_host[r1] - base.rowptr_host[r0])
-        lr, off, sr, sb = long_row_plan(base.rowptr_host[r0:r1 + 1])
-        self.long_rows = torch.from_numpy(lr).to(device)
-        self.long_seg_off = torch.from_numpy(off).to(device)
-        self.seg_row = torch.from_numpy(sr).to(device)
-        self.seg_beg = torch.from_numpy(sb).to(device)
-        self.n_long, self.n_seg = int(lr.size), int(sr.size)
-        self.seg_order = _seg_order_device(base.col_host, sb, device)
+        _PlanArrays.__init__(self, base.rowptr_host[r0:r1 + 1], base.col_host, device, base.col_cuts)
 
     def descriptor(self) -> _lib.CSR:
-        b = self.base
-        return _lib.CSR(b.rowptr.data_ptr() + 8 * self.r0, b.col.data_ptr(), b.val.data_ptr(), self.n_rows,
-                        b.col.numel(), self.long_rows.data_ptr(), self.long_seg_off.data_ptr(),
-                        self.seg_row.data_ptr(), self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN,
-                        LONG_THRESHOLD, _ptr(self.seg_order))
+        return self._desc(self.base.rowptr.data_ptr() + 8 * self.r0, self.base.val)
 
 
 class DeviceGraph:
@@ -257,7 +305,7 @@ class DeviceGraph:
         np.cumsum(np.bincount(col, minlength=self.n_nodes), out=rowptr_t[1:])
         self.perm_t = torch.from_numpy(perm_t.astype(np.int32)).to(device)
         self.AT = _DeviceCSR(rowptr_t, rows[perm_t].astype(np.int32),
-                             torch.empty(col.size, dtype=torch.float32, device=device), device)
+                             torch.empty(col.size, dtype=torch.float32, device=device), device, col_cuts=False)
         # refresh edge list (model.py:318-366)
         self.edge_heads = torch.from_numpy(layout.heads.astype(np.int32)).to(device)
         self.edge_tails = torch.from_numpy(layout.tails.astype(np.int32)).to(device)

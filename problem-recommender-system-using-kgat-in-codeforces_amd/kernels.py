@@ -1260,8 +1260,8 @@ def row_softmax(graph: DeviceGraph, slot_logits: torch.Tensor) -> None:
 
 def row_softmax_csr(A, slot_logits: torch.Tensor, val: torch.Tensor) -> None:
     """val <- softmax over each row's stored entries of a device CSR (graph._DeviceCSR or a shard's),
-    hub rows by their long-row plan segments (kgat_row_softmax_plan_f32)."""
-    desc = A.descriptor()
+    hub rows by their fixed-length long-row plan segments (kgat_row_softmax_plan_f32)."""
+    desc = A.softmax_descriptor()
     work = torch.empty(max(int(_lib.lib().kgat_row_softmax_work_floats(ctypes.byref(desc))), 1),
                        dtype=torch.float32, device=slot_logits.device)
     tok = _ev_begin("row_softmax")

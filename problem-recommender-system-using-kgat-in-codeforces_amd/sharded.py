@@ -267,7 +267,7 @@ class RowShard:
         self._trp, self._tcol = trp, np.ascontiguousarray(tcol, np.int32)
         self.A = _DeviceCSR(lrp, lcol, torch.from_numpy(lval.copy()).to(self.device), self.device)
         self.AT = _DeviceCSR(trp, self._tcol, torch.from_numpy(np.asarray(tval, np.float32).copy()).to(self.device),
-                             self.device)
+                             self.device, col_cuts=False)
         self.nnz = int(lcol.size)
         # the local CSR's row pointers / values under the names the attention refresh uses
         self.local_rowptr = self.A.rowptr

@@ -107,6 +107,49 @@ def test_long_row_plan_matches_c_helper():
         assert begs[0] == rowptr[r] and np.all(np.diff(begs) == 512) and begs[-1] < rowptr[r + 1]
 
 
+def _plan_cols_loops(rowptr, col, T, seg_len, col_block, min_piece):
+    """Pure-Python statement of kgat_csr_plan_cols' cut rule (small cases only)."""
+    lr, off, sr, sb = [], [0], [], []
+    for r in range(rowptr.size - 1):
+        a, b = int(rowptr[r]), int(rowptr[r + 1])
+        if b - a <= T:
+            continue
+        lr.append(r)
+        s = a
+        for i in range(a + 1, b):
+            if i - s >= seg_len or (col[i] // col_block != col[i - 1] // col_block and i - s >= min_piece):
+                sr.append(r)
+                sb.append(s)
+                s = i
+        sr.append(r)
+        sb.append(s)
+        off.append(len(sr))
+    return [np.array(x, dt) for x, dt in ((lr, np.int32), (off, np.int32), (sr, np.int32), (sb, np.int64))]
+
+
+@pytest.mark.parametrize("col_block,min_piece", [(64, 8), (1000, 32), (1 << 30, 32)])
+def test_long_row_plan_cols(col_block, min_piece):
+    """kgat_csr_plan_cols == its loop statement; segments tile each long row, hold <= seg_len entries and
+    cross no col_block boundary once they hold min_piece; an unreachable col_block is kgat_csr_plan's plan."""
+    rng = np.random.default_rng(col_block)
+    deg = rng.integers(0, 40, 3000)
+    deg[rng.integers(0, 3000, 25)] = rng.integers(300, 3000, 25)
+    rowptr = np.zeros(deg.size + 1, np.int64)
+    np.cumsum(deg, out=rowptr[1:])
+    col = np.concatenate([np.sort(rng.choice(20000, d, replace=False)) for d in deg]).astype(np.int32)
+    got = graph.long_row_plan_cols(rowptr, col, 256, 512, col_block, min_piece)
+    want = _plan_cols_loops(rowptr, col, 256, 512, col_block, min_piece)
+    for x, y in zip(got, want):
+        np.testing.assert_array_equal(x, y)
+    lr, off, sr, sb = got
+    for i, r in enumerate(lr):
+        begs = np.r_[sb[off[i]:off[i + 1]], rowptr[r + 1]]
+        assert begs[0] == rowptr[r] and np.all(np.diff(begs) >= 1) and np.all(np.diff(begs) <= 512)
+    if col_block >= 1 << 30:
+        for x, y in zip(got, graph.long_row_plan(rowptr, 256, 512)):
+            np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize("n_seg", [0, 1, 5, 37, 64, 1001])
 def test_seg_launch_order_matches_c_helper(n_seg):
     """kgat_csr_seg_order == graph.seg_launch_order; a permutation of the segments (padding = n_seg);
