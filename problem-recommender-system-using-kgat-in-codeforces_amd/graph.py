@@ -228,6 +228,7 @@ class _PlanArrays:
 
     def __init__(self, rowptr: np.ndarray, col_host: np.ndarray, device, col_cuts: bool = True):
         self.col_cuts = col_cuts
+        self.long_threshold = LONG_THRESHOLD  # 128 for the column-cut plan measured 5-15 us slower per step
         lr, off, sr, sb = long_row_plan_cols(rowptr, col_host) if col_cuts else long_row_plan(rowptr)
         self.long_rows = torch.from_numpy(lr).to(device)
         self.long_seg_off = torch.from_numpy(off).to(device)
@@ -243,7 +244,7 @@ class _PlanArrays:
         b = getattr(self, "base", self)
         return _lib.CSR(rowptr_ptr, b.col.data_ptr(), val.data_ptr(), self.n_rows, b.col.numel(),
                         self.long_rows.data_ptr(), self.long_seg_off.data_ptr(), self.seg_row.data_ptr(),
-                        self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN, LONG_THRESHOLD,
+                        self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN, self.long_threshold,
                         _ptr(self.seg_order))
 
     def softmax_descriptor(self) -> _lib.CSR:
@@ -253,6 +254,7 @@ class _PlanArrays:
         d.long_rows, d.long_seg_off, d.seg_row, d.seg_beg = (lr.data_ptr(), off.data_ptr(), sr.data_ptr(),
                                                             sb.data_ptr())
         d.n_long, d.n_seg = self._fixed_n
+        d.long_threshold = LONG_THRESHOLD
         d.seg_order = None
         return d
 
