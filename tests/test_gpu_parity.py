@@ -123,6 +123,38 @@ def test_spmm_empty_rows_and_deterministic(pkg):
     np.testing.assert_allclose(a.cpu().numpy(), torch.sparse.mm(A, X.cpu()).numpy(), rtol=RTOL, atol=1e-4)
 
 
+def test_spmm_segment_plans_and_launch_order(pkg):
+    """A's hub rows under the column-cut plan (kgat_csr_plan_cols) and the XCD-grouped launch order
+    (kgat_csr::seg_order): the order is scheduling only -- identity, the built order and a reversed one give
+    the same bits; the column-cut and the fixed-length plans both match the sparse product."""
+    from types import SimpleNamespace
+
+    graph_mod, kernels = _mods(pkg)
+    n = 40000
+    lay, A = random_graph(graph_mod, n, 6, hubs=12, hub_deg=6000, seed=5, mids=40, mid_deg=400)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    fixed = graph_mod.long_row_plan(lay.rowptr)
+    assert g.A.col_cuts and g.A.seg_order is not None and g.A.n_seg > fixed[2].size  # column cuts happened
+    X = torch.randn(n, 64, device=DEV)
+    Y = kernels.spmm(g, X)
+    order = g.A.seg_order
+    try:
+        g.A.seg_order = None
+        Y_id = kernels.spmm(g, X)
+        g.A.seg_order = torch.flip(order, [0]).contiguous()
+        Y_rev = kernels.spmm(g, X)
+    finally:
+        g.A.seg_order = order
+    assert torch.equal(Y, Y_id) and torch.equal(Y, Y_rev)
+    ref = torch.sparse.mm(A, X.cpu()).numpy()
+    atol = 1e-3  # 6,000-term hub sums of magnitude ~100: fp32 summation-order differences reach ~1.5e-4
+    np.testing.assert_allclose(Y.cpu().numpy(), ref, rtol=RTOL, atol=atol)
+    csr_fixed = graph_mod._DeviceCSR(lay.rowptr, lay.col, g.A.val, DEV, col_cuts=False)
+    assert csr_fixed.n_seg == fixed[2].size
+    Y_fixed = kernels.spmm(SimpleNamespace(A=csr_fixed, AT=g.AT, n_nodes=n), X)
+    np.testing.assert_allclose(Y_fixed.cpu().numpy(), ref, rtol=RTOL, atol=atol)
+
+
 BI_SHAPES = [(64, 64), (64, 32), (32, 16), (128, 64), (64, 16), (128, 128), (16, 16)]
 
 
