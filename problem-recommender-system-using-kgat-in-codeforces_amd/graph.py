@@ -175,14 +175,9 @@ def long_row_plan_cols(rowptr: np.ndarray, col: np.ndarray, long_threshold: int 
                        seg_len: int = SEG_LEN, col_block: int | None = None, min_piece: int = SEG_MIN_PIECE):
     """The SpMM's long-row plan with column-aware cuts (kgat_csr_plan_cols, host C): like
     :func:`long_row_plan`, but a segment also ends where its column crosses a multiple of
-    ``col_block`` once it holds ``min_piece`` entries.  ``KGAT_SEG_COLBLOCK=0`` (A/B switch) gives
-    the fixed-length plan."""
-    import os
-
+    ``col_block`` (default :data:`SEG_COL_BLOCK`) once it holds ``min_piece`` entries."""
     if col_block is None:
-        col_block = int(os.environ.get("KGAT_SEG_COLBLOCK", SEG_COL_BLOCK))
-    if col_block <= 0:
-        return long_row_plan(rowptr, long_threshold, seg_len)
+        col_block = SEG_COL_BLOCK
     rp = np.ascontiguousarray(rowptr, np.int64)
     cl = np.ascontiguousarray(col, np.int32)
     n = rp.size - 1
@@ -203,9 +198,7 @@ def _ptr(t) -> int:
 
 
 def _seg_order_device(col: np.ndarray, seg_beg: np.ndarray, device):
-    import os
-
-    if seg_beg.size == 0 or os.environ.get("KGAT_SEG_ORDER", "1") == "0":
+    if seg_beg.size == 0:
         return None
     return torch.from_numpy(seg_launch_order(col, seg_beg)).to(device)
 
@@ -226,8 +219,12 @@ class _PlanArrays:
     column-cut plan with its launch order (:meth:`descriptor`), and the fixed-length plan the row
     softmax's hub-segment arithmetic assumes (:meth:`softmax_descriptor`)."""
 
-    def __init__(self, rowptr: np.ndarray, col_host: np.ndarray, device, col_cuts: bool = True):
-        self.col_cuts = col_cuts
+    def __init__(self, rowptr: np.ndarray, col_host: np.ndarray, device, col_cuts: bool = True, n_cols: int = 0):
+        # Both only pay when the source table spans more than one column block per XCD: C3's 16k-node
+        # table (L2-resident) measured 1.69 -> 1.75-1.77 ms per step with the cuts
+        # (profiles/r05_seg_order_ab.md), C2's 1M-node one 1.88 -> 1.86 ms.
+        wide = n_cols >= N_XCDS * SEG_COL_BLOCK
+        self.col_cuts = col_cuts = col_cuts and wide
         self.long_threshold = LONG_THRESHOLD  # 128 for the column-cut plan measured 5-15 us slower per step
         lr, off, sr, sb = long_row_plan_cols(rowptr, col_host) if col_cuts else long_row_plan(rowptr)
         self.long_rows = torch.from_numpy(lr).to(device)
@@ -235,7 +232,7 @@ class _PlanArrays:
         self.seg_row = torch.from_numpy(sr).to(device)
         self.seg_beg = torch.from_numpy(sb).to(device)
         self.n_long, self.n_seg = int(lr.size), int(sr.size)
-        self.seg_order = _seg_order_device(col_host, sb, device)
+        self.seg_order = _seg_order_device(col_host, sb, device) if wide else None
         flr, foff, fsr, fsb = long_row_plan(rowptr)
         self._fixed = [torch.from_numpy(a).to(device) for a in (flr, foff, fsr, fsb)]
         self._fixed_n = (int(flr.size), int(fsr.size))
@@ -270,7 +267,8 @@ class _DeviceCSR(_PlanArrays):
         self.val = val
         self.max_deg = int(np.diff(rowptr).max()) if self.n_rows else 0
         self.col_host = np.ascontiguousarray(col, np.int32)
-        _PlanArrays.__init__(self, self.rowptr_host, self.col_host, device, col_cuts)
+        self.n_cols = int(self.col_host.max()) + 1 if self.col_host.size else 0
+        _PlanArrays.__init__(self, self.rowptr_host, self.col_host, device, col_cuts, self.n_cols)
 
     def descriptor(self) -> _lib.CSR:
         return self._desc(self.rowptr.data_ptr(), self.val)
@@ -284,7 +282,7 @@ class _CSRRowView(_PlanArrays):
     def __init__(self, base: _DeviceCSR, r0: int, r1: int, device):
         self.base, self.r0, self.n_rows = base, int(r0), int(r1) - int(r0)
         self.nnz = int(base.rowptr_host[r1] - base.rowptr_host[r0])
-        _PlanArrays.__init__(self, base.rowptr_host[r0:r1 + 1], base.col_host, device, base.col_cuts)
+        _PlanArrays.__init__(self, base.rowptr_host[r0:r1 + 1], base.col_host, device, base.col_cuts, base.n_cols)
 
     def descriptor(self) -> _lib.CSR:
         return self._desc(self.base.rowptr.data_ptr() + 8 * self.r0, self.base.val)

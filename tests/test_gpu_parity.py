@@ -130,7 +130,7 @@ def test_spmm_segment_plans_and_launch_order(pkg):
     from types import SimpleNamespace
 
     graph_mod, kernels = _mods(pkg)
-    n = 40000
+    n = 80000  # > 8 column blocks of 8192: the column cuts and the launch order apply
     lay, A = random_graph(graph_mod, n, 6, hubs=12, hub_deg=6000, seed=5, mids=40, mid_deg=400)
     g = graph_mod.DeviceGraph(lay, DEV)
     fixed = graph_mod.long_row_plan(lay.rowptr)
@@ -146,6 +146,8 @@ def test_spmm_segment_plans_and_launch_order(pkg):
     finally:
         g.A.seg_order = order
     assert torch.equal(Y, Y_id) and torch.equal(Y, Y_rev)
+    small = graph_mod.DeviceGraph(random_graph(graph_mod, 3000, 9, hubs=5, hub_deg=2000, seed=1)[0], DEV)
+    assert not small.A.col_cuts and small.A.seg_order is None  # a table within 8 column blocks: fixed plan
     ref = torch.sparse.mm(A, X.cpu()).numpy()
     atol = 1e-3  # 6,000-term hub sums of magnitude ~100: fp32 summation-order differences reach ~1.5e-4
     np.testing.assert_allclose(Y.cpu().numpy(), ref, rtol=RTOL, atol=atol)
