@@ -62,6 +62,8 @@ def main() -> None:
     failures = []
     syncs = [None] * 9
     for step in range(3):
+        if rank == 0:
+            print(f"dp_worker world {dist.get_world_size()} dims {dims}: step {step}", flush=True)
         b = [torch.from_numpy(x).cuda() for x in (rng.integers(0, U, 64), rng.integers(0, E // 10, 64),
                                                   rng.integers(0, E // 10, 64))]
         for k, m in enumerate(models):

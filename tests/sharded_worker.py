@@ -85,6 +85,8 @@ def main() -> None:
     for a, b in zip(m._cf_weights(), ref._cf_weights()):
         close("aggregator after cf adam", a, b, ATOL_PARAM)
 
+    if rank == 0:
+        print(f"sharded_worker world {world}: CF step done", flush=True)
     # ---- KG step (from identical parameters again)
     m.load_full_state(ref.state_dict())
     heads_all = [rng.integers(0, U + E, 32) for _ in range(world)]
@@ -107,6 +109,8 @@ def main() -> None:
     close("table after kg adam", m._user_entity_embedding_shard, ref._user_entity_embedding.weight[lo:hi],
           ATOL_PARAM)
 
+    if rank == 0:
+        print(f"sharded_worker world {world}: KG step done", flush=True)
     # ---- UPDATE_ATTENTION (eval: MHA dropout off), then PREDICT on the refreshed graph
     m.load_full_state(ref.state_dict())
     ref.eval()

@@ -31,6 +31,17 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _run_logged(cmd, env, log_name: str, timeout: int):
+    """Run a multi-rank command with its stdout / stderr streamed into gpurun_out/<log_name> as it runs (the
+    ranks' progress lines show up there), then read it back: (returncode, stdout, stderr)."""
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    fo, fe = out / f"{log_name}.out", out / f"{log_name}.err"
+    with open(fo, "w") as so, open(fe, "w") as se:
+        rc = subprocess.run(cmd, cwd=ROOT, env=env, stdout=so, stderr=se, text=True, timeout=timeout).returncode
+    return subprocess.CompletedProcess(cmd, rc, fo.read_text(), fe.read_text())
+
+
 def test_sharded_world1_matches_kgat(pkg):
     graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
     sh = __import__(pkg.__name__ + ".sharded", fromlist=["sharded"])
@@ -93,7 +104,8 @@ def test_sharded_world1_matches_kgat(pkg):
 
 
 @pytest.mark.parametrize("world,dims,chunk", [(2, "64:64,32", 0), (2, "256:256,128,64", 0), (4, "256:256,128,64", 0),
-                                              (3, "256:256,128,64", 64)])
+                                              (3, "256:256,128,64", 64), (8, "256:256,128,64", 0),
+                                              (8, "64:64,32", 0)])
 def test_sharded_ranks_one_gpu(world, dims, chunk):
     """tests/sharded_worker.py on `world` ranks sharing this GPU (gloo, host-staged): the row-sharded
     model vs single-GPU KGAT on the global batch -- at the C2 shape and at C5's (d = 256, layers
@@ -105,10 +117,7 @@ def test_sharded_ranks_one_gpu(world, dims, chunk):
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "sharded_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / f"sharded_world{world}_d{dims.split(':')[0]}_c{chunk}.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, f"sharded_world{world}_d{dims.split(':')[0]}_c{chunk}", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert p.stdout.count("sharded parity ok") == world, p.stdout[-2000:]
     if chunk == 0:
@@ -124,10 +133,7 @@ def test_dp_sharded_grad_sync_world2_matches_allreduce():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / "dp_world2.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, "dp_world2", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
 
 
@@ -141,10 +147,7 @@ def test_dp_exchange_paths_world4():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / "dp_world4.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, "dp_world4", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
 
 
@@ -158,14 +161,11 @@ def test_dp_replicated_exchange_wide_layer0_world2():
     env["DP_WORKER_DIMS"] = "128:128,64"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / "dp_world2_wide.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, "dp_world2_wide", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_exchange_paths_c4_shape(world):
     """C4's exact shape (d = 128, layers [128, 64, 32], configs[3]) through every
     data-parallel exchange path of tests/dp_worker.py on `world` ranks sharing this GPU (gloo) -- the
@@ -177,10 +177,7 @@ def test_dp_exchange_paths_c4_shape(world):
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "dp_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / f"dp_world{world}_c4shape.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, f"dp_world{world}_c4shape", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert p.stdout.count(": OK") == world, p.stdout[-2000:]
 
@@ -192,16 +189,14 @@ def test_rccl_world1_collectives_match_gloo():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "rccl_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    log = ROOT / "gpurun_out" / "rccl_world1.log"
-    log.parent.mkdir(exist_ok=True)
-    log.write_text(f"rc={p.returncode}\n--- stdout\n{p.stdout}\n--- stderr\n{p.stderr}\n")
+    p = _run_logged(cmd, env, "rccl_world1", timeout=600)
     assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
     assert "rccl world1: OK" in p.stdout, p.stdout[-2000:]
 
 
 @pytest.mark.parametrize("dp,gpus,config,scale", [("replicated", 2, "small", 0.2), ("sharded", 2, "small", 0.2),
-                                                  ("replicated", 4, "small", 0.2), ("sharded", 2, "c4", 0.01)])
+                                                  ("replicated", 4, "small", 0.2), ("sharded", 2, "c4", 0.01),
+                                                  ("replicated", 8, "c2", 0.02), ("sharded", 8, "c4", 0.002)])
 def test_bench_two_ranks_gloo_rehearsal(dp, gpus, config, scale):
     """bench.py --gpus 2 end to end (launch, process group, DP replicas with the table exchange, timing,
     max-over-ranks, one JSON line) with both ranks on this one GPU over gloo (KGAT_BENCH_BACKEND):
@@ -214,9 +209,9 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus, config, scale):
     env = dict(os.environ, KGAT_BENCH_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--config", config, "--scale", str(scale),
-                        "--steps", "3", "--warmup", "1", "--dp", dp], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=240)
+    p = _run_logged([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--config", config, "--scale",
+                     str(scale), "--steps", "3", "--warmup", "1", "--dp", dp], env, f"bench_{dp}_{gpus}_{config}",
+                    timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, p.stdout
@@ -230,6 +225,31 @@ def test_bench_two_ranks_gloo_rehearsal(dp, gpus, config, scale):
         assert sum(fr["dp_table_exchange_steps"].values()) == 4
     if config == "c4":
         assert rec["config"]["embed_dim"] == 128 and rec["config"]["layer_size"] == [128, 64, 32]
+
+
+def test_bench_c5_eight_ranks_gloo_rehearsal():
+    """bench.py --gpus 8 --config c5 end to end at a tiny scale, all eight ranks on this one GPU
+    over gloo -- shard_bounds with 8 cuts, the N mod 8 tail rows, the 7-peer all-peer gathers of the pipelined
+    forward and the hop backward, the global-batch BPR -- with the frontier leg bit-identical to the
+    whole-shard step on every rank (the row-sharded path the driver's 8-GPU run takes, minus RCCL)."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, KGAT_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = _run_logged([sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--config", "c5", "--scale", "0.0005",
+                     "--steps", "2", "--warmup", "1"], env, "bench_c5_world8_gloo", timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "row-sharded x8"
+    rows = rec["config"]["shard_rows"]
+    assert len(rows) == 8 and sum(rows) == rec["config"]["nodes"] and min(rows) > 0
+    assert rec["rehearsal"].startswith("gloo") and rec["value"] > 0 and np.isfinite(rec["final_loss"])
+    assert rec["frontier_forward"]["bit_identical_to_full"]["pass"] is True, rec["frontier_forward"]
 
 
 def test_bench_c5_rank_share_small():
