@@ -453,6 +453,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
     # the table gradient's layer-0 A^T product runs fused with the table's Adam step inside
     # update_cf_weights (same bits; --no-fused-update: product and Adam as two passes)
     model.fuse_table_update = not args.no_fused_update
+    model.direct_backward = True  # the timed loop's plain loss.backward() (no DDP wrapper; model._StepLoss)
     B = cfg["batch"]
     # batches (host sampling is outside the hot path, main.py:300-305): uniform users,
     # a positive from the user's interactions, a uniform negative item

@@ -53,6 +53,11 @@ typedef struct kgat_csr {
   const int64_t *seg_beg;      /* [n_seg] */
   int32_t n_long;
   int32_t n_seg;
+  /* the segment length of a fixed-length plan (kgat_csr_plan: every segment but a
+   * row's last holds exactly seg_len entries); 0 for a plan whose segments vary in
+   * length (kgat_csr_plan_cols).  The SpMM kernels take a segment's end from the
+   * next segment's start and accept either; the row softmax's hub-segment
+   * arithmetic needs the fixed 512-entry plan and rejects any other. */
   int32_t seg_len;
   int32_t long_threshold;
   /* [4 * ceil(n_seg / 4)] or null (= identity): the segment each launch slot of the

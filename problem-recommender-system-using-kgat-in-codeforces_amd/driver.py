@@ -190,6 +190,7 @@ def train(args) -> dict:
     # every whole-table reader -- the CF phase, evaluation, state_dict -- flushes first)
     model.lazy_kg_adam = True
     model.capture_kg_step = True  # each KG step's forward / backward / update replays a captured HIP graph (same bits)
+    model.direct_backward = True  # this loop's plain loss.backward() without the autograd engine (no DDP hooks here)
     refresh = [torch.from_numpy(np.asarray(x, np.int64)).to(dev)
                for x in (layout.heads, layout.rels, layout.tails, layout.rel_order)]
     train_dict, val_dict = ds.interaction_dict("train"), ds.interaction_dict("validation")

@@ -241,8 +241,8 @@ class _PlanArrays:
         b = getattr(self, "base", self)
         return _lib.CSR(rowptr_ptr, b.col.data_ptr(), val.data_ptr(), self.n_rows, b.col.numel(),
                         self.long_rows.data_ptr(), self.long_seg_off.data_ptr(), self.seg_row.data_ptr(),
-                        self.seg_beg.data_ptr(), self.n_long, self.n_seg, SEG_LEN, self.long_threshold,
-                        _ptr(self.seg_order))
+                        self.seg_beg.data_ptr(), self.n_long, self.n_seg, 0 if self.col_cuts else SEG_LEN,
+                        self.long_threshold, _ptr(self.seg_order))
 
     def softmax_descriptor(self) -> _lib.CSR:
         """The descriptor with the fixed-length plan (kgat_row_softmax_plan_f32)."""
@@ -251,7 +251,7 @@ class _PlanArrays:
         d.long_rows, d.long_seg_off, d.seg_row, d.seg_beg = (lr.data_ptr(), off.data_ptr(), sr.data_ptr(),
                                                             sb.data_ptr())
         d.n_long, d.n_seg = self._fixed_n
-        d.long_threshold = LONG_THRESHOLD
+        d.seg_len, d.long_threshold = SEG_LEN, LONG_THRESHOLD
         d.seg_order = None
         return d
 

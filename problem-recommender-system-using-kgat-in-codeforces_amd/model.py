@@ -719,19 +719,27 @@ class _StepLoss(torch.Tensor):
     inputs, the reference training loops' call (main.py:312, 340) -- runs its step's backward directly
     (``grad_fn.fast_backward``) instead of through the autograd engine: no ones_like fill launch and no
     hand-off to the engine's device thread (~30-50 us of host time per call, the bulk of a captured KG
-    step's host cost).  Anything else (a scaled or summed loss, ``torch.autograd.backward``, ``retain_graph``)
-    takes the engine and the node's ordinary backward, the same state transitions either way; a second
-    backward raises as the engine's would.  Every other operation sees a plain tensor."""
+    step's host cost).  Opt-in: the node carries a ``fast_backward`` only when the model's
+    ``direct_backward`` is on (``driver.py`` and ``bench.py`` turn it on for their own loops).  It skips
+    every hook the engine would run, and the hooks C++ code installs on a leaf's AccumulateGrad node (DDP's
+    reducer, ``register_multi_grad_hook``) are not visible from Python -- so a model wrapped that way must
+    leave ``direct_backward`` off, its default.  Even when on, the engine takes over for anything else: a
+    scaled or summed loss, ``torch.autograd.backward``, ``retain_graph`` / ``create_graph`` / ``inputs``, a
+    hook on the loss itself, a leaf with Python-visible gradient hooks or a non-leaf parameter -- the same
+    state transitions either way; a second backward raises as the engine's would.  The direct call runs
+    under ``no_grad`` as the engine's backward does.  Every other operation sees a plain tensor."""
 
     __torch_function__ = torch._C._disabled_torch_function_impl
 
     def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
         node = self.grad_fn
         fast = getattr(node, "fast_backward", None) if node is not None else None
-        if fast is not None and gradient is None and not retain_graph and not create_graph and inputs is None:
+        if (fast is not None and gradient is None and not retain_graph and not create_graph and inputs is None
+                and not self._backward_hooks):
             node.fast_backward = None
             try:
-                fast(node)
+                with torch.no_grad():
+                    fast(node)
                 return None
             except _UseEngine:
                 pass
@@ -739,6 +747,10 @@ class _StepLoss(torch.Tensor):
 
 
 def _kg_fast_backward(ctx) -> None:
+    if any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
+           for p in ctx.leaves):
+        ctx.fast_backward = _kg_fast_backward
+        raise _UseEngine
     step, ctx.step = ctx.step, None
     if step is None:
         raise RuntimeError("Trying to backward through the graph a second time")
@@ -752,7 +764,8 @@ class _KGGraphLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, step, ids, opt, states, emb, rel_emb, trans):
         ctx.step = step
-        ctx.fast_backward = _kg_fast_backward
+        ctx.leaves = (emb, rel_emb, trans)
+        ctx.fast_backward = _kg_fast_backward if step.model.direct_backward else None
         return step.forward(ids, opt, *states).clone().view(()).as_subclass(_StepLoss)
 
     @staticmethod
@@ -1139,9 +1152,10 @@ _ONE: dict = {}  # device -> a resident fp32 1.0 (the plain backward's upstream 
 def _cf_fast_backward(ctx) -> None:
     """``loss.backward()`` of a TRAIN_CF loss without the engine (model._StepLoss): the node's backward with
     upstream gradient 1, its gradients accumulated into the leaves as the engine's AccumulateGrad does (set, or
-    added in place).  A leaf with gradient hooks (DDP and the like) sends the call through the engine."""
+    added in place).  Only reached with ``KGAT.direct_backward`` on (see _StepLoss); a non-leaf parameter or a
+    leaf with Python-visible gradient hooks still sends the call through the engine."""
     leaves = ctx.leaves
-    if any(getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
+    if any(not p.is_leaf or getattr(p, "_post_accumulate_grad_hooks", None) or getattr(p, "_backward_hooks", None)
            for p in leaves if p is not None):
         ctx.fast_backward = _cf_fast_backward
         raise _UseEngine
@@ -1241,6 +1255,10 @@ class KGAT(nn.Module):
         # Opt-in: TRAIN_CF's forward computes each layer on the rows the loss can reach only
         # (_frontier_forward) -- same loss, gradients and updates, bit for bit
         self.frontier_forward = False
+        # Opt-in: a plain ``loss.backward()`` of a TRAIN_CF / captured TRAIN_KG loss runs the step's backward
+        # without the autograd engine (_StepLoss).  Leave it off under wrappers that hook the leaves' gradient
+        # accumulators from C++ (DistributedDataParallel): the direct call cannot see those hooks
+        self.direct_backward = False
 
     @property
     def lazy_kg_adam(self) -> bool:
@@ -1419,7 +1437,10 @@ class KGAT(nn.Module):
             ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
                                   g.device)
         cfg = (g, drops, seeds, float(self._regularization_params[0]), hook, self._table_update, frontier, marks)
-        return _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
+        loss = _CFLoss.apply(*ids, cfg, self._user_entity_embedding.weight, *self._cf_weights())
+        if not self.direct_backward and loss.grad_fn is not None:
+            loss.grad_fn.fast_backward = None  # the autograd engine (the default; _StepLoss)
+        return loss
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
         dev = self._user_entity_embedding.weight.device

@@ -6,6 +6,7 @@ atol 1e-5 on O(1) values, atol 1e-6 on gradients of size ~1e-3).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import sys
 
@@ -664,6 +665,40 @@ def test_row_softmax_short_and_long_rows(pkg):
         e0, e1 = int(lay.rowptr[r0]), int(lay.rowptr[r1])
         assert torch.equal(part[e0:e1].cpu(), got[e0:e1]), (r0, r1)
         assert torch.isnan(part[:e0]).all() and torch.isnan(part[e1:]).all()  # nothing written outside
+
+
+def test_row_softmax_wide_graph_column_cut_plan(pkg):
+    """on a graph wide enough for the SpMM's column-cut plan (>= 8 x 8192 columns: A.descriptor()'s
+    hub segments end at 8192-column boundaries, variable length) the row softmax runs on the fixed 512-entry
+    plan (softmax_descriptor) and matches torch.sparse.softmax -- hub rows crossing many column blocks, the
+    whole CSR and row views of it bit for bit -- and kgat_row_softmax_plan_f32 rejects the column-cut
+    descriptor (seg_len 0) instead of computing wrong hub-row values."""
+    graph_mod, kernels = _mods(pkg)
+    lay, A = random_graph(graph_mod, 80000, 6, hubs=6, hub_deg=4000, seed=23, mids=200, mid_deg=120)
+    g = graph_mod.DeviceGraph(lay, DEV)
+    assert g.A.col_cuts and g.A.n_long >= 6
+    desc, sdesc = g.A.descriptor(), g.A.softmax_descriptor()
+    assert desc.seg_len == 0 and sdesc.seg_len == graph_mod.SEG_LEN and desc.n_seg > sdesc.n_seg
+    logits = (torch.randn(lay.nnz) * 3).to(DEV)
+    kernels.row_softmax(g, logits)
+    got = g.A.val.detach().cpu()
+    ref = torch.sparse.softmax(torch.sparse_coo_tensor(A.indices(), logits.cpu(), A.shape).coalesce(), dim=1)
+    np.testing.assert_allclose(got.numpy(), ref.values().numpy(), rtol=1e-5, atol=1e-7)
+    for r0, r1 in ((0, 80000), (11, 79001), (40000, 40517)):
+        view = graph_mod._CSRRowView(g.A, r0, r1, DEV)
+        assert view.descriptor().seg_len == 0
+        part = torch.full((lay.nnz,), float("nan"), device=DEV)
+        kernels.row_softmax_csr(view, logits, part)
+        e0, e1 = int(lay.rowptr[r0]), int(lay.rowptr[r1])
+        assert torch.equal(part[e0:e1].cpu(), got[e0:e1]), (r0, r1)
+    lib = __import__(pkg.__name__ + "._lib", fromlist=["_lib"])
+    work = torch.empty(2 * desc.n_seg + 2, device=DEV)
+    out = torch.empty(lay.nnz, device=DEV)
+    rc = lib.lib().kgat_row_softmax_plan_f32(ctypes.byref(desc), ctypes.c_void_p(logits.data_ptr()),
+                                             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(work.data_ptr()),
+                                             ctypes.c_int64(work.numel()),
+                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 1001  # KGAT_ERR_INVALID: the column-cut plan is not the softmax's
 
 
 def test_biinter_bwd_rows_matches_dense(pkg):
@@ -1448,6 +1483,9 @@ def test_fused_table_update_bit_identical(pkg, layers):
         m.train()
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
         m.fuse_table_update = fused
+        # the fused model's plain backward also skips the autograd engine (model._StepLoss): the real
+        # _cf_fast_backward against the engine's path, bit for bit
+        m.direct_backward = fused
         models.append(m)
     rng = np.random.default_rng(4)
     R = len(lay.rel_order)
@@ -1456,7 +1494,9 @@ def test_fused_table_update_bit_identical(pkg, layers):
         kg = [torch.from_numpy(rng.integers(0, hi, 32)).to(DEV) for hi in (U + E, R, U + E, U + E)]
         for m in models:
             torch.manual_seed(100 + step)  # same dropout seeds
-            m(*ids, mode=pkg.KGATMode.TRAIN_CF).backward()
+            loss = m(*ids, mode=pkg.KGATMode.TRAIN_CF)
+            assert (getattr(loss.grad_fn, "fast_backward", None) is not None) == m.direct_backward
+            loss.backward()
             deferred = m._table_update.pending is not None
             assert deferred == (m._user_entity_embedding.weight.grad is None)
             if m.fuse_table_update and layers == [64, 32]:
@@ -1990,6 +2030,7 @@ def test_captured_kg_step_bit_identical(pkg, dim):
         m.train()
         m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
         m.fuse_table_update = m.fuse_kg_table_update = m.lazy_kg_adam = True
+        m.direct_backward = True  # plain loss.backward() calls take the direct path (model._StepLoss)
         m.capture_kg_step = cap
         models.append(m)
     rng = np.random.default_rng(4)

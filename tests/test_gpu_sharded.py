@@ -182,6 +182,19 @@ def test_dp_exchange_paths_c4_shape(world):
     assert p.stdout.count(": OK") == world, p.stdout[-2000:]
 
 
+def test_ddp_wrapped_kgat_gradients_are_rank_means():
+    """KGAT inside torch.nn.parallel.DistributedDataParallel (gloo, two ranks on this GPU,
+    tests/ddp_worker.py): with the direct backward off (its default) a plain ``loss.backward()`` goes through
+    the autograd engine, DDP's reducer runs, and the table / aggregator gradients are the mean over ranks."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "tests" / "ddp_worker.py")]
+    p = _run_logged(cmd, env, "ddp_world2", timeout=300)
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert p.stdout.count("DDP OK") == 2, p.stdout[-2000:]
+
+
 def test_rccl_world1_collectives_match_gloo():
     """every collective of replicas.py / sharded.py through RCCL (backend "nccl",
     world 1 on the box's GPU, forced) vs the gloo / no-exchange paths (tests/rccl_worker.py)."""

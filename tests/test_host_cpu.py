@@ -348,3 +348,17 @@ def test_step_loss_plain_backward_takes_the_direct_path():
     F.apply(x).backward()  # a leaf with hooks: the engine (the hook runs)
     assert calls[-2:] == ["engine", "hook"]
     h.remove()
+    x.grad = None
+    loss = F.apply(x)
+    loss.register_hook(lambda g: calls.append("loss hook"))
+    loss.backward()  # a hook on the loss itself: the engine (the hook runs)
+    assert calls[-2:] == ["loss hook", "engine"]
+    x.grad = None
+
+    def grad_mode(ctx):  # the direct call runs under no_grad, as the engine's backward does
+        calls.append(f"grad enabled {torch.is_grad_enabled()}")
+    F2 = type("F2", (F,), {})
+    F2.forward = staticmethod(lambda ctx, x: (setattr(ctx, "fast_backward", grad_mode), (2 * x).sum())[1]
+                              .as_subclass(model._StepLoss))
+    F2.apply(x).backward()
+    assert calls[-1] == "grad enabled False"

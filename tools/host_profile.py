@@ -29,6 +29,7 @@ def main():
     m.train()
     m.build_optimizer(cf_lr=1e-3, kg_lr=1e-4)
     m.fuse_table_update = True
+    m.direct_backward = True
     m.frontier_forward = not full
     rng = np.random.default_rng(1)
     batches = [[torch.from_numpy(rng.integers(0, hi, 256)).to(dev) for hi in (U, int(E * 0.1), int(E * 0.1))]
