@@ -382,7 +382,9 @@ def roofline(events, cfg_name: str, n: int, nnz: int, d0: int, steps: int, kerne
 
 
 # --------------------------------------------------------------------------- timing
-def timed(step, batches, warmup: int, steps: int, world: int, dev):
+def timed(step, batches, warmup: int, steps: int, world: int, dev, wire_log=None):
+    """Warm-up steps, then ``steps`` timed steps (max over ranks).  ``wire_log`` (comm.WireLog): its byte
+    counts are taken over the timed steps only (``timed.wire_bytes``)."""
     kernels = importlib.import_module(PKG + ".kernels")
     for i in range(warmup):
         step(batches[i])
@@ -390,6 +392,8 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    if wire_log is not None:
+        wire_log.reset()
     # HIP events around the SpMM launches of every EVENT_EVERY-th timed step (each record costs the
     # stream a few us; --event-every 1 instruments every step)
     events_all = []
@@ -414,6 +418,7 @@ def timed(step, batches, warmup: int, steps: int, world: int, dev):
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
     timed.host_ms_per_step = float(np.median(host)) * 1e3
+    timed.wire_bytes = dict(wire_log.bytes) if wire_log is not None else None
     return elapsed, events, float(loss.item())
 
 
@@ -894,6 +899,7 @@ class ShareComm:
     def gather_at(self, send, out, starts, sizes):
         sh = importlib.import_module(PKG + ".sharded")
         lo, n_own = int(starts[0]), int(sizes[0])
+        _comm_mod().count_gather(self, out, n_own)  # what rank 0 would send to its share's 7 peers
         own = out[lo:lo + n_own]
         if n_own and send.data_ptr() != own.data_ptr():
             own.copy_(send)
@@ -914,20 +920,49 @@ class ShareComm:
         return self.gather_at(send, out, b[:-1], [hi - lo for lo, hi in zip(b[:-1], b[1:])])
 
     def exchange(self, send, recv):
+        _comm_mod().wire(self).add(send.numel() * send.element_size())
         return importlib.import_module(PKG + ".sharded")._Pending([])
 
     def all_to_all_v(self, send, send_off, recv, recv_off):
+        _comm_mod().wire(self).add(send.element_size() * (int(send_off[-1]) - int(send_off[1])))
         recv[int(recv_off[0]):int(recv_off[1])].copy_(send[int(send_off[0]):int(send_off[1])])
 
     def all_reduce_(self, t):
+        _comm_mod().count_all_reduce(self, t)
         return t
 
     def all_gather(self, t):
+        _comm_mod().count_all_gather(self, t)
         peers = self.peer_ids
         if peers is not None and t.dtype == torch.int64 and tuple(t.shape) == tuple(peers[0].shape):
             self.peer_ids = None
             return torch.stack([t] + [p.to(t.device) for p in peers])
         return t.unsqueeze(0).expand(self.world, *t.shape).contiguous()
+
+
+def _comm_mod():
+    return importlib.import_module(PKG + ".comm")
+
+
+def wire_per_step(counts: dict | None, steps: int, world: int, dev) -> dict | None:
+    """comm.WireLog counts over the timed steps -> bytes per step and rank by phase ("forward", "backward",
+    "other"); at world > 1 every rank's totals and the max over ranks (the wire-bound rank)."""
+    if counts is None:
+        return None
+    out = {k: v / steps for k, v in sorted(counts.items())}
+    total = sum(out.values())
+    out["total"] = total
+    if world > 1:
+        t = torch.tensor([float(out.get("forward", 0.0)), float(out.get("backward", 0.0)), total], device=dev)
+        allr = [torch.empty_like(t) for _ in range(world)]
+        torch.distributed.all_gather(allr, t)
+        per = torch.stack(allr).cpu().numpy()
+        out["per_rank_total"] = [float(x) for x in per[:, 2]]
+        out["max_rank_forward"] = float(per[:, 0].max())
+        out["max_rank_total"] = float(per[:, 2].max())
+    out["what"] = ("bytes this rank sends per CF step (comm.WireLog: a row gather = its rows x (G-1) peers, "
+                   "a ring all-reduce 2(G-1)/G of the buffer, an all-gather (G-1) x its part)")
+    return out
 
 
 def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
@@ -991,7 +1026,9 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         model.update_cf_weights()
         return loss
 
-    elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev)
+    wlog = _comm_mod().wire(comm)
+    elapsed, events, final_loss = timed(step, batches, args.warmup, args.steps, world, dev, wire_log=wlog)
+    wire_full = wire_per_step(timed.wire_bytes, args.steps, world, dev)
     ms = elapsed / args.steps * 1e3
     if args.timeline:
         # one more step with the pipelined forward's block marks (sharded.TIMELINE): per rank, GPU time of
@@ -1027,6 +1064,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
                    "graph": f"graph.HashedCKG (per-rank rows; {ckg.n_triples:,} distinct triples, repeats redrawn: "
                             f"E = {nnz:,} = {nnz / max(2 * ckg.n_triples, 1):.4f} x 2T)"},
         "bpr_pairs_per_s": B * world / (ms * 1e-3), "final_loss": final_loss, "spmm": spmm, "roofline": roof,
+        "wire_bytes_per_step": wire_full,
         "cpu_baseline": None,
         "cpu_baseline_note": "not run: the row-sharded config never runs at N = 1 and its CPU step "
                              "(50M x 704 fp32 tables + autograd state) exceeds host RAM",
@@ -1036,11 +1074,12 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         # on the first hop F + N(F) (this rank's part, marked from its A^T rows), the lower layers whole --
         # the rows the loss reads, with the whole-shard forward's bits (checked below); not in `value`
         model.frontier_forward = True
-        fel, fev, _ = timed(step, batches, args.warmup, args.steps, world, dev)
+        fel, fev, _ = timed(step, batches, args.warmup, args.steps, world, dev, wire_log=wlog)
         model.frontier_forward = False
         fms = fel / args.steps * 1e3
         res["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
+            "wire_bytes_per_step": wire_per_step(timed.wire_bytes, args.steps, world, dev),
             "bit_identical_to_full": sharded_frontier_matches_full(model, pkg, batches[0]) if not share else {
                 "pass": None, "what": "not checked in a rank share: the peers' rows of every gathered buffer are "
                                       "never computed, so the two forwards read different (uninitialised) rows"},

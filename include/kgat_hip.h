@@ -788,6 +788,19 @@ int kgat_ids_check_multi(const kgat_ids *ids, const int64_t *bounds, int64_t *ou
  * host's sorted unique ids).  kgat_frontier_reset(ids, n, node_map) restores -1. */
 int kgat_map_build(const int32_t *ids, int64_t n, int32_t *node_map, void *stream);
 
+/* kgat_map_build for a row list gathered from other processes (the row-sharded hop backward's
+ * all-peer gather of every rank's hop rows, sharded.py _hop_layer), which nothing on this rank
+ * has validated: an entry outside [-1, n_nodes) is not mapped, is overwritten with -1 (so
+ * kgat_frontier_reset skips it too), and sets *bad_host (pinned host-mapped memory, may be null)
+ * and *bad_dev (the optimiser kernels' skip flag, may be null).  No out-of-range access. */
+int kgat_map_build_checked(int32_t *ids, int64_t n, int32_t *node_map, int64_t n_nodes, int32_t *bad_host,
+                           int32_t *bad_dev, void *stream);
+
+/* The same check without a map: ids[i] outside [-1, bound) is overwritten with -1 and sets the
+ * flags (the row-sharded frontier forward's gathered row-set ids, before they place rows). */
+int kgat_ids_sanitize_i32(int32_t *ids, int64_t n, int64_t bound, int32_t *bad_host, int32_t *bad_dev,
+                          void *stream);
+
 /* out[i] = a[i] < 0 ? -1 : (b ? b[a[i]] : a[i]) + offset, -1 where b[a[i]] < 0 (out may alias a
  * when b is null).  Index plumbing of the row-sharded hop backward: a batch row's compact index
  * -> its position in a hop list (b = the hop list's node map), local -> global row ids (b null,

@@ -200,6 +200,8 @@ _SIGNATURES = {
     "kgat_gather_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kgat_fill_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_vp]),
     "kgat_map_build": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "kgat_map_build_checked": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kgat_ids_sanitize_i32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "kgat_map_compose": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "kgat_adam_lazy_catchup_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp,
                                                   c_vp, c_vp, c_i32, c_f32, c_f32, c_f32, c_vp]),

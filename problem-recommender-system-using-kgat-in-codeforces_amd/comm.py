@@ -26,6 +26,52 @@ from . import _lib
 _LOADED = False
 
 
+class WireLog:
+    """Bytes this rank puts on the wire, by phase (the row-sharded CF step sets ``phase`` to "forward" /
+    "backward"; everything else counts as "other").  Counted per collective from its shapes, the same rule
+    for every transport: a row gather sends this rank's rows to each of the G-1 peers, a ring all-reduce
+    2 (G-1) / G of the buffer, an all-gather (G-1) copies of this rank's part, an all-to-all the blocks
+    addressed to peers.  The bench reports it as ``wire_bytes_per_step`` (VERDICT r5 #3)."""
+
+    def __init__(self):
+        self.phase = "other"
+        self.bytes: dict[str, int] = {}
+
+    def add(self, nbytes: int) -> None:
+        if nbytes > 0:
+            self.bytes[self.phase] = self.bytes.get(self.phase, 0) + int(nbytes)
+
+    def reset(self) -> None:
+        self.bytes = {}
+
+
+def wire(comm) -> WireLog:
+    """The comm object's WireLog (created on first use)."""
+    w = comm.__dict__.get("_wire")
+    if w is None:
+        w = comm.__dict__["_wire"] = WireLog()
+    return w
+
+
+def count_gather(comm, out: torch.Tensor, n_own: int) -> None:
+    """A row gather / block post: this rank's n_own rows of ``out`` to each of the G-1 peers."""
+    if comm.world > 1 or getattr(comm, "counts_as", 0) > 1:
+        g = max(comm.world, getattr(comm, "counts_as", 0))
+        wire(comm).add(int(n_own) * out.stride(0) * out.element_size() * (g - 1))
+
+
+def count_all_reduce(comm, t: torch.Tensor) -> None:
+    g = max(comm.world, getattr(comm, "counts_as", 0))
+    if g > 1:
+        wire(comm).add(2 * (g - 1) * t.numel() * t.element_size() // g)
+
+
+def count_all_gather(comm, t: torch.Tensor) -> None:
+    g = max(comm.world, getattr(comm, "counts_as", 0))
+    if g > 1:
+        wire(comm).add((g - 1) * t.numel() * t.element_size())
+
+
 def _load_rccl() -> None:
     global _LOADED
     if _LOADED:
@@ -132,6 +178,7 @@ class RcclComm:
         self._check(send, "send")
         row = out.stride(0) * out.element_size()
         offs = (ctypes.c_int64 * (self.world + 1))(*[int(b) * row for b in bounds])
+        count_gather(self, out, int(bounds[self.rank + 1]) - int(bounds[self.rank]))
         st = self._begin(send, out)
         _lib.call("kgat_comm_allgatherv", self._h, send.data_ptr(), out.data_ptr(), offs, st)
         return self._end()
@@ -145,6 +192,7 @@ class RcclComm:
         nb = (ctypes.c_int64 * self.world)(*[int(z) * row for z in sizes])
         if int(sizes[self.rank]):
             self._check(send, "send")
+        count_gather(self, out, int(sizes[self.rank]))
         st = self._begin(send, out)
         _lib.call("kgat_comm_gather_at", self._h, send.data_ptr() if int(sizes[self.rank]) else None, out.data_ptr(),
                   offs, nb, st)
@@ -158,6 +206,8 @@ class RcclComm:
         es = send.element_size()
         so = (ctypes.c_int64 * (self.world + 1))(*[int(x) * es for x in send_off])
         ro = (ctypes.c_int64 * (self.world + 1))(*[int(x) * es for x in recv_off])
+        wire(self).add(es * (int(send_off[-1]) - int(send_off[0]) - (int(send_off[self.rank + 1]) -
+                                                                      int(send_off[self.rank]))))
         st = self._begin(send, recv)
         _lib.call("kgat_comm_alltoallv", self._h, send.data_ptr(), so, recv.data_ptr(), ro, st)
         self._end().wait()
@@ -169,6 +219,7 @@ class RcclComm:
         nbytes = send.numel() * send.element_size()
         if recv.numel() * recv.element_size() != nbytes:
             raise ValueError("exchange: send and recv sizes differ")
+        wire(self).add(nbytes)
         st = self._begin(send, recv)
         _lib.call("kgat_comm_ring_exchange", self._h, send.data_ptr(), recv.data_ptr(), nbytes, st)
         return self._end()
@@ -180,6 +231,7 @@ class RcclComm:
         self._check(t, "t")
         if t.dtype != torch.float32:
             raise ValueError("all_reduce_: fp32 only")
+        count_all_reduce(self, t)
         st = self._begin(t)
         _lib.call("kgat_comm_allreduce_sum_f32", self._h, t.data_ptr(), t.data_ptr(), t.numel(), st)
         self._end().wait()
@@ -192,6 +244,7 @@ class RcclComm:
         t = t.contiguous()
         self._check(t, "t")
         out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        count_all_gather(self, t)
         st = self._begin(t, out)
         _lib.call("kgat_comm_allgather_rows", self._h, t.data_ptr(), out.data_ptr(), t.numel() * t.element_size(), st)
         self._end().wait()

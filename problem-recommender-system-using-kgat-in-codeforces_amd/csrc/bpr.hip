@@ -80,8 +80,10 @@ __global__ __launch_bounds__(256) void bpr_fwd_kernel(kgat_tables T, const int64
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's term store has completed
   __syncthreads();
+  // acq_rel: releases this block's term stores to every XCD's L2 before its arrival counts, and the last
+  // arrival acquires every other block's before the sum reads them (the memory model, not the s_waitcnt)
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;  // block-uniform
   bpr_loss_sum(term, batch, loss, red, true);

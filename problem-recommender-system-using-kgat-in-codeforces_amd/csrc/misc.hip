@@ -81,6 +81,48 @@ __global__ __launch_bounds__(256) void map_build_kernel(const int32_t* __restric
     if (ids[i] >= 0) node_map[ids[i]] = static_cast<int32_t>(i);
 }
 
+// kgat_map_build over ids that came from another process (a row-sharded peer's gathered hop rows): an
+// id outside [-1, n_nodes) is not mapped -- it is set to -1 in place, so kgat_frontier_reset skips it
+// too -- and raises the host flag (pinned, host-mapped; plain store) and the device skip flag.
+__global__ __launch_bounds__(256) void map_build_checked_kernel(int32_t* __restrict__ ids, int64_t n,
+                                                                int32_t* __restrict__ node_map, int64_t n_nodes,
+                                                                int32_t* bad_host, int32_t* bad_dev) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  bool flag = false;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int32_t x = ids[i];
+    if (x >= 0 && x < n_nodes) {
+      node_map[x] = static_cast<int32_t>(i);
+    } else if (x != -1) {
+      ids[i] = -1;
+      flag = true;
+    }
+  }
+  if (flag) {  // every writer stores 1 (as ids_check_kernel): no atomic needed
+    if (bad_host != nullptr) *bad_host = 1;
+    if (bad_dev != nullptr) *bad_dev = 1;
+  }
+}
+
+// ids outside [-1, bound) become -1 in place and raise the flags (a gathered row list from other
+// processes, checked before anything indexes with it)
+__global__ __launch_bounds__(256) void ids_sanitize_kernel(int32_t* __restrict__ ids, int64_t n, int64_t bound,
+                                                           int32_t* bad_host, int32_t* bad_dev) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  bool flag = false;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int32_t x = ids[i];
+    if (x < -1 || x >= bound) {
+      ids[i] = -1;
+      flag = true;
+    }
+  }
+  if (flag) {  // every writer stores 1 (as ids_check_kernel)
+    if (bad_host != nullptr) *bad_host = 1;
+    if (bad_dev != nullptr) *bad_dev = 1;
+  }
+}
+
 // out[i] = a[i] < 0 ? -1 : (b ? b[a[i]] : a[i]) + offset  (b[.] < 0 stays -1)
 __global__ __launch_bounds__(256) void map_compose_kernel(const int32_t* __restrict__ a, int64_t n,
                                                           const int32_t* __restrict__ b, int32_t offset,
@@ -629,6 +671,27 @@ extern "C" int kgat_map_build(const int32_t* ids, int64_t n, int32_t* node_map, 
   if (n == 0) return KGAT_OK;
   hipLaunchKernelGGL(kgat::map_build_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), ids, n, node_map);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_map_build_checked(int32_t* ids, int64_t n, int32_t* node_map, int64_t n_nodes, int32_t* bad_host,
+                                      int32_t* bad_dev, void* stream) {
+  if (!node_map || n < 0 || (n && !ids) || n > INT32_MAX || n_nodes < 0 || n_nodes > INT32_MAX)
+    return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::map_build_checked_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ids, n, node_map, n_nodes, bad_host, bad_dev);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+extern "C" int kgat_ids_sanitize_i32(int32_t* ids, int64_t n, int64_t bound, int32_t* bad_host, int32_t* bad_dev,
+                                     void* stream) {
+  if (n < 0 || (n && !ids) || bound < 0) return KGAT_ERR_INVALID;
+  if (n == 0) return KGAT_OK;
+  hipLaunchKernelGGL(kgat::ids_sanitize_kernel, dim3(kgat::blocks_for(n, 256, kgat::kCUs * 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ids, n, bound, bad_host, bad_dev);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void lists_mark_kernel(const int32_t* __restri
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int64_t g = i / cap;
-  if (i - g * cap >= counts[g]) return;
+  if (i - g * cap >= counts[g]) return;  // (a count past cap reads nothing beyond list g: i - g * cap < cap)
   const int32_t r = lists[i];
   if (r >= 0 && r < n) atomicOr(&bits[r >> 5], 1u << (r & 31));
 }
@@ -548,12 +548,13 @@ __global__ __launch_bounds__(256) void lists_merge_kernel(const int32_t* __restr
     int32_t pos = -1;
     if (lane < G) {  // lane g: lower bound of node in list g
       const int32_t* lg = lists + static_cast<int64_t>(lane) * cap;
-      int32_t lo = 0, hi = counts[lane];
+      const int32_t cnt = min(max(counts[lane], 0), cap);  // a corrupt gathered count stays inside list g
+      int32_t lo = 0, hi = cnt;
       while (lo < hi) {
         const int32_t mid = (lo + hi) >> 1;
         if (lg[mid] < node) lo = mid + 1; else hi = mid;
       }
-      if (lo < counts[lane] && lg[lo] == node) pos = lo;
+      if (lo < cnt && lg[lo] == node) pos = lo;
     }
     wpos[lane] = pos;
     __builtin_amdgcn_wave_barrier();

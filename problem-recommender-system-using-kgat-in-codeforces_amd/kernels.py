@@ -1014,9 +1014,10 @@ _TICKETS: dict = {}
 
 def ticket_word(device: torch.device, slot: int) -> torch.Tensor:
     """A device uint32 word that is 0 between launches (the in-launch reductions' arrival counters,
-    e.g. kgat_bpr_fwd_ex_f32's): per device, one slot per kernel kind; launches sharing one are
-    stream-ordered (every caller in this package issues them on the device's current stream)."""
-    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    e.g. kgat_bpr_fwd_ex_f32's): per (device, stream), one slot per kernel kind -- launches sharing a
+    word are ordered by their stream, so two streams running the same kernel kind never share one."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (device.type, idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _TICKETS.get(key)
     if buf is None:
         buf = _TICKETS[key] = torch.zeros(64, dtype=torch.int32, device=device)

@@ -435,6 +435,9 @@ class ShardedGradSync:
         if n == 1 and not self.force:
             return
         bc, self._bcast, self._stepped = self._bcast, [], set()
+        # the step is complete (stepped, or abandoned before this call): its owner-block counters may no
+        # longer be taken back by a later abandon_step
+        self._advanced = []
         for w in bc:  # the pipelined blocks' broadcasts: the current stream waits for the last of them
             w.wait()
         rank = _rank()

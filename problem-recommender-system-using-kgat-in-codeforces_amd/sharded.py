@@ -56,6 +56,7 @@ from torch import nn
 
 from . import kernels
 from . import _lib
+from .comm import count_all_gather, count_all_reduce, count_gather, wire
 from .graph import GraphLayout, RefreshPlan, _CSRRowView, _DeviceCSR, degree_weights, stream_ptr
 from . import model as _model
 from .model import Aggregator, KGATArgs, KGATMode, MultiHeadAttention
@@ -104,6 +105,7 @@ class Comm:
 
     def exchange(self, send: torch.Tensor, recv: torch.Tensor) -> _Pending:
         """Start: send -> next rank, prev rank -> recv.  wait() completes both."""
+        wire(self).add(send.numel() * send.element_size())
         if self.host:
             s, r = send.detach().cpu(), torch.empty(recv.shape, dtype=recv.dtype)
             ops = [dist.P2POp(dist.isend, s, self.next, self.group), dist.P2POp(dist.irecv, r, self.prev, self.group)]
@@ -130,6 +132,7 @@ class Comm:
             own.copy_(send)
         if not self.active or self.world == 1:
             return _Pending([])
+        count_gather(self, out, n_own)
         peers = [r for r in range(self.world) if r != k]
         if self.host:
             s = own.detach().cpu() if n_own else None
@@ -160,6 +163,8 @@ class Comm:
         if not self.active or self.world == 1:
             return
         peers = [r for r in range(self.world) if r != k]
+        wire(self).add(send.element_size() * (int(send_off[-1]) - int(send_off[0]) - (int(send_off[k + 1]) -
+                                                                                       int(send_off[k]))))
         src = send.detach().cpu() if self.host else send
         dst = torch.empty(recv.shape, dtype=recv.dtype) if self.host else recv
         ops = []
@@ -181,6 +186,7 @@ class Comm:
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if not self.active:
             return t
+        count_all_reduce(self, t)
         if self.host:
             c = t.detach().cpu()
             dist.all_reduce(c, group=self.group)
@@ -193,6 +199,7 @@ class Comm:
         """[world, *t.shape], rank order."""
         if not self.active:
             return t.unsqueeze(0)
+        count_all_gather(self, t)
         if self.host:
             c = t.detach().cpu().contiguous()
             parts = [torch.empty_like(c) for _ in range(self.world)]
@@ -228,6 +235,49 @@ def _transpose_rows(rowptr: np.ndarray, col: np.ndarray, val: np.ndarray, lo: in
     np.cumsum(np.bincount(tr, minlength=hi - lo), out=rp[1:])
     del n
     return rp, rows[order].astype(np.int32), np.asarray(val, np.float32)[sel][order]
+
+
+class _PeerIdGuard:
+    """The hop backward's check of the row ids other ranks sent.  The all-peer gather of
+    every rank's hop rows (``_hop_layer``) hands this rank ids no local code produced; they index its node
+    map.  ``kgat_map_build_checked`` maps only ids inside [0, N), overwrites any other with -1 (so nothing
+    downstream -- the masked A^T product, which looks rows up through the map, and the map reset -- reads
+    or writes out of range) and raises a flag in pinned host memory and one on the device.  The flag is
+    read before the optimiser step (``RowShardedKGAT.update_cf_weights``) and before a deferred table
+    gradient is materialised: the step is abandoned -- no parameter or Adam moment moves, its gradients and
+    deferred update are dropped -- and IndexError is raised, instead of a GPU fault.  Every rank receives
+    the same gathered ids, so every rank abandons the same step."""
+
+    def __init__(self, device):
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self.event = torch.cuda.Event()
+        self.pending = False
+
+    def map_build(self, ids: torch.Tensor, total: int, node_map: torch.Tensor, n_nodes: int) -> None:
+        _lib.call("kgat_map_build_checked", ids.data_ptr(), total, node_map.data_ptr(), n_nodes,
+                  self.host.data_ptr(), self.dev.data_ptr(), stream_ptr(ids.device))
+        self.event.record()
+        self.pending = True
+
+    def sanitize(self, ids: torch.Tensor, total: int, n_nodes: int) -> None:
+        """Gathered ids outside [-1, N) become -1 (nothing indexes with them) and raise the flags."""
+        _lib.call("kgat_ids_sanitize_i32", ids.data_ptr(), total, n_nodes, self.host.data_ptr(), self.dev.data_ptr(),
+                  stream_ptr(ids.device))
+        self.event.record()
+        self.pending = True
+
+    def take(self) -> bool:
+        """True (and the flags cleared) if a gathered id since the last call was out of range."""
+        if not self.pending:
+            return False
+        self.event.synchronize()
+        self.pending = False
+        if not int(self.host[0]):
+            return False
+        self.host.zero_()
+        self.dev.zero_()
+        return True
 
 
 class RowShard:
@@ -276,20 +326,30 @@ class RowShard:
         self.node_map = torch.full((self.n_nodes,), -1, dtype=torch.int32, device=self.device)
         self._ident = None
 
-    def hop_buffers(self):
+    def peer_ids(self) -> _PeerIdGuard:
+        """The check of the hop rows gathered from the peers (allocated once)."""
+        g = self.__dict__.get("_peer_ids")
+        if g is None:
+            g = self._peer_ids = _PeerIdGuard(self.device)
+        return g
+
+    def hop_buffers(self, slot: int = 0):
         """Scratch of the hop backward (allocated once): local row flags, local row -> hop position,
-        the hop rows (local ids), device count, kgat_hop_compact's scan work."""
-        hb = self.__dict__.get("_hop")
+        the hop rows (local ids), device count, kgat_hop_compact's scan work.  ``slot`` 1: a second set
+        (the frontier forward's second hop, listed while the first hop's list is still in use)."""
+        key = "_hop" if slot == 0 else f"_hop{slot}"
+        hb = self.__dict__.get(key)
         if hb is None:
             n, dev = self.n, self.device
             work = int(_lib.lib().kgat_hop_compact_work_bytes(n))
             if work < 0:
                 raise ValueError("shard too large for the hop compaction")
-            hb = self._hop = (torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
-                              torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev),
-                              torch.empty(max(n, 1), dtype=torch.int32, device=dev),
-                              torch.zeros(1, dtype=torch.int32, device=dev),
-                              torch.empty(max(work, 1), dtype=torch.uint8, device=dev))
+            hb = (torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+                  torch.full((max(n, 1),), -1, dtype=torch.int32, device=dev),
+                  torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                  torch.zeros(1, dtype=torch.int32, device=dev),
+                  torch.empty(max(work, 1), dtype=torch.uint8, device=dev))
+            self.__dict__[key] = hb
         return hb
 
     def ident(self, n: int) -> torch.Tensor:
@@ -333,12 +393,98 @@ class RowShard:
         return plan
 
 
+# The frontier forward's layer inputs travel as row sets (_RowSet: only the rows the next product reads)
+# when those rows are at most this fraction of the nodes; beyond it the whole-table gather moves about as
+# many bytes without the ids and the placement pass.  KGAT_ROW_SET_GATHERS=0: whole-table gathers only.
+COMPACT_FRACTION = 0.6
+ROW_SET_GATHERS = os.environ.get("KGAT_ROW_SET_GATHERS", "1") != "0"
+
+
+class _RowSet:
+    """The rows of a layer input that the next product reads, per rank -- the frontier forward's row-set
+    gathers (model.py:124-140 reads layer L-1's input on N(F) only, layer L-2's on N(hop1)).
+    Holds this rank's rows (local ids, ascending: the first ``m`` of ``rows``), every rank's count, the
+    global ids of every rank's rows in rank order (one int32 all-peer gather, range-checked: _PeerIdGuard)
+    and, for a pipelined producer, every rank's per-block counts.  Only these rows travel; the receiver
+    places them at their global rows of the [N, d] buffer the single-GPU SpMM reads, so every row the
+    product reads holds the bits the whole-table gather would have put there (the others are never read)."""
+
+    def __init__(self, shard: RowShard, comm, rows: torch.Tensor, m: int, counts, block_counts=None):
+        dev = shard.device
+        self.m = int(m)
+        self.counts = np.asarray(counts, np.int64).reshape(-1)
+        self.off = np.concatenate([[0], np.cumsum(self.counts)]).astype(np.int64)
+        self.total = int(self.off[-1])
+        self.k = comm.rank if comm.active else 0
+        self.rows = rows[:self.m] if self.m else torch.full((1,), -1, dtype=torch.int32, device=dev)
+        ids = torch.empty(max(self.total, 1), dtype=torch.int32, device=dev)
+        own = ids[int(self.off[self.k]):int(self.off[self.k + 1])]
+        if self.m:
+            kernels.map_compose(self.rows, None, shard.lo, out=own)
+        comm.gather_v(own, ids, self.off).wait()
+        if self.total:
+            shard.peer_ids().sanitize(ids, self.total, shard.n_nodes)
+        self.ids = ids
+        self.block_counts = self.block_off = None
+        if block_counts is not None:
+            bc = np.asarray(block_counts, np.int64)  # [G, K]
+            self.block_counts = bc
+            self.block_off = np.concatenate([np.zeros((bc.shape[0], 1), np.int64), np.cumsum(bc, 1)], 1)
+
+    def buffer(self, d: int, dev) -> torch.Tensor:
+        """The compact receive buffer: every rank's rows, rank order (= ``ids`` order)."""
+        return torch.empty(max(self.total, 1), d, dtype=torch.float32, device=dev)
+
+    def post_block(self, comm, h: torch.Tensor, Pc: torch.Tensor, b: int):
+        """Post block b's rows of the set (rows of h, a pipelined layer's output) to every peer, compact."""
+        k, G = self.k, self.counts.size
+        a, z = int(self.block_off[k][b]), int(self.block_off[k][b + 1])
+        own = Pc[int(self.off[k]) + a:int(self.off[k]) + z]
+        if z > a:
+            kernels.gather_rows(h, self.rows[a:z], out=own)
+        starts = [int(self.off[r] + self.block_off[r][b]) for r in range(G)]
+        sizes = [int(self.block_counts[r][b]) for r in range(G)]
+        return comm.gather_at(own, Pc, starts, sizes)
+
+    def place(self, buf: torch.Tensor, Pc: torch.Tensor) -> None:
+        """Every rank's compact rows into their global rows of ``buf``."""
+        if self.total:
+            kernels.scatter_rows(buf, self.ids[:self.total], Pc[:self.total], accumulate=False)
+
+    def gather(self, shard: RowShard, comm, X: torch.Tensor) -> torch.Tensor:
+        """[N, d]: every rank's rows of this set of X at their global rows (the rest never written)."""
+        d = X.shape[1]
+        Pc = self.buffer(d, X.device)
+        own = Pc[int(self.off[self.k]):int(self.off[self.k + 1])]
+        if self.m:
+            kernels.gather_rows(X, self.rows, out=own)
+        comm.gather_v(own, Pc, self.off).wait()
+        buf = torch.empty(shard.n_nodes, d, dtype=torch.float32, device=X.device)
+        self.place(buf, Pc)
+        return buf
+
+
+def _ids_bitmap(shard: RowShard, ids: torch.Tensor, total: int) -> torch.Tensor:
+    """int32 bitmap over the N nodes with the bits of ``ids`` (global, distinct, checked) set: through
+    the node map (kgat_map_build, kgat_map_bits, then the map reset)."""
+    N = shard.n_nodes
+    bits = torch.empty(2 * ((N + 63) // 64) + 2, dtype=torch.int32, device=shard.device)
+    if total:
+        _lib.call("kgat_map_build", ids.data_ptr(), total, shard.node_map.data_ptr(), stream_ptr(shard.device))
+    kernels.map_bits(shard.node_map, bits)
+    if total:
+        kernels.frontier_reset(ids[:total], shard.node_map)
+    return bits
+
+
 def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-                  transpose: bool = False, rows=None, pre=None) -> torch.Tensor:
+                  transpose: bool = False, rows=None, pre=None, need: "_RowSet | None" = None) -> torch.Tensor:
     """out (+)= csr . Xg, Xg = [N, d] every rank's rows of X (all-peer gather), csr = shard.A (forward)
     or shard.AT (backward).  Column chunks of GATHER_CHUNK: chunk c+1 is on the wire while chunk c's
     product runs; each product is the single-GPU kernel on the local rows.  ``rows`` = (list, device
-    count, bitmap) of local output rows: only those rows are produced (kgat_spmm_csr_rows_f32)."""
+    count, bitmap) of local output rows: only those rows are produced (kgat_spmm_csr_rows_f32).
+    ``need``: the rows of X the product reads, per rank (_RowSet) -- only those travel (compact), the rest
+    of Xg is never read."""
     n, d = X.shape
 
     def product(src, dst):
@@ -350,6 +496,8 @@ def gathered_spmm(shard: RowShard, comm, csr, X: torch.Tensor, out: torch.Tensor
         return product(X, out)
     if pre is not None:  # gathered by the previous (pipelined) layer's block posts
         return product(_gathered(shard, comm, X, pre), out)
+    if need is not None:  # only the rows the product reads travel
+        return product(need.gather(shard, comm, X), out)
     w = min(d, GATHER_CHUNK) if GATHER_CHUNK > 0 else d
     chunks = [(c, min(c + w, d)) for c in range(0, d, w)]
     N, lo, hi = shard.n_nodes, shard.lo, shard.hi
@@ -419,24 +567,30 @@ def _gathered(shard: RowShard, comm, X: torch.Tensor, pre) -> torch.Tensor:
     """[N, d] every rank's rows of X: the blocks a pipelined layer already posted (``pre`` = (buffer,
     pending posts)), else one whole-width all-peer gather."""
     if pre is not None:
-        buf, pends = pre
+        buf, pends = pre[:2]
         for i, pd in enumerate(pends):
             pd.wait()
             _mark(f"width {buf.shape[1]}: block {i} post landed")
+        if len(pre) == 4:  # compact block posts (a _RowSet): every rank's rows into place
+            rs, Pc = pre[2], pre[3]
+            rs.place(buf, Pc)
         return buf
     return gather_table(shard, comm, X)
 
 
 def _layer_pipelined(shard: RowShard, comm, blocks: _RowBlocks, Xg: torch.Tensor, x: torch.Tensor, W1, b1, W2, b2,
-                     drop: float, seed: int, st, s: torch.Tensor):
+                     drop: float, seed: int, st, s: torch.Tensor, need_next: "_RowSet | None" = None):
     """One whole-shard layer forward computed in row blocks, each block's output rows posted to every peer
     (the next layer's gathered input) as soon as they exist: the next layer's gather travels under this
     layer's remaining blocks instead of after the layer.  Per row: the SpMM of its edges in order (a row
     view of A), the bi-interaction with its own dropout draws and state (the tile-list / row-list kernels)
-    -- the whole launch's bits.  Returns (this rank's output rows, (next gathered buffer, pending posts))."""
+    -- the whole launch's bits.  Returns (this rank's output rows, (next gathered buffer, pending posts)).
+    ``need_next`` (a _RowSet with per-block counts): only the block's rows the next layer reads are posted
+    (compact; placed into the gathered buffer once every post has landed)."""
     dout = W1.shape[0]
     h = torch.empty(shard.n, dout, dtype=torch.float32, device=x.device)
     nxt = torch.empty(shard.n_nodes, dout, dtype=torch.float32, device=x.device)
+    Pc = need_next.buffer(dout, x.device) if need_next is not None else None
     pends = []
     for b in range(blocks.K):
         a0, a1 = blocks.mine[b], blocks.mine[b + 1]
@@ -448,9 +602,12 @@ def _layer_pipelined(shard: RowShard, comm, blocks: _RowBlocks, Xg: torch.Tensor
             else:
                 kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drop, seed, h, blocks.bits[b], state=st)
         _mark(f"width {dout}: block {b} computed")
-        pends.append(comm.gather_at(h[a0:a1], nxt, blocks.starts[b], blocks.sizes[b]))
+        if need_next is None:
+            pends.append(comm.gather_at(h[a0:a1], nxt, blocks.starts[b], blocks.sizes[b]))
+        else:
+            pends.append(need_next.post_block(comm, h, Pc, b))
         _mark(f"width {dout}: block {b} posted")
-    return h, (nxt, pends)
+    return h, ((nxt, pends) if need_next is None else (nxt, pends, need_next, Pc))
 
 
 def gather_table(shard: RowShard, comm, X: torch.Tensor) -> torch.Tensor:
@@ -511,7 +668,7 @@ def _host_bits(ids: np.ndarray, n: int, device) -> torch.Tensor:
     return torch.from_numpy(b.view(np.int32)).to(device, non_blocking=True)
 
 
-def _frontier_sets(shard: RowShard, comm, rows, L: int):
+def _frontier_sets(shard: RowShard, comm, rows, L: int, blocks: _RowBlocks | None = None):
     """The row sets the CF loss reaches, per layer (this rank's part): the last layer's output is read
     on the batch rows F only (model.py:189-191), layer L-2's on the first hop F + N(F) (the last layer
     gathers its A rows there).  Returns [set for layer l] with None = the whole shard, else
@@ -519,9 +676,17 @@ def _frontier_sets(shard: RowShard, comm, rows, L: int):
     F from the host's batch ids; the first hop marked on the device from this rank's rows of A^T
     (row j is in it iff j is in F or A^T[j, f] != 0 for some f in F: kgat_csr_mark_rows), kept when
     the global set holds at most model.HOP_DENSE_FRACTION of the nodes (the counts are all-gathered,
-    one host sync) -- the backward then runs layer L-2 on the same set."""
+    one host sync) -- the backward then runs layer L-2 on the same set.
+
+    Also returns ``needs``: per layer, None (its input is gathered whole) or the _RowSet of input rows its
+    product reads.  Layer L-1 reads its input on N(F), inside the first hop -- every rank's
+    first-hop rows travel (the layer L-2 output rows that exist).  Layer L-2 reads its input on the second
+    hop N(hop1): each owner marks its rows j with A^T[j, h] != 0 for an h of the global first hop (whose
+    ids the first row set just gathered), and they travel when the global set holds at most
+    COMPACT_FRACTION of the nodes -- posted block by block when a pipelined layer produces them."""
     dev = shard.device
     sets = [None] * L
+    needs = [None] * L
     m = rows.n_frontier
     sets[L - 1] = (rows.frontier, torch.tensor([m], dtype=torch.int32).to(dev, non_blocking=True),
                    _host_bits(rows.frontier_np, shard.n, dev), m)
@@ -536,7 +701,22 @@ def _frontier_sets(shard: RowShard, comm, rows, L: int):
             kernels.map_bits(hmap[:shard.n], bits)
             k = comm.rank if comm.active else 0
             sets[L - 2] = (hrows, count.clone(), bits, int(counts[k]))
-    return sets
+            if comm.active and ROW_SET_GATHERS:
+                hop1 = needs[L - 1] = _RowSet(shard, comm, hrows, int(counts[k]), counts)
+                gb = _ids_bitmap(shard, hop1.ids, hop1.total)
+                hit2, hmap2, hrows2, count2, work2 = shard.hop_buffers(1)
+                kernels.csr_mark_rows(shard.AT, gb, shard.n_nodes, shard.lo, hit2)
+                kernels.hop_list(hit2[:shard.n], hmap2, hrows2, count2, work2)
+                # a pipelined layer L-3 posts its output block by block: every rank's per-block counts too
+                piped = blocks is not None and L >= 3
+                parts = [count2.long()]
+                if piped:
+                    parts += [hit2[a:b].sum().reshape(1) for a, b in zip(blocks.mine[:-1], blocks.mine[1:])]
+                g2 = comm.all_gather(torch.cat(parts)).reshape(-1, len(parts)).cpu().numpy().astype(np.int64)
+                if int(g2[:, 0].sum()) <= COMPACT_FRACTION * shard.n_nodes:
+                    needs[L - 2] = _RowSet(shard, comm, hrows2, int(g2[k, 0]), g2[:, 0],
+                                           g2[:, 1:] if piped else None)
+    return sets, needs
 
 
 class _ShardTableUpdate:
@@ -627,7 +807,8 @@ def _hop_layer(shard: RowShard, comm, l: int, tables, sides, states, ws, drops, 
     for p in pend:
         p.wait()
     if total:
-        _lib.call("kgat_map_build", ids.data_ptr(), total, shard.node_map.data_ptr(), stream_ptr(dev))
+        # the peers' blocks were never validated here: ids outside [0, N) are dropped, not indexed
+        shard.peer_ids().map_build(ids, total, shard.node_map, shard.n_nodes)
     if l == 0 and defer is not None:
         defer.defer(shard, Pg, ids, total, din)  # the table's product runs fused with its Adam step
         return None, True
@@ -648,7 +829,8 @@ class _ShardedCFLoss(torch.autograd.Function):
         # frontier forward: layers whose output the loss reads on a row set only run on that set (the
         # rest of their tables is never read: the next layer's A rows, the BPR rows and the backward
         # all stay inside it); per row the whole-shard call's bits
-        sets = _frontier_sets(shard, comm, rows, L) if frontier else [None] * L
+        wire(comm).phase = "forward"
+        sets, needs = _frontier_sets(shard, comm, rows, L, blocks) if frontier else ([None] * L, [None] * L)
         x = X0
         pre = None  # the next layer's gathered input, posted block by block by a pipelined layer
         for l in range(L):
@@ -657,14 +839,14 @@ class _ShardedCFLoss(torch.autograd.Function):
             st = kernels.make_state(x.shape[0], W1.shape[1], W1.shape[0], x.device)
             if sets[l] is None and blocks is not None and l + 1 < L and comm.active:
                 x, pre = _layer_pipelined(shard, comm, blocks, _gathered(shard, comm, x, pre), x, W1, b1, W2, b2,
-                                          drops[l], seeds[l], st, s)
+                                          drops[l], seeds[l], st, s, need_next=needs[l + 1])
             elif sets[l] is None:
-                gathered_spmm(shard, comm, shard.A, x, s, pre=pre)
+                gathered_spmm(shard, comm, shard.A, x, s, pre=pre, need=needs[l])
                 pre = None
                 x = kernels.biinter_fwd(x, s, W1, b1, W2, b2, drops[l], seeds[l], state=st)
             else:
                 rws, cnt, bits, m = sets[l]
-                gathered_spmm(shard, comm, shard.A, x, s, rows=(rws, cnt, bits), pre=pre)
+                gathered_spmm(shard, comm, shard.A, x, s, rows=(rws, cnt, bits), pre=pre, need=needs[l])
                 pre = None
                 h = torch.empty(shard.n, W1.shape[0], dtype=torch.float32, device=x.device)
                 if st.kind == "gemm":
@@ -679,11 +861,13 @@ class _ShardedCFLoss(torch.autograd.Function):
         ctx.cfg, ctx.saved = cfg, (tables, sides, states, Tc, coef, ws)
         ctx.ids = (cu, cp, cn)
         ctx.forced = {l for l in range(L - 1) if sets[l] is not None}
+        wire(comm).phase = "other"
         return loss.view(())
 
     @staticmethod
     def backward(ctx, gout):
         shard, comm, drops, seeds, reg, rows, _frontier, tu, _blocks = ctx.cfg
+        wire(comm).phase = "backward"
         tables, sides, states, Tc, coef, ws = ctx.saved
         cu, cp, cn = ctx.ids
         gout = gout.reshape(1).to(torch.float32).contiguous()
@@ -744,6 +928,7 @@ class _ShardedCFLoss(torch.autograd.Function):
             gathered_spmm(shard, comm, shard.AT, dS, dXd, accumulate=True, transpose=True)
             dX = dXd
         ctx.saved = None
+        wire(comm).phase = "other"
         return (None, None, None, None, dX, *wgrads)
 
 
@@ -1004,11 +1189,28 @@ class RowShardedKGAT(nn.Module):
         self._cf_optimizer = FusedAdam(self.parameters(), lr=cf_lr)
         self._kg_optimizer = FusedAdam(self.parameters(), lr=kg_lr)
 
+    def _raise_on_bad_peer_ids(self) -> None:
+        """IndexError (the step abandoned: gradients and the deferred table update dropped, nothing
+        stepped) if the last hop backward received an out-of-range row id from a peer (_PeerIdGuard)."""
+        if self.shard.peer_ids().take():
+            tu = self._table_update
+            if tu.pending is not None:
+                shard, _, ids, total, _ = tu.pending
+                tu.pending = None
+                tu._release(shard, ids, total)
+            for p in self.parameters():
+                p.grad = None
+            raise IndexError("row-sharded CF backward: a peer's gathered hop row id is out of range "
+                             f"[0, {self.shard.n_nodes}); the step was abandoned (no parameter moved)")
+
     def materialize_table_grad(self) -> None:
         """Write a deferred table gradient (fuse_table_update) into the shard's .grad."""
+        if self._table_update.pending is not None:
+            self._raise_on_bad_peer_ids()
         self._table_update.materialize(self._user_entity_embedding_shard)
 
     def update_cf_weights(self) -> None:
+        self._raise_on_bad_peer_ids()
         tu, param = self._table_update, self._user_entity_embedding_shard
         fused = None
         if tu.pending is not None:

@@ -103,6 +103,68 @@ def test_sharded_world1_matches_kgat(pkg):
                                    ref(users, items, mode=pkg.KGATMode.PREDICT).cpu().numpy(), atol=1e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("fuse", [False, True])
+def test_bad_gathered_hop_id_raises_index_error(pkg, fuse):
+    """the hop backward's all-peer gather hands a rank row ids no local code produced (the
+    round-5 fault: uninitialised peer blocks used as rows).  With one gathered id out of range the step
+    does not fault: kgat_map_build_checked drops it, update_cf_weights raises IndexError with no parameter
+    or Adam moment moved and the deferred table update dropped, and the next good step equals a fresh
+    model's same step bit for bit.  (World 1 over gloo with the transport forced on: the rank's own block
+    of the gathered id list is corrupted in flight, as a peer's would be.)"""
+    graph = __import__(pkg.__name__ + ".graph", fromlist=["graph"])
+    sh = __import__(pkg.__name__ + ".sharded", fromlist=["sharded"])
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+
+    class CorruptIds(sh.Comm):
+        corrupted = 0
+
+        def gather_at(self, send, out, starts, sizes):
+            pend = super().gather_at(send, out, starts, sizes)
+            if out.dtype == torch.int32 and out.dim() == 1 and self.arm and int(sizes[0]) > 3:
+                out[3] = 1 << 30  # a peer's corrupt row id
+                CorruptIds.corrupted += 1
+            return pend
+
+    U, E, inter, trip = graph.synthetic_ckg(8000, 60000, seed=9)
+    lay = graph.build_layout(U, E, inter, trip)
+    args = pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32],
+                        message_dropout=[0.0, 0.0])
+    torch.manual_seed(3)
+    ref = pkg.KGAT(args)
+    models = []
+    for arm in (True, False):
+        comm = CorruptIds(force=True)
+        comm.arm = arm
+        m = sh.RowShardedKGAT(args, lay, comm, DEV)
+        m.load_full_state(ref.state_dict())
+        m.build_optimizer(1e-3, 1e-4)
+        m.fuse_table_update = fuse
+        models.append(m)
+    bad, good = models
+    rng = np.random.default_rng(1)
+    n_items = int(inter[:, 1].max()) + 1
+    b = [torch.from_numpy(x).to(DEV) for x in (rng.integers(0, U, 128), rng.integers(0, n_items, 128),
+                                                  rng.integers(0, n_items, 128))]
+    before = {k: v.detach().clone() for k, v in bad.state_dict().items() if not v.is_sparse}
+    bad(*b, mode=pkg.KGATMode.TRAIN_CF).backward()
+    assert CorruptIds.corrupted >= 1  # the hop layer's gathered id list went through the corrupting gather
+    with pytest.raises(IndexError):
+        bad.update_cf_weights()
+    after = {k: v.detach() for k, v in bad.state_dict().items() if not v.is_sparse}
+    assert all(torch.equal(before[k], after[k]) for k in before)
+    assert not bad._cf_optimizer.state and bad._table_update.pending is None
+    assert all(p.grad is None for p in bad.parameters())
+    # the next (good) step: the same bits as a model that never saw the bad one
+    bad.comm.arm = False
+    for m in models:
+        m(*b, mode=pkg.KGATMode.TRAIN_CF).backward()
+        m.update_cf_weights()
+    for (k, pa), (_, pb) in zip(bad.named_parameters(), good.named_parameters()):
+        if not pa.is_sparse:
+            assert torch.equal(pa, pb), k
+
+
 @pytest.mark.parametrize("world,dims,chunk", [(2, "64:64,32", 0), (2, "256:256,128,64", 0), (4, "256:256,128,64", 0),
                                               (3, "256:256,128,64", 64), (8, "256:256,128,64", 0),
                                               (8, "64:64,32", 0)])
