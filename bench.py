@@ -37,6 +37,7 @@ propagation, CF loss and table gradient on the full graph).
 from __future__ import annotations
 
 import argparse
+import gc
 import importlib
 import json
 import os
@@ -879,34 +880,36 @@ def gpu_parity_inputs(model, pkg, batch):
 
 
 class ShareComm:
-    """--rank-share K: rank 0 of a K-rank row-sharded run, alone on its GPU.  Every collective keeps only this
-    rank's part: a gathered layer buffer holds this rank's rows (the other ranks' rows are whatever the buffer
-    held), all-reduces are the identity, all-gathers hand back this rank's tensor for every rank -- except the
-    global batch ids, for which the bench supplies the other K - 1 ranks' batches (``peer_ids``).  The step
-    then runs rank 0's whole compute on the full-size shapes (its rows of A and A^T, the [N, d] gathered
-    inputs, the global batch's frontier) with no data moving: the per-rank compute of DESIGN §6.2's budget,
-    not the wire.  A timing harness only (sharded.Comm's interface)."""
+    """--rank-share K [--share-rank r]: rank r of a K-rank row-sharded run, alone on its GPU.  Every collective
+    keeps only this rank's part: a gathered layer buffer holds this rank's rows (the other ranks' rows are
+    whatever the buffer held), all-reduces are the identity, all-gathers hand back this rank's tensor for every
+    rank -- except the global batch ids, for which the bench supplies the other K - 1 ranks' batches
+    (``peer_ids``).  The step then runs rank r's whole compute on the full-size shapes (its rows of A and A^T,
+    the [N, d] gathered inputs, the global batch's frontier) with no data moving: the per-rank compute of
+    DESIGN §6.2's budget, not the wire (whose bytes comm.WireLog counts as the K-rank run would send them).
+    A timing harness only (sharded.Comm's interface)."""
 
     host = False
     force = False
     active = True
 
-    def __init__(self, world: int, bounds):
-        self.rank, self.world = 0, int(world)
+    def __init__(self, world: int, bounds, rank: int = 0):
+        self.rank, self.world = int(rank), int(world)
         self.bounds = [int(x) for x in bounds]
         self.peer_ids = None
 
     def gather_at(self, send, out, starts, sizes):
         sh = importlib.import_module(PKG + ".sharded")
-        lo, n_own = int(starts[0]), int(sizes[0])
-        _comm_mod().count_gather(self, out, n_own)  # what rank 0 would send to its share's 7 peers
+        r = self.rank
+        lo, n_own = int(starts[r]), int(sizes[r])
+        _comm_mod().count_gather(self, out, n_own)  # what this rank would send to its share's K - 1 peers
         own = out[lo:lo + n_own]
         if n_own and send.data_ptr() != own.data_ptr():
             own.copy_(send)
         if out.dtype == torch.int32 and out.dim() == 1:
             # a gathered id list (the hop layer's global hop rows): the peers' blocks must be ids their rows
             # hold -- evenly spaced distinct rows of each peer's range (ascending, as the real gather's)
-            for k in range(1, self.world):
+            for k in (k for k in range(self.world) if k != r):
                 s0, n = int(starts[k]), int(sizes[k])
                 if n:
                     b0, b1 = self.bounds[k], self.bounds[k + 1]
@@ -924,8 +927,10 @@ class ShareComm:
         return importlib.import_module(PKG + ".sharded")._Pending([])
 
     def all_to_all_v(self, send, send_off, recv, recv_off):
-        _comm_mod().wire(self).add(send.element_size() * (int(send_off[-1]) - int(send_off[1])))
-        recv[int(recv_off[0]):int(recv_off[1])].copy_(send[int(send_off[0]):int(send_off[1])])
+        r = self.rank
+        mine = int(send_off[r + 1]) - int(send_off[r])
+        _comm_mod().wire(self).add(send.element_size() * (int(send_off[-1]) - int(send_off[0]) - mine))
+        recv[int(recv_off[r]):int(recv_off[r + 1])].copy_(send[int(send_off[r]):int(send_off[r + 1])])
 
     def all_reduce_(self, t):
         _comm_mod().count_all_reduce(self, t)
@@ -936,12 +941,16 @@ class ShareComm:
         peers = self.peer_ids
         if peers is not None and t.dtype == torch.int64 and tuple(t.shape) == tuple(peers[0].shape):
             self.peer_ids = None
-            return torch.stack([t] + [p.to(t.device) for p in peers])
+            ps = [p.to(t.device) for p in peers]  # the other ranks' batches, rank order without this one
+            return torch.stack(ps[:self.rank] + [t] + ps[self.rank:])
         return t.unsqueeze(0).expand(self.world, *t.shape).contiguous()
 
 
 def _comm_mod():
     return importlib.import_module(PKG + ".comm")
+
+
+_CKG_CACHE: dict = {}
 
 
 def wire_per_step(counts: dict | None, steps: int, world: int, dev) -> dict | None:
@@ -977,17 +986,29 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     parts = share or world
     t0 = time.perf_counter()
     threads = max(1, min(16, (os.cpu_count() or 1) // max(world, 1)))
-    log(f"generating the synthetic CKG ({cfg['workload']}) row-sharded over {parts} ranks, {threads} threads each ...")
-    ckg = graph_mod.HashedCKG(cfg["nodes"], cfg["triples"], seed=2024, threads=threads)
-    log(f"  distinct triples drawn ({time.perf_counter() - t0:.1f}s)")
-    bounds = sh.shard_bounds(ckg.row_offsets(), parts)
+    key = (cfg["nodes"], cfg["triples"])
+    ckg = _CKG_CACHE.get(key)
+    if ckg is None:  # (several --share-rank shares of one graph: drawn once per process)
+        log(f"generating the synthetic CKG ({cfg['workload']}) row-sharded over {parts} ranks, {threads} threads "
+            f"each ...")
+        ckg = _CKG_CACHE[key] = graph_mod.HashedCKG(cfg["nodes"], cfg["triples"], seed=2024, threads=threads)
+        log(f"  distinct triples drawn ({time.perf_counter() - t0:.1f}s)")
+    rw = getattr(args, "row_weight", None)
+    bounds = sh.shard_bounds(ckg.row_offsets(), parts, **({} if rw is None else {"row_weight": rw}))
+    if share:
+        # the share's rank: a number, or the rank with the most rows / the most entries of A
+        sr = str(getattr(args, "share_rank_current", 0))
+        rows_per, nnz_per = np.diff(bounds), np.diff(ckg.row_offsets()[bounds])
+        rank = int(np.argmax(rows_per) if sr == "maxrows" else np.argmax(nnz_per) if sr == "maxedges" else int(sr))
+        if not 0 <= rank < share:
+            raise ValueError(f"--share-rank {sr}: not a rank of {share}")
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
     rowptr, col, val = ckg.shard(lo, hi)
     log(f"  rank {rank} rows [{lo}, {hi}): {col.size:,} entries ({time.perf_counter() - t0:.1f}s)")
     shard = sh.RowShard(rowptr, col, val, bounds, rank, dev, local=True, transpose=ckg.shard(lo, hi, transpose=True))
     whole = (rowptr, col, val) if parts == 1 and not args.no_parity else None  # the oracle's graph (parity leg)
     del rowptr, col, val
-    comm = ShareComm(share, bounds) if share else sh.Comm()
+    comm = ShareComm(share, bounds, rank) if share else sh.Comm()
     nnz_t = torch.tensor([shard.nnz], dtype=torch.int64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(nnz_t)
@@ -1012,7 +1033,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
                         for x in (u, it, rng.integers(0, ckg.item_num, B))])
         if share:  # the other ranks' batches of the same step (their own rng streams, as their processes)
             peers = []
-            for k in range(1, share):
+            for k in (k for k in range(share) if k != rank):
                 pr = np.random.default_rng(10_000 * (len(batches)) + 7 + k)
                 pu, pit = ckg.sample_interactions(pr, B)
                 peers.append(torch.from_numpy(np.stack([pu, pit, pr.integers(0, ckg.item_num, B)]).astype(np.int64)))
@@ -1090,12 +1111,12 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         res["parity"] = sharded_parity(model, pkg, batches[0], whole, ckg.n_nodes, cfg)
     if share:
         res["rank_share"] = {
-            "ranks": share, "rank": 0, "shard_rows": int(shard.n), "shard_nnz_A": int(shard.nnz),
+            "ranks": share, "rank": rank, "shard_rows": int(shard.n), "shard_nnz_A": int(shard.nnz),
             "shard_nnz_AT": int(shard.AT.col.numel()), "step_ms": ms,
             "frontier_step_ms": res.get("frontier_forward", {}).get("ms_per_step"),
             "hbm_peak_bytes": int(peak), "hbm_planned_bytes": float(sharded_bytes_per_gpu(cfg, share)),
             "design_budget_ms": 220.0,
-            "note": f"rank 0 of {share} alone on one GPU (ShareComm): its rows of A / A^T, the full [N, d] gathered "
+            "note": f"rank {rank} of {share} alone on one GPU (ShareComm): its rows of A / A^T, the full [N, d] gathered "
                     f"layer buffers and the global batch, every collective local -- the per-rank compute of one "
                     f"row-sharded step at full size, no wire; `value` = the whole graph's layer-edges over this "
                     f"rank's step (the wire-hidden bound), not a measurement of {share} GPUs"}
@@ -1192,7 +1213,12 @@ def main() -> int:
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and join the process group (gloo, no GPU), report, exit")
     ap.add_argument("--rank-share", type=int, default=0,
-                    help="c5, one process: time rank 0 of K row-sharded ranks alone (per-rank compute, no wire)")
+                    help="c5, one process: time rank r of K row-sharded ranks alone (per-rank compute, no wire)")
+    ap.add_argument("--share-rank", default="0",
+                    help="--rank-share's rank(s): comma-separated numbers, 'maxrows' or 'maxedges'; several run "
+                         "one after another on one drawn graph, the line reports the slowest (max over ranks)")
+    ap.add_argument("--row-weight", type=float, default=None,
+                    help="c5: shard_bounds' per-row weight in edges (default: sharded.SHARD_ROW_WEIGHT)")
     ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",
                     help="N>1 table-gradient exchange (c2/c4): replicated = all-gather of the compact layer-0 "
                          "hop-set terms, every rank computes the mean gradient and full Adam; sharded = row-block "
@@ -1261,7 +1287,21 @@ def main() -> int:
             raise RuntimeError(f"{dist.get_world_size()} ranks joined, --gpus {args.gpus}")
     dev = torch.device("cuda", local)
     run = run_sharded if cfg["mode"] == "sharded" else run_dp
-    res = run(args, cfg, world, rank, dev)
+    if cfg["mode"] == "sharded" and args.rank_share and "," in args.share_rank:
+        shares = []
+        for sr in args.share_rank.split(","):
+            args.share_rank_current = sr.strip()
+            shares.append(run(args, cfg, world, rank, dev))
+            gc.collect()
+            torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(dev)
+        res = max(shares, key=lambda x: x["ms_per_step"])  # the per-rank compute bound: the slowest rank
+        res["rank_share_all"] = [dict(x["rank_share"], wire_bytes_per_step=x.get("wire_bytes_per_step"),
+                                      roofline_frac=x["roofline"]["frac"],
+                                      fwd_spmm_ms_per_step=x["spmm"]["fwd_spmm_ms_per_step"]) for x in shares]
+    else:
+        args.share_rank_current = args.share_rank
+        res = run(args, cfg, world, rank, dev)
     result = {
         "metric": "CKG edges/sec (KGAT propagation step) + BPR pairs/sec at 1/2/4/8 MI355X",
         "value": res.pop("value"), "unit": "layer-edges/s", "n_gpus": res.pop("n_gpus"), "steps": args.steps,

@@ -18,6 +18,7 @@
 // (torch.sparse.softmax(dim=1), model.py:364): rows by length class (4-lane
 // groups, 16-lane groups, 512-entry segments of hub rows).
 #include <cmath>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -315,9 +316,9 @@ __device__ __forceinline__ void group4_softmax(float (&x)[S], int64_t beg, int64
 // row pointers, then all their entries, in flight together before the first reduction.
 constexpr int kSoftmaxRG = 2;
 
+template <int R = kSoftmaxRG>
 __device__ __forceinline__ void wave_rows_softmax(const int64_t* __restrict__ rowptr, int64_t n_rows, int64_t row0,
                                                   int lane, const float* __restrict__ logit, float* __restrict__ val) {
-  constexpr int R = kSoftmaxRG;
   const int j = lane & 3, g = lane >> 4, gl = lane & 15, g4 = lane >> 2;
   int64_t beg[R], end[R];
 #pragma unroll
@@ -394,14 +395,14 @@ __global__ __launch_bounds__(256) void row_softmax_kernel(const int64_t* __restr
 // exp(x - M) / S.  A hub row of 10^5 entries runs on ~200 waves instead of one block's three serial passes.
 constexpr int kSoftmaxSeg = 512;
 
+template <int RG>
 __global__ __launch_bounds__(256) void row_softmax_stats_kernel(kgat_csr A, const float* __restrict__ logit,
                                                                 float* __restrict__ val, float* __restrict__ stat,
                                                                 int seg_blocks) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // rows of <= 256 entries, 16 per wave
-    const int64_t row0 =
-        (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + (threadIdx.x & ~63)) / 4 * kSoftmaxRG;
-    if (row0 < A.n_rows) wave_rows_softmax(A.rowptr, A.n_rows, row0, lane, logit, val);
+  if (static_cast<int>(blockIdx.x) >= seg_blocks) {  // rows of <= 256 entries, 16 RG per wave
+    const int64_t row0 = (static_cast<int64_t>(blockIdx.x - seg_blocks) * blockDim.x + (threadIdx.x & ~63)) / 4 * RG;
+    if (row0 < A.n_rows) wave_rows_softmax<RG>(A.rowptr, A.n_rows, row0, lane, logit, val);
     return;
   }
   const int sg = blockIdx.x * 4 + wave;
@@ -538,10 +539,18 @@ extern "C" int kgat_row_softmax_plan_f32(const kgat_csr* A, const float* slot_lo
   if (!work || work_floats < kgat_row_softmax_work_floats(A)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int seg_blocks = (A->n_seg + 3) / 4;
-  const int64_t grid = seg_blocks + (A->n_rows * 4 / kgat::kSoftmaxRG + 255) / 256;
+  static const int rg = [] {  // A/B switch (profiles/r06_softmax_ab.md): 16 x RG short rows per wave
+    const char* e = getenv("KGAT_SOFTMAX_RG");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  const int64_t grid = seg_blocks + (A->n_rows * 4 / rg + 255) / 256;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::row_softmax_stats_kernel, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
-                     seg_blocks);
+  if (rg == 4)
+    hipLaunchKernelGGL(kgat::row_softmax_stats_kernel<4>, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
+                       seg_blocks);
+  else
+    hipLaunchKernelGGL(kgat::row_softmax_stats_kernel<2>, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
+                       seg_blocks);
   KGAT_LAUNCH_CHECK();
   if (A->n_seg > 0) {
     hipLaunchKernelGGL(kgat::row_softmax_seg_write_kernel, dim3(seg_blocks), dim3(256), 0, st, *A, slot_logits, work,

@@ -9,10 +9,16 @@ The reference builds TWO independent instances over the same parameters
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from . import kernels
+
+
+# The small tensors' Adam beside a fused launch: on a side stream (1, the default) or after it on the
+# current stream (0) -- an A/B switch (profiles/r06_small_adam_ab.md)
+SMALL_ADAM_SIDE = os.environ.get("KGAT_SMALL_ADAM_SIDE", "1") != "0"
 
 
 class FusedAdam:
@@ -77,7 +83,7 @@ class FusedAdam:
                 st, step_size, bc2s = self._advance(key, pv)
                 items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
         ready = None
-        if items and runs and items[0][0].is_cuda:
+        if items and runs and items[0][0].is_cuda and SMALL_ADAM_SIDE:
             ready = torch.cuda.Event()
             ready.record()  # every gradient of this step is in place (current stream)
         for launch, st, step_size, bc2s in runs:

@@ -211,10 +211,18 @@ class Comm:
 
 
 # ---------------------------------------------------------------- the plan
-def shard_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
-    """Contiguous row ranges balancing edges + rows (a row weighs its degree plus the mean degree)."""
+# shard_bounds' price of a row in edges (None: the graph's mean degree).  See shard_bounds.
+SHARD_ROW_WEIGHT: float | None = None
+
+
+def shard_bounds(rowptr: np.ndarray, world: int, row_weight: float | None = None) -> np.ndarray:
+    """Contiguous row ranges balancing edges + rows: a row weighs its degree plus ``row_weight`` edges
+    (default SHARD_ROW_WEIGHT; None = the mean degree) -- a rank's step time is its edges' gathers plus its
+    rows' dense work (bi-interaction GEMMs, the table update, the gathered buffers' placement)."""
     n = rowptr.size - 1
-    mean = rowptr[-1] / max(n, 1)
+    if row_weight is None:
+        row_weight = SHARD_ROW_WEIGHT
+    mean = rowptr[-1] / max(n, 1) if row_weight is None else float(row_weight)
     cum = rowptr.astype(np.float64) + mean * np.arange(n + 1)
     targets = cum[-1] * np.arange(1, world) / world
     cuts = np.searchsorted(cum, targets)
