@@ -1101,6 +1101,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         res["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
             "wire_bytes_per_step": wire_per_step(timed.wire_bytes, args.steps, world, dev),
+            "row_sets": dict(sh.ROW_SET_STATS),
             "bit_identical_to_full": sharded_frontier_matches_full(model, pkg, batches[0]) if not share else {
                 "pass": None, "what": "not checked in a rank share: the peers' rows of every gathered buffer are "
                                       "never computed, so the two forwards read different (uninitialised) rows"},

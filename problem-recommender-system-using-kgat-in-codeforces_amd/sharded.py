@@ -406,6 +406,7 @@ class RowShard:
 # many bytes without the ids and the placement pass.  KGAT_ROW_SET_GATHERS=0: whole-table gathers only.
 COMPACT_FRACTION = 0.6
 ROW_SET_GATHERS = os.environ.get("KGAT_ROW_SET_GATHERS", "1") != "0"
+ROW_SET_STATS: dict = {}  # the last frontier forward's global set sizes (bench.py reports them)
 
 
 class _RowSet:
@@ -724,6 +725,8 @@ def _frontier_sets(shard: RowShard, comm, rows, L: int, blocks: _RowBlocks | Non
                 if int(g2[:, 0].sum()) <= COMPACT_FRACTION * shard.n_nodes:
                     needs[L - 2] = _RowSet(shard, comm, hrows2, int(g2[k, 0]), g2[:, 0],
                                            g2[:, 1:] if piped else None)
+                ROW_SET_STATS.update(nodes=int(shard.n_nodes), hop1=int(hop1.total), hop2=int(g2[:, 0].sum()),
+                                     hop2_compact=needs[L - 2] is not None)
     return sets, needs
 
 
