@@ -527,6 +527,7 @@ def run_dp(args, cfg, world: int, rank: int, dev) -> dict:
         result["frontier_forward"] = {
             "ms_per_step": fms, "bpr_pairs_per_s": B * world / (fms * 1e-3), "speedup_vs_full": ms / fms,
             "first_hop_rows_last_step": int(est[0][0]) if est is not None and L >= 2 else None,
+            "host_launch_ms_per_step": timed.host_ms_per_step,
             "bit_identical_to_full": same,
             "note": "TRAIN_CF forward restricted to the rows the BPR loss reaches (layer L-2 on the first hop "
                     "F + N(F), the last layer on the batch rows F, layer 0 of 3 whole); not counted in value (it "
@@ -1095,6 +1096,7 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         # on the first hop F + N(F) (this rank's part, marked from its A^T rows), the lower layers whole --
         # the rows the loss reads, with the whole-shard forward's bits (checked below); not in `value`
         model.frontier_forward = True
+        sh.ROW_SET_STATS.clear()
         fel, fev, _ = timed(step, batches, args.warmup, args.steps, world, dev, wire_log=wlog)
         model.frontier_forward = False
         fms = fel / args.steps * 1e3
@@ -1298,6 +1300,9 @@ def main() -> int:
             torch.cuda.reset_peak_memory_stats(dev)
         res = max(shares, key=lambda x: x["ms_per_step"])  # the per-rank compute bound: the slowest rank
         res["rank_share_all"] = [dict(x["rank_share"], wire_bytes_per_step=x.get("wire_bytes_per_step"),
+                                      frontier_wire_bytes_per_step=x.get("frontier_forward", {}).get(
+                                          "wire_bytes_per_step"),
+                                      row_sets=x.get("frontier_forward", {}).get("row_sets"),
                                       roofline_frac=x["roofline"]["frac"],
                                       fwd_spmm_ms_per_step=x["spmm"]["fwd_spmm_ms_per_step"]) for x in shares]
     else:

@@ -593,7 +593,10 @@ class HashedCKG:
     def close(self) -> None:
         h, self._h = getattr(self, "_h", None), None
         if h is not None and h.value and _lib is not None:
-            _lib.lib().kgat_synth_close(h)
+            try:
+                _lib.lib().kgat_synth_close(h)
+            except (TypeError, AttributeError):  # interpreter shutdown: the module's globals are gone
+                pass
 
     __del__ = close
 

@@ -211,8 +211,10 @@ class Comm:
 
 
 # ---------------------------------------------------------------- the plan
-# shard_bounds' price of a row in edges (None: the graph's mean degree).  See shard_bounds.
-SHARD_ROW_WEIGHT: float | None = None
+# shard_bounds' price of a row in edges (None: the graph's mean degree).  Fitted in round 6 to the full-size C5
+# rank shares (profiles/r06_c5_rank_share_0_5.log: a rank's step ~ a E + b R; rank 0, 200M edges / 2.5M rows,
+# 68.1 ms; rank 5, 27.5M edges / 11.1M rows, 120.0 ms -> b / a = 48 edges per row, the frontier leg alike).
+SHARD_ROW_WEIGHT: float | None = 48.0
 
 
 def shard_bounds(rowptr: np.ndarray, world: int, row_weight: float | None = None) -> np.ndarray:
@@ -597,8 +599,10 @@ def _layer_pipelined(shard: RowShard, comm, blocks: _RowBlocks, Xg: torch.Tensor
     ``need_next`` (a _RowSet with per-block counts): only the block's rows the next layer reads are posted
     (compact; placed into the gathered buffer once every post has landed)."""
     dout = W1.shape[0]
-    h = torch.empty(shard.n, dout, dtype=torch.float32, device=x.device)
     nxt = torch.empty(shard.n_nodes, dout, dtype=torch.float32, device=x.device)
+    # the layer's output rows live in their own slot of the next layer's gathered buffer: no pack copy before
+    # the posts (a row-heavy C5 rank copied ~11 GB per step), no separate [rows, d] allocation
+    h = nxt[shard.lo:shard.hi]
     Pc = need_next.buffer(dout, x.device) if need_next is not None else None
     pends = []
     for b in range(blocks.K):
