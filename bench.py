@@ -995,7 +995,10 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
         ckg = _CKG_CACHE[key] = graph_mod.HashedCKG(cfg["nodes"], cfg["triples"], seed=2024, threads=threads)
         log(f"  distinct triples drawn ({time.perf_counter() - t0:.1f}s)")
     rw = getattr(args, "row_weight", None)
-    bounds = sh.shard_bounds(ckg.row_offsets(), parts, **({} if rw is None else {"row_weight": rw}))
+    # the cost model's item-row factor (sharded.HUB_EDGE_SCALE; --hub-edge-scale 1 = edges and rows only)
+    hub = sh.HUB_EDGE_SCALE if args.hub_edge_scale is None else args.hub_edge_scale
+    bounds = sh.shard_bounds(ckg.row_offsets(), parts, **({} if rw is None else {"row_weight": rw}),
+                             edge_scale=[(ckg.user_num, ckg.user_num + ckg.item_num, hub)])
     if share:
         # the share's rank: a number, or the rank with the most rows / the most entries of A
         sr = str(getattr(args, "share_rank_current", 0))
@@ -1222,6 +1225,8 @@ def main() -> int:
                          "one after another on one drawn graph, the line reports the slowest (max over ranks)")
     ap.add_argument("--row-weight", type=float, default=None,
                     help="c5: shard_bounds' per-row weight in edges (default: sharded.SHARD_ROW_WEIGHT)")
+    ap.add_argument("--hub-edge-scale", type=float, default=None,
+                    help="c5: shard_bounds' weight of an item row's entry (default: sharded.HUB_EDGE_SCALE)")
     ap.add_argument("--dp", choices=("auto", "replicated", "sharded"), default="auto",
                     help="N>1 table-gradient exchange (c2/c4): replicated = all-gather of the compact layer-0 "
                          "hop-set terms, every rank computes the mean gradient and full Adam; sharded = row-block "

@@ -211,21 +211,34 @@ class Comm:
 
 
 # ---------------------------------------------------------------- the plan
-# shard_bounds' price of a row in edges (None: the graph's mean degree).  Fitted in round 6 to the full-size C5
-# rank shares (profiles/r06_c5_rank_share_0_5.log: a rank's step ~ a E + b R; rank 0, 200M edges / 2.5M rows,
-# 68.1 ms; rank 5, 27.5M edges / 11.1M rows, 120.0 ms -> b / a = 48 edges per row, the frontier leg alike).
+# shard_bounds' cost model of a rank's CF step, fitted in round 6 to four full-size C5 rank shares (bench.py
+# --rank-share 8 --share-rank ...; profiles/r06_c5_rank_share_0_5.log, r06_c5_rank_share_w48.log):
+#   t ~ c_r R + c_e E + c_i E_item,  c_r = 10.3 ms per M rows (the bi-interaction GEMMs + epilogues, the table
+#   update, the gathered-buffer copies), c_e = 0.21 ms per M entries (user / entity rows: their gathers hit the
+#   Zipf-popular item rows in the caches), c_i = 0.47 ms per M entries of item rows (hub rows whose entries
+#   gather uniformly random 1 KB user rows: HBM-bound).  Measured: rank 0 of the mean-degree bounds (users,
+#   200M entries / 2.5M rows) 68.1 ms, rank 5 (entities, 27.5M / 11.1M) 120.0 ms; with the row weight alone,
+#   rank 4 (entities, 20.8M / 8.4M) 87.6 ms, rank 2 (items, 292M / 2.8M) 166.6 ms.
+# SHARD_ROW_WEIGHT = c_r / c_e in entries (None: the graph's mean degree); HUB_EDGE_SCALE = c_i / c_e.
 SHARD_ROW_WEIGHT: float | None = 48.0
+HUB_EDGE_SCALE = 2.2
 
 
-def shard_bounds(rowptr: np.ndarray, world: int, row_weight: float | None = None) -> np.ndarray:
-    """Contiguous row ranges balancing edges + rows: a row weighs its degree plus ``row_weight`` edges
-    (default SHARD_ROW_WEIGHT; None = the mean degree) -- a rank's step time is its edges' gathers plus its
-    rows' dense work (bi-interaction GEMMs, the table update, the gathered buffers' placement)."""
+def shard_bounds(rowptr: np.ndarray, world: int, row_weight: float | None = None,
+                 edge_scale: list | None = None) -> np.ndarray:
+    """Contiguous row ranges balancing the cost model above: a row weighs its entries plus ``row_weight``
+    entries (default SHARD_ROW_WEIGHT; None = the mean degree); ``edge_scale`` = [(lo, hi, factor)]: the
+    entries of rows [lo, hi) weigh ``factor`` each (the C5 bench passes the item rows with HUB_EDGE_SCALE)."""
     n = rowptr.size - 1
     if row_weight is None:
         row_weight = SHARD_ROW_WEIGHT
     mean = rowptr[-1] / max(n, 1) if row_weight is None else float(row_weight)
     cum = rowptr.astype(np.float64) + mean * np.arange(n + 1)
+    for lo, hi, factor in edge_scale or ():
+        lo, hi = max(0, int(lo)), min(n, int(hi))
+        if hi > lo:
+            idx = np.clip(np.arange(n + 1), lo, hi)
+            cum += (float(factor) - 1.0) * (rowptr[idx] - rowptr[lo]).astype(np.float64)
     targets = cum[-1] * np.arange(1, world) / world
     cuts = np.searchsorted(cum, targets)
     b = np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64)

@@ -11,3 +11,6 @@ for i in 1 2; do for rg in 2 4; do
   echo "RG=$rg $(grep row_softmax gpurun_out/sm_ab_${rg}_$i.log)"
 done; done
 bash tools/ab_env.sh KGAT_SMALL_ADAM_SIDE 1 0 ${PAIRS:-2}
+# (3) host cost of the CF step's launches (small graph: host-bound), frontier and full forward
+timeout -k 10 200 python -u tools/host_profile.py > gpurun_out/host_cf_frontier.txt 2>&1 && head -3 gpurun_out/host_cf_frontier.txt
+timeout -k 10 200 python -u tools/host_profile.py --full > gpurun_out/host_cf_full.txt 2>&1 && head -3 gpurun_out/host_cf_full.txt
