@@ -38,6 +38,24 @@ def test_shard_bounds_cover_and_balance(world):
     assert max(load) <= 1.25 * (sum(load) / world) + 2000  # hubs make exact balance impossible
 
 
+def test_shard_bounds_cost_model():
+    """The round-6 cost model: rows weigh SHARD_ROW_WEIGHT entries, entries of the ``edge_scale`` ranges their
+    factor -- every rank's modelled cost within one heavy row of the mean, an empty scale list = none."""
+    rowptr, _, _ = _random_csr(20000, 200000, 5)
+    for world in (2, 8):
+        plain = sharded.shard_bounds(rowptr, world)
+        assert np.array_equal(plain, sharded.shard_bounds(rowptr, world, edge_scale=[]))
+        lo, hi, f = 3000, 9000, 2.2
+        b = sharded.shard_bounds(rowptr, world, edge_scale=[(lo, hi, f)])
+        assert b[0] == 0 and b[-1] == 20000 and np.all(np.diff(b) > 0)
+        w = sharded.SHARD_ROW_WEIGHT
+        deg = np.diff(rowptr).astype(np.float64)
+        cost_row = deg * np.where((np.arange(20000) >= lo) & (np.arange(20000) < hi), f, 1.0) + w
+        cost = [cost_row[b[k]:b[k + 1]].sum() for k in range(world)]
+        assert max(cost) - min(cost) <= 2 * cost_row.max() + 1e-6
+        assert not np.array_equal(b, plain)  # the item-like range moved the cuts
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_row_shard_reassembles_A_and_AT(world):
     """Every rank's A rows (global columns) and A^T rows reassemble A and A^T, columns ascending."""
@@ -97,7 +115,11 @@ def _comm_worker(rank: int, world: int, port: int, q) -> None:
         a2a_ok = torch.equal(recv, torch.cat([torch.full((c,), float(10 * p + rank)) for p, c in enumerate(recv_cnt)]))
         red = comm.all_reduce_(torch.full((4,), float(rank + 1)))
         gat = comm.all_gather(torch.tensor([rank, 10 * rank]))
-        q.put((rank, ring_ok, gather_ok, a2a_ok, red.tolist(), gat.tolist()))
+        # comm.WireLog: the bytes this rank sent, by the counting rule of each collective
+        want_wire = ((3 + rank) * 2 * 4 + sizes[rank] * 3 * 4 * (world - 1)
+                     + 4 * (int(send_off[-1]) - send_cnt[rank]) + 2 * (world - 1) * 16 // world + (world - 1) * 2 * 8)
+        wire_ok = sharded.wire(comm).bytes == {"other": want_wire}
+        q.put((rank, ring_ok, gather_ok, a2a_ok and wire_ok, red.tolist(), gat.tolist()))
     finally:
         dist.destroy_process_group()
 
