@@ -695,55 +695,71 @@ def _host_bits(ids: np.ndarray, n: int, device) -> torch.Tensor:
 
 
 def _frontier_sets(shard: RowShard, comm, rows, L: int, blocks: _RowBlocks | None = None):
-    """The row sets the CF loss reaches, per layer (this rank's part): the last layer's output is read
-    on the batch rows F only (model.py:189-191), layer L-2's on the first hop F + N(F) (the last layer
-    gathers its A rows there).  Returns [set for layer l] with None = the whole shard, else
-    (rows int32 -- the first count valid --, count int32 [1] on the device, int32 bitmap, count):
-    F from the host's batch ids; the first hop marked on the device from this rank's rows of A^T
-    (row j is in it iff j is in F or A^T[j, f] != 0 for some f in F: kgat_csr_mark_rows), kept when
-    the global set holds at most model.HOP_DENSE_FRACTION of the nodes (the counts are all-gathered,
-    one host sync) -- the backward then runs layer L-2 on the same set.
+    """The row sets the CF loss reaches, per layer (this rank's part).  The last layer's output is read on
+    the batch rows F only (model.py:189-191), so the last layer runs on F; it reads its input on N_A(F),
+    inside the first hop h1 = F + N_A(F), so layer L-2 need only run on h1; that one reads its input on
+    h2 = h1 + N_A(h1), and so on down the layers.  h_j is marked on the device by each owner from its rows
+    of A^T and the global bitmap of h_(j-1) (row j is in it iff j is in h_(j-1) or A^T[j, h] != 0 for an h
+    of it: kgat_csr_mark_rows); the counts are all-gathered (one host sync per hop) and layer L-1-j runs
+    on h_j while the global h_j holds at most model.HOP_DENSE_FRACTION of the nodes -- the backward then
+    runs that layer on the same set (its hop chain flags the same rows).  The chain stops at the first
+    layer that runs whole (its input is then read on every row).  Returns (sets, needs):
 
-    Also returns ``needs``: per layer, None (its input is gathered whole) or the _RowSet of input rows its
-    product reads.  Layer L-1 reads its input on N(F), inside the first hop -- every rank's
-    first-hop rows travel (the layer L-2 output rows that exist).  Layer L-2 reads its input on the second
-    hop N(hop1): each owner marks its rows j with A^T[j, h] != 0 for an h of the global first hop (whose
-    ids the first row set just gathered), and they travel when the global set holds at most
-    COMPACT_FRACTION of the nodes -- posted block by block when a pipelined layer produces them."""
+    ``sets[l]``: None (layer l runs on the whole shard) or (rows int32 -- the first count valid --, count
+    int32 [1] on the device, int32 bitmap, count).
+
+    ``needs[l]``: None (layer l's input is gathered whole) or the _RowSet of input rows its product reads
+    (VERDICT r5 #3): h_(L-l) -- every rank's rows of it travel, compact, when the global set holds at most
+    COMPACT_FRACTION of the nodes (posted block by block when a pipelined whole layer produces them).  At
+    full C5 (G = 8: 5.5k batch rows) h1 holds 0.25 % of the nodes and h2 14 % (every user is in it), so layer
+    0 runs on h2 too and X0 travels on h3 (tools/c5_hop_fractions.py, profiles/r06_c5_hop_fractions.json)."""
     dev = shard.device
+    N = shard.n_nodes
     sets = [None] * L
     needs = [None] * L
     m = rows.n_frontier
     sets[L - 1] = (rows.frontier, torch.tensor([m], dtype=torch.int32).to(dev, non_blocking=True),
                    _host_bits(rows.frontier_np, shard.n, dev), m)
-    if L >= 2 and _model.HOP_DENSE_FRACTION > 0:
-        hit, hmap, hrows, count, work = shard.hop_buffers()
-        fb = _host_bits(rows.uniq_np, shard.n_nodes, dev)
-        kernels.csr_mark_rows(shard.AT, fb, shard.n_nodes, shard.lo, hit)
+    ROW_SET_STATS.update(nodes=int(N), hops=[], restricted=[L - 1], compact=[])
+    if L < 2 or _model.HOP_DENSE_FRACTION <= 0:
+        return sets, needs
+    k = comm.rank if comm.active else 0
+    prev_bits = _host_bits(rows.uniq_np, N, dev)  # the global bitmap of h0 = F (host data)
+    for j in range(1, L + 1):
+        l = L - 1 - j  # the layer that may run on h_j (-1: none -- h_L only sizes the gather of X0)
+        hit, hmap, hrows, count, work = shard.hop_buffers(j - 1)
+        kernels.csr_mark_rows(shard.AT, prev_bits, N, shard.lo, hit)
         kernels.hop_list(hit[:shard.n], hmap, hrows, count, work)
-        counts = comm.all_gather(count).reshape(-1).cpu().numpy().astype(np.int64)
-        if int(counts.sum()) <= _model.HOP_DENSE_FRACTION * shard.n_nodes:
+        # a whole layer l posts its output block by block when pipelined: every rank's per-block counts too
+        piped = l >= 0 and blocks is not None and comm.active
+        parts = [count.long()]
+        if piped:
+            parts += [hit[a:b].sum().reshape(1) for a, b in zip(blocks.mine[:-1], blocks.mine[1:])]
+        g = comm.all_gather(torch.cat(parts)).reshape(-1, len(parts)).cpu().numpy().astype(np.int64)
+        counts, total = g[:, 0], int(g[:, 0].sum())
+        ROW_SET_STATS["hops"].append(total)
+        restrict = l >= 0 and total <= _model.HOP_DENSE_FRACTION * N
+        if restrict:
             bits = torch.empty(2 * ((shard.n + 63) // 64) + 2, dtype=torch.int32, device=dev)
             kernels.map_bits(hmap[:shard.n], bits)
-            k = comm.rank if comm.active else 0
-            sets[L - 2] = (hrows, count.clone(), bits, int(counts[k]))
-            if comm.active and ROW_SET_GATHERS:
-                hop1 = needs[L - 1] = _RowSet(shard, comm, hrows, int(counts[k]), counts)
-                gb = _ids_bitmap(shard, hop1.ids, hop1.total)
-                hit2, hmap2, hrows2, count2, work2 = shard.hop_buffers(1)
-                kernels.csr_mark_rows(shard.AT, gb, shard.n_nodes, shard.lo, hit2)
-                kernels.hop_list(hit2[:shard.n], hmap2, hrows2, count2, work2)
-                # a pipelined layer L-3 posts its output block by block: every rank's per-block counts too
-                piped = blocks is not None and L >= 3
-                parts = [count2.long()]
-                if piped:
-                    parts += [hit2[a:b].sum().reshape(1) for a, b in zip(blocks.mine[:-1], blocks.mine[1:])]
-                g2 = comm.all_gather(torch.cat(parts)).reshape(-1, len(parts)).cpu().numpy().astype(np.int64)
-                if int(g2[:, 0].sum()) <= COMPACT_FRACTION * shard.n_nodes:
-                    needs[L - 2] = _RowSet(shard, comm, hrows2, int(g2[k, 0]), g2[:, 0],
-                                           g2[:, 1:] if piped else None)
-                ROW_SET_STATS.update(nodes=int(shard.n_nodes), hop1=int(hop1.total), hop2=int(g2[:, 0].sum()),
-                                     hop2_compact=needs[L - 2] is not None)
+            sets[l] = (hrows, count.clone(), bits, int(counts[k]))
+            ROW_SET_STATS["restricted"].append(l)
+        rs = None
+        if comm.active and ROW_SET_GATHERS and total <= COMPACT_FRACTION * N:
+            rs = needs[L - j] = _RowSet(shard, comm, hrows, int(counts[k]), counts,
+                                        g[:, 1:] if piped and not restrict else None)
+            ROW_SET_STATS["compact"].append(L - j)
+        if not restrict or j == L:
+            break
+        # the global bitmap of h_j, the next hop's seed: from every rank's ids (gathered by the row set), or,
+        # on one rank, from the local list itself
+        if rs is not None:
+            prev_bits = _ids_bitmap(shard, rs.ids, rs.total)
+        elif not comm.active:
+            prev_bits = _ids_bitmap(shard, kernels.map_compose(hrows[:max(int(counts[k]), 1)], None, shard.lo),
+                                    int(counts[k]))
+        else:  # (unreachable: a set small enough to run a layer on is small enough to travel compact)
+            break
     return sets, needs
 
 

@@ -147,6 +147,28 @@ def main() -> None:
     fr_grads = [p.grad.detach().clone() for p in m.parameters() if not p.is_sparse and p.grad is not None]
     exact["frontier_vs_full"] = len(fr_grads) == len(full_grads) and all(
         torch.equal(a, b) for a, b in zip(fr_grads, full_grads))
+    # the same with every layer's hop set taken (HOP_DENSE_FRACTION raised) and every layer input gathered as a
+    # row set (COMPACT_FRACTION 1): the whole frontier chain down to X0's gather on h_L -- full and frontier
+    # steps both under the raised fractions (the backward then runs every layer on its hop set either way)
+    model_mod = __import__(pkg.__name__ + ".model", fromlist=["model"])
+    saved_fr = (model_mod.HOP_DENSE_FRACTION, sh.COMPACT_FRACTION)
+    model_mod.HOP_DENSE_FRACTION, sh.COMPACT_FRACTION = 0.95, 1.0
+    try:
+        outs = []
+        for frontier in (False, True):
+            m.zero_grad(set_to_none=True)
+            m.frontier_forward = frontier
+            m(*mine, mode=pkg.KGATMode.TRAIN_CF).backward()
+            outs.append([p.grad.detach().clone() for p in m.parameters() if not p.is_sparse and p.grad is not None])
+        m.frontier_forward = False
+        chain = dict(sh.ROW_SET_STATS)
+    finally:
+        model_mod.HOP_DENSE_FRACTION, sh.COMPACT_FRACTION = saved_fr
+    exact["frontier_vs_full_all_hops"] = len(outs[0]) == len(outs[1]) and all(
+        torch.equal(a, b) for a, b in zip(*outs))
+    close("cf d table shard (all hops, frontier)", outs[1][0], ref._user_entity_embedding.weight.grad[lo:hi], ATOL_GRAD)
+    if world > 1 and rank == 0:
+        print(f"sharded_worker world {world}: frontier chain {chain}", flush=True)
     # the table's Adam step fused into its last product (fuse_table_update) vs the unfused step
     snap = {k: v.detach().clone() for k, v in m.state_dict().items()}
     s0, res = m._step, []
