@@ -1019,6 +1019,8 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
     nnz = int(nnz_t.item()) if not share else 2 * ckg.n_triples  # rank share: the whole graph's E (~2T)
     log(f"  device shards built ({time.perf_counter() - t0:.1f}s); total nnz {nnz:,}")
     log(f"graph: N={ckg.n_nodes} interactions={ckg.n_interactions} kg={ckg.n_kg} nnz={nnz}")
+    if share:  # the key tools/pmc_parse.py files a rank share's counters under
+        log(f"share graph: N={shard.n} nnz={shard.nnz} (rank {rank} of {share})")
     L = len(cfg["layers"])
     torch.manual_seed(2024)
     model = sh.RowShardedKGAT(pkg.KGATArgs(user_num=ckg.user_num, entity_num=ckg.entity_num, relation_num=10,
@@ -1072,8 +1074,9 @@ def run_sharded(args, cfg, world: int, rank: int, dev) -> dict:
             (out / f"c5_timeline_rank{rank}.txt").write_text("\n".join(lines) + "\n")
     d0 = cfg["dim"]
     chunked = comm.active and d0 > sh.GATHER_CHUNK > 0
-    roof, spmm = roofline(events, args.config, ckg.n_nodes if parts == 1 else shard.n, nnz if parts == 1 else 0,
-                          d0, timed.instrumented,
+    # a rank share's counters are its own (profiles/pmc_c5_share.json, keyed by the share's rows / entries of A)
+    roof, spmm = roofline(events, "c5_share" if share else args.config, ckg.n_nodes if parts == 1 else shard.n,
+                          nnz if parts == 1 else (shard.nnz if share else 0), d0, timed.instrumented,
                           f"spmm_main_kernel<{sh.GATHER_CHUNK if chunked else d0}, 0> on the local rows of A "
                           f"(all-peer gathered layer input{', column chunks' if chunked else ''})")
     spmm["fwd_spmm_layer_edges_per_s_rank0"] = shard.nnz * L / (spmm["fwd_spmm_ms_per_step"] * 1e-3)

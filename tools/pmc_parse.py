@@ -56,7 +56,9 @@ def main():
         out["table_update_hbm_bytes_per_launch"] = tu_k["hbm_bytes"] + (tu_fix["hbm_bytes"] if tu_fix else 0.0)
     if len(sys.argv) > 5:  # the bench log of the profiled run: the graph size the counters belong to
         import re
-        m = re.search(r"graph: N=(\d+) .*nnz=(\d+)", Path(sys.argv[5]).read_text())
+        text = Path(sys.argv[5]).read_text()
+        # a rank share (bench.py --rank-share) files its counters under its own rows / entries of A
+        m = re.search(r"share graph: N=(\d+) nnz=(\d+)", text) or re.search(r"graph: N=(\d+) .*nnz=(\d+)", text)
         if m:
             out["nodes"], out["nnz"] = int(m.group(1)), int(m.group(2))
     dst.write_text(json.dumps(out, indent=1))
