@@ -45,17 +45,32 @@ def main():
 
     hop1 = expand(F)
     hop2 = expand(hop1)
+    hop3 = expand(hop2)
+    print(f"hops {hop1.size} {hop2.size} {hop3.size} ({time.perf_counter() - t0:.0f}s)", file=sys.stderr, flush=True)
     out = {"nodes": N, "nnz": int(col.size), "G": G, "batch_rows": int(F.size), "hop1": int(hop1.size),
-           "hop2": int(hop2.size), "hop1_frac": hop1.size / N, "hop2_frac": hop2.size / N}
-    for w in (None, 48.0):
-        b = sh.shard_bounds(rowptr, G, row_weight=w if w is not None else float(rowptr[-1] / N))
+           "hop2": int(hop2.size), "hop3": int(hop3.size), "hop1_frac": hop1.size / N, "hop2_frac": hop2.size / N,
+           "hop3_frac": hop3.size / N}
+    dims = [256, 256, 128]  # the inputs of layers 0, 1, 2 at C5
+    hops = [hop3, hop2, hop1]  # the rows layer 0 / 1 / 2 reads its input on (sharded._frontier_sets)
+    items = [(ckg.user_num, ckg.user_num + ckg.item_num, sh.HUB_EDGE_SCALE)]
+    for name, kw in (("mean_degree", dict(row_weight=float(rowptr[-1] / N))), ("row_weight_48", {}),
+                     ("cost_model", dict(edge_scale=items))):
+        b = sh.shard_bounds(rowptr, G, **kw)
         ranks = []
         for r in range(G):
             lo, hi = int(b[r]), int(b[r + 1])
-            ranks.append({"rows": hi - lo, "edges": int(rowptr[hi] - rowptr[lo]),
-                          "hop1": int(((hop1 >= lo) & (hop1 < hi)).sum()),
-                          "hop2": int(((hop2 >= lo) & (hop2 < hi)).sum())})
-        out[f"ranks_row_weight_{'mean' if w is None else int(w)}"] = ranks
+            own = [int(((h >= lo) & (h < hi)).sum()) for h in hops]
+            rec = {"rows": hi - lo, "edges": int(rowptr[hi] - rowptr[lo]), "hop1": own[2], "hop2": own[1],
+                   "hop3": own[0]}
+            # the frontier forward's sends (G - 1 peers): each layer input on its hop's rows while the global hop
+            # holds <= COMPACT_FRACTION of the nodes, else the whole shard
+            fwd = 0
+            for h, o, d in zip(hops, own, dims):
+                fwd += (o if h.size <= sh.COMPACT_FRACTION * N else hi - lo) * 4 * d * (G - 1)
+            rec["frontier_forward_wire_bytes"] = fwd
+            rec["whole_forward_wire_bytes"] = (hi - lo) * 4 * sum(dims) * (G - 1)
+            ranks.append(rec)
+        out[f"ranks_{name}"] = ranks
     print(json.dumps(out, indent=1))
 
 
