@@ -9,16 +9,10 @@ The reference builds TWO independent instances over the same parameters
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from . import kernels
-
-
-# The small tensors' Adam beside a fused launch: on a side stream (1, the default) or after it on the
-# current stream (0) -- an A/B switch (profiles/r06_small_adam_ab.md)
-SMALL_ADAM_SIDE = os.environ.get("KGAT_SMALL_ADAM_SIDE", "1") != "0"
 
 
 class FusedAdam:
@@ -28,7 +22,6 @@ class FusedAdam:
         self.beta1, self.beta2 = float(betas[0]), float(betas[1])
         self.eps = float(eps)
         self.state: dict[int, dict] = {}
-        self._side: dict = {}  # device -> side stream of step()
 
     def _advance(self, key, like: torch.Tensor) -> tuple[dict, float, float]:
         """Count one more step for state ``key`` (created zeroed like ``like``): (state, step_size, bc2_sqrt)."""
@@ -82,25 +75,12 @@ class FusedAdam:
             for key, pv, gv in views:
                 st, step_size, bc2s = self._advance(key, pv)
                 items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
-        ready = None
-        if items and runs and items[0][0].is_cuda and SMALL_ADAM_SIDE:
-            ready = torch.cuda.Event()
-            ready.record()  # every gradient of this step is in place (current stream)
         for launch, st, step_size, bc2s in runs:
             launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
-        if ready is not None:
-            # the small tensors' Adam (one short launch) runs on a side stream beside the fused launch(es),
-            # which hold every CU for hundreds of microseconds (issued first, so the host work of the fork
-            # overlaps them); the current stream waits for it at the end
-            dev = items[0][0].device
-            side = self._side.get(dev)
-            if side is None:
-                side = self._side[dev] = torch.cuda.Stream(device=dev)
-            side.wait_event(ready)
-            with torch.cuda.stream(side):
-                kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
-            torch.cuda.current_stream(dev).wait_stream(side)
-        elif items:
+        if items:
+            # after the fused launch(es), on the same stream: run beside them on a side stream (round 5) the
+            # small tensors' Adam waited ~120 us for CU slots and its join cost the C2 step 15-17 us
+            # (profiles/r06_small_adam_ab.md: full 1.858 -> 1.838 ms, frontier 0.837 -> 0.820 ms)
             kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
