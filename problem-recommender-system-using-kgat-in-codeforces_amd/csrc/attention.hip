@@ -18,7 +18,6 @@
 // (torch.sparse.softmax(dim=1), model.py:364): rows by length class (4-lane
 // groups, 16-lane groups, 512-entry segments of hub rows).
 #include <cmath>
-#include <cstdlib>
 
 #include "common.hpp"
 
@@ -539,18 +538,12 @@ extern "C" int kgat_row_softmax_plan_f32(const kgat_csr* A, const float* slot_lo
   if (!work || work_floats < kgat_row_softmax_work_floats(A)) return KGAT_ERR_WORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int seg_blocks = (A->n_seg + 3) / 4;
-  static const int rg = [] {  // A/B switch (profiles/r06_softmax_ab.md): 16 x RG short rows per wave
-    const char* e = getenv("KGAT_SOFTMAX_RG");
-    return e && atoi(e) == 4 ? 4 : 2;
-  }();
-  const int64_t grid = seg_blocks + (A->n_rows * 4 / rg + 255) / 256;
+  // 16 x kSoftmaxRG short rows per wave (RG = 4, all 64 rows' loads in flight: 48.9 vs 43.8 us at C2,
+  // profiles/r06_softmax_ab.md)
+  const int64_t grid = seg_blocks + (A->n_rows * 4 / kgat::kSoftmaxRG + 255) / 256;
   if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
-  if (rg == 4)
-    hipLaunchKernelGGL(kgat::row_softmax_stats_kernel<4>, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
-                       seg_blocks);
-  else
-    hipLaunchKernelGGL(kgat::row_softmax_stats_kernel<2>, dim3(grid), dim3(256), 0, st, *A, slot_logits, val, work,
-                       seg_blocks);
+  hipLaunchKernelGGL(kgat::row_softmax_stats_kernel<kgat::kSoftmaxRG>, dim3(grid), dim3(256), 0, st, *A, slot_logits,
+                     val, work, seg_blocks);
   KGAT_LAUNCH_CHECK();
   if (A->n_seg > 0) {
     hipLaunchKernelGGL(kgat::row_softmax_seg_write_kernel, dim3(seg_blocks), dim3(256), 0, st, *A, slot_logits, work,
