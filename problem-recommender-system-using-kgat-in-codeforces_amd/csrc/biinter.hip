@@ -862,17 +862,21 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     }
   }
 
-  // one slab per wave: [dW1 | dW2 | db1 | db2]
+  // one slab per block: [dW1 | dW2 | db1 | db2] = ((wave 0 + wave 1) + wave 2) + wave 3, the four waves'
+  // partials added through LDS (the staging images are free once every wave has left the loop) -- a quarter of
+  // the slab bytes written here and read by slab_reduce_kernel (C2's layer-0 hop backward: 34 -> 8.5 MB)
   constexpr int kSlab = 2 * DOUT * DIN + 2 * DOUT;
-  float* out = slab + (static_cast<int64_t>(blockIdx.x) * 4 + wave) * kSlab;
+  static_assert(4 * kSlab <= F::kTotal, "the four wave slabs must fit the staging LDS");
+  __syncthreads();  // every wave is done with its image (no DMA in flight past the last sub-tile)
+  float* ws = smem + wave * kSlab;
 #pragma unroll
   for (int ob = 0; ob < NCB; ++ob)
 #pragma unroll
     for (int ib = 0; ib < NIB; ++ib)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        out[(ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw1[ob][ib][i];
-        out[DOUT * DIN + (ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw2[ob][ib][i];
+        ws[(ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw1[ob][ib][i];
+        ws[DOUT * DIN + (ob * 16 + q * 4 + i) * DIN + ib * 16 + c] = dw2[ob][ib][i];
       }
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -882,10 +886,14 @@ __global__ __launch_bounds__(256, 1) void biinter_bwd_saved_kernel(
     b += __shfl_xor(b, 16);
     b += __shfl_xor(b, 32);
     if (q == 0) {
-      out[2 * DOUT * DIN + cb * 16 + c] = a;
-      out[2 * DOUT * DIN + DOUT + cb * 16 + c] = b;
+      ws[2 * DOUT * DIN + cb * 16 + c] = a;
+      ws[2 * DOUT * DIN + DOUT + cb * 16 + c] = b;
     }
   }
+  __syncthreads();
+  float* out = slab + static_cast<int64_t>(blockIdx.x) * kSlab;
+  for (int j = threadIdx.x; j < kSlab; j += 256)
+    out[j] = ((smem[j] + smem[kSlab + j]) + smem[2 * kSlab + j]) + smem[3 * kSlab + j];
 }
 
 // Sum the per-block slabs: one 1024-thread block per 64 outputs, 16 waves
@@ -985,7 +993,7 @@ static int64_t bwd_workspace(int64_t n) {
   const int64_t width = 2LL * DIN * DOUT + 2LL * DOUT;
   int64_t slabs = bwd_grid<DIN, DOUT>(n);
   if constexpr (SavedBwd<DIN, DOUT>::kOk) {
-    const int64_t sl = 4LL * saved_grid<DIN, DOUT>(n);
+    const int64_t sl = saved_grid<DIN, DOUT>(n);
     if (sl > slabs) slabs = sl;
   }
   return slabs * width;
@@ -1002,7 +1010,7 @@ static int launch_saved(const float* X, int64_t ldx, const float* S, int64_t lds
   using F = SavedBwd<DIN, DOUT>;
   const int width = 2 * DOUT * DIN + 2 * DOUT;
   const int grid = saved_grid<DIN, DOUT>(n);
-  *nslab = 4 * grid;
+  *nslab = grid;  // one slab per block (the four waves' partials summed in the kernel)
   if (ws == nullptr || ws_floats < static_cast<int64_t>(*nslab) * width) return KGAT_ERR_WORKSPACE;
   const size_t lds_bytes = F::kTotal * sizeof(float);
   static bool attr_set = false;
