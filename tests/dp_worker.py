@@ -152,7 +152,9 @@ def main() -> None:
             if tag in "BC" and (not torch.equal(pa.data, po.data) if dist.get_world_size() == 2
                                 else not torch.allclose(pa.data, po.data, rtol=0, atol=4 * 2e-5)):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
-            if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=2e-5):
+            # D / E associate the table gradient's sums differently at every world size: the same per-step
+            # Adam bound over the 4 applied steps
+            if tag in "DE" and not torch.allclose(pa.data, po.data, rtol=0, atol=4 * 2e-5):
                 failures.append(f"{tag} {na}: max |diff| {(pa.data - po.data).abs().max().item():.3e}")
         for tag, (_, po) in zip("ABCDEFGHI", named):
             other = po.data.clone()
