@@ -30,6 +30,10 @@ for step in "$@"; do
       python3 tools/step_timeline.py "$T" bpr_fwd_kernel 30 > gpurun_out/${TAG}_c2_frontier_step.txt
       tail -1 gpurun_out/${TAG}_c2_full_step.txt; tail -1 gpurun_out/${TAG}_c2_frontier_step.txt
       grep "^{" gpurun_out/${TAG}_c2_bench.log | tail -1 | cut -c1-300 ;;
+    c2plain)
+      timeout -k 10 900 python3 -u bench.py > gpurun_out/${TAG}_c2plain_bench.log 2>&1 \
+        || { tail -30 gpurun_out/${TAG}_c2plain_bench.log; exit 1; }
+      grep "^{" gpurun_out/${TAG}_c2plain_bench.log | tail -1 | cut -c1-300 ;;
     c3|c4)
       timeout -k 10 900 python3 -u bench.py --config $step --no-cpu-baseline > gpurun_out/${TAG}_${step}_bench.log 2>&1 \
         || { tail -30 gpurun_out/${TAG}_${step}_bench.log; exit 1; }
