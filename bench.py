@@ -1206,8 +1206,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="HIP events (the roofline's live kernel times) around the SpMMs of every k-th timed step")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="HIP events (the roofline's live kernel times) around the SpMMs of every k-th timed step "
+                         "(each record costs the stream ~5 us between two kernels: tools/event_gap_probe.py)")
     ap.add_argument("--exchange-at-1", action="store_true",
                     help="c2/c4 at N=1: run the N-rank table exchange anyway (RCCL world 1) to time its overhead")
     ap.add_argument("--no-frontier-leg", action="store_true",

@@ -202,7 +202,9 @@ __global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __r
 // The prologue of a TRAIN_CF step in one block: the id check of kgat_ids_check_ex (an id outside
 // [0, bound) becomes 0 in out and sets *bad / *bad_dev), the batch numbering of kgat_frontier_build
 // on the checked ids, and the zeroing of the two hop bitmaps kgat_frontier_hop marks next
-// (clr0 / clr1, clr_words uint32 each; nullable).
+// (clr0 / clr1, clr_words uint32 each; nullable).  tag > 0: *bad is a tagged word instead, written once
+// by thread 0 after the check, stored through to memory: (tag << 1) | any id bad | its old bit 0 -- the
+// host learns the check is done from the tag itself, with no event record behind the launch.
 __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restrict__ users,
                                                         const int64_t* __restrict__ pos,
                                                         const int64_t* __restrict__ neg, int batch, int64_t bound,
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restric
                                                         int32_t* __restrict__ bad_dev, int32_t* __restrict__ node_map,
                                                         int32_t* __restrict__ rows, int32_t* __restrict__ count,
                                                         uint32_t* __restrict__ clr0, uint32_t* __restrict__ clr1,
-                                                        int64_t clr_words) {
+                                                        int64_t clr_words, int32_t tag) {
   const int slots = 3 * batch;
   int64_t ids[kSlotsPer];
   bool flag = false;
@@ -227,8 +229,15 @@ __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restric
     }
   }
   if (flag) {  // every writer stores 1 (bad may be host-mapped pinned memory)
-    *bad = 1;
+    if (tag == 0) *bad = 1;
     if (bad_dev != nullptr) *bad_dev = 1;
+  }
+  if (tag > 0) {
+    const int any = __syncthreads_or(flag ? 1 : 0);
+    if (threadIdx.x == 0) {
+      const int32_t old = __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(bad, (tag << 1) | (old & 1) | any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   if (clr0 != nullptr) {
     // 16-byte stores where the bitmaps allow them (torch allocations are 16-byte aligned)
@@ -455,17 +464,27 @@ extern "C" int kgat_bpr_bwd_multi_f32(const kgat_tables* T, int32_t t0, const in
   return KGAT_OK;
 }
 
-extern "C" int kgat_cf_begin(const int64_t* users, const int64_t* pos, const int64_t* neg, int32_t batch,
-                             int64_t bound, int64_t* ids_out, int32_t* bad, int32_t* bad_dev, int32_t* node_map,
-                             int32_t* rows, int32_t* count, uint32_t* clear0, uint32_t* clear1, int64_t clear_words,
-                             void* stream) {
+extern "C" int kgat_cf_begin_ex(const int64_t* users, const int64_t* pos, const int64_t* neg, int32_t batch,
+                                int64_t bound, int64_t* ids_out, int32_t* bad, int32_t* bad_dev, int32_t* node_map,
+                                int32_t* rows, int32_t* count, uint32_t* clear0, uint32_t* clear1,
+                                int64_t clear_words, int32_t tag, void* stream) {
   if (!users || !pos || !neg || !ids_out || !bad || !node_map || !rows || !count || batch <= 0 ||
-      3 * batch > kgat::kBatchSlots || bound <= 0 || clear_words < 0 || ((clear0 == nullptr) != (clear1 == nullptr)))
+      3 * batch > kgat::kBatchSlots || bound <= 0 || clear_words < 0 || ((clear0 == nullptr) != (clear1 == nullptr)) ||
+      tag < 0 || tag >= (1 << 29))
     return KGAT_ERR_INVALID;
   if (clear0 != nullptr && ((reinterpret_cast<uintptr_t>(clear0) | reinterpret_cast<uintptr_t>(clear1)) & 15))
     return KGAT_ERR_INVALID;
   hipLaunchKernelGGL(kgat::cf_begin_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), users, pos,
-                     neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1, clear_words);
+                     neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1, clear_words,
+                     tag);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
+}
+
+extern "C" int kgat_cf_begin(const int64_t* users, const int64_t* pos, const int64_t* neg, int32_t batch,
+                             int64_t bound, int64_t* ids_out, int32_t* bad, int32_t* bad_dev, int32_t* node_map,
+                             int32_t* rows, int32_t* count, uint32_t* clear0, uint32_t* clear1, int64_t clear_words,
+                             void* stream) {
+  return kgat_cf_begin_ex(users, pos, neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1,
+                          clear_words, 0, stream);
 }

@@ -409,7 +409,9 @@ __global__ __launch_bounds__(256) void bits_list_kernel(const uint32_t* __restri
       s_prefix = prefix;
       if (blk == static_cast<int>(gridDim.x) - 1) {
         *count = prefix + agg;
-        if (count_host != nullptr) *count_host = prefix + agg;  // pinned host mirror: no copy launch
+        // pinned host mirror (no copy launch), stored through to memory: the host reads it without an event
+        if (count_host != nullptr)
+          __hip_atomic_store(count_host, prefix + agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -506,7 +508,8 @@ __global__ __launch_bounds__(256) void hop_finish_kernel(const int32_t* __restri
   const bool h = hit[i] != 0;
   if (i == n - 1) {
     *count = pos + (h ? 1 : 0);
-    if (count_host != nullptr) *count_host = pos + (h ? 1 : 0);
+    if (count_host != nullptr)
+      __hip_atomic_store(count_host, pos + (h ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (h) {
     rows[pos] = static_cast<int32_t>(i);

@@ -90,11 +90,13 @@ HOP_DENSE_FRACTION = 0.4
 
 
 def _hop_estimate(graph, l: int):
-    """Layer l's hop-set size at the previous step (None before the first is known)."""
+    """Layer l's hop-set size at a previous step (None before any listing was launched): read from the
+    pinned mirror as it stands -- the listing kernels store it through to memory themselves, so the
+    newest completed count is there without an event (an older one while the GPU runs behind)."""
     ent = getattr(graph, "_hop_est", {}).get(l)
-    if ent is None or not ent[1].query():
+    if ent is None:
         return None
-    return int(ent[0].item())
+    return int(ent[0][0])
 
 
 def _hop_small(graph, l: int, n_nodes: int) -> bool:
@@ -114,9 +116,13 @@ def _hop_host(graph, l: int) -> torch.Tensor:
     return ent[0]
 
 
-def _hop_record(graph, l: int) -> None:
-    """Mark the point after which layer l's host count is valid (the next step's choice)."""
-    graph._hop_est[l][1].record()
+def _hop_record(graph, l: int, exact: bool = False) -> None:
+    """Layer l's hop set was just listed.  ``exact``: this step's backward reads the count on the host (a wide
+    layer sizing its compact problem) -- an event is recorded behind the listing for that read; otherwise
+    none (each record costs the stream ~5 us between two kernels), the estimate reads the mirror as is."""
+    if exact:
+        graph._hop_est[l][1].record()
+    graph.__dict__.setdefault("_hop_exact", {})[l] = exact
 
 
 # A layer that went dense on its last-known hop-set size re-measures the set every this many dense steps.
@@ -152,19 +158,41 @@ class _IdGuard:
     def __init__(self):
         self._host = self._event = self._dev = None
         self._pending = None
+        self._tag = 0  # the last tag a TRAIN_CF check (kgat_cf_begin_ex) was launched with
+        self._tag_stream = None  # its stream, while that check is the pending one (no event behind it)
 
     def skip_flag(self) -> torch.Tensor | None:
         """The device int32 flag the optimiser kernels read (None before any device-id check)."""
         return self._dev
 
+    def _ensure(self, device) -> None:
+        if self._host is None:
+            # pinned host words written by the check kernels themselves (host-mapped: no copy launch per
+            # call): [0] the flag of kgat_ids_check_ex / _multi, [1] kgat_cf_begin_ex's tagged word
+            self._host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            self._event = torch.cuda.Event()
+            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+
     def raise_pending(self, block: bool = False) -> None:
-        if self._pending is None or (not block and not self._event.query()):
+        if self._pending is None:
             return
-        self._event.synchronize()
+        if self._tag_stream is not None:
+            # a TRAIN_CF check: done when its tag is in the word (stored through to memory by the kernel)
+            if (int(self._host[1]) >> 1) != self._tag:
+                if not block:
+                    return
+                self._tag_stream.synchronize()
+        else:
+            if not block and not self._event.query():
+                return
+            self._event.synchronize()
         what = self._pending
-        self._pending = None
-        if int(self._host[0]):
-            self._host.zero_()
+        self._pending = self._tag_stream = None
+        tagged = int(self._host[1])
+        if int(self._host[0]) or tagged & 1:
+            # every check launched so far is complete (the pending one was the last): no kernel writes the words
+            self._host[0] = 0
+            self._host[1] = tagged & ~1
             if self._dev is not None:
                 kernels.fill(self._dev.view(torch.float32), 0.0)  # int32 0 == float 0.0 bits
             raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed, "
@@ -184,12 +212,7 @@ class _IdGuard:
                     if t.numel() and (int(t.min()) < 0 or int(t.max()) >= b):
                         raise IndexError(f"{what}: id out of range [0, {b}) (min {int(t.min())}, max {int(t.max())})")
             return [t.to(device).long().reshape(-1).contiguous() for t in flat]
-        if self._host is None:
-            # the flag lives in pinned host memory, written by the check kernel itself (host-mapped:
-            # no copy launch per call)
-            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._event = torch.cuda.Event()
-            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self._ensure(device)
         given, outs = outs, []
         for gi, (g, b) in enumerate(groups):
             src = [torch.as_tensor(t).to(device).long().reshape(-1).contiguous() for t in g]
@@ -211,7 +234,7 @@ class _IdGuard:
                           self._dev.data_ptr(), stream_ptr(device))
             outs += list(out[:sum(sizes)].split(sizes))
         self._event.record()
-        self._pending = what
+        self._pending, self._tag_stream = what, None
         return outs
 
     def check_cf(self, what: str, ids, bound: int, device, node_map: torch.Tensor, clear=None):
@@ -228,14 +251,12 @@ class _IdGuard:
             for t in ts:
                 if int(t.min()) < 0 or int(t.max()) >= bound:
                     raise IndexError(f"{what}: id out of range [0, {bound}) (min {int(t.min())}, max {int(t.max())})")
-        if self._host is None:
-            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._event = torch.cuda.Event()
-            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self._ensure(device)
         src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
-        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear)
-        self._event.record()
-        self._pending = what
+        self._tag = self._tag % ((1 << 29) - 1) + 1
+        # the completion tag instead of an event record (~5 us of GPU time per record between two kernels)
+        out, rows, count = kernels.cf_begin(*src, bound, self._host[1:], self._dev, node_map, clear, tag=self._tag)
+        self._pending, self._tag_stream = what, torch.cuda.current_stream(src[0].device)
         return tuple(out.split(B)), rows, count
 
     def check_multi(self, what: str, ts, bounds, out: torch.Tensor, device) -> None:
@@ -243,10 +264,7 @@ class _IdGuard:
         against their own bounds (a ctypes int64 array) and copied, concatenated, into the preallocated ``out``
         in one launch (kgat_ids_check_multi)."""
         self.raise_pending()
-        if self._host is None:
-            self._host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self._event = torch.cuda.Event()
-            self._dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self._ensure(device)
         d = _lib.Ids()
         for k, t in enumerate(ts):
             d.ptr[k], d.n[k] = t.data_ptr(), t.numel()
@@ -254,7 +272,7 @@ class _IdGuard:
         _lib.call("kgat_ids_check_multi", ctypes.byref(d), bounds, out.data_ptr(), self._host.data_ptr(),
                   self._dev.data_ptr(), stream_ptr(device))
         self._event.record()
-        self._pending = what
+        self._pending, self._tag_stream = what, None
 
 
 class _TableUpdate:
@@ -1021,7 +1039,7 @@ class _CFLoss(torch.autograd.Function):
             else:
                 hrows, hmap, hcount, bits, fbits = kernels.frontier_hop(graph, rows, count_host=_hop_host(graph, nxt),
                                                                         precleared=tok.take_cleared())
-                _hop_record(graph, nxt)
+                _hop_record(graph, nxt, exact=states[nxt] is None or states[nxt].kind != "fused")
             # hop position -> frontier position of the batch rows (the G rows layer L-2's backward adds)
             gidx = None
             if fold2:
@@ -1051,7 +1069,10 @@ class _CFLoss(torch.autograd.Function):
                 pending = None
                 if not fused:  # the wide kinds size their compact problem on the host
                     est = graph._hop_est[l]
-                    est[1].synchronize()
+                    if graph._hop_exact.get(l):
+                        est[1].synchronize()
+                    else:  # listed by a forward that recorded no event (a data-parallel early first hop)
+                        torch.cuda.current_stream(users.device).synchronize()
                     n_hop = int(est[0][0])
             elif sparse and fused:
                 # hop size stays on the device (no host sync); the sparse/dense choice uses the

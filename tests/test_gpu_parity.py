@@ -1703,6 +1703,40 @@ def test_device_id_error_moves_no_parameter(pkg, fused):
     assert not torch.equal(m._user_entity_embedding.weight.detach(), before["_user_entity_embedding.weight"])
 
 
+def test_tagged_cf_check_keeps_a_bad_step_reported(pkg):
+    """TRAIN_CF's id check reports completion through its own tagged pinned word (kgat_cf_begin_ex: no event
+    record behind the launch).  A bad step followed by a good one launched before the host saw the first
+    (the GPU held busy) still raises: the second launch keeps the word's bad bit.  After the raise the
+    word is clean and the next steps run."""
+    graph_mod, _ = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(3000, 20000, seed=4)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32]))
+    m.attach_graph(lay, DEV)
+    ok = torch.arange(8, device=DEV)
+    bad = torch.full((8,), U + E + 3, dtype=torch.int64, device=DEV)
+    m(ok, ok + 1, ok + 2, mode=pkg.KGATMode.TRAIN_CF)
+    m.raise_pending(block=True)
+    busy = torch.empty(1 << 26, device=DEV)
+    for _ in range(40):  # ~10 ms of GPU work ahead of the two checks
+        busy.fill_(1.0)
+    m(ok, bad, ok, mode=pkg.KGATMode.TRAIN_CF)
+    raised = False
+    try:
+        m(ok, ok + 1, ok + 2, mode=pkg.KGATMode.TRAIN_CF)  # its check's tag follows the bad one's
+    except IndexError:
+        raised = True  # the GPU caught up before this call looked
+    if not raised:
+        with pytest.raises(IndexError):
+            m.raise_pending(block=True)
+    tagged = int(m._ids._host[1])
+    assert tagged & 1 == 0 and tagged >> 1 == m._ids._tag
+    for _ in range(3):
+        loss = m(ok, ok + 1, ok + 2, mode=pkg.KGATMode.TRAIN_CF)
+    m.raise_pending(block=True)
+    assert torch.isfinite(loss)
+
+
 @pytest.mark.parametrize("dim,layers", [(64, [64]), (64, [64, 32]), (64, [64, 64]), (64, [64, 32, 16]),
                                         (128, [128, 64, 32])])
 def test_frontier_forward_bit_identical(pkg, dim, layers, monkeypatch):
