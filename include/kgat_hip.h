@@ -528,11 +528,12 @@ int kgat_frontier_reset(const int32_t *rows, int32_t n, int32_t *node_map, void 
 int kgat_cf_begin(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch, int64_t bound,
                   int64_t *ids_out, int32_t *bad, int32_t *bad_dev, int32_t *node_map, int32_t *rows, int32_t *count,
                   uint32_t *clear0, uint32_t *clear1, int64_t clear_words, void *stream);
-/* kgat_cf_begin with a completion tag: tag = 0 is kgat_cf_begin; 0 < tag < 2^29 makes *bad a tagged
- * word, written once after the check by one thread with a store through to memory: (tag << 1) | (an id
- * was out of range) | (bit 0 of its old value, so a bad step stays reported until the host clears it).
- * The host polls the word for its tag instead of recording an event behind the launch (an event record
- * costs ~5 us of GPU time between two dependent kernels). */
+/* kgat_cf_begin with a completion tag: tag = 0 is kgat_cf_begin; 0 < tag < 2^29: bad points to two
+ * words (host-mapped pinned memory), written once after the check by one thread with stores through to
+ * memory: bad[0] = 1 when an id was out of range (never cleared by the kernel: the caller clears it),
+ * then bad[1] = tag (a release store behind bad[0] when that was written).  The host polls bad[1] for
+ * its tag instead of recording an event behind the launch (an event record costs ~5 us of GPU time
+ * between two dependent kernels). */
 int kgat_cf_begin_ex(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch, int64_t bound,
                      int64_t *ids_out, int32_t *bad, int32_t *bad_dev, int32_t *node_map, int32_t *rows,
                      int32_t *count, uint32_t *clear0, uint32_t *clear1, int64_t clear_words, int32_t tag,

@@ -202,8 +202,8 @@ __global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __r
 // The prologue of a TRAIN_CF step in one block: the id check of kgat_ids_check_ex (an id outside
 // [0, bound) becomes 0 in out and sets *bad / *bad_dev), the batch numbering of kgat_frontier_build
 // on the checked ids, and the zeroing of the two hop bitmaps kgat_frontier_hop marks next
-// (clr0 / clr1, clr_words uint32 each; nullable).  tag > 0: *bad is a tagged word instead, written once
-// by thread 0 after the check, stored through to memory: (tag << 1) | any id bad | its old bit 0 -- the
+// (clr0 / clr1, clr_words uint32 each; nullable).  tag > 0: bad[1] receives the tag once the check is done,
+// from thread 0, stored through to memory after bad[0] = 1 when an id was bad (a release store then) -- the
 // host learns the check is done from the tag itself, with no event record behind the launch.
 __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restrict__ users,
                                                         const int64_t* __restrict__ pos,
@@ -235,8 +235,12 @@ __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restric
   if (tag > 0) {
     const int any = __syncthreads_or(flag ? 1 : 0);
     if (threadIdx.x == 0) {
-      const int32_t old = __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(bad, (tag << 1) | (old & 1) | any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (any) {  // rare: the flag, then the tag ordered behind it
+        __hip_atomic_store(bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(bad + 1, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __hip_atomic_store(bad + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
   if (clr0 != nullptr) {

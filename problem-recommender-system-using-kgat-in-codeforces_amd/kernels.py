@@ -1071,8 +1071,8 @@ def cf_begin(users, pos, neg, bound: int, bad_host: torch.Tensor, bad_dev: torch
              node_map: torch.Tensor, clear: tuple | None = None, tag: int = 0):
     """kgat_cf_begin_ex: (checked int64 ids [3B] = users | pos | neg, frontier rows int32 [3B], count int32 [1]).
     ``clear`` = (bits0, bits1, words): kgat_frontier_hop's bitmaps, zeroed by the same launch; ``tag`` > 0:
-    ``bad_host`` is the tagged completion word ((tag << 1) | bad | its old bit 0, written when the check is
-    done)."""
+    ``bad_host`` holds two pinned words, [0] the bad flag (set only) and [1] the tag, written when the
+    check is done."""
     for t, nm in ((users, "users"), (pos, "pos"), (neg, "neg")):
         _req(t, nm, dtype=torch.int64, dim=1)
     B = users.numel()
@@ -1087,8 +1087,8 @@ def cf_begin(users, pos, neg, bound: int, bad_host: torch.Tensor, bad_dev: torch
     if clear is not None:
         b0, b1, words = clear
         c0, c1 = b0.data_ptr(), b1.data_ptr()
-    if not 0 <= tag < (1 << 29):
-        raise ValueError("cf_begin: tag in [0, 2^29)")
+    if not 0 <= tag < (1 << 29) or (tag and bad_host.numel() < 2):
+        raise ValueError("cf_begin: tag in [0, 2^29); a tag needs two pinned words")
     _lib.call("kgat_cf_begin_ex", users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, int(bound), ids.data_ptr(),
               bad_host.data_ptr(), bad_dev.data_ptr() if bad_dev is not None else None, node_map.data_ptr(),
               rows.data_ptr(), count.data_ptr(), c0, c1, int(words), int(tag), stream_ptr(dev))

@@ -168,7 +168,7 @@ class _IdGuard:
     def _ensure(self, device) -> None:
         if self._host is None:
             # pinned host words written by the check kernels themselves (host-mapped: no copy launch per
-            # call): [0] the flag of kgat_ids_check_ex / _multi, [1] kgat_cf_begin_ex's tagged word
+            # call): [0] the bad-id flag (every check kernel sets it; cleared here), [1] kgat_cf_begin_ex's tag
             self._host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
             self._event = torch.cuda.Event()
             self._dev = torch.zeros(1, dtype=torch.int32, device=device)
@@ -178,7 +178,7 @@ class _IdGuard:
             return
         if self._tag_stream is not None:
             # a TRAIN_CF check: done when its tag is in the word (stored through to memory by the kernel)
-            if (int(self._host[1]) >> 1) != self._tag:
+            if int(self._host[1]) != self._tag:
                 if not block:
                     return
                 self._tag_stream.synchronize()
@@ -188,11 +188,9 @@ class _IdGuard:
             self._event.synchronize()
         what = self._pending
         self._pending = self._tag_stream = None
-        tagged = int(self._host[1])
-        if int(self._host[0]) or tagged & 1:
-            # every check launched so far is complete (the pending one was the last): no kernel writes the words
+        if int(self._host[0]):
+            # every check launched so far is complete (the pending one was the last): no kernel writes the flag
             self._host[0] = 0
-            self._host[1] = tagged & ~1
             if self._dev is not None:
                 kernels.fill(self._dev.view(torch.float32), 0.0)  # int32 0 == float 0.0 bits
             raise IndexError(f"{what}: id out of range (detected on the device; the call ran with it zeroed, "
@@ -255,7 +253,7 @@ class _IdGuard:
         src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
         self._tag = self._tag % ((1 << 29) - 1) + 1
         # the completion tag instead of an event record (~5 us of GPU time per record between two kernels)
-        out, rows, count = kernels.cf_begin(*src, bound, self._host[1:], self._dev, node_map, clear, tag=self._tag)
+        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear, tag=self._tag)
         self._pending, self._tag_stream = what, torch.cuda.current_stream(src[0].device)
         return tuple(out.split(B)), rows, count
 

@@ -1704,10 +1704,10 @@ def test_device_id_error_moves_no_parameter(pkg, fused):
 
 
 def test_tagged_cf_check_keeps_a_bad_step_reported(pkg):
-    """TRAIN_CF's id check reports completion through its own tagged pinned word (kgat_cf_begin_ex: no event
+    """TRAIN_CF's id check reports completion through a tag in pinned memory (kgat_cf_begin_ex: no event
     record behind the launch).  A bad step followed by a good one launched before the host saw the first
-    (the GPU held busy) still raises: the second launch keeps the word's bad bit.  After the raise the
-    word is clean and the next steps run."""
+    (the GPU held busy) still raises: the flag word is only ever set by the kernels.  After the raise the
+    flag is clear, the tag is the last launch's, and the next steps run."""
     graph_mod, _ = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(3000, 20000, seed=4)
     lay = graph_mod.build_layout(U, E, inter, trip)
@@ -1729,8 +1729,7 @@ def test_tagged_cf_check_keeps_a_bad_step_reported(pkg):
     if not raised:
         with pytest.raises(IndexError):
             m.raise_pending(block=True)
-    tagged = int(m._ids._host[1])
-    assert tagged & 1 == 0 and tagged >> 1 == m._ids._tag
+    assert int(m._ids._host[0]) == 0 and int(m._ids._host[1]) == m._ids._tag
     for _ in range(3):
         loss = m(ok, ok + 1, ok + 2, mode=pkg.KGATMode.TRAIN_CF)
     m.raise_pending(block=True)
