@@ -251,9 +251,10 @@ class _IdGuard:
                     raise IndexError(f"{what}: id out of range [0, {bound}) (min {int(t.min())}, max {int(t.max())})")
         self._ensure(device)
         src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
-        self._tag = self._tag % ((1 << 29) - 1) + 1
+        tag = self._tag % ((1 << 29) - 1) + 1
         # the completion tag instead of an event record (~5 us of GPU time per record between two kernels)
-        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear, tag=self._tag)
+        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear, tag=tag)
+        self._tag = tag  # launched: the tag the host now waits for
         self._pending, self._tag_stream = what, torch.cuda.current_stream(src[0].device)
         return tuple(out.split(B)), rows, count
 
