@@ -528,16 +528,20 @@ int kgat_frontier_reset(const int32_t *rows, int32_t n, int32_t *node_map, void 
 int kgat_cf_begin(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch, int64_t bound,
                   int64_t *ids_out, int32_t *bad, int32_t *bad_dev, int32_t *node_map, int32_t *rows, int32_t *count,
                   uint32_t *clear0, uint32_t *clear1, int64_t clear_words, void *stream);
-/* kgat_cf_begin with a completion tag: tag = 0 is kgat_cf_begin; 0 < tag < 2^29: bad points to two
- * words (host-mapped pinned memory), written once after the check by one thread with stores through to
- * memory: bad[0] = 1 when an id was out of range (never cleared by the kernel: the caller clears it),
- * then bad[1] = tag (a release store behind bad[0] when that was written).  The host polls bad[1] for
- * its tag instead of recording an event behind the launch (an event record costs ~5 us of GPU time
- * between two dependent kernels). */
+/* kgat_cf_begin with a completion tag and the first hop's marking.  tag = 0: *bad as in kgat_cf_begin;
+ * 0 < tag < 2^29: bad points to two words (host-mapped pinned memory), written once after the check by
+ * one thread with stores through to memory: bad[0] = 1 when an id was out of range (never cleared by the
+ * kernel: the caller clears it), then bad[1] = tag (a release store behind bad[0] when that was written).
+ * The host polls bad[1] for its tag instead of recording an event behind the launch (an event record
+ * costs ~5 us of GPU time between two dependent kernels).  mark0 / mark1 (nullable; zero on entry, a
+ * different pair from clear0 / clear1, A's n_rows >= bound): the same launch marks the batch's first hop
+ * there as kgat_frontier_hop does (mark0: the batch rows, mark1: those rows and every column of their
+ * rows of A) -- then call kgat_frontier_hop_ex with n0 = 0 and KGAT_HOP_PRECLEARED to list it.  Clearing
+ * one bitmap pair while marking the other lets a caller alternate two pairs across steps (model.py). */
 int kgat_cf_begin_ex(const int64_t *users, const int64_t *pos, const int64_t *neg, int32_t batch, int64_t bound,
                      int64_t *ids_out, int32_t *bad, int32_t *bad_dev, int32_t *node_map, int32_t *rows,
-                     int32_t *count, uint32_t *clear0, uint32_t *clear1, int64_t clear_words, int32_t tag,
-                     void *stream);
+                     int32_t *count, uint32_t *clear0, uint32_t *clear1, int64_t clear_words, const kgat_csr *A,
+                     uint32_t *mark0, uint32_t *mark1, int32_t tag, void *stream);
 
 /* a5 -- TransR KG loss (model.py:204-261): h' = e_h W_r etc., scalar loss
  * written to *loss.  work (kgat_transr_work_floats) keeps per-sample terms and

@@ -137,7 +137,7 @@ _SIGNATURES = {
     "kgat_cf_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_i64, c_vp]),
     "kgat_cf_begin_ex": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                        c_vp, c_i64, c_i32, c_vp]),
+                                        c_vp, c_i64, ctypes.POINTER(CSR), c_vp, c_vp, c_i32, c_vp]),
     "kgat_row_softmax_work_floats": (c_i64, [ctypes.POINTER(CSR)]),
     "kgat_row_softmax_plan_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
     "kgat_frontier_build": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),

@@ -205,6 +205,10 @@ __global__ __launch_bounds__(1024) void frontier_build_kernel(const int64_t* __r
 // (clr0 / clr1, clr_words uint32 each; nullable).  tag > 0: bad[1] receives the tag once the check is done,
 // from thread 0, stored through to memory after bad[0] = 1 when an id was bad (a release store then) -- the
 // host learns the check is done from the tag itself, with no event record behind the launch.
+// mark0 / mark1 (nullable, zero on entry, not the cleared pair): blocks 1.. mark the batch's first hop
+// there as kgat_frontier_hop's frontier_mark_kernel does -- mark0 the batch rows, mark1 those rows and
+// every column of their rows of A -- from the checked ids directly (four slots per block, 256 threads
+// each; a repeated id marks the same bits again), beside block 0's numbering.
 __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restrict__ users,
                                                         const int64_t* __restrict__ pos,
                                                         const int64_t* __restrict__ neg, int batch, int64_t bound,
@@ -212,8 +216,25 @@ __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restric
                                                         int32_t* __restrict__ bad_dev, int32_t* __restrict__ node_map,
                                                         int32_t* __restrict__ rows, int32_t* __restrict__ count,
                                                         uint32_t* __restrict__ clr0, uint32_t* __restrict__ clr1,
-                                                        int64_t clr_words, int32_t tag) {
+                                                        int64_t clr_words, int32_t tag, kgat_csr A,
+                                                        uint32_t* __restrict__ mark0, uint32_t* __restrict__ mark1) {
   const int slots = 3 * batch;
+  if (blockIdx.x > 0) {
+    const int k = (blockIdx.x - 1) * 4 + (threadIdx.x >> 8);
+    const int t = threadIdx.x & 255;
+    if (k >= slots) return;
+    const int64_t v = batch_id(users, pos, neg, batch, k);
+    const int32_t i = v >= 0 && v < bound ? static_cast<int32_t>(v) : 0;  // block 0's substitution
+    if (t == 0) {
+      atomicOr(&mark0[i >> 5], 1u << (i & 31));
+      atomicOr(&mark1[i >> 5], 1u << (i & 31));
+    }
+    for (int64_t e = A.rowptr[i] + t; e < A.rowptr[i + 1]; e += 256) {
+      const int32_t j = A.col[e];
+      atomicOr(&mark1[j >> 5], 1u << (j & 31));
+    }
+    return;
+  }
   int64_t ids[kSlotsPer];
   bool flag = false;
 #pragma unroll
@@ -471,16 +492,23 @@ extern "C" int kgat_bpr_bwd_multi_f32(const kgat_tables* T, int32_t t0, const in
 extern "C" int kgat_cf_begin_ex(const int64_t* users, const int64_t* pos, const int64_t* neg, int32_t batch,
                                 int64_t bound, int64_t* ids_out, int32_t* bad, int32_t* bad_dev, int32_t* node_map,
                                 int32_t* rows, int32_t* count, uint32_t* clear0, uint32_t* clear1,
-                                int64_t clear_words, int32_t tag, void* stream) {
+                                int64_t clear_words, const kgat_csr* A, uint32_t* mark0, uint32_t* mark1, int32_t tag,
+                                void* stream) {
   if (!users || !pos || !neg || !ids_out || !bad || !node_map || !rows || !count || batch <= 0 ||
       3 * batch > kgat::kBatchSlots || bound <= 0 || clear_words < 0 || ((clear0 == nullptr) != (clear1 == nullptr)) ||
-      tag < 0 || tag >= (1 << 29))
+      tag < 0 || tag >= (1 << 29) || ((mark0 == nullptr) != (mark1 == nullptr)))
+    return KGAT_ERR_INVALID;
+  if (mark0 != nullptr && (!A || !A->rowptr || !A->col || A->n_rows < bound || mark0 == clear0 || mark0 == clear1 ||
+                           mark1 == clear0 || mark1 == clear1 || mark0 == mark1))
     return KGAT_ERR_INVALID;
   if (clear0 != nullptr && ((reinterpret_cast<uintptr_t>(clear0) | reinterpret_cast<uintptr_t>(clear1)) & 15))
     return KGAT_ERR_INVALID;
-  hipLaunchKernelGGL(kgat::cf_begin_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), users, pos,
-                     neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1, clear_words,
-                     tag);
+  kgat_csr a{};
+  if (mark0 != nullptr) a = *A;
+  const int grid = mark0 != nullptr ? 1 + (3 * batch + 3) / 4 : 1;
+  hipLaunchKernelGGL(kgat::cf_begin_kernel, dim3(grid), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), users,
+                     pos, neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1, clear_words,
+                     tag, a, mark0, mark1);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -490,5 +518,5 @@ extern "C" int kgat_cf_begin(const int64_t* users, const int64_t* pos, const int
                              int32_t* rows, int32_t* count, uint32_t* clear0, uint32_t* clear1, int64_t clear_words,
                              void* stream) {
   return kgat_cf_begin_ex(users, pos, neg, batch, bound, ids_out, bad, bad_dev, node_map, rows, count, clear0, clear1,
-                          clear_words, 0, stream);
+                          clear_words, nullptr, nullptr, nullptr, 0, stream);
 }

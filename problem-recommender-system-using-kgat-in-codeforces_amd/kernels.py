@@ -405,17 +405,44 @@ def hop_bitmaps(graph: DeviceGraph):
     return hb[7], hb[6], (graph.n_nodes + 31) // 32
 
 
+def hop_bitmaps_next(graph: DeviceGraph):
+    """The TRAIN_CF prologue's bitmap plan (kgat_cf_begin_ex marks the batch's first hop itself): the
+    graph keeps a second (frontier, hop set) pair that is all zero between steps; the step marks that
+    one and zeroes the pair the previous step used, in the same launch.  Returns (mark = (bits0, bits1)
+    of the next pair, clear = the current pair (bits0, bits1, words)); hop_bitmaps_commit makes the
+    marked pair current once the launch is queued."""
+    hb = graph.hop_buffers()
+    alt = graph.__dict__.get("_hop_alt")
+    if alt is None:  # the spare pair, zero (the invariant every commit keeps)
+        alt = graph._hop_alt = (torch.zeros_like(hb[7]), torch.zeros_like(hb[6]))
+    return alt, (hb[7], hb[6], (graph.n_nodes + 31) // 32)
+
+
+def hop_bitmaps_commit(graph: DeviceGraph) -> None:
+    """Swap the pairs after a kgat_cf_begin_ex launch that marked the spare one and zeroed the current
+    one: the marked pair is the hop buffers' (hb[7], hb[6]) now, the zeroed one the spare."""
+    hb = graph.hop_buffers()
+    b0, b1 = graph._hop_alt
+    graph._hop = hb[:6] + (b1, b0) + hb[8:]
+    graph._hop_alt = (hb[7], hb[6])
+
+
+PRECLEARED, PREMARKED = 1, 2  # frontier_hop's ``precleared`` states (_MarkedBatch.take_cleared)
+
+
 def frontier_hop(graph: DeviceGraph, rows0: torch.Tensor, count_host: torch.Tensor | None = None,
-                 precleared: bool = False):
+                 precleared: int = 0):
     """The first hop set of the backward chain from the batch frontier rows0 (frontier_build's
     rows, -1 padded): (hop rows int32 [N] ascending -- first count valid --, node_map, count int32 [1]
     on the device, hop-set bitmap, frontier bitmap).  No graph scan: the frontier rows' A edges are
-    marked (kgat_frontier_hop_ex); ``precleared``: kgat_cf_begin zeroed the bitmaps already."""
+    marked (kgat_frontier_hop_ex); ``precleared``: PRECLEARED -- kgat_cf_begin zeroed the bitmaps already,
+    PREMARKED -- kgat_cf_begin_ex marked the first hop in them too (only the listing runs)."""
     _req(rows0, "rows0", dtype=torch.int32, dim=1)
     hb = graph.hop_buffers()
     _, node_map, rows, count, _, _, bits1, bits0, work = hb[:9]
     desc = graph.A.descriptor()
-    _lib.call("kgat_frontier_hop_ex", ctypes.byref(desc), rows0.data_ptr(), rows0.numel(), bits0.data_ptr(),
+    n0 = 0 if precleared == PREMARKED else rows0.numel()
+    _lib.call("kgat_frontier_hop_ex", ctypes.byref(desc), rows0.data_ptr(), n0, bits0.data_ptr(),
               bits1.data_ptr(), node_map.data_ptr(), rows.data_ptr(), count.data_ptr(), _host_ptr(count_host),
               hb[9].data_ptr(), work.data_ptr(), work.numel(), _lib.KGAT_HOP_PRECLEARED if precleared else 0,
               stream_ptr(rows0.device))
@@ -1068,11 +1095,12 @@ def bpr_bwd_multi(tables: list[torch.Tensor], t0: int, users, pos, neg, reg: flo
 
 
 def cf_begin(users, pos, neg, bound: int, bad_host: torch.Tensor, bad_dev: torch.Tensor | None,
-             node_map: torch.Tensor, clear: tuple | None = None, tag: int = 0):
+             node_map: torch.Tensor, clear: tuple | None = None, tag: int = 0, mark=None):
     """kgat_cf_begin_ex: (checked int64 ids [3B] = users | pos | neg, frontier rows int32 [3B], count int32 [1]).
     ``clear`` = (bits0, bits1, words): kgat_frontier_hop's bitmaps, zeroed by the same launch; ``tag`` > 0:
     ``bad_host`` holds two pinned words, [0] the bad flag (set only) and [1] the tag, written when the
-    check is done."""
+    check is done.  ``mark`` = (graph, (bits0, bits1)): the same launch marks the batch's first hop in that
+    (zero) pair, a different one from ``clear`` (hop_bitmaps_next)."""
     for t, nm in ((users, "users"), (pos, "pos"), (neg, "neg")):
         _req(t, nm, dtype=torch.int64, dim=1)
     B = users.numel()
@@ -1089,9 +1117,16 @@ def cf_begin(users, pos, neg, bound: int, bad_host: torch.Tensor, bad_dev: torch
         c0, c1 = b0.data_ptr(), b1.data_ptr()
     if not 0 <= tag < (1 << 29) or (tag and bad_host.numel() < 2):
         raise ValueError("cf_begin: tag in [0, 2^29); a tag needs two pinned words")
+    desc = m0 = m1 = None
+    if mark is not None:
+        g, (b0, b1) = mark
+        if g.n_nodes != int(bound) or b0.numel() * 32 < bound or b1.numel() * 32 < bound:
+            raise ValueError("cf_begin: the marked bitmaps must cover the graph's nodes")
+        desc = ctypes.byref(g.A.descriptor())
+        m0, m1 = b0.data_ptr(), b1.data_ptr()
     _lib.call("kgat_cf_begin_ex", users.data_ptr(), pos.data_ptr(), neg.data_ptr(), B, int(bound), ids.data_ptr(),
               bad_host.data_ptr(), bad_dev.data_ptr() if bad_dev is not None else None, node_map.data_ptr(),
-              rows.data_ptr(), count.data_ptr(), c0, c1, int(words), int(tag), stream_ptr(dev))
+              rows.data_ptr(), count.data_ptr(), c0, c1, int(words), desc, m0, m1, int(tag), stream_ptr(dev))
     return ids, rows, count
 
 

@@ -235,10 +235,11 @@ class _IdGuard:
         self._pending, self._tag_stream = what, None
         return outs
 
-    def check_cf(self, what: str, ids, bound: int, device, node_map: torch.Tensor, clear=None):
+    def check_cf(self, what: str, ids, bound: int, device, node_map: torch.Tensor, clear=None, mark=None):
         """TRAIN_CF's ids checked (the rules of ``check``) and numbered as the batch frontier in one launch
-        (kgat_cf_begin: kgat_ids_check_ex + kgat_frontier_build, and the hop bitmaps zeroed when ``clear``
-        = kernels.hop_bitmaps(graph)).  Returns ((users, pos, neg), rows, count) or None when the ids do not
+        (kgat_cf_begin_ex: kgat_ids_check_ex + kgat_frontier_build, a bitmap pair zeroed when ``clear`` =
+        (bits0, bits1, words), and the batch's first hop marked in the pair ``mark`` = (graph, (bits0, bits1))
+        -- kernels.hop_bitmaps_next).  Returns ((users, pos, neg), rows, count) or None when the ids do not
         take this path (sizes differ, 3B > 4096, an id array is empty)."""
         ts = [torch.as_tensor(t) for t in ids]
         B = ts[0].numel()
@@ -253,7 +254,7 @@ class _IdGuard:
         src = [t.to(device).long().reshape(-1).contiguous() for t in ts]
         tag = self._tag % ((1 << 29) - 1) + 1
         # the completion tag instead of an event record (~5 us of GPU time per record between two kernels)
-        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear, tag=tag)
+        out, rows, count = kernels.cf_begin(*src, bound, self._host, self._dev, node_map, clear, tag=tag, mark=mark)
         self._tag = tag  # launched: the tag the host now waits for
         self._pending, self._tag_stream = what, torch.cuda.current_stream(src[0].device)
         return tuple(out.split(B)), rows, count
@@ -799,14 +800,16 @@ class _MarkedBatch:
     """The batch rows a forward marked in ``graph.node_map`` (and, with 2 layers, the first hop it left
     in the graph's hop buffers) for its own backward -- at most one outstanding per graph."""
 
-    def __init__(self, rows: torch.Tensor, count: torch.Tensor | None = None, cleared: bool = False):
+    def __init__(self, rows: torch.Tensor, count: torch.Tensor | None = None, cleared: int = 0):
         self.rows = rows
         self.count = count
         self.stale = False
-        self.cleared = cleared  # kgat_cf_begin zeroed the hop bitmaps, and no kgat_frontier_hop has run since
+        # kernels.PRECLEARED: kgat_cf_begin zeroed the hop bitmaps, PREMARKED: kgat_cf_begin_ex also marked the
+        # batch's first hop in them -- and no kgat_frontier_hop has run since
+        self.cleared = cleared
 
-    def take_cleared(self) -> bool:
-        c, self.cleared = self.cleared, False
+    def take_cleared(self) -> int:
+        c, self.cleared = self.cleared, 0
         return c
 
 
@@ -816,7 +819,7 @@ def _release_marks(graph) -> None:
     tok = getattr(graph, "_marked", None)
     if tok is not None:
         tok.stale = True
-        tok.cleared = False  # the next step's kgat_cf_begin / kgat_frontier_hop own the bitmaps now
+        tok.cleared = 0  # the next step's kgat_cf_begin / kgat_frontier_hop own the bitmaps now
         kernels.frontier_reset(tok.rows, graph.node_map)
         graph._marked = None
 
@@ -1444,14 +1447,17 @@ class KGAT(nn.Module):
         frontier = self.frontier_forward and torch.is_grad_enabled()
         marks = None
         if torch.is_grad_enabled():
-            # ids checked and numbered as the batch frontier, and the hop bitmaps zeroed, in one launch
-            # (kgat_cf_begin); the marks go to this step's backward (and frontier forward / DP hop exchange)
+            # ids checked and numbered as the batch frontier, the batch's first hop marked in the spare bitmap
+            # pair and the pair the last step used zeroed, in one launch (kgat_cf_begin_ex); the marks go to
+            # this step's backward (and frontier forward / DP hop exchange)
             _release_marks(g)
+            mark, clear = kernels.hop_bitmaps_next(g)
             r = self._ids.check_cf("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
-                                   g.device, g.node_map, kernels.hop_bitmaps(g))
+                                   g.device, g.node_map, clear, mark=(g, mark))
             if r is not None:
+                kernels.hop_bitmaps_commit(g)
                 ids, rows, fcount = r
-                g._marked = tok = _MarkedBatch(rows, fcount, cleared=True)
+                g._marked = tok = _MarkedBatch(rows, fcount, cleared=kernels.PREMARKED)
                 marks = (rows, fcount, tok)
         if marks is None:
             ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,

@@ -1736,6 +1736,38 @@ def test_tagged_cf_check_keeps_a_bad_step_reported(pkg):
     assert torch.isfinite(loss)
 
 
+def test_cf_prologue_marks_first_hop_in_alternating_pairs(pkg):
+    """kgat_cf_begin_ex marks the batch's first hop (F and every column of A's rows F) in the spare bitmap
+    pair and zeroes the pair the previous step used, in the id check's launch; the listing that follows
+    (kgat_frontier_hop_ex, n0 = 0) yields exactly F + N(F), step after step with the pairs alternating, and
+    the spare pair is zero between steps."""
+    graph_mod, kernels = _mods(pkg)
+    U, E, inter, trip = graph_mod.synthetic_ckg(3000, 20000, seed=6)
+    lay = graph_mod.build_layout(U, E, inter, trip)
+    m = pkg.KGAT(pkg.KGATArgs(user_num=U, entity_num=E, relation_num=len(lay.rel_order), layer_size=[64, 32]))
+    m.attach_graph(lay, DEV)
+    g = m.graph()
+    rp, col = g.A.rowptr_host, g.A.col_host
+    rng = np.random.default_rng(3)
+    for step in range(4):
+        ids = [rng.integers(0, hi, 64) for hi in (U, U + E, U + E)]
+        ids[1][:5] = ids[0][:5]  # repeated ids: marked more than once, listed once
+        m(*[torch.from_numpy(i).to(DEV) for i in ids], mode=pkg.KGATMode.TRAIN_CF)
+        tok = g._marked
+        assert tok.cleared == kernels.PREMARKED
+        hrows, _, hcount, bits1, bits0 = kernels.frontier_hop(g, tok.rows, precleared=tok.take_cleared())
+        torch.cuda.synchronize()
+        F = np.unique(np.concatenate(ids))
+        want = np.unique(np.concatenate([F] + [col[rp[i]:rp[i + 1]] for i in F]))
+        n = int(hcount.item())
+        assert np.array_equal(hrows[:n].cpu().numpy(), want), step
+        fb = np.unpackbits(bits0.cpu().numpy().view(np.uint8), bitorder="little")[:g.n_nodes]
+        assert np.array_equal(np.flatnonzero(fb), F), step
+        for t in g._hop_alt:
+            assert int(t.count_nonzero()) == 0, step
+        m.raise_pending(block=True)
+
+
 @pytest.mark.parametrize("dim,layers", [(64, [64]), (64, [64, 32]), (64, [64, 64]), (64, [64, 32, 16]),
                                         (128, [128, 64, 32])])
 def test_frontier_forward_bit_identical(pkg, dim, layers, monkeypatch):
