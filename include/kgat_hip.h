@@ -714,6 +714,17 @@ int kgat_adam_multi_f32(const kgat_adam_tensor *tensors, int32_t count, float be
 /* ... with the optimiser skip flag (see kgat_spmm_csr_masked_adam_ex_f32). */
 int kgat_adam_multi_ex_f32(const kgat_adam_tensor *tensors, int32_t count, float beta1, float beta2, float eps,
                            const int32_t *skip, void *stream);
+/* kgat_spmm_csr_masked_adam_ex_f32 that also steps n_extra (<= KGAT_ADAM_MAX_TENSORS) further tensors in
+ * its second launch: the long rows' fix-up and kgat_adam_multi_ex_f32's step of `extra` (same beta1 /
+ * beta2 / eps and skip flag, each tensor its own step size and bias correction) share one launch -- the
+ * CF step's table update and the aggregator weights' Adam (model.py:404-413), bit for bit the two calls.
+ * n_extra = 0: kgat_spmm_csr_masked_adam_ex_f32. */
+int kgat_spmm_csr_masked_adam_multi_f32(const kgat_csr *A, const int32_t *src_map, const float *Xc, int64_t ldxc,
+                                        const float *Yc_init, int64_t ldyc, const uint64_t *src_rank, float *p,
+                                        float *m, float *v, int64_t ldp, int32_t d, float step_size, float beta1,
+                                        float beta2, float bc2_sqrt, float eps, const int32_t *skip,
+                                        float *workspace, int64_t workspace_floats, const kgat_adam_tensor *extra,
+                                        int32_t n_extra, void *stream);
 
 /* a9 for the KG step's table (model.py:414-419 after the TransR backward, whose table gradient is
  * nonzero on the <= 3B rows of the batch only): the dense Adam step over p / m / v [n_rows x d]

@@ -179,6 +179,10 @@ _SIGNATURES = {
                                             c_vp]),
     "kgat_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp]),
     "kgat_adam_multi_ex_f32": (ctypes.c_int, [ctypes.POINTER(AdamTensor), c_i32, c_f32, c_f32, c_f32, c_vp, c_vp]),
+    "kgat_spmm_csr_masked_adam_multi_f32": (ctypes.c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                                           c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
+                                                           c_f32, c_vp, c_vp, c_i64, ctypes.POINTER(AdamTensor), c_i32,
+                                                           c_vp]),
     "kgat_edge_logits_gemm_work_floats": (c_i64, [c_i64, c_i32]),
     "kgat_edge_logits_gemm_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                  c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_f32, c_u64, c_vp, c_vp,

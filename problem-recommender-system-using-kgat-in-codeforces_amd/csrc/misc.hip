@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "adam.hpp"
 #include "common.hpp"
 
 namespace kgat {
@@ -159,51 +160,6 @@ extern "C" int kgat_version(void) { return 1; }
 
 namespace kgat {
 
-// A captured optimiser step's scalars on the device (a HIP graph replays the same kernel arguments every
-// step): t = *t + add (the captured update's first Adam launch applies *t + 1 and hands the number on
-// through out; the second reads it there and writes it back to t), step size and sqrt(1 - beta2^t) =
-// sz[t] / bc[t] -- tables the host filled with FusedAdam's own expressions, so the same floats the
-// by-value launches get.  t == nullptr: the by-value arguments.
-struct StepSched {
-  const int32_t* t;
-  const float* sz;
-  const float* bc;
-  int32_t add = 0;         // the step applied is *t + add
-  int32_t* out = nullptr;  // nullable: block 0 / thread 0 writes that step number there (the next launch's t)
-};
-
-// The step a scheduled launch applies; its number handed on to the next launch of the captured update.
-__device__ __forceinline__ int32_t sched_step(const StepSched& s) {
-  const int32_t t = *s.t + s.add;
-  if (s.out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *s.out = t;
-  return t;
-}
-
-// Every tensor of one optimiser step in ONE launch: the tensor table travels in
-// the kernel arguments; block b works on chunk b of the concatenated float4
-// index space (tensor chosen by a scan of <= 16 chunk offsets).
-struct AdamTable {
-  kgat_adam_tensor t[KGAT_ADAM_MAX_TENSORS];
-  int64_t chunk_off[KGAT_ADAM_MAX_TENSORS + 1];  // first chunk of tensor i
-  int32_t count;
-};
-
-constexpr int kAdamChunk = 256 * 4 * 4;  // floats per block-iteration: 256 threads x float4 x 4
-
-template <int V>
-__device__ __forceinline__ float4 ld4(const float* p) {
-  if constexpr (V == 2) {
-    const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(p));
-    return make_float4(v[0], v[1], v[2], v[3]);
-  }
-  return *reinterpret_cast<const float4*>(p);
-}
-template <int V>
-__device__ __forceinline__ void st4(float* p, float4 v) {
-  if constexpr (V == 2) __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(p));
-  else *reinterpret_cast<float4*>(p) = v;
-}
-
 // V = 0: per float4 load -> update -> store; V >= 1: a chunk's 16 float4 loads issued first
 // (all four arrays, four float4 per lane), then the updates, then the stores; V = 2 with
 // non-temporal loads/stores (every byte is touched once per step).
@@ -214,70 +170,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamTable T, float b1, 
   // entries of the host-computed schedule, t read on the device (and handed on before a skip returns)
   const int32_t ts = sched.t != nullptr ? sched_step(sched) : 0;
   if (skip != nullptr && *skip != 0) return;  // the step's ids were out of range: no parameter moves
-  const float w1 = 1.f - b1, w2 = 1.f - b2;
-  const int64_t total = T.chunk_off[T.count];
-  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
-    int i = 0;
-    while (i + 1 < T.count && T.chunk_off[i + 1] <= c) ++i;
-    const kgat_adam_tensor& a = T.t[i];
-    const int64_t base = (c - T.chunk_off[i]) * kAdamChunk;
-    const float step_size = sched.t != nullptr ? sched.sz[ts] : a.step_size;
-    const float bc2s = sched.t != nullptr ? sched.bc[ts] : a.bc2_sqrt;
-    if (V >= 1 && base + kAdamChunk <= a.n) {
-      float4 pp[4], mm[4], vv[4], gg[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
-        pp[u] = ld4<V>(a.p + e);
-        mm[u] = ld4<V>(a.m + e);
-        vv[u] = ld4<V>(a.v + e);
-        gg[u] = ld4<V>(a.g + e);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float* P = &pp[u].x;
-        float* Mv = &mm[u].x;
-        float* Vv = &vv[u].x;
-        const float* G = &gg[u].x;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], Vv[k], w1, b2, w2, step_size, bc2s, eps);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
-        st4<V>(a.p + e, pp[u]);
-        st4<V>(a.m + e, mm[u]);
-        st4<V>(a.v + e, vv[u]);
-      }
-      continue;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t e = base + (static_cast<int64_t>(u) * 256 + threadIdx.x) * 4;
-      if (e + 4 <= a.n) {
-        float4 pp = *reinterpret_cast<float4*>(a.p + e), mm = *reinterpret_cast<float4*>(a.m + e);
-        float4 vv = *reinterpret_cast<float4*>(a.v + e);
-        const float4 gg = *reinterpret_cast<const float4*>(a.g + e);
-        float* P = &pp.x;
-        float* Mv = &mm.x;
-        float* V_ = &vv.x;
-        const float* G = &gg.x;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) adam_elem(P[k], G[k], Mv[k], V_[k], w1, b2, w2, step_size, bc2s, eps);
-        *reinterpret_cast<float4*>(a.p + e) = pp;
-        *reinterpret_cast<float4*>(a.m + e) = mm;
-        *reinterpret_cast<float4*>(a.v + e) = vv;
-      } else {
-        for (int64_t k = e; k < a.n && k < e + 4; ++k) {
-          float pp = a.p[k], mm = a.m[k], vv = a.v[k];
-          adam_elem(pp, a.g[k], mm, vv, w1, b2, w2, step_size, bc2s, eps);
-          a.p[k] = pp;
-          a.m[k] = mm;
-          a.v[k] = vv;
-        }
-      }
-    }
-  }
+  adam_multi_chunks<V>(T, b1, b2, eps, sched, ts, blockIdx.x, gridDim.x);
 }
 
 // The table's Adam step whose gradient is nonzero on a few rows only (the KG step: TransR reads
@@ -346,21 +239,10 @@ extern "C" int kgat_adam_multi_sched_f32(const kgat_adam_tensor* tensors, int32_
   if (t_dev != nullptr && (!sched_sz || !sched_bc)) return KGAT_ERR_INVALID;
   const kgat::StepSched sched{t_dev, sched_sz, sched_bc, t_add, t_out};
   kgat::AdamTable T{};
-  T.count = count;
-  int64_t off = 0;
-  for (int i = 0; i < count; ++i) {
-    const kgat_adam_tensor& a = tensors[i];
-    if (!a.p || !a.g || !a.m || !a.v || a.n < 0) return KGAT_ERR_INVALID;
-    if ((reinterpret_cast<uintptr_t>(a.p) | reinterpret_cast<uintptr_t>(a.g) | reinterpret_cast<uintptr_t>(a.m) |
-         reinterpret_cast<uintptr_t>(a.v)) & 15)
-      return KGAT_ERR_INVALID;
-    T.t[i] = a;
-    T.chunk_off[i] = off;
-    off += (a.n + kgat::kAdamChunk - 1) / kgat::kAdamChunk;
-  }
-  T.chunk_off[count] = off;
+  if (int e = kgat::adam_table(tensors, count, T)) return e;
+  const int64_t off = T.chunk_off[count];
   if (off == 0) return KGAT_OK;
-  const int grid = static_cast<int>(off < kgat::kCUs * 8 ? off : kgat::kCUs * 8);
+  const int grid = kgat::adam_grid(T);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // the <2> access pattern: C2 table (64M parameters) 314 us vs 346 us for <0> / <1> on the same box
   hipLaunchKernelGGL(kgat::adam_multi_kernel<2>, dim3(grid), dim3(256), 0, st, T, beta1, beta2, eps, skip, sched);

@@ -25,6 +25,7 @@
 // from a compact Yc through the same map.  Skipped edges contribute exactly
 // 0, so the result equals the dense product with zero rows.
 #include "common.hpp"
+#include "adam.hpp"
 #include "spmm_core.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -219,13 +220,11 @@ __global__ __launch_bounds__(256) void spmm_main_kernel(kgat_csr A, SpmmIo io, i
 // partials are added in group order through LDS -- a fixed order, so the
 // result is deterministic, and a 196-segment hub row takes 13 steps, not 196.
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) {
+__device__ __forceinline__ void fixup_row(const kgat_csr& A, const SpmmIo& io, int lr) {
   constexpr int L = D / 4;
   constexpr int G = 256 / L;
   __shared__ float4 red[G][L];
-  const int lr = blockIdx.x;
   const int g = threadIdx.x / L, gl = threadIdx.x % L;
-  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
   const int row = A.long_rows[lr];
   if ((MODE == kMaskedRows || MODE == kRows) && !bit_of(io.out_bits, row)) return;  // block-uniform
   const float4* P = reinterpret_cast<const float4*>(io.part);
@@ -242,6 +241,26 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) 
 }
 
 template <int D, int MODE>
+__global__ __launch_bounds__(256) void spmm_fixup_kernel(kgat_csr A, SpmmIo io) {
+  if ((MODE == kMaskedAdam) && io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  fixup_row<D, MODE>(A, io, blockIdx.x);
+}
+
+// The fused table update's fix-up launch carrying the step's other tensors (the aggregator weights): blocks
+// [0, n_long) sum the long rows' partials into their Adam step, the rest run adam_multi_kernel<2>'s
+// chunks of T (independent parameters; the same arithmetic and skip flag) -- one launch fewer per step.
+template <int D>
+__global__ __launch_bounds__(256) void spmm_fixup_adam_kernel(kgat_csr A, SpmmIo io, AdamTable T) {
+  if (io.adam.skip != nullptr && *io.adam.skip != 0) return;
+  if (static_cast<int64_t>(blockIdx.x) < A.n_long) {
+    fixup_row<D, kMaskedAdam>(A, io, blockIdx.x);
+    return;
+  }
+  adam_multi_chunks<2>(T, io.adam.b1, io.adam.b2, io.adam.eps, StepSched{nullptr, nullptr, nullptr},
+                       0, blockIdx.x - A.n_long, gridDim.x - A.n_long);
+}
+
+template <int D, int MODE>
 static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   using S = SpmmShape<D>;
   const int seg_blocks = (A.n_seg + 3) / 4;
@@ -253,6 +272,22 @@ static int launch_mode(const kgat_csr& A, const SpmmIo& io, hipStream_t st) {
   KGAT_LAUNCH_CHECK();
   if (A.n_long > 0) {
     hipLaunchKernelGGL((spmm_fixup_kernel<D, MODE>), dim3(A.n_long), dim3(256), 0, st, A, io);
+    KGAT_LAUNCH_CHECK();
+  }
+  return KGAT_OK;
+}
+
+template <int D>
+static int launch_adam_multi(const kgat_csr& A, const SpmmIo& io, const AdamTable& T, hipStream_t st) {
+  using S = SpmmShape<D>;
+  const int seg_blocks = (A.n_seg + 3) / 4;
+  const int64_t grid = seg_blocks + (A.n_rows + S::kRowsPerBlock - 1) / S::kRowsPerBlock;
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL((spmm_main_kernel<D, kMaskedAdam>), dim3(grid), dim3(256), 0, st, A, io, seg_blocks);
+  KGAT_LAUNCH_CHECK();
+  const int64_t fix = static_cast<int64_t>(A.n_long) + adam_grid(T);
+  if (fix > 0) {
+    hipLaunchKernelGGL((spmm_fixup_adam_kernel<D>), dim3(fix), dim3(256), 0, st, A, io, T);
     KGAT_LAUNCH_CHECK();
   }
   return KGAT_OK;
@@ -638,6 +673,42 @@ extern "C" int kgat_spmm_csr_masked_adam_ex_f32(const kgat_csr* A, const int32_t
   return kgat_spmm_csr_masked_adam_block_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, 0, src_rank, p, m, v, ldp, d,
                                              step_size, beta1, beta2, bc2_sqrt, eps, skip, workspace,
                                              workspace_floats, stream);
+}
+
+extern "C" int kgat_spmm_csr_masked_adam_multi_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,
+                                                   int64_t ldxc, const float* Yc_init, int64_t ldyc,
+                                                   const uint64_t* src_rank, float* p, float* m, float* v, int64_t ldp,
+                                                   int32_t d, float step_size, float beta1, float beta2,
+                                                   float bc2_sqrt, float eps, const int32_t* skip, float* workspace,
+                                                   int64_t workspace_floats, const kgat_adam_tensor* extra,
+                                                   int32_t n_extra, void* stream) {
+  using namespace kgat;
+  if (n_extra == 0)
+    return kgat_spmm_csr_masked_adam_ex_f32(A, src_map, Xc, ldxc, Yc_init, ldyc, src_rank, p, m, v, ldp, d,
+                                            step_size, beta1, beta2, bc2_sqrt, eps, skip, workspace,
+                                            workspace_floats, stream);
+  AdamTable T{};
+  if (int e = adam_table(extra, n_extra, T)) return e;
+  if (!A || !src_map || !Xc || !p || !m || !v || A->n_rows <= 0 || ldxc < d || ldp < d || (ldxc & 3) || (ldp & 3))
+    return KGAT_ERR_INVALID;
+  if (misaligned(Xc) || misaligned(p) || misaligned(m) || misaligned(v) ||
+      (Yc_init && (misaligned(Yc_init) || ldyc < d || (ldyc & 3))))
+    return KGAT_ERR_INVALID;
+  if (src_rank != nullptr && (reinterpret_cast<uintptr_t>(src_rank) & 7)) return KGAT_ERR_INVALID;
+  if (A->n_seg > 0 && (workspace == nullptr || workspace_floats < static_cast<int64_t>(A->n_seg) * d))
+    return KGAT_ERR_WORKSPACE;
+  SpmmIo io{Xc, ldxc, nullptr, 0, workspace, src_map, Yc_init, ldyc, nullptr, 0, nullptr, src_rank,
+            nullptr, nullptr, nullptr, nullptr};
+  io.adam = SpmmAdam{p, m, v, ldp, step_size, beta1, beta2, bc2_sqrt, eps, skip};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (d) {
+    case 16: return launch_adam_multi<16>(*A, io, T, st);
+    case 32: return launch_adam_multi<32>(*A, io, T, st);
+    case 64: return launch_adam_multi<64>(*A, io, T, st);
+    case 128: return launch_adam_multi<128>(*A, io, T, st);
+    case 256: return launch_adam_multi<256>(*A, io, T, st);
+    default: return KGAT_ERR_UNSUPPORTED_DIM;
+  }
 }
 
 extern "C" int kgat_spmm_csr_masked_adam_block_f32(const kgat_csr* A, const int32_t* src_map, const float* Xc,

@@ -319,10 +319,12 @@ def _skip_ptr(skip: torch.Tensor | None):
 def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor, Yc_init: torch.Tensor | None,
                      src_rank: torch.Tensor | None, p: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
                      step_size: float, beta1: float, beta2: float, bc2_sqrt: float, eps: float,
-                     skip: torch.Tensor | None = None) -> None:
+                     skip: torch.Tensor | None = None, extra=None) -> None:
     """The table's Adam step fused into its gradient's last product: row r of the masked A^T product
     (spmm_masked(..., transpose=True)) is the gradient of table row r and goes straight into r's Adam
-    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi)."""
+    update of p / m / v (adam_multi's arithmetic: the same bits as spmm_masked + adam_multi).  ``extra``:
+    <= KGAT_ADAM_MAX_TENSORS adam_multi items [(p, g, m, v, step_size, bc2_sqrt), ...] stepped in the
+    launch pair's fix-up launch (kgat_spmm_csr_masked_adam_multi_f32: the same bits as adam_multi)."""
     _req(src_map, "src_map", dtype=torch.int32, dim=1)
     _req(Xc, "Xc", dim=2)
     n, d = graph.n_nodes, Xc.shape[1]
@@ -346,9 +348,18 @@ def spmm_masked_adam(graph: DeviceGraph, src_map: torch.Tensor, Xc: torch.Tensor
     yc = (Yc_init.data_ptr() if Yc_init is not None else None, _ld(Yc_init) if Yc_init is not None else 0)
     rank = _rank_ptr(src_rank, src_map)
 
-    _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(), _ld(Xc),
-              yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1, beta2, bc2_sqrt,
-              eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
+    if extra:
+        if len(extra) > _lib.KGAT_ADAM_MAX_TENSORS:
+            raise ValueError("spmm_masked_adam: at most KGAT_ADAM_MAX_TENSORS extra tensors")
+        arr = _adam_array(extra)
+        _lib.call("kgat_spmm_csr_masked_adam_multi_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
+                  _ld(Xc), yc[0], yc[1], rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
+                  beta2, bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), arr, len(extra),
+                  stream_ptr(Xc.device))
+    else:
+        _lib.call("kgat_spmm_csr_masked_adam_block_f32", ctypes.byref(desc), src_map.data_ptr(), Xc.data_ptr(),
+                  _ld(Xc), yc[0], yc[1], 0, rank, p.data_ptr(), m.data_ptr(), v.data_ptr(), d, d, step_size, beta1,
+                  beta2, bc2_sqrt, eps, _skip_ptr(skip), ws.data_ptr(), ws.numel(), stream_ptr(Xc.device))
     if ev is not None:
         e1.record()
         ev.append((e0, e1, d, True, "fused_adam"))
@@ -1330,23 +1341,31 @@ def adam(p, g, m, v, step_size: float, beta1: float, beta2: float, bc2_sqrt: flo
               beta2, bc2_sqrt, eps, stream_ptr(p.device))
 
 
+ADAM_MAX_TENSORS = _lib.KGAT_ADAM_MAX_TENSORS  # tensors per adam_multi launch / per fused update's extra
+
+
 def adam_multi(items, beta1: float, beta2: float, eps: float, skip: torch.Tensor | None = None) -> None:
     """One launch per <= 16 tensors: items = [(p, g, m, v, step_size, bc2_sqrt), ...]; ``skip``: the
     optimiser skip flag (nothing moves when it is set)."""
     tok = _ev_begin("adam_multi")
     for i in range(0, len(items), _lib.KGAT_ADAM_MAX_TENSORS):
         chunk = items[i:i + _lib.KGAT_ADAM_MAX_TENSORS]
-        arr = (_lib.AdamTensor * len(chunk))()
-        for a, (p, g, m, v, step_size, bc2s) in zip(arr, chunk):
-            for t, nm in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
-                _req(t, nm)
-                if not t.is_contiguous():
-                    raise ValueError(f"{nm} must be contiguous")
-            a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
-            a.n, a.step_size, a.bc2_sqrt = p.numel(), step_size, bc2s
-        _lib.call("kgat_adam_multi_ex_f32", arr, len(chunk), beta1, beta2, eps, _skip_ptr(skip),
+        _lib.call("kgat_adam_multi_ex_f32", _adam_array(chunk), len(chunk), beta1, beta2, eps, _skip_ptr(skip),
                   stream_ptr(chunk[0][0].device))
     _ev_end(tok)
+
+
+def _adam_array(items):
+    """The kgat_adam_tensor array of adam_multi items (contiguous float32 tensors)."""
+    arr = (_lib.AdamTensor * len(items))()
+    for a, (p, g, m, v, step_size, bc2s) in zip(arr, items):
+        for t, nm in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+            _req(t, nm)
+            if not t.is_contiguous():
+                raise ValueError(f"{nm} must be contiguous")
+        a.p, a.g, a.m, a.v = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        a.n, a.step_size, a.bc2_sqrt = p.numel(), step_size, bc2s
+    return arr
 
 
 def fill(t: torch.Tensor, value: float) -> torch.Tensor:

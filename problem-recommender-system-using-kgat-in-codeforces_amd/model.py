@@ -322,8 +322,10 @@ class _TableUpdate:
         self.pending = None
         p = self.param.data
 
-        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None):
-            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip)
+        def run(m, v, step_size, bc2s, b1, b2, eps, skip=None, extra=None):
+            kernels.spmm_masked_adam(graph, src_map, Xc, Yc, rank, p, m, v, step_size, b1, b2, bc2s, eps, skip,
+                                     extra=extra)
+        run.takes_extra = True  # FusedAdam.step may hand it the step's other tensors (their Adam in its fix-up)
         return run
 
 

@@ -75,12 +75,19 @@ class FusedAdam:
             for key, pv, gv in views:
                 st, step_size, bc2s = self._advance(key, pv)
                 items.append((pv, gv, st["exp_avg"], st["exp_avg_sq"], step_size, bc2s))
-        for launch, st, step_size, bc2s in runs:
-            launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
-        if items:
-            # after the fused launch(es), on the same stream: run beside them on a side stream (round 5) the
-            # small tensors' Adam waited ~120 us for CU slots and its join cost the C2 step 15-17 us
-            # (profiles/r06_small_adam_ab.md: full 1.858 -> 1.838 ms, frontier 0.837 -> 0.820 ms)
+        # the other tensors' Adam rides in the last fused launch pair's fix-up launch when it can take them
+        # (_TableUpdate: kgat_spmm_csr_masked_adam_multi_f32, one launch fewer per CF step); otherwise it follows
+        # the fused launch(es) on the same stream -- beside them on a side stream (round 5) it waited ~120 us
+        # for CU slots and its join cost the C2 step 15-17 us (profiles/r06_small_adam_ab.md)
+        carry = bool(items) and bool(runs) and getattr(runs[-1][0], "takes_extra", False) \
+            and len(items) <= kernels.ADAM_MAX_TENSORS
+        for k, (launch, st, step_size, bc2s) in enumerate(runs):
+            if carry and k == len(runs) - 1:
+                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip,
+                       extra=items)
+            else:
+                launch(st["exp_avg"], st["exp_avg_sq"], step_size, bc2s, self.beta1, self.beta2, self.eps, skip)
+        if items and not carry:
             kernels.adam_multi(items, self.beta1, self.beta2, self.eps, skip)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
