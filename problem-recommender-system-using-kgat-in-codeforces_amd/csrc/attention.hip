@@ -9,7 +9,7 @@
 //   o  = LayerNorm(W_o v + b_o)       (eps 1e-5, affine)
 //   logit_e = sum_j tanh(o_j) / (log1p(deg_h) + log1p(deg_t))   (per-relation degrees)
 // Edges are processed in 16-edge tiles of ONE relation (a relation-sorted
-// permutation built once per graph), one tile per wave: the three d x d
+// permutation built once per graph), one tile per wave (two from d = 64): the three d x d
 // contractions are fp32 MFMA (v_mfma_f32_16x16x4_f32) chains computed
 // transposed, so each product's accumulators are the next one's operand (no
 // relayout); dropout, LayerNorm, tanh and the sum are fused epilogues.
@@ -85,7 +85,7 @@ __device__ __forceinline__ float tanh_fast(float x) {
 //   t'^T = W_r^T e_t^T : A[m][kk] = W_r[q*KQ + t][mb*16 + c], B = e_t[c][q*KQ + t] (load_a's layout)
 //   v^T  = W_v t'^T     : A = W_v[mb*16 + c][kb*16 + q*4 + i], B = t'^T from the accumulators
 //   o^T  = W_o v^T
-template <int D, bool WLDS, int NW>
+template <int D, bool WLDS, int NW, int P>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 4 : 1))) void edge_score_t_kernel(EdgeScoreArgs a) {
   constexpr int KQ = D / 4, NB = D / 16, WLD = D + 4;
   constexpr int kDepth = D / 8;  // 8 heads (multi_head_attention.py:6)
@@ -114,106 +114,157 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(D <= 64
   }
   __syncthreads();
   const float scale = a.p > 0.f ? 1.f / (1.f - a.p) : 1.f;
-  for (int tl = blockIdx.x * NW + wave; tl < a.n_tiles; tl += gridDim.x * NW) {
-    const int beg = a.tile_beg[tl], cnt = a.tile_beg[tl + 1] - beg;
-    const int64_t r = a.tile_rel[tl];
-    const int ec = c < cnt ? a.rel_perm[beg + c] : -1;  // this lane's edge
-    float x[KQ];
-    load_a<D>(a.emb, a.ld_emb, ec >= 0 ? static_cast<int64_t>(a.tails[ec]) : -1, q, x);
-    uint64_t keep_lo = ~0ull, keep_hi = ~0ull;  // train-mode dropout bits, pair = edge * 8 + head
-    if (a.p > 0.f) {
-      const int er = lane >> 3, head = lane & 7;
-      const int64_t e0 = er < cnt ? a.rel_perm[beg + er] : 0;
-      const int64_t e1 = er + 8 < cnt ? a.rel_perm[beg + er + 8] : 0;
-      keep_lo = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e0) * 8 + head, a.p));
-      keep_hi = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e1) * 8 + head, a.p));
+  // P consecutive tiles per wave (relation-sorted, so nearly always one relation): every weight value loaded
+  // feeds P MFMA chains, one per tile; each tile's chains are the P = 1 chains, so the same bits.
+  const int n_groups = (a.n_tiles + P - 1) / P;
+  for (int tg = blockIdx.x * NW + wave; tg < n_groups; tg += gridDim.x * NW) {
+    int ec[P];
+    int64_t r[P];
+    uint64_t keep[P];
+    float x[P][KQ];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const int tl = tg * P + j;
+      const bool live = tl < a.n_tiles;  // wave-uniform
+      const int beg = live ? a.tile_beg[tl] : 0, cnt = live ? a.tile_beg[tl + 1] - beg : 0;
+      r[j] = live ? a.tile_rel[tl] : r[0];
+      ec[j] = c < cnt ? a.rel_perm[beg + c] : -1;  // this lane's edge of tile j
+      load_a<D>(a.emb, a.ld_emb, ec[j] >= 0 ? static_cast<int64_t>(a.tails[ec[j]]) : -1, q, x[j]);
+      uint64_t keep_lo = ~0ull, keep_hi = ~0ull;  // train-mode dropout bits, pair = edge * 8 + head
+      if (a.p > 0.f) {
+        const int er = lane >> 3, head = lane & 7;
+        const int64_t e0 = er < cnt ? a.rel_perm[beg + er] : 0;
+        const int64_t e1 = er + 8 < cnt ? a.rel_perm[beg + er + 8] : 0;
+        keep_lo = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e0) * 8 + head, a.p));
+        keep_hi = __ballot(dropout_keep(a.seed, static_cast<uint64_t>(e1) * 8 + head, a.p));
+      }
+      keep[j] = (c < 8 ? keep_lo : keep_hi) >> ((c & 7) * 8);  // this edge's 8 head bits
     }
-    const uint64_t keep = (c < 8 ? keep_lo : keep_hi) >> ((c & 7) * 8);  // this edge's 8 head bits
-    floatx4 acc[NB];
-    const float* Wr = a.trans + r * D * D;
+    floatx4 acc[P][NB];
+    bool one_rel = true;
 #pragma unroll
-    for (int mb = 0; mb < NB; ++mb) {
-      // (product 1: the column blocks' chains interleave)
-      floatx4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 1; j < P; ++j) one_rel = one_rel && r[j] == r[0];
+    // t'^T = W_r^T e_t^T.  A relation boundary inside the group (rare: at most one group per relation)
+    // takes one pass per tile, each keeping the chains of the tiles of its relation.
+    const int npass = one_rel ? 1 : P;  // wave-uniform
+#pragma unroll 1
+    for (int ps = 0; ps < npass; ++ps) {
+      const int64_t rp = r[ps];
+      const float* Wr = a.trans + rp * D * D;
 #pragma unroll
-      for (int t = 0; t < KQ; ++t) s = mfma16x4(Wr[(q * KQ + t) * D + mb * 16 + c], x[t], s);
-      acc[mb] = s;
+      for (int mb = 0; mb < NB; ++mb) {
+        __builtin_amdgcn_sched_barrier(0);  // one column block's W_r loads in flight at a time
+        floatx4 s[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) s[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < KQ; ++t) {
+          const float w = Wr[(q * KQ + t) * D + mb * 16 + c];
+#pragma unroll
+          for (int j = 0; j < P; ++j) s[j] = mfma16x4(w, x[j][t], s[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+          if (ps == 0 || r[j] == rp) acc[j][mb] = s[j];
+      }
     }
     // v^T = W_v t'^T + b_v, dropped per (edge, head)
-    floatx4 acc2[NB];
+    floatx4 acc2[P][NB];
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) {
       if (mb % 2 == 0) __builtin_amdgcn_sched_barrier(0);  // two column blocks' chains interleave
-      floatx4 s = {0.f, 0.f, 0.f, 0.f};
+      floatx4 s[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j) s[j] = floatx4{0.f, 0.f, 0.f, 0.f};
       const float* w = wv + (mb * 16 + c) * wld + q * 4;
 #pragma unroll
       for (int kb = 0; kb < NB; ++kb) {
         const float4 wk = *reinterpret_cast<const float4*>(w + kb * 16);
-        s = mfma16x4(wk.x, acc[kb][0], s);
-        s = mfma16x4(wk.y, acc[kb][1], s);
-        s = mfma16x4(wk.z, acc[kb][2], s);
-        s = mfma16x4(wk.w, acc[kb][3], s);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          s[j] = mfma16x4(wk.x, acc[j][kb][0], s[j]);
+          s[j] = mfma16x4(wk.y, acc[j][kb][1], s[j]);
+          s[j] = mfma16x4(wk.z, acc[j][kb][2], s[j]);
+          s[j] = mfma16x4(wk.w, acc[j][kb][3], s[j]);
+        }
       }
       const float4 b = *reinterpret_cast<const float4*>(cst + mb * 16 + q * 4);
       const float bb[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = s[i] + bb[i];
-        const int head = (mb * 16 + q * 4 + i) / kDepth;
-        s[i] = (keep >> head) & 1 ? (a.p > 0.f ? v * scale : v) : 0.f;
+      for (int j = 0; j < P; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = s[j][i] + bb[i];
+          const int head = (mb * 16 + q * 4 + i) / kDepth;
+          s[j][i] = (keep[j] >> head) & 1 ? (a.p > 0.f ? v * scale : v) : 0.f;
+        }
+        acc2[j][mb] = s[j];
       }
-      acc2[mb] = s;
     }
     // o^T = W_o v^T + b_o, then LayerNorm over the features and the tanh sum
-    float sum = 0.f;
+    float sum[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) sum[j] = 0.f;
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) {
       if (mb % 2 == 0) __builtin_amdgcn_sched_barrier(0);  // two column blocks' chains interleave
-      floatx4 s = {0.f, 0.f, 0.f, 0.f};
+      floatx4 s[P];
+#pragma unroll
+      for (int j = 0; j < P; ++j) s[j] = floatx4{0.f, 0.f, 0.f, 0.f};
       const float* w = wo + (mb * 16 + c) * wld + q * 4;
 #pragma unroll
       for (int kb = 0; kb < NB; ++kb) {
         const float4 wk = *reinterpret_cast<const float4*>(w + kb * 16);
-        s = mfma16x4(wk.x, acc2[kb][0], s);
-        s = mfma16x4(wk.y, acc2[kb][1], s);
-        s = mfma16x4(wk.z, acc2[kb][2], s);
-        s = mfma16x4(wk.w, acc2[kb][3], s);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          s[j] = mfma16x4(wk.x, acc2[j][kb][0], s[j]);
+          s[j] = mfma16x4(wk.y, acc2[j][kb][1], s[j]);
+          s[j] = mfma16x4(wk.z, acc2[j][kb][2], s[j]);
+          s[j] = mfma16x4(wk.w, acc2[j][kb][3], s[j]);
+        }
       }
       const float4 b = *reinterpret_cast<const float4*>(cst + D + mb * 16 + q * 4);
-      s[0] += b.x;
-      s[1] += b.y;
-      s[2] += b.z;
-      s[3] += b.w;
-      sum += (s[0] + s[1]) + (s[2] + s[3]);
-      acc[mb] = s;
-    }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
-    const float mean = sum / static_cast<float>(D);
-    float v2 = 0.f;
 #pragma unroll
-    for (int mb = 0; mb < NB; ++mb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float dl = acc[mb][i] - mean;
-        v2 = fmaf(dl, dl, v2);
+      for (int j = 0; j < P; ++j) {
+        s[j][0] += b.x;
+        s[j][1] += b.y;
+        s[j][2] += b.z;
+        s[j][3] += b.w;
+        sum[j] += (s[j][0] + s[j][1]) + (s[j][2] + s[j][3]);
+        acc[j][mb] = s[j];
       }
-    v2 += __shfl_xor(v2, 16);
-    v2 += __shfl_xor(v2, 32);
-    const float rstd = 1.f / sqrtf(v2 / static_cast<float>(D) + kLnEps);
-    float ts = 0.f;
-#pragma unroll
-    for (int mb = 0; mb < NB; ++mb) {
-      const float4 lw = *reinterpret_cast<const float4*>(cst + 2 * D + mb * 16 + q * 4);
-      const float4 lb = *reinterpret_cast<const float4*>(cst + 3 * D + mb * 16 + q * 4);
-      ts += tanh_fast((acc[mb][0] - mean) * rstd * lw.x + lb.x);
-      ts += tanh_fast((acc[mb][1] - mean) * rstd * lw.y + lb.y);
-      ts += tanh_fast((acc[mb][2] - mean) * rstd * lw.z + lb.z);
-      ts += tanh_fast((acc[mb][3] - mean) * rstd * lw.w + lb.w);
     }
-    ts += __shfl_xor(ts, 16);
-    ts += __shfl_xor(ts, 32);
-    if (q == 0 && ec >= 0) a.logits[a.out_pos ? a.out_pos[ec] : ec] = ts * a.edge_weight[ec];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      float sm = sum[j];
+      sm += __shfl_xor(sm, 16);
+      sm += __shfl_xor(sm, 32);
+      const float mean = sm / static_cast<float>(D);
+      float v2 = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < NB; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float dl = acc[j][mb][i] - mean;
+          v2 = fmaf(dl, dl, v2);
+        }
+      v2 += __shfl_xor(v2, 16);
+      v2 += __shfl_xor(v2, 32);
+      const float rstd = 1.f / sqrtf(v2 / static_cast<float>(D) + kLnEps);
+      float ts = 0.f;
+#pragma unroll
+      for (int mb = 0; mb < NB; ++mb) {
+        const float4 lw = *reinterpret_cast<const float4*>(cst + 2 * D + mb * 16 + q * 4);
+        const float4 lb = *reinterpret_cast<const float4*>(cst + 3 * D + mb * 16 + q * 4);
+        ts += tanh_fast((acc[j][mb][0] - mean) * rstd * lw.x + lb.x);
+        ts += tanh_fast((acc[j][mb][1] - mean) * rstd * lw.y + lb.y);
+        ts += tanh_fast((acc[j][mb][2] - mean) * rstd * lw.z + lb.z);
+        ts += tanh_fast((acc[j][mb][3] - mean) * rstd * lw.w + lb.w);
+      }
+      ts += __shfl_xor(ts, 16);
+      ts += __shfl_xor(ts, 32);
+      if (q == 0 && ec[j] >= 0) a.logits[a.out_pos ? a.out_pos[ec[j]] : ec[j]] = ts * a.edge_weight[ec[j]];
+    }
   }
 }
 
@@ -518,9 +569,13 @@ __global__ __launch_bounds__(256) void row_softmax_long_kernel(const int64_t* __
 template <int D>
 static int launch_scores(const EdgeScoreArgs& a, hipStream_t st) {
   constexpr bool wlds = D <= 64;
-  const int grid = blocks_for(a.n_tiles, 4, kCUs * 8);
+  // two tiles per wave from d = 64 (every weight load feeds two chains; tools/score_ab.py on the C2 graph, bit
+  // for bit: d = 128 25.5 -> 21.0 ms, 0.49 -> 0.60 of the fp32 MFMA peak; d = 64 5.56 -> 5.40 ms; four tiles
+  // at d = 64 5.45 ms, 2 waves / SIMD)
+  constexpr int P = D >= 64 ? 2 : 1;
+  const int grid = blocks_for((a.n_tiles + P - 1) / P, 4, kCUs * 8);
   // (4 waves per block: 8-wave blocks at 6 waves / SIMD measured 6.14 vs 6.05 ms at C2 -- not occupancy-bound)
-  hipLaunchKernelGGL((edge_score_t_kernel<D, wlds, 4>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((edge_score_t_kernel<D, wlds, 4, P>), dim3(grid), dim3(256), 0, st, a);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }

@@ -1287,10 +1287,11 @@ def test_adam_multi_matches_single_bit_exact(pkg):
             assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("dim", [64, 256])
+@pytest.mark.parametrize("dim", [64, 128, 256])
 def test_attention_refresh_synthetic_vs_oracle(pkg, dim):
-    """UPDATE_ATTENTION on a synthetic CKG vs the oracle: d=64 runs the fused MFMA scorer, d=256 (C5) the
-    rocBLAS GEMM scorer (csrc/attention_gemm.hip); several chunks and relation runs per chunk."""
+    """UPDATE_ATTENTION on a synthetic CKG vs the oracle: d=64 / 128 run the fused MFMA scorer (tiles paired
+    per wave; relation boundaries inside a pair), d=256 (C5) the GEMM scorer (csrc/attention_gemm.hip);
+    several chunks and relation runs per chunk."""
     graph_mod, kernels = _mods(pkg)
     U, E, inter, trip = graph_mod.synthetic_ckg(3000, 24000, seed=21)
     lay = graph_mod.build_layout(U, E, inter, trip)
