@@ -294,6 +294,19 @@ int kgat_biinter_fwd_tiles_f32(const float *X, int64_t ldx, const float *S, int6
                                int64_t n_rows, const uint32_t *row_bits, int32_t d_in, int32_t d_out,
                                float dropout_p, uint64_t seed, float *norm_out, uint64_t *mask_out, void *stream);
 
+/* kgat_biinter_fwd_f32 on the 4-row quads (rows 4k .. 4k+3) holding a listed
+ * node: rows[0 .. *count) (int32, device count, read as at most cap; -1 =
+ * padding; cap = the list's capacity, which also bounds the grid), e.g. the ascending row list of a
+ * hop set (kgat_frontier_hop) or the batch rows (kgat_cf_begin_ex).  H,
+ * norm_out and the state words of those quads are written exactly as the
+ * whole-table call writes them (a quad listed twice is written twice with the
+ * same bits), the rest is untouched.  aggregator.py:57-65 on a row set. */
+int kgat_biinter_fwd_list_f32(const float *X, int64_t ldx, const float *S, int64_t lds, const float *W1,
+                              const float *b1, const float *W2, const float *b2, float *H, int64_t ldh,
+                              int64_t n_rows, const int32_t *rows, const int32_t *count, int64_t cap,
+                              int32_t d_in, int32_t d_out, float dropout_p, uint64_t seed, float *norm_out,
+                              uint64_t *mask_out, void *stream);
+
 /* kgat_biinter_fwd_f32 on rows [node0, node0 + n_rows) of a larger table: X, S,
  * H, norm_out, mask_out point at that block's first row (mask_out at word
  * (node0 / 16) * 64), the dropout draws use the global node ids.  node0 a

@@ -123,6 +123,8 @@ _SIGNATURES = {
                                               c_vp, c_i64, c_vp]),
     "kgat_biinter_fwd_tiles_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                                   c_vp, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
+    "kgat_biinter_fwd_list_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                                 c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_u64, c_vp, c_vp, c_vp]),
     "kgat_biinter_bwd_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                             c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32,

@@ -108,6 +108,10 @@ __device__ __forceinline__ void stage_weights(float* w1s, float* w2s, const floa
 // A-operand layout (lane (q, c): row c, k in [q*KQ, (q+1)*KQ)), W staged in
 // LDS.  Writes H, the row norms and the per-lane state word.  Shared by
 // the whole-table and the tile-list forward, so both produce the same bits.
+// The forward epilogue of one 16-row sub-tile st: u = X+S and m = X*S in the
+// A-operand layout (lane (q, c): row c, k in [q*KQ, (q+1)*KQ)), W staged in
+// LDS.  Writes H, the row norms and the per-lane state word.  Shared by
+// the whole-table and the tile-list forward, so both produce the same bits.
 template <int DIN, int DOUT, bool SB = true>
 __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const float (&m)[DIN / 4], int64_t st,
                                                int lane, const float* w1s, const float* w2s,
@@ -170,6 +174,72 @@ __device__ __forceinline__ void bi_fwd_subtile(const float (&u)[DIN / 4], const 
   }
 }
 
+// bi_fwd_subtile for a row list: the lane's rows are those of 4-row quad `quad` (rows 4*quad + i; -1 = none,
+// nothing written) and its state word is the one the whole-table launch writes for that quad (there: quad
+// st*4 + q), so row-list launches fill the same layout.  The whole-table launch keeps its own copy above (a
+// shared form with the quad index arithmetic measured ~10 us slower per C2 launch of it).
+template <int DIN, int DOUT>
+__device__ __forceinline__ void bi_fwd_quad(const float (&u)[DIN / 4], const float (&m)[DIN / 4], int64_t quad,
+                                            int lane, const float* w1s, const float* w2s,
+                                            const float (&bias1)[DOUT / 16], const float (&bias2)[DOUT / 16],
+                                            float p, float scale, uint32_t thr, uint64_t seed,
+                                            float* __restrict__ H, int64_t ldh, int64_t n,
+                                            float* __restrict__ norm_out, uint64_t* __restrict__ mask_out,
+                                            int64_t node0) {
+  using B = BiShape<DIN, DOUT>;
+  const int q = lane >> 4, c = lane & 15;
+  const int64_t qb = quad * 4;  // first row of this lane's quad
+  float g[B::NCB][4];
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NG = (B::NCB + 3) / 4;
+  uint64_t word[NG];  // saved state, word g: 3 bits per (cb in [4g, 4g+4), i) -- pre_sum > 0, pre_mul > 0, kept
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) word[gi] = 0;
+  uint64_t dh_[4][NG];
+  if (p > 0.f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) dh_[i][gi] = bi_drop_hash<DOUT>(seed, node0 + qb + i, gi, c);
+  }
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    floatx4 acc1, acc2;
+    __builtin_amdgcn_sched_barrier(0);  // keep one column block's W reads/accumulators live at a time
+    bi_block<DIN>(u, m, w1s, w2s, B::WLD, q, c, cb, acc1, acc2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pa = acc1[i] + bias1[cb], pb = acc2[i] + bias2[cb];
+      float v = lrelu(pa) + lrelu(pb);
+      bool keep = true;
+      if (p > 0.f) {
+        keep = bi_drop_keep(dh_[i][cb / 4], cb, thr);
+        v = keep ? v * scale : 0.f;
+      }
+      word[cb / 4] |= static_cast<uint64_t>((pa > 0.f) | ((pb > 0.f) << 1) | (keep << 2)) << (((cb & 3) * 4 + i) * 3);
+      g[cb][i] = v;
+      sq[i] = fmaf(v, v, sq[i]);
+    }
+  }
+  if (mask_out != nullptr && quad >= 0) {
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) mask_out[((quad >> 2) * NG + gi) * 64 + (quad & 3) * 16 + c] = word[gi];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float nrm = sqrtf(sum16(sq[i]));
+    const float inv = 1.f / fmaxf(nrm, kNormEps);
+    const int64_t row = qb + i;
+    if (quad >= 0 && row < n) {
+      float* h = H + row * ldh + c;
+#pragma unroll
+      for (int cb = 0; cb < B::NCB; ++cb) __builtin_nontemporal_store(g[cb][i] * inv, h + cb * 16);
+      // saved norm; negative = the clamp was active (F.normalize's eps)
+      if (norm_out != nullptr && c == 0) norm_out[row] = nrm >= kNormEps ? nrm : -kNormEps;
+    }
+  }
+}
+
 // Waves per block of the standalone forward: 4, or 8 where the two staged W
 // copies leave room for one block per CU only (128 -> 128: 135 KB of LDS), so
 // that one block still puts two waves on every SIMD.
@@ -178,19 +248,14 @@ struct BiFwdWaves {
   static constexpr int k = 2 * DOUT * (DIN + 4) * 4 > 80 * 1024 ? 8 : 4;
 };
 
-// TL: only the 16-row sub-tiles holding a member of the node set row_bits (a hop set's
-// bitmap: the tile's 16 bits are one half-word; other tiles are skipped by the wave that
-// tests them), the same per-tile arithmetic as the whole-table launch.
-template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4, bool TL = false>
+template <int DIN, int DOUT, bool PF, int MINW, int NWV = 4>
 __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float* __restrict__ X, int64_t ldx,
                                                           const float* __restrict__ S, int64_t lds,
                                                           const float* __restrict__ W1, const float* __restrict__ b1,
                                                           const float* __restrict__ W2, const float* __restrict__ b2,
                                                           float* __restrict__ H, int64_t ldh, int64_t n, float p,
                                                           uint64_t seed, float* __restrict__ norm_out,
-                                                          uint64_t* __restrict__ mask_out, int64_t node0,
-                                                          const uint32_t* __restrict__ row_bits = nullptr) {
-  static_assert(!(TL && PF), "the tile-list forward has no prefetch");
+                                                          uint64_t* __restrict__ mask_out, int64_t node0) {
   using B = BiShape<DIN, DOUT>;
   __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
   float* w1s = smem;
@@ -218,7 +283,6 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
   }
   for (; k < nsub; k += stride) {
     const int64_t st = k;
-    if (TL && ((row_bits[st >> 1] >> ((st & 1) * 16)) & 0xffffu) == 0) continue;  // wave-uniform
     if (!PF) {
       load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
       load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
@@ -235,6 +299,146 @@ __global__ __launch_bounds__(64 * NWV, MINW) void biinter_fwd_kernel(const float
     }
     bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
                               mask_out, node0);
+  }
+}
+
+// The row-set forward (kgat_biinter_fwd_tiles_f32): the 16-row sub-tiles holding a member of the node set
+// row_bits (a hop set's bitmap: a tile's 16 bits are one half-word), with the whole-table launch's per-tile
+// arithmetic (bi_fwd_subtile), so the same bits.  A block owns a chunk of 4 * NWV consecutive tiles: every
+// wave reads the chunk's half-words (one coalesced load) and ballots them, a chunk with no member returns
+// before staging W, and the waves take the member tiles round-robin -- no grid-stride walk of dependent
+// bitmap loads over the whole table.
+template <int DIN, int DOUT, int NWV>
+__global__ __launch_bounds__(64 * NWV, 2) void biinter_fwd_set_kernel(const float* __restrict__ X, int64_t ldx,
+                                                                      const float* __restrict__ S, int64_t lds,
+                                                                      const float* __restrict__ W1,
+                                                                      const float* __restrict__ b1,
+                                                                      const float* __restrict__ W2,
+                                                                      const float* __restrict__ b2,
+                                                                      float* __restrict__ H, int64_t ldh, int64_t n,
+                                                                      float p, uint64_t seed,
+                                                                      float* __restrict__ norm_out,
+                                                                      uint64_t* __restrict__ mask_out,
+                                                                      const uint32_t* __restrict__ row_bits) {
+  using B = BiShape<DIN, DOUT>;
+  constexpr int kTiles = 4 * NWV;  // <= 64: one ballot
+  static_assert(kTiles <= 64, "one ballot per chunk");
+  __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15;
+  const int64_t nsub = (n + 15) / 16;
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kTiles;
+  uint32_t hw = 0;
+  if (lane < kTiles && t0 + lane < nsub) hw = (row_bits[(t0 + lane) >> 1] >> (((t0 + lane) & 1) * 16)) & 0xffffu;
+  const uint64_t members = __ballot(hw != 0);  // the same in every wave of the block
+  if (members == 0) return;                    // block-uniform
+  float* w1s = smem;
+  float* w2s = smem + DOUT * B::WLD;
+  stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
+  __syncthreads();
+  const int q = lane >> 4;
+  float bias1[B::NCB], bias2[B::NCB];
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    bias1[cb] = b1[cb * 16 + c];
+    bias2[cb] = b2[cb * 16 + c];
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = bi_drop_threshold(p);
+  int k = 0;
+  for (uint64_t mm = members; mm != 0; mm &= mm - 1, ++k) {
+    if (k % NWV != wave) continue;  // wave-uniform
+    const int64_t st = t0 + __ffsll(static_cast<long long>(mm)) - 1;
+    float nx[B::KQ], ns[B::KQ], u[B::KQ], m[B::KQ];
+    load_rows<DIN>(X, ldx, st * 16 + c, n, q, nx);
+    load_rows<DIN>(S, lds, st * 16 + c, n, q, ns);
+#pragma unroll
+    for (int t = 0; t < B::KQ; ++t) {
+      u[t] = nx[t] + ns[t];
+      m[t] = nx[t] * ns[t];
+    }
+    bi_fwd_subtile<DIN, DOUT>(u, m, st, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
+                              mask_out, 0);
+  }
+}
+
+// The row-list forward (kgat_biinter_fwd_list_f32): the rows of a listed node set (rows[0 .. *count), -1 =
+// padding; a sorted list, e.g. a hop set, computes each quad once) in 16-row sub-tiles of four 4-row quads --
+// the quads of the list, not every 16-row tile holding a member: a 15.6k-row hop set spreads over several
+// thousand tiles.  Per quad row the whole-table arithmetic (bi_fwd_quad; the A operand's row c is row c & 3 of
+// the sub-tile's quad c >> 2), so the same bits in H, the norms and the state words.  A block takes windows of
+// 4 * NWV list entries (<= NWV sub-tiles, one per wave); a quad belongs to the window of its first entry.
+template <int DIN, int DOUT, int NWV>
+__global__ __launch_bounds__(64 * NWV, 2) void biinter_fwd_list_kernel(const float* __restrict__ X, int64_t ldx,
+                                                                       const float* __restrict__ S, int64_t lds,
+                                                                       const float* __restrict__ W1,
+                                                                       const float* __restrict__ b1,
+                                                                       const float* __restrict__ W2,
+                                                                       const float* __restrict__ b2,
+                                                                       float* __restrict__ H, int64_t ldh, int64_t n,
+                                                                       float p, uint64_t seed,
+                                                                       float* __restrict__ norm_out,
+                                                                       uint64_t* __restrict__ mask_out,
+                                                                       const int32_t* __restrict__ rows,
+                                                                       const int32_t* __restrict__ count,
+                                                                       int64_t cap) {
+  using B = BiShape<DIN, DOUT>;
+  constexpr int kWin = 4 * NWV;  // list entries per window: at most kWin quads, NWV sub-tiles
+  static_assert(kWin <= 64, "one wave builds a window");
+  __shared__ __attribute__((aligned(16))) float smem[2 * DOUT * B::WLD];
+  __shared__ int32_t s_quad[kWin];
+  __shared__ int32_t s_nq;
+  const int64_t c0 = *count;
+  const int64_t cnt = c0 < 0 ? 0 : (c0 > cap ? cap : c0);  // never past the list
+  const int64_t n_win = (cnt + kWin - 1) / kWin;
+  if (static_cast<int64_t>(blockIdx.x) >= n_win) return;  // block-uniform
+  float* w1s = smem;
+  float* w2s = smem + DOUT * B::WLD;
+  stage_weights<DIN, DOUT>(w1s, w2s, W1, W2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  float bias1[B::NCB], bias2[B::NCB];
+#pragma unroll
+  for (int cb = 0; cb < B::NCB; ++cb) {
+    bias1[cb] = b1[cb * 16 + c];
+    bias2[cb] = b2[cb * 16 + c];
+  }
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = bi_drop_threshold(p);
+  auto quad_of = [&](int64_t pos) -> int32_t {
+    const int32_t r = pos >= 0 && pos < cnt ? rows[pos] : -1;
+    return r >= 0 && r < n ? (r >> 2) : -1;
+  };
+  for (int64_t win = blockIdx.x; win < n_win; win += gridDim.x) {
+    const int64_t pos0 = win * kWin;
+    if (wave == 0) {
+      const int32_t Q = lane < kWin ? quad_of(pos0 + lane) : -1;
+      int32_t prev = __shfl_up(Q, 1);
+      if (lane == 0) prev = quad_of(pos0 - 1);
+      const bool head = Q >= 0 && Q != prev;
+      const uint64_t hm = __ballot(head);
+      if (head) s_quad[__popcll(hm & ((uint64_t{1} << lane) - 1))] = Q;
+      if (lane == 0) s_nq = __popcll(hm);
+    }
+    __syncthreads();  // (the first round: W staged too)
+    const int nq = s_nq;
+    if (4 * wave < nq) {  // wave-uniform
+      int32_t qd[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qd[j] = 4 * wave + j < nq ? s_quad[4 * wave + j] : -1;
+      const int32_t qa = (c >> 2) == 0 ? qd[0] : (c >> 2) == 1 ? qd[1] : (c >> 2) == 2 ? qd[2] : qd[3];
+      const int32_t qc = q == 0 ? qd[0] : q == 1 ? qd[1] : q == 2 ? qd[2] : qd[3];
+      const int64_t arow = qa >= 0 ? static_cast<int64_t>(qa) * 4 + (c & 3) : -1;
+      float nx[B::KQ], ns[B::KQ], u[B::KQ], m[B::KQ];
+      load_rows<DIN>(X, ldx, arow, n, q, nx);
+      load_rows<DIN>(S, lds, arow, n, q, ns);
+#pragma unroll
+      for (int t = 0; t < B::KQ; ++t) {
+        u[t] = nx[t] + ns[t];
+        m[t] = nx[t] * ns[t];
+      }
+      bi_fwd_quad<DIN, DOUT>(u, m, qc, lane, w1s, w2s, bias1, bias2, p, scale, thr, seed, H, ldh, n, norm_out,
+                             mask_out, 0);
+    }
+    __syncthreads();  // the window's quads are read before the next window writes them
   }
 }
 
@@ -975,9 +1179,28 @@ static int launch_fwd_tiles(const float* X, int64_t ldx, const float* S, int64_t
                             float p, uint64_t seed, float* norm, uint64_t* mask, const uint32_t* row_bits,
                             hipStream_t st) {
   constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
-  const int grid = blocks_for(n, 16 * NWV, kCUs * 8 * 4 / NWV);
-  hipLaunchKernelGGL((biinter_fwd_kernel<DIN, DOUT, false, 2, NWV, true>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx,
-                     S, lds, W1, b1, W2, b2, H, ldh, n, p, seed, norm, mask, int64_t{0}, row_bits);
+  // one block per chunk of 4 * NWV tiles (probe at C2, rocprof kernel time, bit-identical: a 15.6k-row hop set
+  // 89.6 -> 79.7 us at 64 -> 64, the ~720 batch rows 20.8 -> 13.5 us, against the grid-stride walk over every
+  // tile's bitmap word; tools/tiles_probe_prof.sh)
+  const int64_t grid = ((n + 15) / 16 + 4 * NWV - 1) / (4 * NWV);
+  if (grid > 0x7fffffff) return KGAT_ERR_INVALID;
+  hipLaunchKernelGGL((biinter_fwd_set_kernel<DIN, DOUT, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S, lds, W1,
+                     b1, W2, b2, H, ldh, n, p, seed, norm, mask, row_bits);
+  KGAT_LAUNCH_CHECK();
+  return KGAT_OK;
+}
+
+template <int DIN, int DOUT>
+static int launch_fwd_list(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,
+                           const float* b1, const float* W2, const float* b2, float* H, int64_t ldh, int64_t n,
+                           float p, uint64_t seed, float* norm, uint64_t* mask, const int32_t* rows,
+                           const int32_t* count, int64_t cap, hipStream_t st) {
+  constexpr int NWV = BiFwdWaves<DIN, DOUT>::k;
+  // one round of blocks (W staged once per block), windows strided over them; blocks past the set's windows
+  // return after reading the count
+  const int grid = blocks_for(cap, 4 * NWV, kCUs * 4 * 4 / NWV);
+  hipLaunchKernelGGL((biinter_fwd_list_kernel<DIN, DOUT, NWV>), dim3(grid), dim3(64 * NWV), 0, st, X, ldx, S, lds, W1,
+                     b1, W2, b2, H, ldh, n, p, seed, norm, mask, rows, count, cap);
   KGAT_LAUNCH_CHECK();
   return KGAT_OK;
 }
@@ -1148,6 +1371,25 @@ extern "C" int kgat_biinter_fwd_tiles_f32(const float* X, int64_t ldx, const flo
                                                          seed, norm_out, mask_out, row_bits, st)
   KGAT_BI_DISPATCH(KGAT_FWDT_CALL)
 #undef KGAT_FWDT_CALL
+}
+
+extern "C" int kgat_biinter_fwd_list_f32(const float* X, int64_t ldx, const float* S, int64_t lds,
+                                         const float* W1, const float* b1, const float* W2, const float* b2,
+                                         float* H, int64_t ldh, int64_t n_rows, const int32_t* rows,
+                                         const int32_t* count, int64_t cap, int32_t d_in, int32_t d_out,
+                                         float dropout_p, uint64_t seed, float* norm_out, uint64_t* mask_out,
+                                         void* stream) {
+  if (!X || !S || !W1 || !b1 || !W2 || !b2 || !H || !rows || !count || n_rows < 0 || cap < 0) return KGAT_ERR_INVALID;
+  if (!aligned16(X) || !aligned16(S) || !aligned16(W1) || !aligned16(W2) || (ldx & 3) || (lds & 3))
+    return KGAT_ERR_INVALID;
+  if (ldx < d_in || lds < d_in || ldh < d_out || !(dropout_p >= 0.f && dropout_p < 1.f)) return KGAT_ERR_INVALID;
+  if ((norm_out == nullptr) != (mask_out == nullptr) || (mask_out != nullptr && d_out > 128)) return KGAT_ERR_INVALID;
+  if (n_rows == 0 || cap == 0) return KGAT_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define KGAT_FWDL_CALL(a, b) kgat::launch_fwd_list<a, b>(X, ldx, S, lds, W1, b1, W2, b2, H, ldh, n_rows, dropout_p, \
+                                                        seed, norm_out, mask_out, rows, count, cap, st)
+  KGAT_BI_DISPATCH(KGAT_FWDL_CALL)
+#undef KGAT_FWDL_CALL
 }
 
 extern "C" int kgat_biinter_fwd_f32(const float* X, int64_t ldx, const float* S, int64_t lds, const float* W1,

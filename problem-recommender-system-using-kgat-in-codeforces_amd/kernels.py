@@ -671,6 +671,36 @@ def biinter_fwd_tiles(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: to
     return out
 
 
+def biinter_fwd_list(X, S, W1, b1, W2, b2, dropout_p: float, seed: int, out: torch.Tensor,
+                     rows: torch.Tensor, count: torch.Tensor, state: BiState | None = None) -> torch.Tensor:
+    """biinter_fwd on the 4-row quads holding a listed node only (kgat_biinter_fwd_list_f32): rows[0..*count)
+    (int32, count a device int32; -1 = padding).  H / state rows of those quads get the whole-table call's
+    bits, the rest of ``out`` and the state are left as they are."""
+    for t, nm in ((X, "X"), (S, "S"), (W1, "W1"), (W2, "W2"), (out, "out")):
+        _req(t, nm, dim=2)
+    n, din = X.shape
+    dout = W1.shape[0]
+    _req(rows, "rows", dtype=torch.int32, dim=1)
+    if count.dtype != torch.int32 or count.numel() < 1 or not count.is_cuda or not rows.is_contiguous():
+        raise ValueError("rows / count must be contiguous int32 device tensors")
+    if S.shape != X.shape or W1.shape != (dout, din) or W2.shape != (dout, din) or tuple(out.shape) != (n, dout):
+        raise ValueError("bi-interaction shape mismatch")
+    if not fused_supported(din, dout) or dout > 128:
+        raise ValueError(f"no fused forward for {din}->{dout}")
+    if not (W1.is_contiguous() and W2.is_contiguous()):
+        raise ValueError("W must be contiguous")
+    words = (dout + 63) // 64
+    if state is not None and (state.kind not in ("fused", "bits") or state.norm.numel() < n
+                              or state.mask.numel() < (n + 15) // 16 * 64 * words):
+        raise ValueError("bi-interaction state too small")
+    _lib.call("kgat_biinter_fwd_list_f32", X.data_ptr(), _ld(X), S.data_ptr(), _ld(S), W1.data_ptr(), b1.data_ptr(),
+              W2.data_ptr(), b2.data_ptr(), out.data_ptr(), _ld(out), n, rows.data_ptr(), count.data_ptr(),
+              rows.numel(), din, dout, float(dropout_p), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+              state.norm.data_ptr() if state is not None else None,
+              state.mask.data_ptr() if state is not None else None, stream_ptr(X.device))
+    return out
+
+
 def biinter_bwd_hop(X, S, dH, W1, W2, dropout_p: float, rows, count, H, state: BiState, out_rows: int,
                     dh_compact: bool = False, out=None, G: torch.Tensor | None = None,
                     gidx: torch.Tensor | None = None, gmap: torch.Tensor | None = None):

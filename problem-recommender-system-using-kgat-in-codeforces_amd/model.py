@@ -857,7 +857,7 @@ def _early_first_hop(graph, users, pos, neg, ws, L: int, hook, marks=None):
 
 
 def _tile_forward_ok(din: int, dout: int) -> bool:
-    """Shapes whose forward can run on a row set's 16-row tiles (kgat_biinter_fwd_tiles_f32: the fused
+    """Shapes whose forward can run on a row set (kgat_biinter_fwd_list_f32 / _tiles_f32: the fused
     kernels with their saved state -- norm + sign/keep words)."""
     return kernels.fused_supported(din, dout) and dout <= 128 and (
         kernels.saved_state_supported(din, dout) or kernels.bits_supported(din, dout))
@@ -870,7 +870,7 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks
     on the first hop F + N(F) (the last layer gathers its A rows from there) -- the same row sets the
     backward's hop chain runs on; with 3 layers layer 0 stays whole (its output is read on the second
     hop, most rows at C4).  Each restricted layer runs kgat_spmm_csr_rows_f32 on its set's rows and
-    kgat_biinter_fwd_tiles_f32 on the 16-row tiles holding them (the set's bitmap): every row the step
+    kgat_biinter_fwd_list_f32 on the 4-row quads holding them (the set's row list): every row the step
     reads gets the full forward's bits (same edges, order and dropout draws), rows outside are never
     read.  At C2 layer 0's set is 1.7 % of the rows (35 % of the edges), layer 1's the ~768 batch rows.
     Returns (tables, sides, states, early) -- early as _early_first_hop's, for the backward -- or
@@ -910,9 +910,9 @@ def _frontier_forward(graph, users, pos, neg, X0, ws, drops, seeds, early, marks
             out_rows, out_count, out_bits = sets[l]
             s = kernels.spmm_rows(graph, x, torch.empty(n, dims[l], dtype=torch.float32, device=x.device), out_rows,
                                   out_count, out_bits)
-            x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l],
-                                          torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device),
-                                          out_bits, state=st)
+            x = kernels.biinter_fwd_list(x, s, W1, b1, W2, b2, drops[l], seeds[l],
+                                         torch.empty(n, dims[l + 1], dtype=torch.float32, device=x.device),
+                                         out_rows, out_count, state=st)
         sides.append(s)
         states.append(st)
         tables.append(x)

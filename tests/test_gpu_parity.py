@@ -1769,6 +1769,72 @@ def test_cf_prologue_marks_first_hop_in_alternating_pairs(pkg):
         m.raise_pending(block=True)
 
 
+@pytest.mark.parametrize("din,dout", [(64, 64), (64, 32), (128, 128)])
+def test_biinter_row_set_forwards_match_whole_table(pkg, din, dout):
+    """kgat_biinter_fwd_list_f32 (4-row quads of a row list: unsorted, a repeated row, two rows of one quad,
+    -1 padding, the table's ragged last quad) and kgat_biinter_fwd_tiles_f32 (16-row tiles of a bitmap) against
+    the whole-table forward: H, the norms and the state words of every row they cover are the same bits (train
+    mode: dropout draws keyed by node), and nothing else is written.  128 -> 128 keeps two state words per lane."""
+    _, kernels = _mods(pkg)
+    n = 5003  # ragged last quad and tile
+    g = torch.Generator().manual_seed(31)
+    X, S = (torch.randn(n, din, generator=g).to(DEV) for _ in range(2))
+    W1, W2 = (torch.randn(dout, din, generator=g).mul_(0.1).to(DEV) for _ in range(2))
+    b1, b2 = (torch.randn(dout, generator=g).mul_(0.1).to(DEV) for _ in range(2))
+    full = kernels.make_state(n, din, dout, X.device)
+    Href = torch.empty(n, dout, device=DEV)
+    kernels._lib.call("kgat_biinter_fwd_f32", X.data_ptr(), din, S.data_ptr(), din, W1.data_ptr(), b1.data_ptr(),
+                      W2.data_ptr(), b2.data_ptr(), Href.data_ptr(), dout, n, din, dout, 0.1, ctypes.c_uint64(77),
+                      full.norm.data_ptr(), full.mask.data_ptr(), kernels.stream_ptr(X.device))
+    words = (dout + 63) // 64
+    rows = np.array([4100, 17, 5002, 16, 17, 900, 903, 2, 4999, -1, 3000, -1], np.int32)  # (padding inside)
+    listed = rows[rows >= 0]
+    cover = np.unique(np.concatenate([(listed >> 2) * 4 + k for k in range(4)]))
+    cover = cover[cover < n]
+
+    def fresh():
+        st = kernels.make_state(n, din, dout, X.device)
+        st.norm.fill_(-7.0)
+        st.mask.fill_(0x5A5A)
+        return torch.full((n, dout), -9.0, device=DEV), st
+
+    def check(H, st, rows_cov):
+        r = torch.from_numpy(rows_cov.astype(np.int64)).to(DEV)
+        assert torch.equal(H[r], Href[r]) and torch.equal(st.norm[r], full.norm[r])
+        quads = np.unique(rows_cov >> 2)
+        idx = []
+        for qd in quads:
+            for gi in range(words):
+                base = ((qd >> 2) * words + gi) * 64 + (qd & 3) * 16
+                idx.extend(range(base, base + 16))
+        w = torch.tensor(idx, device=DEV)
+        assert torch.equal(st.mask[w], full.mask[w])
+        untouched = np.setdiff1d(np.arange(n), rows_cov)
+        u = torch.from_numpy(untouched).to(DEV)
+        assert bool((H[u] == -9.0).all()) and bool((st.norm[u] == -7.0).all())
+
+    H, st = fresh()
+    rt = torch.from_numpy(rows).to(DEV)
+    kernels.biinter_fwd_list(X, S, W1, b1, W2, b2, 0.1, 77, H, rt, torch.tensor([rows.size], dtype=torch.int32,
+                                                                                 device=DEV), state=st)
+    check(H, st, cover)
+    # a count short of the list: only the first 4 entries' quads
+    H, st = fresh()
+    kernels.biinter_fwd_list(X, S, W1, b1, W2, b2, 0.1, 77, H, rt, torch.tensor([4], dtype=torch.int32, device=DEV),
+                             state=st)
+    first = rows[:4]
+    check(H, st, np.unique(np.concatenate([(first >> 2) * 4 + k for k in range(4)])).clip(max=n - 1))
+    # the chunked tile forward on the same set's bitmap: whole 16-row tiles
+    bits = np.zeros((n + 31) // 32, np.uint32)
+    np.bitwise_or.at(bits, listed >> 5, np.uint32(1) << (listed & 31).astype(np.uint32))
+    H, st = fresh()
+    kernels.biinter_fwd_tiles(X, S, W1, b1, W2, b2, 0.1, 77, H, torch.from_numpy(bits.view(np.int32)).to(DEV),
+                              state=st)
+    tiles = np.unique(listed >> 4)
+    tcov = np.concatenate([t * 16 + np.arange(16) for t in tiles])
+    check(H, st, tcov[tcov < n])
+
+
 @pytest.mark.parametrize("dim,layers", [(64, [64]), (64, [64, 32]), (64, [64, 64]), (64, [64, 32, 16]),
                                         (128, [128, 64, 32])])
 def test_frontier_forward_bit_identical(pkg, dim, layers, monkeypatch):
