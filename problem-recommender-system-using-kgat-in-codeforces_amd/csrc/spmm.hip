@@ -322,7 +322,8 @@ __global__ __launch_bounds__(256) void frontier_mark_kernel(kgat_csr A, const in
   }
   for (int64_t e = A.rowptr[i] + threadIdx.x; e < A.rowptr[i + 1]; e += blockDim.x) {
     const int32_t j = A.col[e];
-    atomicOr(&bits1[j >> 5], 1u << (j & 31));
+    const uint32_t b = 1u << (j & 31);
+    if ((bits1[j >> 5] & b) == 0u) atomicOr(&bits1[j >> 5], b);  // test before set (see cf_begin_kernel)
   }
 }
 

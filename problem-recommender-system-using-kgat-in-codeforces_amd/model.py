@@ -1454,12 +1454,18 @@ class KGAT(nn.Module):
             # this step's backward (and frontier forward / DP hop exchange)
             _release_marks(g)
             mark, clear = kernels.hop_bitmaps_next(g)
+            # the marking only where a consumer will list the first hop (C3's dense graph: every slot's row
+            # holds thousands of entries and the hop path is off there -- 291 us of atomics for nothing);
+            # otherwise the current pair is zeroed and a backward that does take the hop path marks it itself
+            premark = self._first_hop_wanted(g, drops, frontier or hook is not None)
             r = self._ids.check_cf("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
-                                   g.device, g.node_map, clear, mark=(g, mark))
+                                   g.device, g.node_map, clear, mark=(g, mark) if premark else None)
             if r is not None:
-                kernels.hop_bitmaps_commit(g)
+                if premark:
+                    kernels.hop_bitmaps_commit(g)
                 ids, rows, fcount = r
-                g._marked = tok = _MarkedBatch(rows, fcount, cleared=kernels.PREMARKED)
+                g._marked = tok = _MarkedBatch(rows, fcount,
+                                               cleared=kernels.PREMARKED if premark else kernels.PRECLEARED)
                 marks = (rows, fcount, tok)
         if marks is None:
             ids = self._ids.check("TRAIN_CF ids", (user_ids, positive_item_ids, negative_item_ids), g.n_nodes,
@@ -1469,6 +1475,19 @@ class KGAT(nn.Module):
         if not self.direct_backward and loss.grad_fn is not None:
             loss.grad_fn.fast_backward = None  # the autograd engine (the default; _StepLoss)
         return loss
+
+    def _first_hop_wanted(self, g, drops, forward_sets: bool) -> bool:
+        """Whether this step's first hop F + N(F) is likely listed: the hop path is on, layer L-2's hop set
+        was small at the last step (or is unknown), and a consumer exists -- the frontier forward or the
+        replicas' hop exchange (``forward_sets``), or the backward's hop chain, which needs layer L-2's fused
+        saved state.  A wrong guess costs time only: unmarked, the backward marks the hop itself."""
+        L = len(drops)
+        if HOP_DENSE_FRACTION <= 0 or (L >= 2 and not _hop_small(g, L - 2, g.n_nodes)):
+            return False
+        if forward_sets or L < 2:
+            return True
+        W1 = self._cf_weights()[4 * (L - 2)]
+        return kernels.saved_state_supported(W1.shape[1], W1.shape[0])
 
     def _calc_kg_loss(self, heads, relations, positive_tails, negative_tails) -> torch.Tensor:
         dev = self._user_entity_embedding.weight.device

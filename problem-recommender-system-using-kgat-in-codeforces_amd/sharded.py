@@ -895,8 +895,8 @@ class _ShardedCFLoss(torch.autograd.Function):
                 h = torch.empty(shard.n, W1.shape[0], dtype=torch.float32, device=x.device)
                 if st.kind == "gemm":
                     x = kernels.biinter_fwd_gemm_rows(x, s, rws, m, W1, b1, W2, b2, drops[l], seeds[l], h, st)
-                else:
-                    x = kernels.biinter_fwd_tiles(x, s, W1, b1, W2, b2, drops[l], seeds[l], h, bits, state=st)
+                else:  # the set's 4-row quads (kgat_biinter_fwd_list_f32), as the single-GPU frontier forward
+                    x = kernels.biinter_fwd_list(x, s, W1, b1, W2, b2, drops[l], seeds[l], h, rws, cnt, state=st)
             sides.append(s)
             states.append(st)
             tables.append(x)
