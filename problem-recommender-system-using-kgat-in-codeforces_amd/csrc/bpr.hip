@@ -234,7 +234,8 @@ __global__ __launch_bounds__(1024) void cf_begin_kernel(const int64_t* __restric
     for (int64_t e = A.rowptr[i] + t; e < A.rowptr[i + 1]; e += 256) {
       const int32_t j = A.col[e];
       const uint32_t b = 1u << (j & 31);
-      if ((mark1[j >> 5] & b) == 0u) atomicOr(&mark1[j >> 5], b);
+      if ((__hip_atomic_load(&mark1[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & b) == 0u)
+        atomicOr(&mark1[j >> 5], b);
     }
     return;
   }

@@ -323,7 +323,9 @@ __global__ __launch_bounds__(256) void frontier_mark_kernel(kgat_csr A, const in
   for (int64_t e = A.rowptr[i] + threadIdx.x; e < A.rowptr[i + 1]; e += blockDim.x) {
     const int32_t j = A.col[e];
     const uint32_t b = 1u << (j & 31);
-    if ((bits1[j >> 5] & b) == 0u) atomicOr(&bits1[j >> 5], b);  // test before set (see cf_begin_kernel)
+    // test before set (see cf_begin_kernel); a relaxed atomic load: the word is being OR-ed by other threads
+    if ((__hip_atomic_load(&bits1[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & b) == 0u)
+      atomicOr(&bits1[j >> 5], b);
   }
 }
 
